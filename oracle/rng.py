@@ -1,0 +1,65 @@
+"""numpy restatement of the counter-based dropout RNG the HIP kernels use.
+
+TEST INFRASTRUCTURE (see oracle/__init__.py).
+
+The reference draws dropout masks with ``torch.bernoulli_`` (CPU generator,
+``torch.nn.functional.dropout`` -> ``at::native::_dropout_impl``); that stream
+cannot be reproduced on the GPU.  The build therefore defines its own
+counter-based mask (spec below, kernel side in ``csrc/common.h``) and the
+parity fixtures inject exactly these masks into the reference through a
+patched ``F.dropout`` (tests/golden/gen_golden.py).  Dropout application itself
+follows the reference: ``y = x * (mask / (1 - p))`` (``_dropout_impl``).
+
+Spec (all u32 arithmetic, wrapping):
+    mix32(x)      = lowbias32 finaliser
+    site_key      = mix32(lo(seed) ^ mix32(hi(seed) + site * 0x9E3779B9))
+    bits(key, i)  = mix32(mix32(i ^ key) + key)
+    keep(i)       = (bits >> 8) >= round(p * 2^24)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+M32 = 0xFFFFFFFF
+
+
+def mix32_np(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.uint32, copy=True)
+    x ^= x >> np.uint32(16)
+    x *= np.uint32(0x7FEB352D)
+    x ^= x >> np.uint32(15)
+    x *= np.uint32(0x846CA68B)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def mix32_int(x: int) -> int:
+    x &= M32
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & M32
+    x ^= x >> 16
+    return x
+
+
+def site_key(seed: int, site: int) -> int:
+    lo, hi = seed & M32, (seed >> 32) & M32
+    return mix32_int(lo ^ mix32_int((hi + site * 0x9E3779B9) & M32))
+
+
+def thresh24(p: float) -> int:
+    return min(1 << 24, int(round(float(p) * (1 << 24))))
+
+
+def keep_mask(seed: int, site: int, p: float, shape) -> np.ndarray:
+    """Boolean keep-mask over a tensor of ``shape`` indexed by its C-order linear index."""
+    n = int(np.prod(shape))
+    key = np.uint32(site_key(seed, site))
+    idx = np.arange(n, dtype=np.uint32)
+    b = mix32_np(mix32_np(idx ^ key) + key)
+    return ((b >> np.uint32(8)) >= np.uint32(thresh24(p))).reshape(shape)
+
+
+def dropout_scale(p: float) -> np.float32:
+    return np.float32(1.0) / np.float32(1.0 - p)

@@ -1,0 +1,89 @@
+"""Deterministic synthetic params / batches / fingerprints for parity fixtures.
+
+TEST INFRASTRUCTURE (see oracle/__init__.py).  The same functions run in the
+golden generator (which feeds them to the reference) and in the tests on the
+GPU box (which feed them to the HIP path), so large fixtures only need to store
+seeds + fingerprints, not weights.
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+
+
+def _key_seed(seed: int, key: str) -> int:
+    return (seed * 1_000_003 + zlib.crc32(key.encode())) & 0xFFFFFFFF
+
+
+def make_params(shapes, seed: int, pad_id: int = 0):
+    """Reference-like init (nn.Embedding N(0,1), nn.Linear U(+-1/sqrt(fan_in))), perturbed so
+    norms/biases are non-trivial.  ``shapes``: list of (state_dict key, shape)."""
+    out = {}
+    for k, shp in shapes:
+        r = np.random.default_rng(_key_seed(seed, k))
+        if "cat_embs" in k or "emb_att" in k or "emb_rep" in k or "pbias.rel" in k:
+            a = r.standard_normal(shp)
+            if ("emb_att" in k or "emb_rep" in k):
+                a[pad_id] = 0.0
+        elif k.endswith("norm1.w") or k.endswith("norm2.w") or k.endswith("pre_norm.w"):
+            a = 1.0 + 0.1 * r.standard_normal(shp)
+        elif k in ("qnn.U", "qnn.V"):
+            a = 0.2 * r.standard_normal(shp)
+        elif k in ("num_embed.weight", "mask_embed.weight"):
+            a = 0.3 * r.standard_normal(shp)
+        elif k == "num_embed.bias":
+            a = 0.1 * r.standard_normal(shp)
+        else:
+            fan_in = shp[-1] if len(shp) > 1 else max(1, shp[0])
+            bound = 1.0 / np.sqrt(fan_in)
+            a = r.uniform(-bound, bound, shp)
+        out[k] = a.astype(np.float32)
+    return out
+
+
+def make_batch(B, Fn, Fm, cards, L, vocab, seed, pad_id=0, edge_rows=True, lognormal=False, pos_rate=0.3):
+    r = np.random.default_rng(seed)
+    X_num = r.standard_normal((B, Fn)).astype(np.float32)
+    if lognormal and Fn > 0:
+        sel = r.random((B, Fn)) < 0.3
+        X_num[sel] = np.minimum(r.lognormal(0.0, 2.0, sel.sum()), 1e6).astype(np.float32)
+    X_mask = (r.random((B, Fm)) < 0.1).astype(np.uint8)
+    if Fn == Fm and Fn > 0:
+        X_num[X_mask.astype(bool)] = 0.0
+    X_cat = np.stack([r.integers(0, c, B) for c in cards], axis=1).astype(np.int32) if cards else \
+        np.zeros((B, 0), np.int32)
+    seq = np.full((B, L), pad_id, dtype=np.int32)
+    lens = r.integers(0, L + 1, B)
+    for b in range(B):
+        n = int(lens[b])
+        if n:
+            seq[b, L - n:] = r.integers(1, vocab, n)        # right-aligned, left-padded
+    if edge_rows and B >= 4:
+        seq[0] = pad_id                                     # empty history
+        seq[1] = pad_id
+        seq[1, L - 3:] = r.integers(1, vocab, 3)            # fewer than K real tokens
+        seq[2, L // 2:] = r.integers(1, vocab)              # one token repeated
+        seq[3] = r.integers(1, vocab, L)                    # full row
+    y = (r.random(B) < pos_rate).astype(np.int8)
+    if B >= 2:
+        y[0], y[1] = 1, 0
+    groups = r.integers(0, 2**31 - 1, B).astype(np.int64)
+    return dict(X_num=X_num, X_mask=X_mask, X_cat=X_cat, seq=seq, y=y, groups=groups)
+
+
+def fingerprint(a: np.ndarray, seed: int = 7, n: int = 2048):
+    """Size-independent summary: sampled elements + float64 sum / sumsq / random projection."""
+    a = np.asarray(a, dtype=np.float32).ravel()
+    r = np.random.default_rng(seed + a.size)
+    idx = np.sort(r.choice(a.size, size=min(n, a.size), replace=False)).astype(np.int64)
+    proj = r.standard_normal(a.size).astype(np.float32)
+    a64 = a.astype(np.float64)
+    return dict(idx=idx, vals=a[idx], sum=a64.sum(), sumsq=(a64 * a64).sum(),
+                proj=float(a64 @ proj.astype(np.float64)))
+
+
+def fingerprint_proj_vec(size: int, seed: int = 7):
+    r = np.random.default_rng(seed + size)
+    r.choice(size, size=min(2048, size), replace=False)
+    return r.standard_normal(size).astype(np.float32)

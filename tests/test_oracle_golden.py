@@ -1,0 +1,60 @@
+"""Pin the CPU oracle (oracle/model.py) against the reference's own outputs (tests/golden/*.npz)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import CASES, Fixture, to_torch_batch
+from oracle import rng
+from oracle.model import Dropper, TrainState, forward
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_matches_reference(case):
+    fx = Fixture(case)
+    m, A = fx.meta, fx.arch
+    tr = m["train"]
+    P = {k: torch.from_numpy(v) for k, v in fx.params0().items()}
+    st = TrainState(P, A, tr["lr"], tr["wd"], tr["clip"], ema_cfg=m["cfg"].get("ema") if
+                    m["cfg"].get("ema", {}).get("enabled") else None)
+    assert sorted(A.grad_params()) == sorted(m["grad_keys"])
+    for t in range(m["steps"]):
+        b = fx.batch(t)
+        rec = {}
+        loss, (z, p, a), grads, gn = st.step(to_torch_batch(b), torch.from_numpy(b["y"]).float(),
+                                             m["lrs"][t], m["seeds"][t], record=rec)
+        fx.check(f"out{t}/logits", z, 1e-5, 1e-6)
+        fx.check(f"out{t}/prob", p, 1e-5, 1e-7)
+        fx.check(f"out{t}/aux", a, 1e-5, 1e-6)
+        assert abs(float(loss) - float(fx.z[f"out{t}/loss"])) < 1e-5 * max(1, abs(float(loss)))
+        if tr["clip"] > 0:
+            assert abs(float(gn) - float(fx.z[f"out{t}/gnorm"])) < 1e-5 * float(gn)
+        assert np.array_equal(rec["topk_idx"].numpy(), fx.z[f"out{t}/topk_idx"])
+        fx.check(f"out{t}/topk_vals", rec["topk_vals"], 1e-6, 1e-5)
+        if t == 0:
+            for k, g in grads.items():
+                fx.check(f"grad0/{k}", g, 1e-5, 1e-8)
+    # AdamW turns gradients that are pure rounding noise (e.g. the MHA key bias: softmax is shift-invariant,
+    # so its exact gradient is 0) into +-lr-sized steps; elementwise tolerance is therefore one Adam step.
+    adam_step = 2.0 * max(m["lrs"])
+    for k, v in st.P.items():
+        fx.check(f"pT/{k}", v.detach(), 1e-4, adam_step)
+    for k in st.grad_keys:
+        fx.check(f"mT/{k}", st.m[k], 1e-4, 1e-9)
+        fx.check(f"vT/{k}", st.v[k], 1e-4, 1e-12)
+    if st.shadow is not None:
+        for k, v in st.shadow.items():
+            fx.check(f"emaT/{k}", v, 1e-5, 1e-7)
+    with torch.no_grad():
+        z, p, a = forward(st.P, to_torch_batch(fx.batch(m["steps"] - 1)), A, Dropper(0, training=False))
+    fx.check("eval/logits", z, 1e-5, 1e-6)
+    fx.check("eval/aux", a, 1e-5, 1e-6)
+
+
+def test_rng_mask_rate_and_determinism():
+    k1 = rng.keep_mask(12345, 3, 0.1, (1000, 100))
+    k2 = rng.keep_mask(12345, 3, 0.1, (1000, 100))
+    assert np.array_equal(k1, k2)
+    assert abs(k1.mean() - 0.9) < 0.005
+    k3 = rng.keep_mask(12345, 4, 0.1, (1000, 100))
+    assert (k1 != k3).mean() > 0.1
+    assert rng.keep_mask(1, 1, 0.0, (10,)).all()
