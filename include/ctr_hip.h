@@ -1,0 +1,220 @@
+/* C-ABI of libctrhip.so -- the MI355X (gfx950) kernels behind the CTRModel training hot path.
+ *
+ * The reference (biyotteu/toss-next-ctr-prediction) is pure PyTorch: it has no FFI.  Each entry
+ * point below replaces the torch ops of one reference function, cited as path:line relative to the
+ * reference root.  The Python host side (tossctr/_lib.py) binds these through ctypes; see
+ * INTEGRATION.md for the binding a maintainer would add to the reference itself.
+ *
+ * Conventions (all entries):
+ *   - device pointers are plain fp32 / int32 / uint32 arrays owned by the caller (PyTorch's caching
+ *     allocator); the library never allocates on the hot path; scratch comes in via `ws` pointers
+ *     sized by the matching *_ws_size query.
+ *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); no host sync inside.
+ *   - return 0 on success, negative on error; ctr_last_error() returns a thread-local message.
+ *   - dropout everywhere uses the counter-based mask {key, thresh24, scale} of csrc/common.h
+ *     (spec shared with oracle/rng.py); thresh24 == 0 disables it.
+ */
+#ifndef CTR_HIP_H
+#define CTR_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* ctr_last_error(void);
+int ctr_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Dense GEMM on fp32 MFMA (v_mfma_f32_16x16x4_f32):  C[M,N] = op(A)[M,K] * op(B)[K,N] (+ epilogue)
+ * Replaces every nn.Linear / matmul on the path: MHA in/out projections (torch MHA via
+ * src/models/dare.py:43,64), FFN (src/models/dare.py:45-48), QNN A=z@U (src/models/qnn_alpha.py:92),
+ * MLP (src/models/qnn_alpha.py:78-84,129), fc head (src/models/wrapper.py:95-100) and their
+ * backward dX / dW products.
+ *   ta: A stored [K,M] (A^T row-major) instead of [M,K];  tb: B stored [N,K] instead of [K,N].
+ *   splits > 1: K split across workgroups into ws (splits*M*N floats), reduced in fixed order.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  const float* bias;     /* [N] added after the product (nullable)                                */
+  const float* add;      /* [M,N] addend, row stride ld_add (nullable)                            */
+  int ld_add;
+  int act;               /* 0 none, 1 relu, 2 gelu(erf)                                           */
+  float* pre;            /* store pre-activation (after bias/add), row stride ldc (nullable)      */
+  int dact;              /* backward: 0 none, 1 relu'(aux), 2 gelu'(aux); multiplies the product   */
+  const float* aux;      /* [M,N] pre-activation from the forward, row stride ldc                 */
+  uint32_t drop_key, drop_thresh; /* dropout over linear index row*N+col (fwd: apply, bwd: mask)  */
+  float drop_scale;
+  const float* resid;    /* fused residual + RMSNorm over the whole row (requires N <= 64):       */
+  int ld_resid;          /*   h = resid + (acc + bias); C = (w*h) * rsqrt(mean(h^2) + eps)        */
+  const float* norm_w;   /*   src/models/dare.py:12-13, 64-70                                     */
+  float* norm_h;         /*   saved h [M,N] (row stride ldc)                                      */
+  float* norm_r;         /*   saved rsqrt factor [M]                                              */
+  float norm_eps;
+} ctr_gemm_epi_t;
+
+size_t ctr_gemm_ws_size(int M, int N, int splits);
+int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+             float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, void* stream);
+
+
+/* ---------------------------------------------------------------------------------------------
+ * Feature embeddings / context                                                    (embed.hip)
+ * ------------------------------------------------------------------------------------------- */
+/* NumericFeatureEmbedding / BinaryFeatureEmbedding.forward, src/models/feature_embed.py:19-27,42-48:
+ * out[b, f*D + d] (row stride out_ld) = sum_k (x[b,f]*W[f,k] + bias[f,k]) * P[d,k]  (bias nullable) */
+int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, const float* bias, const float* P, int fe,
+                       int D, float* out, long out_ld, void* stream);
+size_t ctr_feat_embed_bwd_ws(int B, int F, int D);
+int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, const float* bias, const float* P, int fe, int D,
+                       const float* dout, long dout_ld, float* dW, float* dbias, float* dP, float* ws, void* stream);
+/* CTRModel._embed_cats + emb_dropout, src/models/wrapper.py:106-112,149-150: hashed-bucket gather of
+ * X_cat[b,c] from table c (arena + tab_off[c], row width dims[c]) projected by P_c (arena + proj_off[c]).
+ * cat_e = pre-dropout (B, Fc, D); xf (nullable) receives the dropped copy at row stride xf_ld.      */
+int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const long* tab_off, const long* proj_off,
+                      const int* dims, int D, float* cat_e, float* xf, long xf_ld, uint32_t drop_key,
+                      uint32_t drop_thresh, float drop_scale, void* stream);
+size_t ctr_cat_embed_bwd_ws(int B, int Fc);
+/* backward: row-grad contributions (B*Fc rows x 64, zero-padded) keyed row_base[c] + X_cat[b,c] for
+ * ctr_rowgrad, and dP_c written into grad_arena + proj_goff[c].                                    */
+int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* arena, const long* tab_off, const long* proj_off,
+                      const int* dims, int D, const float* dcat, const uint32_t* row_base, float* contrib,
+                      uint32_t* keys, float* grad_arena, const long* proj_goff, float* ws, void* stream);
+/* CTRModel._context_vector / _make_query, src/models/wrapper.py:114-136; mode 0 S1, 1 S2, 2 concat */
+int ctr_context_fwd(const float* num_e, long num_ld, int Fn, const float* mask_e, long mask_ld, int Fm,
+                    const float* cat_e, int Fc, int D, int B, int mode, int qi, const float* Wc, const float* bc,
+                    float* ctx, float* hq, float* query, void* stream);
+int ctr_context_bwd(const float* num_e, long num_ld, int Fn, const float* mask_e, long mask_ld, int Fm,
+                    const float* cat_e, int Fc, int D, int B, int mode, int qi, const float* Wc, const float* hq,
+                    const float* dquery, const float* dxf_cat, long dxf_ld, uint32_t drop_key, uint32_t drop_thresh,
+                    float drop_scale, const float* dfc, long dfc_ld, float* dnum, float* dmask, float* dcat,
+                    float* dpre, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DARE                                                                            (dare.hip)
+ * ------------------------------------------------------------------------------------------- */
+/* DARE.topk_select, src/models/dare.py:116-138.  seq (B,L) int32 token ids; decay_log (L) =
+ * log(exp(-(L-1-l)/max(1,tau)) + 1e-8); pads score -1e9; sorted top-K (ties: lower position first).
+ * Outputs idx (B,K) positions, tok (B,K) token ids, vals (B,K), sel (B,K,D) = E_rep[tok].          */
+int ctr_dare_topk_fwd(const int* seq, int B, int L, const float* q, const float* E_att, const float* E_rep, int D,
+                      const float* decay_log, int K, int pad_id, int* idx, int* tok, float* vals, float* sel,
+                      void* stream);
+/* backward: dq (B,D); att row-grad contributions dvals*q (B*K, D) and keys (token or 0xFFFFFFFF for
+ * pads, whose grads padding_idx drops); rep keys (the rep contributions are dsel itself).          */
+int ctr_dare_topk_bwd(const int* tok, int B, int K, const float* q, const float* E_att, int D, const float* dvals,
+                      int pad_id, float* dq, float* att_contrib, uint32_t* att_keys, uint32_t* rep_keys, void* stream);
+/* DARE.forward gating/pool/aux head, src/models/dare.py:150-162; gating 0 softmax, 1 relu */
+int ctr_pool_fwd(const float* x, const float* vals, int B, int K, int D, int gating, uint32_t drop_key,
+                 uint32_t drop_thresh, float drop_scale, const float* waux, const float* baux, float* w, float* u,
+                 float* xf_u, long xf_ld, float* aux, void* stream);
+int ctr_pool_bwd(const float* x, const float* vals, const float* w, int B, int K, int D, int gating, uint32_t drop_key,
+                 uint32_t drop_thresh, float drop_scale, const float* waux, const float* du, long du_ld,
+                 const float* daux, float* dx, float* dvals, void* stream);
+/* PositionalBias + head mean, src/models/dare.py:29-37,56-60: out[d] = mean_h rel[d,h] */
+int ctr_pos_bias_mean(const float* rel, int H, int n, float* out, void* stream);
+int ctr_pos_bias_grad(const float* part, int nparts, int H, int n, float* drel, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Attention core of DAREEncoderLayer (MHA explicit path), src/models/dare.py:53-62    (attn.hip)
+ * qkv (B*K, 3D) from the in-projection GEMM; o (B*K, D); mrow/lrow (B*H*K) row max / sum saved for
+ * the recompute backward; drel_part (B*nparts, 2tk+1) positional-bias grad partials.
+ * ------------------------------------------------------------------------------------------- */
+int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
+                 uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* o, float* mrow, float* lrow,
+                 void* stream);
+int ctr_attn_bwd_nparts(int H, int K, int D);
+int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D, const float* relmean,
+                 int tk, float scale, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const float* mrow,
+                 const float* lrow, float* dqkv, float* drel_part, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Row / column ops                                                                (rowops.hip)
+ * ------------------------------------------------------------------------------------------- */
+/* RMSNorm.forward for long rows (QNN pre_norm, src/models/qnn_alpha.py:110-113) */
+int ctr_rmsnorm_fwd(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy, float* r,
+                    void* stream);
+int ctr_rmsnorm_bwd_nparts(int M, int N);
+/* RMSNorm backward: dh = w*dy*r - h*r^3/N*sum(w*dy*h) (+ add); dw partials (nparts, N) */
+int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long ldh, const float* r, const float* w, int M, int N,
+                    float* dh, long lddh, const float* add, long ld_add, float* dw_part, void* stream);
+size_t ctr_colsum_ws_size(int M, int N);
+/* out[n] = sum_m X[m,n] / div  (bias grads; div = B gives torch .mean(dim=0)) */
+int ctr_colsum(const float* X, long ld, int M, int N, float div, float* out, float* ws, void* stream);
+/* bce_wll_style(logits) + aux_w * bce_wll_style(aux) (src/train.py:71-90,165-168) and d/dlogits, d/daux */
+int ctr_loss(const float* z, const float* za, const float* y, int B, float aux_w, float* loss, float* dz, float* dza,
+             void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * QNN-alpha, src/models/qnn_alpha.py                                                  (qnn.hip)
+ * ------------------------------------------------------------------------------------------- */
+/* U (H,D,R) <-> Ucat (D,H*R) so all heads' A = z @ U_h is one GEMM */
+int ctr_qnn_ucat(const float* src, int H, int D, int R, float* dst, int inverse, void* stream);
+/* _pair_interaction_all reduction (l.86-97): S = sum_F A, quad = S^2 - sum_F A^2, inter = quad @ V_h */
+int ctr_qnn_reduce_fwd(const float* A, int B, int F, int H, int R, const float* V, int P, float* S, float* quad,
+                       float* inter, void* stream);
+int ctr_qnn_reduce_bwd(const float* A, int B, int F, int H, int R, const float* V, int P, const float* S,
+                       const float* dinter, float* dA, void* stream);
+/* SEBlock (l.17-26): gate from the batch mean; scale + QNN dropout (l.120-121) */
+int ctr_se_fwd_gate(const float* mean, int C, int Cr, const float* W1, const float* b1, const float* W2,
+                    const float* b2, float* g1, float* gate, void* stream);
+int ctr_scale_drop(const float* x, int B, int C, const float* gate, uint32_t drop_key, uint32_t drop_thresh,
+                   float drop_scale, float* out, long out_ld, void* stream);
+size_t ctr_se_bwd_ws(int B, int C);
+int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, int Cr, const float* gate,
+               const float* g1, const float* mean, const float* W1, const float* W2, uint32_t drop_key,
+               uint32_t drop_thresh, float drop_scale, float* dx, float* dW1, float* db1, float* dW2, float* db2,
+               float* ws, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Embedding-table gradients: deterministic row dedup (rowgrad.hip) -- replaces
+ * embedding_dense_backward for src/models/dare.py:89-90 and src/models/wrapper.py:34.
+ * keys (n) with 0xFFFFFFFF = dropped; contrib rows at stride ld; outputs sorted unique keys, summed
+ * rows (n_uniq x width) and the device count n_uniq.  key_bits: sort bits (max valid key < 2^bits-1).
+ * ------------------------------------------------------------------------------------------- */
+size_t ctr_rowgrad_ws_size(int n);
+int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, int width, int ld, int key_bits,
+                uint32_t* uniq_keys, float* uniq_grad, uint32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Fused clip_grad_norm_ + AdamW + EMA over the parameter arena                      (optim.hip)
+ * src/train.py:133-139,185-199; torch/optim/adam.py (_single_tensor_adam); src/utils/ema.py:92-131
+ * ------------------------------------------------------------------------------------------- */
+typedef struct {
+  int64_t p_off;            /* element offset of the segment in the arenas (multiple of 4)          */
+  int64_t n;                /* elements                                                             */
+  int32_t width;            /* row width (kind 1)                                                   */
+  int32_t kind;             /* 0 dense grad, 1 sparse table rows, 2 no grad (EMA only)              */
+  int64_t g_off;            /* kind 0: offset into the dense grad arena                             */
+  const uint32_t* keys;     /* kind 1: sorted unique keys (ctr_rowgrad)                             */
+  const float* G;           /* kind 1: summed rows, row stride g_ld                                 */
+  const uint32_t* n_uniq;   /* kind 1: device count                                                 */
+  int32_t g_ld;
+  uint32_t key_base;        /* key of row 0 of this segment                                         */
+} ctr_opt_seg_t;
+typedef struct {
+  int32_t seg, pad;
+  int64_t e0, e1;           /* element range [e0, e1) inside the segment (e0 multiple of 4)         */
+} ctr_opt_chunk_t;
+
+int ctr_opt_chunk_elems(void);
+int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, float* P, float* M, float* V,
+                  float* E, const float* dgrad, const float* coef, float lr, float wd, float beta1, float beta2,
+                  float eps, int step, float ema_decay, int do_adam, int do_ema, void* stream);
+int ctr_norm_nparts_per_call(void);
+int ctr_sqnorm_dense(const float* x, long n, float* part, void* stream);
+int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int width, int ld,
+                    uint32_t invalid_key, float* part, void* stream);
+/* out[0] = global L2 norm, out[1] = min(1, max_norm/(norm+1e-6)) (1 if max_norm <= 0) */
+int ctr_clip_finalize(const float* part, int nparts, float max_norm, float* out, void* stream);
+
+
+/* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */
+int ctr_sigmoid(const float* x, int n, float* y, void* stream);
+int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream);
+int ctr_scatter_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int max_uniq, int width, int ld,
+                     uint32_t key_base, long n_rows, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CTR_HIP_H */

@@ -1,0 +1,233 @@
+"""GPU unit parity of the HIP kernels (called through the C-ABI) against plain torch fp32 references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    from tossctr import _lib
+    return _lib
+
+
+def ptr(t, e=0):
+    return t.data_ptr() + e * t.element_size() if t is not None else None
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", [(300, 96, 32, 0, 1), (257, 384, 32, 0, 1), (130, 32, 384, 0, 1),
+                                         (64, 512, 7552, 0, 1), (384, 32, 5000, 1, 0), (33, 70, 19, 1, 1),
+                                         (1, 32, 4096, 1, 0), (4096, 1, 256, 0, 1), (200, 130, 64, 0, 0)])
+@pytest.mark.parametrize("splits", [1, 7])
+def test_gemm_vs_torch(M, N, K, ta, tb, splits):
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    A = torch.randn((K, M) if ta else (M, K), device="cuda", generator=g)
+    B = torch.randn((N, K) if tb else (K, N), device="cuda", generator=g)
+    C = torch.empty(M, N, device="cuda")
+    ws = torch.empty(splits * M * N + 16, device="cuda")
+    L.call("ctr_gemm", M, N, K, ptr(A), A.shape[1], ta, ptr(B), B.shape[1], tb, ptr(C), N, None, splits, ptr(ws),
+           stream())
+    ref = (A.t() if ta else A).double() @ (B.t() if tb else B).double()
+    assert rel(C.double(), ref) < 1e-5
+
+
+def test_gemm_epilogues():
+    L = _lib()
+    M, N, K = 517, 384, 32
+    x = torch.randn(M, K, device="cuda")
+    W = torch.randn(N, K, device="cuda") * 0.2
+    b = torch.randn(N, device="cuda")
+    out = torch.empty(M, N, device="cuda")
+    pre = torch.empty(M, N, device="cuda")
+    epi = L.GemmEpi(bias=ptr(b), act=2, pre=ptr(pre))
+    L.call("ctr_gemm", M, N, K, ptr(x), K, 0, ptr(W), K, 1, ptr(out), N, epi, 1, None, stream())
+    a_ref = x @ W.t() + b
+    assert rel(pre, a_ref) < 1e-5
+    assert rel(out, torch.nn.functional.gelu(a_ref)) < 1e-5
+    # fused residual + RMSNorm, N = D = 32
+    D = 32
+    W2 = torch.randn(D, N, device="cuda") * 0.05
+    b2 = torch.randn(D, device="cuda")
+    res = torch.randn(M, D, device="cuda")
+    w = torch.rand(D, device="cuda") + 0.5
+    y, h, r = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
+    epi = L.GemmEpi(bias=ptr(b2), resid=ptr(res), ld_resid=D, norm_w=ptr(w), norm_h=ptr(h), norm_r=ptr(r),
+                    norm_eps=1e-6)
+    L.call("ctr_gemm", M, D, N, ptr(out), N, 0, ptr(W2), N, 1, ptr(y), D, epi, 1, None, stream())
+    h_ref = res + (out @ W2.t() + b2)
+    y_ref = w * h_ref * torch.rsqrt(h_ref.pow(2).mean(-1, keepdim=True) + 1e-6)
+    assert rel(h, h_ref) < 1e-5 and rel(y, y_ref) < 1e-5
+    # backward epilogue: relu' x dropout mask
+    aux = torch.randn(M, N, device="cuda")
+    dy = torch.randn(M, D, device="cuda")
+    dgrad = torch.empty(M, N, device="cuda")
+    from tossctr.rng import drop_args
+    key, th, sc = drop_args(99, 5, 0.2, True)
+    epi = L.GemmEpi(dact=1, aux=ptr(aux), drop_key=key, drop_thresh=th, drop_scale=sc)
+    L.call("ctr_gemm", M, N, D, ptr(dy), D, 0, ptr(W2), N, 0, ptr(dgrad), N, epi, 1, None, stream())
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import rng as orng
+    keep = torch.from_numpy(orng.keep_mask(99, 5, 0.2, (M, N))).cuda()
+    ref = (dy @ W2) * keep.float() * sc * (aux > 0).float()
+    assert rel(dgrad, ref) < 1e-5
+
+
+def test_rowgrad_dedup_matches_numpy():
+    L = _lib()
+    rng = np.random.default_rng(0)
+    n, width = 5000, 24
+    keys = rng.integers(0, 700, n).astype(np.uint32)
+    keys[rng.random(n) < 0.05] = 0xFFFFFFFF
+    vals = rng.standard_normal((n, width)).astype(np.float32)
+    kt = torch.from_numpy(keys.view(np.int32)).cuda()
+    vt = torch.from_numpy(vals).cuda()
+    uk = torch.empty(n, dtype=torch.int32, device="cuda")
+    ug = torch.empty(n, width, device="cuda")
+    nu = torch.zeros(1, dtype=torch.int32, device="cuda")
+    wsz = L.query("ctr_rowgrad_ws_size", n)
+    ws = torch.empty(wsz, dtype=torch.uint8, device="cuda")
+    L.call("ctr_rowgrad", ptr(kt), ptr(vt), n, width, width, 10, ptr(uk), ptr(ug), ptr(nu), ptr(ws), wsz, stream())
+    torch.cuda.synchronize()
+    u = int(nu.item())
+    got_k = uk[:u].cpu().numpy().view(np.uint32)
+    ref_k = np.unique(keys)
+    assert np.array_equal(got_k, ref_k)
+    ref = np.zeros((len(ref_k), width))
+    pos = np.searchsorted(ref_k, keys)
+    np.add.at(ref, pos, vals.astype(np.float64))
+    assert np.abs(ug[:u].cpu().numpy() - ref).max() < 1e-4
+    # bitwise reproducible
+    ug2 = torch.empty_like(ug)
+    L.call("ctr_rowgrad", ptr(kt), ptr(vt), n, width, width, 10, ptr(uk), ptr(ug2), ptr(nu), ptr(ws), wsz, stream())
+    assert torch.equal(ug[:u], ug2[:u])
+
+
+@pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (148, 8, 64, 0.1), (37, 2, 16, 0.3)])
+def test_attention_fwd_bwd_vs_torch(K, H, D, p):
+    L = _lib()
+    from tossctr.rng import drop_args
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import rng as orng
+    B, dh = 5, D // H
+    tk = K + 3
+    qkv = torch.randn(B * K, 3 * D, device="cuda", requires_grad=True)
+    rel_w = torch.randn(2 * tk + 1, H, device="cuda", requires_grad=True)
+    dk = drop_args(1234, 7, p, True)
+    relmean = torch.empty(2 * tk + 1, device="cuda")
+    L.call("ctr_pos_bias_mean", ptr(rel_w), H, 2 * tk + 1, ptr(relmean), stream())
+    o = torch.empty(B * K, D, device="cuda")
+    mrow = torch.empty(B * H * K, device="cuda")
+    lrow = torch.empty(B * H * K, device="cuda")
+    scale = float(np.float32(math.sqrt(1.0 / dh)))
+    L.call("ctr_attn_fwd", ptr(qkv), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(o), ptr(mrow), ptr(lrow),
+           stream())
+    # torch reference (MHA explicit path semantics)
+    q, k, v = qkv.view(B, K, 3 * D).split(D, -1)
+    q = q.reshape(B, K, H, dh).transpose(1, 2)
+    k = k.reshape(B, K, H, dh).transpose(1, 2)
+    v = v.reshape(B, K, H, dh).transpose(1, 2)
+    i = torch.arange(K, device="cuda")[:, None]
+    j = torch.arange(K, device="cuda")[None, :]
+    bias = rel_w[(j - i).clamp(-tk, tk) + tk].permute(2, 0, 1).mean(0)
+    s = bias + (q * scale) @ k.transpose(-1, -2)
+    a = torch.softmax(s, -1)
+    if p > 0:
+        keep = torch.from_numpy(orng.keep_mask(1234, 7, p, (B * H, K, K))).cuda().view(B, H, K, K)
+        a = a * keep.float() / (1 - p)
+    o_ref = (a @ v).transpose(1, 2).reshape(B * K, D)
+    assert rel(o, o_ref.detach()) < 2e-6
+    do = torch.randn(B * K, D, device="cuda")
+    o_ref.backward(do)
+    dqkv = torch.empty(B * K, 3 * D, device="cuda")
+    nparts = L.query("ctr_attn_bwd_nparts", H, K, D) * B
+    drp = torch.empty(nparts, 2 * tk + 1, device="cuda")
+    L.call("ctr_attn_bwd", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mrow), ptr(lrow),
+           ptr(dqkv), ptr(drp), stream())
+    drel = torch.empty(2 * tk + 1, H, device="cuda")
+    L.call("ctr_pos_bias_grad", ptr(drp), nparts, H, 2 * tk + 1, ptr(drel), stream())
+    assert rel(dqkv, qkv.grad) < 1e-5
+    assert rel(drel, rel_w.grad) < 1e-5
+
+
+@pytest.mark.parametrize("L_,K,D", [(100, 60, 32), (40, 40, 16), (400, 148, 64), (7, 3, 8)])
+def test_topk_select_vs_torch(L_, K, D):
+    L = _lib()
+    B, vocab = 33, 500
+    g = torch.Generator().manual_seed(L_)
+    E_att = torch.randn(vocab, D, generator=g)
+    E_rep = torch.randn(vocab, D, generator=g)
+    E_att[0] = 0
+    E_rep[0] = 0
+    seq = torch.randint(1, vocab, (B, L_), generator=g)
+    lens = torch.randint(0, L_ + 1, (B,), generator=g)
+    for b in range(B):
+        seq[b, : L_ - int(lens[b])] = 0
+    q = torch.randn(B, D, generator=g)
+    pos = torch.arange(L_)
+    dlog = torch.log(torch.exp(-(L_ - 1 - pos).float() / 64.0) + 1e-8)
+    sc = (E_att[seq] * q[:, None]).sum(-1) + dlog
+    sc = sc.masked_fill(seq == 0, -1e9)
+    vals_ref, idx_ref = sc.topk(K, 1)
+    cu = lambda t: t.cuda().contiguous()
+    seq_d, q_d, Ea, Er, dl = cu(seq.int()), cu(q), cu(E_att), cu(E_rep), cu(dlog)
+    idx = torch.empty(B, K, dtype=torch.int32, device="cuda")
+    tok = torch.empty(B, K, dtype=torch.int32, device="cuda")
+    vals = torch.empty(B, K, device="cuda")
+    sel = torch.empty(B, K, D, device="cuda")
+    L.call("ctr_dare_topk_fwd", ptr(seq_d), B, L_, ptr(q_d), ptr(Ea), ptr(Er), D, ptr(dl), K, 0, ptr(idx), ptr(tok),
+           ptr(vals), ptr(sel), stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(vals.cpu(), vals_ref, rtol=1e-5, atol=1e-5)
+    # index sets agree on the real (non-pad) selections
+    for b in range(B):
+        real = vals_ref[b] > -1e8
+        assert set(idx.cpu()[b][real].tolist()) == set(idx_ref[b][real].tolist())
+    sel_ref = torch.gather(E_rep[seq], 1, idx.cpu().long()[..., None].expand(-1, -1, D))
+    assert torch.equal(sel.cpu(), sel_ref)
+
+
+def test_fused_adamw_matches_torch():
+    """ctr_adamw_ema on a dense segment == torch.optim.AdamW + clip + EMA arithmetic."""
+    L = _lib()
+    n = 10_000
+    p0 = torch.randn(n)
+    g = torch.randn(n)
+    p_t = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([p_t], lr=3e-3, weight_decay=1e-2)
+    shadow_ref = p0.clone()
+    P = p0.cuda().clone()
+    Mm, V, E = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda"), p0.cuda().clone()
+    G = g.cuda()
+    segs = (L.OptSeg * 1)()
+    segs[0].p_off, segs[0].n, segs[0].width, segs[0].kind, segs[0].g_off = 0, n, 1, 0, 0
+    CH = L.query("ctr_opt_chunk_elems")
+    chunks = [(0, e, min(n, e + CH)) for e in range(0, n, CH)]
+    carr = (L.OptChunk * len(chunks))()
+    for i, (s_, a_, b_) in enumerate(chunks):
+        carr[i].seg, carr[i].e0, carr[i].e1 = s_, a_, b_
+    to_dev = lambda arr: torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).cuda()
+    sd, cd = to_dev(segs), to_dev(carr)
+    coef = torch.tensor([0.0, 0.5], device="cuda")
+    for step in range(1, 4):
+        p_t.grad = g.clone() * 0.5
+        opt.step()
+        with torch.no_grad():
+            shadow_ref.mul_(0.9).add_(p_t.detach(), alpha=0.1)
+        L.call("ctr_adamw_ema", ptr(cd), len(chunks), ptr(sd), ptr(P), ptr(Mm), ptr(V), ptr(E), ptr(G), ptr(coef, 1),
+               3e-3, 1e-2, 0.9, 0.999, 1e-8, step, 0.9, 1, 1, stream())
+    torch.cuda.synchronize()
+    assert (P.cpu() - p_t.detach()).abs().max() < 1e-6
+    assert (E.cpu() - shadow_ref).abs().max() < 1e-6

@@ -1,0 +1,358 @@
+// fp32 GEMM on CDNA4 matrix cores (v_mfma_f32_16x16x4_f32) with fused epilogues.
+//
+// One 256-thread workgroup (4 waves, 2x2) computes a BM x BN tile; BK = 16 k-slices are staged
+// global -> registers -> LDS (double buffered, one barrier per k-slice).  LDS rows are strided
+// BM+16 / BN+16 floats (== 16 mod 32 banks) so the two 16-lane halves of a ds_read_b32 that read
+// adjacent k-rows never hit the same bank.  The epilogue re-stages the accumulator tile through
+// LDS so stores are row-contiguous and row-wise epilogues (residual + RMSNorm) see whole rows.
+//
+// f32-input MFMA is bit-for-bit a k-ordered fmaf chain per lane; results differ from the reference's
+// MKL sgemm only by summation order (covered by the 1e-4 parity tolerance).
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct GemmArgs {
+  int M, N, K;
+  const float* A;
+  int lda;
+  const float* B;
+  int ldb;
+  float* C;
+  int ldc;
+  ctr_gemm_epi_t epi;
+  int klen;        // K elements per split
+  float* ws;       // split-K slabs [splits][M][N]
+  int vecA, vecB;  // 16-byte loads legal
+};
+
+__device__ __forceinline__ float epi_elem(const ctr_gemm_epi_t& e, float v, int m, int n, int N, int ldc) {
+  if (e.dact) {
+    if (e.drop_thresh) {
+      Drop d{e.drop_key, e.drop_thresh, e.drop_scale};
+      v = drop_keep(d, (uint32_t)((long)m * N + n)) ? v * e.drop_scale : 0.0f;
+    }
+    const float a = e.aux[(long)m * ldc + n];
+    v = (e.dact == 1) ? (a > 0.f ? v : 0.f) : v * gelu_grad(a);
+  }
+  if (e.bias) v += e.bias[n];
+  if (e.add) v += e.add[(long)m * e.ld_add + n];
+  if (e.pre) e.pre[(long)m * ldc + n] = v;
+  if (e.act == 1) v = v > 0.f ? v : 0.f;
+  else if (e.act == 2) v = gelu_f(v);
+  if (!e.dact && e.drop_thresh) {
+    Drop d{e.drop_key, e.drop_thresh, e.drop_scale};
+    v = drop_apply(d, (uint32_t)((long)m * N + n), v);
+  }
+  return v;
+}
+
+template <int BM, int BN, bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  constexpr int BK = 16;
+  constexpr int SA = BM + 16, SB = BN + 16;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int SC = BN + 4;
+  constexpr int LDS_K = 2 * BK * (SA + SB);
+  constexpr int LDS_E = BM * SC;
+  constexpr int LDS = LDS_K > LDS_E ? LDS_K : LDS_E;
+  __shared__ __attribute__((aligned(16))) float smem[LDS];
+  float* As = smem;
+  float* Bs = smem + 2 * BK * SA;
+
+  constexpr int A_V = BM * BK / 4, B_V = BN * BK / 4;           // float4 slots per tile
+  constexpr int A_IT = (A_V + 255) / 256, B_IT = (B_V + 255) / 256;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid >> 1) * WM, wn = (wid & 1) * WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kz0 = blockIdx.z * g.klen;
+  const int kz1 = min(g.K, kz0 + g.klen);
+  const int nkt = kz1 > kz0 ? (kz1 - kz0 + BK - 1) / BK : 0;
+
+  f32x4 ra[A_IT], rb[B_IT];
+
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int e = tid + it * 256;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (e < A_V) {
+        if (!TA) {  // A[m][k], k contiguous
+          const int i = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+          const int m = m0 + i, k = k0 + kq;
+          if (m < g.M) {
+            const float* p = g.A + (long)m * g.lda + k;
+            if (g.vecA && k + 3 < kz1) v = *(const f32x4*)p;
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (k + j < kz1) ? p[j] : 0.f;
+            }
+          }
+        } else {    // A stored [k][m], m contiguous
+          const int k = e / (BM / 4), iq = (e % (BM / 4)) * 4;
+          const int kk = k0 + k, m = m0 + iq;
+          if (kk < kz1) {
+            const float* p = g.A + (long)kk * g.lda + m;
+            if (g.vecA && m + 3 < g.M) v = *(const f32x4*)p;
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (m + j < g.M) ? p[j] : 0.f;
+            }
+          }
+        }
+      }
+      ra[it] = v;
+    }
+  };
+  auto load_b = [&](int k0) {
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int e = tid + it * 256;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (e < B_V) {
+        if (!TB) {  // B[k][n], n contiguous
+          const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+          const int kk = k0 + k, n = n0 + nq;
+          if (kk < kz1) {
+            const float* p = g.B + (long)kk * g.ldb + n;
+            if (g.vecB && n + 3 < g.N) v = *(const f32x4*)p;
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? p[j] : 0.f;
+            }
+          }
+        } else {    // B stored [n][k], k contiguous
+          const int n = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+          const int nn = n0 + n, k = k0 + kq;
+          if (nn < g.N) {
+            const float* p = g.B + (long)nn * g.ldb + k;
+            if (g.vecB && k + 3 < kz1) v = *(const f32x4*)p;
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (k + j < kz1) ? p[j] : 0.f;
+            }
+          }
+        }
+      }
+      rb[it] = v;
+    }
+  };
+  auto store_ab = [&](int buf) {
+    float* a = As + buf * BK * SA;
+    float* b = Bs + buf * BK * SB;
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int e = tid + it * 256;
+      if (e < A_V) {
+        if (!TA) {
+          const int i = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[(kq + j) * SA + i] = ra[it][j];
+        } else {
+          const int k = e / (BM / 4), iq = (e % (BM / 4)) * 4;
+          *(f32x4*)&a[k * SA + iq] = ra[it];
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int e = tid + it * 256;
+      if (e < B_V) {
+        if (!TB) {
+          const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+          *(f32x4*)&b[k * SB + nq] = rb[it];
+        } else {
+          const int n = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[(kq + j) * SB + n] = rb[it][j];
+        }
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) {
+    load_a(kz0);
+    load_b(kz0);
+    store_ab(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) {
+      load_a(kz0 + (kt + 1) * BK);
+      load_b(kz0 + (kt + 1) * BK);
+    }
+    const float* a = As + cur * BK * SA;
+    const float* b = Bs + cur * BK * SB;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int kr = kk + (lane >> 4);
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = a[kr * SA + wm + i * 16 + (lane & 15)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = b[kr * SB + wn + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) store_ab(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- stage the accumulator tile through LDS: Cs[i][j], row stride SC ----
+  float* Cs = smem;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        Cs[(wm + i * 16 + (lane >> 4) * 4 + r) * SC + wn + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+
+  const ctr_gemm_epi_t& e = g.epi;
+  if (gridDim.z > 1) {  // split-K partial: raw slab, epilogue happens in the reduce kernel
+    float* slab = g.ws + (long)blockIdx.z * g.M * g.N;
+    for (int q = tid; q < BM * BN; q += 256) {
+      const int i = q / BN, j = q % BN, m = m0 + i, n = n0 + j;
+      if (m < g.M && n < g.N) slab[(long)m * g.N + n] = Cs[i * SC + j];
+    }
+    return;
+  }
+  if (e.norm_w) {  // full row in this tile (host guarantees N <= BN, gridDim.y == 1)
+    constexpr int TPR = BN / 4;          // threads per row
+    constexpr int RPP = 256 / TPR;       // rows per pass
+    const int sub = tid % TPR, rr = tid / TPR;
+    for (int i0 = 0; i0 < BM; i0 += RPP) {
+      const int i = i0 + rr, m = m0 + i;
+      float h[4];
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = sub * 4 + j;
+        h[j] = 0.f;
+        if (m < g.M && n < g.N) {
+          float v = Cs[i * SC + n];
+          if (e.bias) v += e.bias[n];
+          h[j] = e.resid[(long)m * e.ld_resid + n] + v;
+          ss += h[j] * h[j];
+        }
+      }
+      ss = group_sum<TPR>(ss);
+      const float r = 1.0f / sqrtf(ss / (float)g.N + e.norm_eps);
+      if (m < g.M) {
+        if (sub == 0 && e.norm_r) e.norm_r[m] = r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = sub * 4 + j;
+          if (n < g.N) {
+            if (e.norm_h) e.norm_h[(long)m * g.ldc + n] = h[j];
+            g.C[(long)m * g.ldc + n] = e.norm_w[n] * h[j] * r;
+          }
+        }
+      }
+    }
+    return;
+  }
+  const bool vecC = ((g.ldc & 3) == 0) && ((((uintptr_t)g.C) & 15) == 0);
+  for (int q = tid; q < BM * BN / 4; q += 256) {
+    const int i = q / (BN / 4), jq = (q % (BN / 4)) * 4;
+    const int m = m0 + i, n = n0 + jq;
+    if (m >= g.M) continue;
+    f32x4 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? epi_elem(e, Cs[i * SC + jq + j], m, n + j, g.N, g.ldc) : 0.f;
+    float* p = g.C + (long)m * g.ldc + n;
+    if (vecC && n + 3 < g.N) *(f32x4*)p = v;
+    else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < g.N) p[j] = v[j];
+    }
+  }
+}
+
+__global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
+  const long MN = (long)g.M * g.N;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < MN; q += (long)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += g.ws[z * MN + q];
+    const int m = (int)(q / g.N), n = (int)(q % g.N);
+    g.C[(long)m * g.ldc + n] = epi_elem(g.epi, s, m, n, g.N, g.ldc);
+  }
+}
+
+template <int BM, int BN>
+static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s) {
+  dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), splits);
+  if (!ta && !tb) gemm_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>(g);
+  else if (!ta && tb) gemm_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>(g);
+  else if (ta && !tb) gemm_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>(g);
+  else gemm_kernel<BM, BN, true, true><<<grid, 256, 0, s>>>(g);
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" size_t ctr_gemm_ws_size(int M, int N, int splits) {
+  return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
+}
+
+extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                        float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, void* stream) {
+  CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative dims");
+  if (M == 0 || N == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  GemmArgs g;
+  g.M = M; g.N = N; g.K = K; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  ctr_gemm_epi_t zero = {};
+  g.epi = epi ? *epi : zero;
+  CTR_REQUIRE(!(g.epi.dact && !g.epi.aux), "dact needs aux");
+  CTR_REQUIRE(!(g.epi.norm_w && (N > 64 || !g.epi.resid)), "fused RMSNorm needs N <= 64 and resid");
+  if (splits < 1) splits = 1;
+  CTR_REQUIRE(!(splits > 1 && (g.epi.norm_w || !ws)), "split-K needs ws and no fused norm");
+  g.vecA = ((lda & 3) == 0) && ((((uintptr_t)A) & 15) == 0);
+  g.vecB = ((ldb & 3) == 0) && ((((uintptr_t)B) & 15) == 0);
+  const int BK = 16;
+  int klen = K;
+  if (splits > 1) {
+    klen = ((K + splits - 1) / splits + BK - 1) / BK * BK;
+    splits = (K + klen - 1) / klen;
+  }
+  g.klen = klen > 0 ? klen : 1;
+  g.ws = ws;
+  if (g.epi.norm_w) {
+    if (N <= 32) launch_tile<128, 32>(g, ta, tb, 1, s);
+    else launch_tile<128, 64>(g, ta, tb, 1, s);
+  } else if (N <= 32) {
+    launch_tile<128, 32>(g, ta, tb, splits, s);
+  } else if (N <= 64) {
+    launch_tile<128, 64>(g, ta, tb, splits, s);
+  } else if (N <= 96) {
+    launch_tile<128, 96>(g, ta, tb, splits, s);
+  } else if (M <= 64) {
+    launch_tile<64, 128>(g, ta, tb, splits, s);
+  } else {
+    launch_tile<128, 128>(g, ta, tb, splits, s);
+  }
+  if (splits > 1) {
+    const long MN = (long)M * N;
+    int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(g, splits);
+  }
+  return check_launch("ctr_gemm");
+}

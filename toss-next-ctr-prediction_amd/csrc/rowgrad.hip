@@ -1,0 +1,133 @@
+// Deterministic row-wise gradient dedup for the embedding tables.
+//
+// Replaces embedding_dense_backward (index_add of row grads into a zero-filled dense grad, one per
+// nn.Embedding: src/models/dare.py:89-90, src/models/wrapper.py:34).  Instead of materialising a
+// 10M x D dense grad, contributions (key = row id, value = one grad row) are
+//   1. stably radix-sorted by key (rocPRIM, library primitive; stable => members of a key keep
+//      their contribution order),
+//   2. run-length encoded into (unique key, count), counts exclusive-scanned into offsets,
+//   3. summed per unique key by one wave each, in contribution order (bitwise reproducible).
+// The optimizer stream (optim.hip) then reads the compact (keys, rows) directly.
+// Keys equal to INVALID (0xFFFFFFFF: pad tokens, whose grads padding_idx drops) sort last.
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_run_length_encode.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+
+__global__ void iota_kernel(uint32_t* v, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ contrib, int ld, int width,
+                                                     const uint32_t* __restrict__ sorted_idx,
+                                                     const uint32_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ offsets,
+                                                     const uint32_t* __restrict__ n_uniq,
+                                                     float* __restrict__ out) {
+  const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (u >= *n_uniq) return;
+  const uint32_t off = offsets[u], cnt = counts[u];
+  if (lane < width) {
+    float acc = 0.f;
+    for (uint32_t i = 0; i < cnt; ++i) acc += contrib[(long)sorted_idx[off + i] * ld + lane];
+    out[(long)u * width + lane] = acc;
+  }
+}
+
+struct RowgradWs {
+  size_t temp_bytes;
+  size_t total;
+  size_t off_iota, off_skeys, off_sidx, off_counts, off_offsets;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static RowgradWs rowgrad_layout(int n) {
+  RowgradWs w{};
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, t1, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                            (uint32_t*)nullptr, (size_t)n, 0, 32);
+  (void)rocprim::run_length_encode(nullptr, t2, (const uint32_t*)nullptr, (unsigned)n, (uint32_t*)nullptr,
+                             (uint32_t*)nullptr, (uint32_t*)nullptr);
+  (void)rocprim::exclusive_scan(nullptr, t3, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
+                          rocprim::plus<uint32_t>());
+  w.temp_bytes = align256(std::max(t1, std::max(t2, t3)));
+  const size_t a = align256((size_t)n * sizeof(uint32_t));
+  w.off_iota = w.temp_bytes;
+  w.off_skeys = w.off_iota + a;
+  w.off_sidx = w.off_skeys + a;
+  w.off_counts = w.off_sidx + a;
+  w.off_offsets = w.off_counts + a;
+  w.total = w.off_offsets + a;
+  return w;
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" size_t ctr_rowgrad_ws_size(int n) { return n > 0 ? rowgrad_layout(n).total : 0; }
+
+extern "C" int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, int width, int ld, int key_bits,
+                           uint32_t* uniq_keys, float* uniq_grad, uint32_t* n_uniq, void* ws, size_t ws_bytes,
+                           void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n == 0) {
+    (void)hipMemsetAsync(n_uniq, 0, sizeof(uint32_t), s);
+    return check_launch("rowgrad");
+  }
+  CTR_REQUIRE(width >= 1 && width <= 64, "row width must be in [1, 64]");
+  CTR_REQUIRE(key_bits >= 1 && key_bits <= 32, "key_bits must be in [1, 32]");
+  RowgradWs w = rowgrad_layout(n);
+  CTR_REQUIRE(ws_bytes >= w.total, "rowgrad workspace too small");
+  char* base = (char*)ws;
+  uint32_t* iota = (uint32_t*)(base + w.off_iota);
+  uint32_t* skeys = (uint32_t*)(base + w.off_skeys);
+  uint32_t* sidx = (uint32_t*)(base + w.off_sidx);
+  uint32_t* counts = (uint32_t*)(base + w.off_counts);
+  uint32_t* offsets = (uint32_t*)(base + w.off_offsets);
+  iota_kernel<<<std::min(cdiv(n, 256), 4096), 256, 0, s>>>(iota, n);
+  size_t tb = w.temp_bytes;
+  hipError_t e = rocprim::radix_sort_pairs(base, tb, keys, skeys, (const uint32_t*)iota, sidx, (size_t)n, 0,
+                                           (unsigned)key_bits, s);
+  CTR_REQUIRE(e == hipSuccess, "radix_sort_pairs failed");
+  tb = w.temp_bytes;
+  e = rocprim::run_length_encode(base, tb, (const uint32_t*)skeys, (unsigned)n, uniq_keys, counts, n_uniq, s);
+  CTR_REQUIRE(e == hipSuccess, "run_length_encode failed");
+  tb = w.temp_bytes;
+  e = rocprim::exclusive_scan(base, tb, (const uint32_t*)counts, offsets, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
+  CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
+  segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib, ld, width, sidx, counts, offsets, n_uniq, uniq_grad);
+  return check_launch("rowgrad");
+}
+
+namespace ctr {
+__global__ void scatter_rows_kernel(const uint32_t* __restrict__ keys, const float* __restrict__ G,
+                                    const uint32_t* __restrict__ n_uniq, int width, int ld, uint32_t key_base,
+                                    long n_rows, float* __restrict__ out) {
+  const uint32_t nu = *n_uniq;
+  const long total = (long)nu * width;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const long u = q / width;
+    const int k = (int)(q % width);
+    const uint32_t key = keys[u];
+    if (key < key_base || (long)(key - key_base) >= n_rows) continue;
+    out[(long)(key - key_base) * width + k] = G[u * ld + k];
+  }
+}
+}  // namespace ctr
+
+// compact -> dense table gradient (only for the torch-autograd compatibility path: loss.backward())
+extern "C" int ctr_scatter_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int max_uniq, int width,
+                                int ld, uint32_t key_base, long n_rows, float* out, void* stream) {
+  if (max_uniq == 0) return 0;
+  int blocks = std::min(cdiv((long)max_uniq * width, 256), 8192);
+  scatter_rows_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(keys, G, n_uniq, width, ld, key_base, n_rows, out);
+  return check_launch("scatter_rows");
+}

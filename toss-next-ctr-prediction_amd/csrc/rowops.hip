@@ -1,0 +1,272 @@
+// Row/column reductions on the hot path:
+//   rmsnorm fwd/bwd : src/models/dare.py:6-13 (encoder norms, rows of D), src/models/qnn_alpha.py:6-12,
+//                     109-113 (QNN pre-norm over F*D = 6400)
+//   colsum          : bias / gain gradients (sum over the batch rows), deterministic two-level tree
+//   loss            : bce_wll_style, src/train.py:71-90 (+ aux term src/train.py:165-168) fused with
+//                     its backward seed (class-balanced: counts are a batch-wide reduction)
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+
+// ---------------- big-row RMSNorm forward: one workgroup per row ----------------
+__global__ __launch_bounds__(256) void rmsnorm_fwd_big(const float* __restrict__ x, long ldx, int N,
+                                                       const float* __restrict__ w, float eps,
+                                                       float* __restrict__ y, long ldy, float* __restrict__ r) {
+  __shared__ float red[4];
+  const long row = blockIdx.x;
+  const float* xr = x + row * ldx;
+  float ss = 0.f;
+  for (int j = threadIdx.x; j < N; j += 256) ss = fmaf(xr[j], xr[j], ss);
+  ss = block_sum(ss, red);
+  const float rr = 1.0f / sqrtf(ss / (float)N + eps);
+  if (threadIdx.x == 0) r[row] = rr;
+  float* yr = y + row * ldy;
+  for (int j = threadIdx.x; j < N; j += 256) yr[j] = w[j] * xr[j] * rr;
+}
+
+// ---------------- RMSNorm backward ----------------
+// dh = w*dy*r - h * r^3/N * sum_k(w_k dy_k h_k) (+ add);  dw partial = sum_rows dy*h*r
+// small rows (N <= 64): TPR threads per row, each covers N/TPR columns (ceil); rows_per_block rows.
+template <int TPR>
+__global__ __launch_bounds__(256) void rmsnorm_bwd_small(const float* __restrict__ dy, long ldy,
+                                                         const float* __restrict__ h, long ldh,
+                                                         const float* __restrict__ r, const float* __restrict__ w,
+                                                         int M, int N, float* __restrict__ dh, long lddh,
+                                                         const float* __restrict__ add, long ld_add,
+                                                         int rows_per_block, float* __restrict__ dw_part) {
+  constexpr int CPT = 64 / TPR;   // columns per thread (N <= 64)
+  const int sub = threadIdx.x % TPR, rr = threadIdx.x / TPR;
+  constexpr int RPP = 256 / TPR;
+  const int m0 = blockIdx.x * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  float dwacc[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) dwacc[c] = 0.f;
+  for (int mb = m0; mb < m1; mb += RPP) {
+    const int m = mb + rr;
+    const bool ok = m < m1;
+    float gy[CPT], hv[CPT];
+    float dot = 0.f;
+    const float rm = ok ? r[m] : 0.f;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int n = sub + c * TPR;
+      gy[c] = 0.f;
+      hv[c] = 0.f;
+      if (ok && n < N) {
+        gy[c] = dy[(long)m * ldy + n];
+        hv[c] = h[(long)m * ldh + n];
+        dot = fmaf(w[n] * gy[c], hv[c], dot);
+      }
+    }
+    dot = group_sum<TPR>(dot);
+    const float coef = rm * rm * rm / (float)N * dot;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int n = sub + c * TPR;
+      if (ok && n < N) {
+        float g = w[n] * gy[c] * rm - hv[c] * coef;
+        if (add) g += add[(long)m * ld_add + n];
+        dh[(long)m * lddh + n] = g;
+        dwacc[c] = fmaf(gy[c] * hv[c], rm, dwacc[c]);
+      }
+    }
+  }
+  // reduce dw across the RPP row groups of the block (fixed order through LDS)
+  __shared__ float sdw[256 * CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) sdw[threadIdx.x * CPT + c] = dwacc[c];
+  __syncthreads();
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const int s = n % TPR, c = n / TPR;
+    float acc = 0.f;
+    for (int g = 0; g < RPP; ++g) acc += sdw[(g * TPR + s) * CPT + c];
+    dw_part[(long)blockIdx.x * N + n] = acc;
+  }
+}
+
+// big rows: one workgroup per row (QNN pre-norm); dw partial per row-chunk of rows_per_block rows
+__global__ __launch_bounds__(256) void rmsnorm_bwd_big(const float* __restrict__ dy, long ldy,
+                                                       const float* __restrict__ h, long ldh,
+                                                       const float* __restrict__ r, const float* __restrict__ w,
+                                                       int M, int N, float* __restrict__ dh, long lddh,
+                                                       int rows_per_block, float* __restrict__ dw_part) {
+  __shared__ float red[4];
+  const int m0 = blockIdx.x * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  for (int m = m0; m < m1; ++m) {
+    const float* gy = dy + (long)m * ldy;
+    const float* hv = h + (long)m * ldh;
+    const float rm = r[m];
+    float dot = 0.f;
+    for (int n = threadIdx.x; n < N; n += 256) dot = fmaf(w[n] * gy[n], hv[n], dot);
+    dot = block_sum(dot, red);
+    const float coef = rm * rm * rm / (float)N * dot;
+    for (int n = threadIdx.x; n < N; n += 256) dh[(long)m * lddh + n] = w[n] * gy[n] * rm - hv[n] * coef;
+  }
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float acc = 0.f;
+    for (int m = m0; m < m1; ++m) acc = fmaf(dy[(long)m * ldy + n] * h[(long)m * ldh + n], r[m], acc);
+    dw_part[(long)blockIdx.x * N + n] = acc;
+  }
+}
+
+// ---------------- column sums: out[n] = sum_m X[m, n] (two-level, fixed order) ----------------
+__global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ X, long ld, int M, int N,
+                                                      int rows_per_block, float* __restrict__ part) {
+  const int m0 = blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    float s = 0.f;
+    for (int m = m0; m < m1; ++m) s += X[(long)m * ld + n];
+    part[(long)blockIdx.y * N + n] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_final(const float* __restrict__ part, int nparts, int N, float div,
+                                                    float* __restrict__ out) {
+  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
+    float s = 0.f;
+    for (int p = 0; p < nparts; ++p) s += part[(long)p * N + n];
+    out[n] = div == 1.0f ? s : s / div;
+  }
+}
+
+// ---------------- loss: bce_wll_style(logits) + aux_w * bce_wll_style(aux) and d/dz ----------------
+__global__ __launch_bounds__(1024) void loss_kernel(const float* __restrict__ z, const float* __restrict__ za,
+                                                    const float* __restrict__ y, int B, float aux_w,
+                                                    float* __restrict__ loss, float* __restrict__ dz,
+                                                    float* __restrict__ dza) {
+  __shared__ float red[16];
+  float npos = 0.f, sp = 0.f, sn = 0.f, spa = 0.f, sna = 0.f;
+  for (int i = threadIdx.x; i < B; i += 1024) {
+    const bool pos = y[i] > 0.5f;
+    npos += pos ? 1.f : 0.f;
+    if (pos) sp += softplus_f(-z[i]);
+    else sn += softplus_f(z[i]);
+    if (za) {
+      if (pos) spa += softplus_f(-za[i]);
+      else sna += softplus_f(za[i]);
+    }
+  }
+  npos = block_sum(npos, red);
+  sp = block_sum(sp, red);
+  sn = block_sum(sn, red);
+  spa = block_sum(spa, red);
+  sna = block_sum(sna, red);
+  const float nneg = (float)B - npos;
+  const float lp = npos > 0.f ? sp / npos : 0.f, ln = nneg > 0.f ? sn / nneg : 0.f;
+  float L = 0.5f * (lp + ln);
+  if (za) {
+    const float lpa = npos > 0.f ? spa / npos : 0.f, lna = nneg > 0.f ? sna / nneg : 0.f;
+    L = L + aux_w * (0.5f * (lpa + lna));
+  }
+  if (threadIdx.x == 0) loss[0] = L;
+  // d softplus(x)/dx = sigmoid(x) (torch: 1 above the threshold 20)
+  for (int i = threadIdx.x; i < B; i += 1024) {
+    const bool pos = y[i] > 0.5f;
+    float g;
+    if (pos) {
+      const float x = -z[i];
+      g = -(x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / npos);
+    } else {
+      const float x = z[i];
+      g = (x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / nneg);
+    }
+    dz[i] = g;
+    if (za) {
+      float ga;
+      if (pos) {
+        const float x = -za[i];
+        ga = -(x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / npos);
+      } else {
+        const float x = za[i];
+        ga = (x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / nneg);
+      }
+      dza[i] = aux_w * ga;
+    }
+  }
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int ctr_rmsnorm_fwd(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy,
+                               float* r, void* stream) {
+  if (M == 0) return 0;
+  rmsnorm_fwd_big<<<M, 256, 0, (hipStream_t)stream>>>(x, ldx, N, w, eps, y, ldy, r);
+  return check_launch("rmsnorm_fwd");
+}
+
+extern "C" int ctr_rmsnorm_bwd_nparts(int M, int N) {
+  if (N <= 64) return cdiv(M, 256);
+  return cdiv(M, 16);
+}
+
+extern "C" int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long ldh, const float* r, const float* w,
+                               int M, int N, float* dh, long lddh, const float* add, long ld_add, float* dw_part,
+                               void* stream) {
+  if (M == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  if (N <= 64) {
+    const int rpb = 256;
+    const int nb = cdiv(M, rpb);
+    if (N <= 16) rmsnorm_bwd_small<4><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, add, ld_add, rpb, dw_part);
+    else if (N <= 32) rmsnorm_bwd_small<8><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, add, ld_add, rpb, dw_part);
+    else rmsnorm_bwd_small<16><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, add, ld_add, rpb, dw_part);
+  } else {
+    CTR_REQUIRE(add == nullptr, "big-row rmsnorm bwd: add unsupported");
+    const int rpb = 16;
+    rmsnorm_bwd_big<<<cdiv(M, rpb), 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
+  }
+  return check_launch("rmsnorm_bwd");
+}
+
+extern "C" size_t ctr_colsum_ws_size(int M, int N) { return (size_t)cdiv(M, 256) * N * sizeof(float); }
+
+// out[n] = (sum_m X[m, n]) / div   (div = 1 for plain sums, B for torch .mean(dim=0))
+extern "C" int ctr_colsum(const float* X, long ld, int M, int N, float div, float* out, float* ws, void* stream) {
+  if (N == 0) return 0;
+  hipStream_t s = (hipStream_t)stream;
+  const int rpb = 256;
+  const int np = M > 0 ? cdiv(M, rpb) : 0;
+  if (np > 0) colsum_partial<<<dim3(cdiv(N, 256), np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
+  colsum_final<<<cdiv(N, 256), 256, 0, s>>>(ws, np, N, div, out);
+  return check_launch("colsum");
+}
+
+extern "C" int ctr_loss(const float* z, const float* za, const float* y, int B, float aux_w, float* loss, float* dz,
+                        float* dza, void* stream) {
+  loss_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(z, aux_w > 0.f ? za : nullptr, y, B, aux_w, loss, dz, dza);
+  return check_launch("loss");
+}
+
+// ---------------- small helpers ----------------
+namespace ctr {
+__global__ void sigmoid_kernel(const float* __restrict__ x, int n, float* __restrict__ y) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = sigmoid_f(x[i]);
+}
+__global__ void copy2d_kernel(const float* __restrict__ src, long lds, float* __restrict__ dst, long ldd, int rows,
+                              int cols) {
+  const long n = (long)rows * cols;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+    const long r = q / cols;
+    const int c = (int)(q % cols);
+    dst[r * ldd + c] = src[r * lds + c];
+  }
+}
+}  // namespace ctr
+
+// prob = sigmoid(logits)  (src/models/wrapper.py:175)
+extern "C" int ctr_sigmoid(const float* x, int n, float* y, void* stream) {
+  if (n == 0) return 0;
+  sigmoid_kernel<<<std::min(cdiv(n, 256), 4096), 256, 0, (hipStream_t)stream>>>(x, n, y);
+  return check_launch("sigmoid");
+}
+
+// strided 2-D copy (feature concatenation for the fc head, src/models/wrapper.py:168-172)
+extern "C" int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream) {
+  if ((long)rows * cols == 0) return 0;
+  int blocks = (int)std::min<long>(((long)rows * cols + 255) / 256, 8192);
+  copy2d_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(src, lds, dst, ldd, rows, cols);
+  return check_launch("copy2d");
+}

@@ -1,0 +1,115 @@
+"""ctypes binding of libctrhip.so (the C ABI in include/ctr_hip.h).
+
+The product path has NO fallback: if the library is missing or fails to load this module raises,
+and every op that needs it fails loudly.  Build with ``make -C toss-next-ctr-prediction_amd``
+(or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libctrhip.so")
+
+p, i, l, f, u, z = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint32, C.c_size_t
+
+
+class GemmEpi(C.Structure):
+    _fields_ = [("bias", p), ("add", p), ("ld_add", i), ("act", i), ("pre", p), ("dact", i), ("aux", p),
+                ("drop_key", u), ("drop_thresh", u), ("drop_scale", f), ("resid", p), ("ld_resid", i),
+                ("norm_w", p), ("norm_h", p), ("norm_r", p), ("norm_eps", f)]
+
+
+class OptSeg(C.Structure):
+    _fields_ = [("p_off", C.c_int64), ("n", C.c_int64), ("width", C.c_int32), ("kind", C.c_int32),
+                ("g_off", C.c_int64), ("keys", p), ("G", p), ("n_uniq", p), ("g_ld", C.c_int32),
+                ("key_base", C.c_uint32)]
+
+
+class OptChunk(C.Structure):
+    _fields_ = [("seg", C.c_int32), ("pad", C.c_int32), ("e0", C.c_int64), ("e1", C.c_int64)]
+
+
+# name: (restype, argtypes) -- keep in the order of include/ctr_hip.h
+SIGS = {
+    "ctr_last_error": (C.c_char_p, []),
+    "ctr_abi_version": (i, []),
+    "ctr_gemm_ws_size": (z, [i, i, i]),
+    "ctr_gemm": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, p]),
+    "ctr_feat_embed_fwd": (i, [p, i, i, p, p, p, i, i, p, l, p]),
+    "ctr_feat_embed_bwd_ws": (z, [i, i, i]),
+    "ctr_feat_embed_bwd": (i, [p, i, i, p, p, p, i, i, p, l, p, p, p, p, p]),
+    "ctr_cat_embed_fwd": (i, [p, i, i, p, p, p, p, i, p, p, l, u, u, f, p]),
+    "ctr_cat_embed_bwd_ws": (z, [i, i]),
+    "ctr_cat_embed_bwd": (i, [p, i, i, p, p, p, p, i, p, p, p, p, p, p, p, p]),
+    "ctr_context_fwd": (i, [p, l, i, p, l, i, p, i, i, i, i, i, p, p, p, p, p, p]),
+    "ctr_context_bwd": (i, [p, l, i, p, l, i, p, i, i, i, i, i, p, p, p, p, l, u, u, f, p, l, p, p, p, p, p]),
+    "ctr_dare_topk_fwd": (i, [p, i, i, p, p, p, i, p, i, i, p, p, p, p, p]),
+    "ctr_dare_topk_bwd": (i, [p, i, i, p, p, i, p, i, p, p, p, p, p]),
+    "ctr_pool_fwd": (i, [p, p, i, i, i, i, u, u, f, p, p, p, p, p, l, p, p]),
+    "ctr_pool_bwd": (i, [p, p, p, i, i, i, i, u, u, f, p, p, l, p, p, p, p]),
+    "ctr_pos_bias_mean": (i, [p, i, i, p, p]),
+    "ctr_pos_bias_grad": (i, [p, i, i, i, p, p]),
+    "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p]),
+    "ctr_attn_bwd_nparts": (i, [i, i, i]),
+    "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
+    "ctr_rmsnorm_fwd": (i, [p, l, i, i, p, f, p, l, p, p]),
+    "ctr_rmsnorm_bwd_nparts": (i, [i, i]),
+    "ctr_rmsnorm_bwd": (i, [p, l, p, l, p, p, i, i, p, l, p, l, p, p]),
+    "ctr_colsum_ws_size": (z, [i, i]),
+    "ctr_colsum": (i, [p, l, i, i, f, p, p, p]),
+    "ctr_loss": (i, [p, p, p, i, f, p, p, p, p]),
+    "ctr_qnn_ucat": (i, [p, i, i, i, p, i, p]),
+    "ctr_qnn_reduce_fwd": (i, [p, i, i, i, i, p, i, p, p, p, p]),
+    "ctr_qnn_reduce_bwd": (i, [p, i, i, i, i, p, i, p, p, p, p]),
+    "ctr_se_fwd_gate": (i, [p, i, i, p, p, p, p, p, p, p]),
+    "ctr_scale_drop": (i, [p, i, i, p, u, u, f, p, l, p]),
+    "ctr_se_bwd_ws": (z, [i, i]),
+    "ctr_se_bwd": (i, [p, l, p, i, i, i, p, p, p, p, p, u, u, f, p, p, p, p, p, p, p]),
+    "ctr_rowgrad_ws_size": (z, [i]),
+    "ctr_rowgrad": (i, [p, p, i, i, i, i, p, p, p, p, z, p]),
+    "ctr_opt_chunk_elems": (i, []),
+    "ctr_adamw_ema": (i, [p, i, p, p, p, p, p, p, p, f, f, f, f, f, i, f, i, i, p]),
+    "ctr_norm_nparts_per_call": (i, []),
+    "ctr_sqnorm_dense": (i, [p, l, p, p]),
+    "ctr_sqnorm_rows": (i, [p, p, p, i, i, u, p, p]),
+    "ctr_clip_finalize": (i, [p, i, f, p, p]),
+    "ctr_sigmoid": (i, [p, i, p, p]),
+    "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
+    "ctr_scatter_rows": (i, [p, p, p, i, i, i, u, l, p, p]),
+}
+
+_lib = None
+
+
+def load():
+    """Load libctrhip.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"HIP kernel library not built: {LIB_PATH} (run `make -C {os.path.dirname(_HERE)}`)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class CtrError(RuntimeError):
+    pass
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise CtrError(f"{name} failed ({rc}): {lib.ctr_last_error().decode()}")
+    return rc
+
+
+def query(name, *args):
+    return getattr(load(), name)(*args)

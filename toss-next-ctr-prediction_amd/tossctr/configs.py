@@ -1,0 +1,71 @@
+"""The BASELINE.json benchmark configurations as cfg dicts.
+
+``/root/reference`` (and its yamls) does not exist on the GPU box, so the values the hot path reads
+are restated here with their yaml line citations.  ``load_yaml`` accepts the reference's own yaml
+files unchanged when they are available.
+"""
+from __future__ import annotations
+
+import copy
+
+# cfgs/dare_qnn_next.yaml:17-51 (cat_cols) and :198-233 (cat_embedding_dims)
+CAT_DIMS_NEXT = {
+    "gender": 8, "age_group": 8, "inventory_id": 16, "day_of_week": 8, "hour": 8,
+    "l_feat_1": 8, "l_feat_2": 8, "l_feat_3": 8, "l_feat_4": 8, "l_feat_5": 33, "l_feat_6": 30,
+    "l_feat_7": 18, "l_feat_8": 8, "l_feat_9": 22, "l_feat_10": 17, "l_feat_11": 40, "l_feat_12": 64,
+    "l_feat_13": 8, "l_feat_14": 57, "l_feat_15": 51, "l_feat_16": 8, "l_feat_17": 22, "l_feat_18": 8,
+    "l_feat_19": 8, "l_feat_20": 8, "l_feat_21": 8, "l_feat_22": 8, "l_feat_23": 8, "l_feat_24": 8,
+    "l_feat_25": 43, "l_feat_26": 8, "l_feat_27": 8, "feat_a_2": 8, "feat_a_8": 8, "feat_a_9": 8,
+}
+N_NUM_NEXT = 82   # cfgs/dare_qnn_next.yaml:52-134 num_cols_explicit (82 columns) -> X_num / X_mask width
+
+
+def dare_qnn_next(emb_dim=32, max_len=100, batch_size=4096, hash_buckets=1_000_000):
+    """BASELINE config 2: cfgs/dare_qnn_next.yaml with hash_buckets=1e6, emb_dim=32, seq_len=100, bs=4096."""
+    cat_cols = list(CAT_DIMS_NEXT)
+    return {
+        "exp_name": "dare_qnn_next", "seed": 777, "device": "cuda", "deterministic": True, "amp": "none",
+        "use_compile": False,
+        "data": {"cat_cols": cat_cols, "hash_buckets": {c: hash_buckets for c in cat_cols},
+                 "hash_buckets_margin": 0},
+        "sequence": {"col": "seq", "max_len": max_len, "pad_id": 0, "top_k": 60, "recency_tau": 512,
+                     "query_mode": "concat", "query_key": "inventory_id", "transformer_block": True,
+                     "tfm": {"n_layers": 3, "n_heads": 8, "mha_dropout": 0.1, "ffn_hidden": 384, "ffn_dropout": 0.1,
+                             "norm": "rms", "gating": "softmax", "add_positional_bias": True}},   # yaml l.177-193
+        "model": {"emb_dim": emb_dim, "dare_dropout": 0.2, "cat_embedding_dims": dict(CAT_DIMS_NEXT),
+                  "qnn_alpha": {"enabled": True, "feature_embed_dim": 32, "heads": 6, "rank": 16, "proj_dim": 192,
+                                "mlp_hidden": [512, 256], "dropout": 0.2, "use_se": True, "se_reduction": 8,
+                                "use_residual": True, "norm": "rms", "pair_grouping": "all",
+                                "aux_head_weight": 0.1}},                                         # yaml l.234-249
+        "train": {"batch_size": batch_size, "epochs": 8, "optimizer": "adamw", "lr": 3e-4, "weight_decay": 1e-4,
+                  "warmup_epochs": 2, "cosine": True, "early_stop_patience": 3, "grad_clip_norm": 0.5},  # l.250-259
+        "cv": {"n_splits": 5, "group_key": "inventory_id"},
+        "calibration": {"enabled": True, "method": "temperature", "lr": 0.05, "iters": 200},
+        "logging": {"log_dir": "./runs", "tb": False, "csv_log": True},
+        "ema": {"enabled": True, "decay": 0.999, "eval_with_ema": True, "start_epoch": 1},       # l.288-292
+    }
+
+
+def dare_qnn_next_k100_s1(**kw):
+    """BASELINE config 3: cfgs/dare_qnn_next_k100_s1.yaml (K=100, query S1) at the cfg2 overrides."""
+    cfg = dare_qnn_next(**kw)
+    cfg["exp_name"] = "dare_qnn_next_k100_s1"
+    cfg["sequence"]["top_k"] = 100
+    cfg["sequence"]["query_mode"] = "S1"
+    return cfg
+
+
+def cat_cardinals(cfg):
+    """src/train.py:119: hash_buckets.get(c, 1000003) + hash_buckets_margin."""
+    d = cfg["data"]
+    return {c: int(d["hash_buckets"].get(c, 1000003)) + int(d.get("hash_buckets_margin", 0)) for c in d["cat_cols"]}
+
+
+def load_yaml(path, **overrides):
+    import yaml
+    with open(path) as f:
+        cfg = yaml.safe_load(f)
+    cfg = copy.deepcopy(cfg)
+    for k, v in overrides.items():
+        cfg[k] = v
+    return cfg

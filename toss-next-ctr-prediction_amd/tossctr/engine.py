@@ -1,0 +1,640 @@
+"""Step engine: drives the HIP kernels (libctrhip.so) for CTRModel forward / backward.
+
+The reference computes this with eager torch ops under autograd (src/models/*.py); here every
+arithmetic op is a hand-written gfx950 kernel and torch is used only for device memory, streams and
+(in tossctr/dist.py) collectives.  Activations live in per-(B, L) preallocated buffers, so a step
+does no allocation and is graph-capturable.
+
+Buffer names follow the reference's tensors (see the call-stack comments in each method).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import GemmEpi, call
+from .arch import QUERY_MODES, Arch
+from .rng import (SITE_DARE, SITE_EMB, SITE_FC, SITE_FFN0, SITE_MLP0, SITE_QNN, SITE_ATTN0, drop_args)
+
+F32 = 4
+INVALID_KEY = 0xFFFFFFFF
+
+
+def ptr(t, elems=0):
+    return t.data_ptr() + elems * t.element_size() if t is not None else None
+
+
+def _align(n, a=64):
+    return (n + a - 1) // a * a
+
+
+def _key_bits(n_keys: int) -> int:
+    return max(1, int(n_keys).bit_length())
+
+
+class ParamArena:
+    """All parameters in ONE flat fp32 device buffer (so clip + AdamW + EMA is a single stream).
+
+    Layout: [dense params that get grads][dense params without grads][embedding tables]; every
+    param starts on a 64-element boundary.  ``views[key]`` are the tensors the nn.Module exposes.
+    The dense-with-grad region is mirrored 1:1 by the dense grad buffer ``grad``.
+    """
+
+    def __init__(self, arch: Arch, device):
+        shapes = arch.param_shapes()
+        ng = arch.no_grad_keys()
+        groups = ([x for x in shapes if x[2] == "dense" and x[0] not in ng],
+                  [x for x in shapes if x[2] == "dense" and x[0] in ng],
+                  [x for x in shapes if x[2] == "table"])
+        self.offsets, self.shapes, self.kind = {}, {}, {}
+        off = 0
+        bounds = []
+        for g in groups:
+            start = off
+            for k, shp, kind in g:
+                self.offsets[k] = off
+                self.shapes[k] = tuple(shp)
+                self.kind[k] = kind
+                off = _align(off + int(np.prod(shp)))
+            bounds.append((start, off))
+        self.n_dense_grad = bounds[0][1]
+        self.nograd_range = bounds[1]
+        self.table_range = bounds[2]
+        self.total = off
+        self.device = device
+        self.buf = torch.zeros(self.total, dtype=torch.float32, device=device)
+        # dense grads for every dense param (the no-grad ones are only written on the autograd-compat
+        # path); the optimizer / clip read just [0, n_dense_grad)
+        self.grad = torch.zeros(max(1, self.nograd_range[1]), dtype=torch.float32, device=device)
+        self.order = [k for k, _, _ in shapes]
+        self.views = {k: self._view(self.buf, k) for k in self.order}
+        self.grad_views = {k: self._view(self.grad, k) for k in self.order if self.kind[k] == "dense"}
+
+    def _view(self, buf, k):
+        o, s = self.offsets[k], self.shapes[k]
+        return buf[o:o + int(np.prod(s))].view(s)
+
+    def numel(self, k):
+        return int(np.prod(self.shapes[k]))
+
+
+class Workspace:
+    """Named, reusable device buffers for one (B, L)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.t = {}
+
+    def get(self, name, shape, dtype=torch.float32):
+        shape = tuple(int(s) for s in shape)
+        t = self.t.get(name)
+        if t is None or t.shape != shape or t.dtype != dtype:
+            t = torch.empty(shape, dtype=dtype, device=self.device)
+            self.t[name] = t
+        return t
+
+
+class Engine:
+    def __init__(self, arch: Arch, arena: ParamArena):
+        self.a = arch
+        self.arena = arena
+        self.P = arena.views
+        self.G = arena.grad_views
+        self.device = arena.device
+        _lib.load()
+        a = arch
+        dev = self.device
+        # categorical metadata (device arrays)
+        self.cat_tab_off = torch.tensor([arena.offsets[f"cat_embs.{c}.weight"] for c in a.cat_names],
+                                        dtype=torch.int64, device=dev)
+        self.cat_proj_off = torch.tensor([arena.offsets[f"cat_proj.{c}.weight"] for c in a.cat_names],
+                                         dtype=torch.int64, device=dev)
+        self.cat_dims_t = torch.tensor(a.cat_dims, dtype=torch.int32, device=dev)
+        base = np.cumsum([0] + a.cat_cards[:-1]).astype(np.uint64)
+        assert int(sum(a.cat_cards)) < 2**32 - 1, "categorical rows exceed 32-bit keys"
+        self.cat_row_base_np = base.astype(np.uint32)
+        self.cat_row_base = torch.from_numpy(self.cat_row_base_np.view(np.int32)).to(dev)
+        self.cat_key_bits = _key_bits(int(sum(a.cat_cards)))
+        self.seq_key_bits = _key_bits(a.seq_vocab)
+        # query column index in the X_cat column order (src/models/wrapper.py:130)
+        self.qi = a.cat_cols.index(a.query_key) if a.query_mode != "S2" else 0
+        # column order of X_cat = cat_cols; tables are in cardinals order -> must coincide
+        if list(a.cat_cols) != list(a.cat_names):
+            raise NotImplementedError("cat_cols_order must match the cat_cardinals order")
+        self._decay = {}
+        self._ws = {}
+        self._splitk = None
+        self._gen = 0
+        self.stream = None
+
+    # ------------------------------------------------------------------ helpers
+    def s(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def ws(self, B, L):
+        key = (B, L)
+        if key not in self._ws:
+            self._ws[key] = Workspace(self.device)
+        return self._ws[key]
+
+    def decay_log(self, L):
+        # log(exp(-(L-1-l)/max(1,tau)) + 1e-8) evaluated with torch fp32 ops on the host exactly as
+        # src/models/dare.py:126-130 does, then uploaded once per L
+        if L not in self._decay:
+            pos = torch.arange(L)
+            d = torch.exp(-(L - 1 - pos).float() / max(1.0, float(self.a.tau)))
+            self._decay[L] = torch.log(d + 1e-8).to(self.device)
+        return self._decay[L]
+
+    def splitk_ws(self, nfloats):
+        if self._splitk is None or self._splitk.numel() < nfloats:
+            self._splitk = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=self.device)
+        return self._splitk
+
+    def gemm(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, splits=1):
+        """C = op(A) op(B) (+ epilogue); A/B/C are raw pointers."""
+        wsp = None
+        if splits > 1:
+            wsp = ptr(self.splitk_ws(splits * M * N))
+        call("ctr_gemm", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, self.s())
+
+    @staticmethod
+    def wgrad_splits(M, N, K):
+        tiles = max(1, math.ceil(M / 128)) * max(1, math.ceil(N / 128))
+        return int(max(1, min(K // 256, math.ceil(1024 / tiles))))
+
+    def colsum(self, X, ld, M, N, out, div=1.0):
+        w = self.splitk_ws(max(1, math.ceil(max(M, 1) / 256)) * N)
+        call("ctr_colsum", X, ld, M, N, float(div), out, ptr(w), self.s())
+
+    def wgrad(self, dY, ldy, X, ldx, M_rows, n_out, n_in, dW, lddw=None, bias_grad=None):
+        """dW[n_out, n_in] = dY^T X over M_rows rows (+ db = colsum(dY))."""
+        sp = self.wgrad_splits(n_out, n_in, M_rows)
+        self.gemm(n_out, n_in, M_rows, dY, ldy, 1, X, ldx, 0, dW, lddw or n_in, None, sp)
+        if bias_grad is not None:
+            self.colsum(dY, ldy, M_rows, n_out, bias_grad)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, X_num, X_mask, X_cat, seq, training: bool, seed: int, save: bool):
+        """CTRModel.forward (src/models/wrapper.py:138-176). Inputs are device tensors:
+        X_num f32 (B,Fn), X_mask f32 (B,Fm), X_cat int32 (B,Fc), seq int32 (B,L).
+        Returns (logits, prob, aux) views into workspace buffers, and the saved context."""
+        a, P = self.a, self.P
+        B, L = int(X_cat.shape[0]), int(seq.shape[1])
+        K, D = a.K_eff(L), a.D
+        F = a.F
+        FD = F * D
+        W = self.ws(B, L)
+        st = self.s()
+        sv = {"B": B, "L": L, "K": K, "training": training, "seed": seed, "X_num": X_num, "X_mask": X_mask,
+              "X_cat": X_cat, "seq": seq}
+        xF = W.get("xF", (B, FD))
+        num_off, mask_off, cat_off = D, D + a.Fn * D, D + (a.Fn + a.Fm) * D
+        # ---- numeric / binary embeddings straight into their xF slots (feature_embed.py:19-27,42-48)
+        if a.Fn > 0:
+            call("ctr_feat_embed_fwd", ptr(X_num), B, a.Fn, ptr(P["num_embed.weight"]), ptr(P["num_embed.bias"]),
+                 ptr(P["num_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, num_off), FD, st)
+        if a.Fm > 0:
+            call("ctr_feat_embed_fwd", ptr(X_mask), B, a.Fm, ptr(P["mask_embed.weight"]), None,
+                 ptr(P["mask_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, mask_off), FD, st)
+        # ---- hashed categorical gather + projection (+ emb dropout into xF) (wrapper.py:106-112,149-150)
+        cat_e = W.get("cat_e", (B, a.Fc, D))
+        dk = drop_args(seed, SITE_EMB, a.p_emb, training)
+        call("ctr_cat_embed_fwd", ptr(X_cat), B, a.Fc, ptr(self.arena.buf), ptr(self.cat_tab_off),
+             ptr(self.cat_proj_off), ptr(self.cat_dims_t), D, ptr(cat_e), ptr(xF, cat_off), FD, *dk, st)
+        # ---- context + query (wrapper.py:114-136)
+        ctx = W.get("ctx", (B, a.nctx * D))
+        hq = W.get("hq", (B, D))
+        query = W.get("query", (B, D))
+        mode = QUERY_MODES[a.query_mode]
+        call("ctr_context_fwd", ptr(xF, num_off), FD, a.Fn, ptr(xF, mask_off), FD, a.Fm, ptr(cat_e), a.Fc, D, B,
+             mode, self.qi, ptr(P["ctx_mlp.0.weight"]), ptr(P["ctx_mlp.0.bias"]), ptr(ctx), ptr(hq), ptr(query), st)
+        # ---- DARE top-K (dare.py:116-138)
+        idx = W.get("topk_idx", (B, K), torch.int32)
+        tok = W.get("topk_tok", (B, K), torch.int32)
+        vals = W.get("topk_vals", (B, K))
+        xs = [W.get("x0", (B, K, D))]
+        call("ctr_dare_topk_fwd", ptr(seq), B, L, ptr(query), ptr(P["dare.emb_att.weight"]),
+             ptr(P["dare.emb_rep.weight"]), D, ptr(self.decay_log(L)), K, a.pad_id, ptr(idx), ptr(tok), ptr(vals),
+             ptr(xs[0]), st)
+        # ---- encoder layers (dare.py:53-70)
+        layers = []
+        M = B * K
+        scale = float(np.float32(math.sqrt(1.0 / float(D // a.H)))) if a.n_layers else 1.0
+        for li in range(a.n_layers):
+            pre = f"dare.layers.{li}."
+            Ls = {}
+            x = xs[-1]
+            qkv = W.get(f"qkv{li}", (M, 3 * D))
+            self.gemm(M, 3 * D, D, ptr(x), D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 1, ptr(qkv), 3 * D,
+                      GemmEpi(bias=ptr(P[pre + "mha.in_proj_bias"])))
+            relmean = None
+            if a.add_pos:
+                relmean = W.get(f"relmean{li}", (2 * a.top_k + 1,))
+                call("ctr_pos_bias_mean", ptr(P[pre + "pbias.rel.weight"]), a.H, 2 * a.top_k + 1, ptr(relmean), st)
+            o = W.get(f"o{li}", (M, D))
+            mrow = W.get(f"mrow{li}", (B * a.H * K,))
+            lrow = W.get(f"lrow{li}", (B * a.H * K,))
+            da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
+            call("ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean), a.top_k, scale, *da, ptr(o), ptr(mrow),
+                 ptr(lrow), st)
+            h1 = W.get(f"h1_{li}", (M, D))
+            r1 = W.get(f"r1_{li}", (M,))
+            x1 = W.get(f"x1_{li}", (M, D))
+            self.gemm(M, D, D, ptr(o), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 1, ptr(x1), D,
+                      GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), ld_resid=D,
+                              norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1), norm_eps=1e-6))
+            FF = a.ffn_hidden
+            act = W.get(f"ffa{li}", (M, FF))
+            fo = W.get(f"ffo{li}", (M, FF))
+            dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
+            self.gemm(M, FF, D, ptr(x1), D, 0, ptr(P[pre + "ffn.0.weight"]), D, 1, ptr(fo), FF,
+                      GemmEpi(bias=ptr(P[pre + "ffn.0.bias"]), act=2, pre=ptr(act), drop_key=dfk[0],
+                              drop_thresh=dfk[1], drop_scale=dfk[2]))
+            h2 = W.get(f"h2_{li}", (M, D))
+            r2 = W.get(f"r2_{li}", (M,))
+            x2 = W.get(f"x{li + 1}", (B, K, D))
+            self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(x2), D,
+                      GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
+                              norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
+            Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, h1=h1, r1=r1, x1=x1, act=act, fo=fo,
+                      h2=h2, r2=r2)
+            layers.append(Ls)
+            xs.append(x2)
+        # ---- gating pool + aux head (dare.py:150-162)
+        w = W.get("pool_w", (B, K))
+        u = W.get("u", (B, D))
+        aux = W.get("aux", (B,))
+        ddr = drop_args(seed, SITE_DARE, a.p_dare, training)
+        fcin = None
+        if a.use_qnn:
+            xf_u, xf_ld = ptr(xF), FD
+        else:
+            nfc = 1 + (a.Fn > 0) + (a.Fm > 0) + a.Fc
+            fcin = W.get("fcin", (B, nfc * D))
+            xf_u, xf_ld = ptr(fcin), nfc * D
+        call("ctr_pool_fwd", ptr(xs[-1]), ptr(vals), B, K, D, 0 if a.gating == "softmax" else 1, *ddr,
+             ptr(P["dare.aux_head.weight"]), ptr(P["dare.aux_head.bias"]), ptr(w), ptr(u), xf_u, xf_ld, ptr(aux), st)
+        logits = W.get("logits", (B,))
+        if a.use_qnn:
+            q = self._qnn_forward(W, xF, B, seed, training, logits)
+        else:
+            q = self._fc_forward(W, fcin, ctx, cat_e, B, seed, training, logits)
+        prob = W.get("prob", (B,))
+        call("ctr_sigmoid", ptr(logits), B, ptr(prob), st)
+        if save:
+            self._gen += 1
+            sv.update(gen=self._gen, xF=xF, cat_e=cat_e, ctx=ctx, hq=hq, query=query, idx=idx, tok=tok, vals=vals,
+                      xs=xs, layers=layers, w=w, u=u, aux=aux, logits=logits, prob=prob, fcin=fcin, qnn=q, W=W)
+        return logits, prob, aux, (sv if save else None)
+
+    def _qnn_forward(self, W, xF, B, seed, training, logits):
+        """QNNAlphaDetailed.forward (qnn_alpha.py:109-130)."""
+        a, P, st = self.a, self.P, self.s()
+        D, F = a.D, a.F
+        FD, C, QR = F * D, a.C, a.qh * a.qr
+        z = W.get("z", (B, FD))
+        rq = W.get("rq", (B,))
+        call("ctr_rmsnorm_fwd", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq), st)
+        ucat = W.get("ucat", (D, QR))
+        call("ctr_qnn_ucat", ptr(P["qnn.U"]), a.qh, D, a.qr, ptr(ucat), 0, st)
+        A = W.get("qA", (B * F, QR))
+        self.gemm(B * F, QR, D, ptr(z), D, 0, ptr(ucat), QR, 0, ptr(A), QR)
+        S = W.get("qS", (B, QR))
+        quad = W.get("qquad", (B, QR))
+        inter_pre = W.get("inter_pre", (B, C))
+        call("ctr_qnn_reduce_fwd", ptr(A), B, F, a.qh, a.qr, ptr(P["qnn.V"]), a.qP, ptr(S), ptr(quad),
+             ptr(inter_pre), st)
+        gate = g1 = mean = None
+        if a.use_se:
+            mean = W.get("se_mean", (C,))
+            self.colsum(ptr(inter_pre), C, B, C, ptr(mean), div=float(B))
+            Cr = C // a.se_r
+            g1 = W.get("se_g1", (Cr,))
+            gate = W.get("se_gate", (C,))
+            call("ctr_se_fwd_gate", ptr(mean), C, Cr, ptr(P["qnn.se.fc.0.weight"]), ptr(P["qnn.se.fc.0.bias"]),
+                 ptr(P["qnn.se.fc.2.weight"]), ptr(P["qnn.se.fc.2.bias"]), ptr(g1), ptr(gate), st)
+        inter = W.get("inter", (B, C))
+        dq_ = drop_args(seed, SITE_QNN, a.qnn_p, training)
+        call("ctr_scale_drop", ptr(inter_pre), B, C, ptr(gate), *dq_, ptr(inter), C, st)
+        # MLP on cat[z, inter] without materialising the concat: W0 = [W0a | W0b]
+        hs, acts = [], []
+        din = FD + C
+        W0 = P["qnn.mlp.0.weight"]
+        H0 = a.mlp_hidden[0] if a.mlp_hidden else 1
+        tmp = W.get("mlp_tmp", (B, H0))
+        self.gemm(B, H0, FD, ptr(z), FD, 0, ptr(W0), din, 1, ptr(tmp), H0)
+        nh = len(a.mlp_hidden)
+        for j in range(nh + 1):
+            last = j == nh
+            wkey, bkey = f"qnn.mlp.{3 * j}.weight", f"qnn.mlp.{3 * j}.bias"
+            n_out = 1 if last else a.mlp_hidden[j]
+            out = logits if last else W.get(f"mlp_h{j}", (B, n_out))
+            pre = None if last else W.get(f"mlp_a{j}", (B, n_out))
+            dm = (0, 0, 1.0) if last else drop_args(seed, SITE_MLP0 + j, a.qnn_p, training)
+            epi = GemmEpi(bias=ptr(P[bkey]), act=0 if last else 1, pre=ptr(pre), drop_key=dm[0], drop_thresh=dm[1],
+                          drop_scale=dm[2])
+            if j == 0:
+                epi.add, epi.ld_add = ptr(tmp), H0
+                self.gemm(B, n_out, C, ptr(inter), C, 0, ptr(P[wkey], FD), din, 1, ptr(out), n_out, epi)
+            else:
+                kin = a.mlp_hidden[j - 1]
+                self.gemm(B, n_out, kin, ptr(hs[-1]), kin, 0, ptr(P[wkey]), kin, 1, ptr(out), n_out, epi)
+            if not last:
+                hs.append(out)
+                acts.append(pre)
+        return dict(z=z, rq=rq, ucat=ucat, A=A, S=S, quad=quad, inter_pre=inter_pre, mean=mean, g1=g1, gate=gate,
+                    inter=inter, hs=hs, acts=acts)
+
+    def _fc_forward(self, W, fcin, ctx, cat_e, B, seed, training, logits):
+        """QNN disabled: fc head on [u, mean(num_e), mean(mask_e), cat_embs] (wrapper.py:95-100,167-173)."""
+        a, P, st = self.a, self.P, self.s()
+        D = a.D
+        nfc = fcin.shape[1] // D
+        col = 1
+        nctx_parts = (a.Fn > 0) + (a.Fm > 0)
+        if nctx_parts:   # the ctx buffer holds [num_mean, mask_mean, cat_mean]
+            call("ctr_copy2d", ptr(ctx), a.nctx * D, ptr(fcin, D), nfc * D, B, nctx_parts * D, st)
+            col += nctx_parts
+        call("ctr_copy2d", ptr(cat_e), a.Fc * D, ptr(fcin, col * D), nfc * D, B, a.Fc * D, st)
+        fa = W.get("fc_a", (B, 512))
+        fh = W.get("fc_h", (B, 512))
+        dfk = drop_args(seed, SITE_FC, 0.1, training)
+        self.gemm(B, 512, nfc * D, ptr(fcin), nfc * D, 0, ptr(P["fc.0.weight"]), nfc * D, 1, ptr(fh), 512,
+                  GemmEpi(bias=ptr(P["fc.0.bias"]), act=1, pre=ptr(fa), drop_key=dfk[0], drop_thresh=dfk[1],
+                          drop_scale=dfk[2]))
+        self.gemm(B, 1, 512, ptr(fh), 512, 0, ptr(P["fc.3.weight"]), 512, 1, ptr(logits), 1,
+                  GemmEpi(bias=ptr(P["fc.3.bias"])))
+        return dict(fa=fa, fh=fh)
+
+    # ------------------------------------------------------------------ loss
+    def loss(self, sv, y):
+        """bce_wll_style(logits, y) + aux_w * bce_wll_style(aux, y) and its grads (src/train.py:71-90,165-168)."""
+        W, B = sv["W"], sv["B"]
+        out = W.get("loss", (1,))
+        dz = W.get("dlogits", (B,))
+        dza = W.get("daux", (B,))
+        call("ctr_loss", ptr(sv["logits"]), ptr(sv["aux"]), ptr(y), B, float(self.a.aux_w), ptr(out), ptr(dz),
+             ptr(dza), self.s())
+        return out, dz, (dza if self.a.aux_w > 0 else None)
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, sv, dlogits, daux):
+        """Backward of the whole model.  Dense grads -> arena.grad; table grads -> compact
+        (sorted unique keys, summed rows, count) in self.tg for the optimizer stream."""
+        if sv["gen"] != self._gen:
+            raise RuntimeError("backward() must follow the most recent training forward (buffers are reused)")
+        a, P, G, st = self.a, self.P, self.G, self.s()
+        B, L, K, D = sv["B"], sv["L"], sv["K"], a.D
+        W = sv["W"]
+        F = a.F
+        FD = F * D
+        M = B * K
+        seed, training = sv["seed"], sv["training"]
+        xF = sv["xF"]
+        num_off, mask_off, cat_off = D, D + a.Fn * D, D + (a.Fn + a.Fm) * D
+        self.arena.grad.zero_()
+        dxF = W.get("dxF", (B, FD))
+        dfc = None
+        # ---------------- head
+        if a.use_qnn:
+            self._qnn_backward(sv, dlogits, dxF)
+            du_ptr, du_ld = ptr(dxF), FD
+        else:
+            dxF.zero_()
+            dfc = self._fc_backward(sv, dlogits)
+            du_ptr, du_ld = ptr(dfc), dfc.shape[1]
+        # ---------------- pool + aux head
+        dx = W.get("dx_a", (B, K, D))
+        dvals = W.get("dvals", (B, K))
+        ddr = drop_args(seed, SITE_DARE, a.p_dare, training)
+        call("ctr_pool_bwd", ptr(sv["xs"][-1]), ptr(sv["vals"]), ptr(sv["w"]), B, K, D,
+             0 if a.gating == "softmax" else 1, *ddr, ptr(P["dare.aux_head.weight"]), du_ptr, du_ld,
+             ptr(daux), ptr(dx), ptr(dvals), st)
+        if daux is not None:
+            self.gemm(1, D, B, ptr(daux), 1, 1, ptr(sv["u"]), D, 0, ptr(G["dare.aux_head.weight"]), D, None,
+                      self.wgrad_splits(1, D, B))
+            self.colsum(ptr(daux), 1, B, 1, ptr(G["dare.aux_head.bias"]))
+        # ---------------- encoder layers, last to first
+        dx_other = W.get("dx_b", (B, K, D))
+        for li in reversed(range(a.n_layers)):
+            dx, dx_other = self._layer_backward(sv, li, dx, dx_other), dx
+        # ---------------- top-K select -> dq, table row contributions
+        tg = self.tg = {}
+        dq = W.get("dq", (B, D))
+        att_c = W.get("att_contrib", (M, D))
+        att_k = W.get("att_keys", (M,), torch.int32)
+        rep_k = W.get("rep_keys", (M,), torch.int32)
+        call("ctr_dare_topk_bwd", ptr(sv["tok"]), B, K, ptr(sv["query"]), ptr(P["dare.emb_att.weight"]), D,
+             ptr(dvals), a.pad_id, ptr(dq), ptr(att_c), ptr(att_k), ptr(rep_k), st)
+        tg["att"] = self._rowgrad(W, "att", att_k, att_c, M, D, D, self.seq_key_bits)
+        tg["rep"] = self._rowgrad(W, "rep", rep_k, dx, M, D, D, self.seq_key_bits)
+        # ---------------- context / query
+        mode = QUERY_MODES[a.query_mode]
+        dcat = W.get("dcat", (B, a.Fc, D))
+        dpre = W.get("dpre", (B, D))
+        dk = drop_args(seed, SITE_EMB, a.p_emb, training)
+        call("ctr_context_bwd", ptr(xF, num_off), FD, a.Fn, ptr(xF, mask_off), FD, a.Fm, ptr(sv["cat_e"]), a.Fc, D,
+             B, mode, self.qi, ptr(P["ctx_mlp.0.weight"]), ptr(sv["hq"]), ptr(dq),
+             ptr(dxF, cat_off) if a.use_qnn else None, FD, *dk, ptr(dfc), dfc.shape[1] if dfc is not None else 0,
+             ptr(dxF, num_off), ptr(dxF, mask_off), ptr(dcat), ptr(dpre), st)
+        if mode != 0:
+            self.wgrad(ptr(dpre), D, ptr(sv["ctx"]), a.nctx * D, B, D, a.nctx * D, ptr(G["ctx_mlp.0.weight"]),
+                       bias_grad=ptr(G["ctx_mlp.0.bias"]))
+        # ---------------- numeric / binary embeddings
+        if a.Fn > 0:
+            wsz = _lib.query("ctr_feat_embed_bwd_ws", B, a.Fn, D)
+            fw = W.get("fe_ws_num", (wsz // 4 + 1,))
+            call("ctr_feat_embed_bwd", ptr(sv["X_num"]), B, a.Fn, ptr(P["num_embed.weight"]),
+                 ptr(P["num_embed.bias"]), ptr(P["num_embed.out_proj.weight"]), a.f_embed, D, ptr(dxF, num_off), FD,
+                 ptr(G["num_embed.weight"]), ptr(G["num_embed.bias"]), ptr(G["num_embed.out_proj.weight"]), ptr(fw),
+                 st)
+        if a.Fm > 0:
+            wsz = _lib.query("ctr_feat_embed_bwd_ws", B, a.Fm, D)
+            fw = W.get("fe_ws_mask", (wsz // 4 + 1,))
+            call("ctr_feat_embed_bwd", ptr(sv["X_mask"]), B, a.Fm, ptr(P["mask_embed.weight"]), None,
+                 ptr(P["mask_embed.out_proj.weight"]), a.f_embed, D, ptr(dxF, mask_off), FD,
+                 ptr(G["mask_embed.weight"]), None, ptr(G["mask_embed.out_proj.weight"]), ptr(fw), st)
+        # ---------------- categorical tables + projections
+        n_cat = B * a.Fc
+        cat_c = W.get("cat_contrib", (n_cat, 64))
+        cat_k = W.get("cat_keys", (n_cat,), torch.int32)
+        cws = W.get("cat_ws", (_lib.query("ctr_cat_embed_bwd_ws", B, a.Fc) // 4 + 1,))
+        call("ctr_cat_embed_bwd", ptr(sv["X_cat"]), B, a.Fc, ptr(self.arena.buf), ptr(self.cat_tab_off),
+             ptr(self.cat_proj_off), ptr(self.cat_dims_t), D, ptr(dcat), ptr(self.cat_row_base), ptr(cat_c),
+             ptr(cat_k), ptr(self.arena.grad), ptr(self.cat_proj_off), ptr(cws), st)
+        tg["cat"] = self._rowgrad(W, "cat", cat_k, cat_c, n_cat, 64, 64, self.cat_key_bits)
+        return tg
+
+    def _rowgrad(self, W, name, keys, contrib, n, width, ld, key_bits):
+        uk = W.get(f"{name}_uk", (n,), torch.int32)
+        ug = W.get(f"{name}_ug", (n, width))
+        nu = W.get(f"{name}_nu", (1,), torch.int32)
+        wsz = _lib.query("ctr_rowgrad_ws_size", n)
+        rws = W.get("rowgrad_ws", (max(wsz, W.t["rowgrad_ws"].numel() if "rowgrad_ws" in W.t else 0),),
+                    torch.uint8)
+        call("ctr_rowgrad", ptr(keys), ptr(contrib), n, width, ld, key_bits, ptr(uk), ptr(ug), ptr(nu), ptr(rws),
+             rws.numel(), self.s())
+        return dict(keys=uk, G=ug, n_uniq=nu, width=width, n=n)
+
+    def _layer_backward(self, sv, li, dx2, dout_buf):
+        """DAREEncoderLayer backward (dare.py:53-70). dx2: grad wrt layer output. Returns grad wrt input."""
+        a, P, G, st = self.a, self.P, self.G, self.s()
+        B, K, D = sv["B"], sv["K"], a.D
+        M, FF = B * K, a.ffn_hidden
+        W = sv["W"]
+        Ls = sv["layers"][li]
+        pre = f"dare.layers.{li}."
+        seed, training = sv["seed"], sv["training"]
+        # x2 = norm2(x1 + ffn(x1))
+        dh2 = W.get("dh2", (M, D))
+        npart = _lib.query("ctr_rmsnorm_bwd_nparts", M, D)
+        dwp = W.get("dw_part", (npart, D))
+        call("ctr_rmsnorm_bwd", ptr(dx2), D, ptr(Ls["h2"]), D, ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]), M, D,
+             ptr(dh2), D, None, 0, ptr(dwp), st)
+        self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm2.w"]))
+        # ffn.3: f @ W2^T + b2
+        self.wgrad(ptr(dh2), D, ptr(Ls["fo"]), FF, M, D, FF, ptr(G[pre + "ffn.3.weight"]),
+                   bias_grad=ptr(G[pre + "ffn.3.bias"]))
+        dact = W.get("dffa", (M, FF))
+        dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
+        self.gemm(M, FF, D, ptr(dh2), D, 0, ptr(P[pre + "ffn.3.weight"]), FF, 0, ptr(dact), FF,
+                  GemmEpi(dact=2, aux=ptr(Ls["act"]), drop_key=dfk[0], drop_thresh=dfk[1], drop_scale=dfk[2]))
+        # ffn.0: x1 @ W1^T + b1
+        self.wgrad(ptr(dact), FF, ptr(Ls["x1"]), D, M, FF, D, ptr(G[pre + "ffn.0.weight"]),
+                   bias_grad=ptr(G[pre + "ffn.0.bias"]))
+        dx1 = W.get("dx1", (M, D))
+        self.gemm(M, D, FF, ptr(dact), FF, 0, ptr(P[pre + "ffn.0.weight"]), D, 0, ptr(dx1), D,
+                  GemmEpi(add=ptr(dh2), ld_add=D))
+        # x1 = norm1(x + attn(x))
+        dh1 = W.get("dh1", (M, D))
+        call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,
+             ptr(dh1), D, None, 0, ptr(dwp), st)
+        self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
+        # out_proj
+        self.wgrad(ptr(dh1), D, ptr(Ls["o"]), D, M, D, D, ptr(G[pre + "mha.out_proj.weight"]),
+                   bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
+        do = W.get("do", (M, D))
+        self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
+        # attention core
+        dqkv = W.get("dqkv", (M, 3 * D))
+        nparts = _lib.query("ctr_attn_bwd_nparts", a.H, K, D) * B
+        nrel = 2 * a.top_k + 1
+        drp = W.get("drel_part", (nparts, nrel))
+        da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
+        scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
+        call("ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale,
+             *da, ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
+        if a.add_pos:
+            call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), st)
+        # in_proj
+        x_in = sv["xs"][li]
+        self.wgrad(ptr(dqkv), 3 * D, ptr(x_in), D, M, 3 * D, D, ptr(G[pre + "mha.in_proj_weight"]),
+                   bias_grad=ptr(G[pre + "mha.in_proj_bias"]))
+        self.gemm(M, D, 3 * D, ptr(dqkv), 3 * D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 0, ptr(dout_buf), D,
+                  GemmEpi(add=ptr(dh1), ld_add=D))
+        return dout_buf
+
+    def _qnn_backward(self, sv, dlogits, dxF):
+        a, P, G, st = self.a, self.P, self.G, self.s()
+        B, D, W = sv["B"], a.D, sv["W"]
+        q = sv["qnn"]
+        F = a.F
+        FD, C, QR = F * D, a.C, a.qh * a.qr
+        din = FD + C
+        seed, training = sv["seed"], sv["training"]
+        nh = len(a.mlp_hidden)
+        # MLP, last layer first; dact epilogues fold relu' and the dropout mask in
+        dcur, ncur = dlogits, 1
+        for j in reversed(range(nh + 1)):
+            wkey, bkey = f"qnn.mlp.{3 * j}.weight", f"qnn.mlp.{3 * j}.bias"
+            if j > 0:
+                kin = a.mlp_hidden[j - 1]
+                self.wgrad(ptr(dcur), ncur, ptr(q["hs"][j - 1]), kin, B, ncur, kin, ptr(G[wkey]),
+                           bias_grad=ptr(G[bkey]))
+                dprev = W.get(f"dmlp_a{j - 1}", (B, kin))
+                dm = drop_args(seed, SITE_MLP0 + j - 1, a.qnn_p, training)
+                self.gemm(B, kin, ncur, ptr(dcur), ncur, 0, ptr(P[wkey]), kin, 0, ptr(dprev), kin,
+                          GemmEpi(dact=1, aux=ptr(q["acts"][j - 1]), drop_key=dm[0], drop_thresh=dm[1],
+                                  drop_scale=dm[2]))
+                dcur, ncur = dprev, kin
+            else:
+                # first layer: W0 = [W0a (over z) | W0b (over inter)]
+                self.gemm(ncur, FD, B, ptr(dcur), ncur, 1, ptr(q["z"]), FD, 0, ptr(G[wkey]), din, None,
+                          self.wgrad_splits(ncur, FD, B))
+                self.gemm(ncur, C, B, ptr(dcur), ncur, 1, ptr(q["inter"]), C, 0, ptr(G[wkey], FD), din, None,
+                          self.wgrad_splits(ncur, C, B))
+                self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
+        W0 = P["qnn.mlp.0.weight"]
+        dinter = W.get("dinter", (B, C))
+        self.gemm(B, C, ncur, ptr(dcur), ncur, 0, ptr(W0, FD), din, 0, ptr(dinter), C)
+        dz_mlp = W.get("dz_mlp", (B, FD))
+        if a.use_residual:
+            self.gemm(B, FD, ncur, ptr(dcur), ncur, 0, ptr(W0), din, 0, ptr(dz_mlp), FD)
+        else:
+            dz_mlp.zero_()
+        # SE + dropout
+        dinter_pre = W.get("dinter_pre", (B, C))
+        dq_ = drop_args(seed, SITE_QNN, a.qnn_p, training)
+        Cr = C // a.se_r if a.use_se else 1
+        sws = W.get("se_ws", (_lib.query("ctr_se_bwd_ws", B, C) // 4 + 1,))
+        call("ctr_se_bwd", ptr(dinter), C, ptr(q["inter_pre"]), B, C, Cr, ptr(q["gate"]), ptr(q["g1"]),
+             ptr(q["mean"]), ptr(P.get("qnn.se.fc.0.weight")), ptr(P.get("qnn.se.fc.2.weight")), *dq_, ptr(dinter_pre),
+             ptr(G.get("qnn.se.fc.0.weight")), ptr(G.get("qnn.se.fc.0.bias")), ptr(G.get("qnn.se.fc.2.weight")),
+             ptr(G.get("qnn.se.fc.2.bias")), ptr(sws), st)
+        # pair interaction
+        dA = W.get("qdA", (B * F, QR))
+        call("ctr_qnn_reduce_bwd", ptr(q["A"]), B, F, a.qh, a.qr, ptr(P["qnn.V"]), a.qP, ptr(q["S"]),
+             ptr(dinter_pre), ptr(dA), st)
+        for h in range(a.qh):   # dV_h = quad_h^T @ dinter_h
+            self.gemm(a.qr, a.qP, B, ptr(q["quad"], h * a.qr), QR, 1, ptr(dinter_pre, h * a.qP), C, 0,
+                      ptr(G["qnn.V"], h * a.qr * a.qP), a.qP, None, self.wgrad_splits(a.qr, a.qP, B))
+        ducat = W.get("ducat", (D, QR))
+        self.gemm(D, QR, B * F, ptr(q["z"]), D, 1, ptr(dA), QR, 0, ptr(ducat), QR, None,
+                  self.wgrad_splits(D, QR, B * F))
+        call("ctr_qnn_ucat", ptr(ducat), a.qh, D, a.qr, ptr(G["qnn.U"]), 1, st)
+        dz = W.get("dz", (B, FD))
+        self.gemm(B * F, D, QR, ptr(dA), QR, 0, ptr(q["ucat"]), QR, 1, ptr(dz), D,
+                  GemmEpi(add=ptr(dz_mlp), ld_add=D))
+        # pre-norm
+        npart = _lib.query("ctr_rmsnorm_bwd_nparts", B, FD)
+        dwp = W.get("dwq_part", (npart, FD))
+        call("ctr_rmsnorm_bwd", ptr(dz), FD, ptr(sv["xF"]), FD, ptr(q["rq"]), ptr(P["qnn.pre_norm.w"]), B, FD,
+             ptr(dxF), FD, None, 0, ptr(dwp), st)
+        self.colsum(ptr(dwp), FD, npart, FD, ptr(G["qnn.pre_norm.w"]))
+
+    def _fc_backward(self, sv, dlogits):
+        a, P, G, st = self.a, self.P, self.G, self.s()
+        B, W = sv["B"], sv["W"]
+        fcin = sv["fcin"]
+        q = sv["qnn"]
+        nin = fcin.shape[1]
+        self.wgrad(ptr(dlogits), 1, ptr(q["fh"]), 512, B, 1, 512, ptr(G["fc.3.weight"]), bias_grad=ptr(G["fc.3.bias"]))
+        dfa = W.get("dfc_a", (B, 512))
+        dfk = drop_args(sv["seed"], SITE_FC, 0.1, sv["training"])
+        self.gemm(B, 512, 1, ptr(dlogits), 1, 0, ptr(P["fc.3.weight"]), 512, 0, ptr(dfa), 512,
+                  GemmEpi(dact=1, aux=ptr(q["fa"]), drop_key=dfk[0], drop_thresh=dfk[1], drop_scale=dfk[2]))
+        self.wgrad(ptr(dfa), 512, ptr(fcin), nin, B, 512, nin, ptr(G["fc.0.weight"]), bias_grad=ptr(G["fc.0.bias"]))
+        dfcin = W.get("dfcin", (B, nin))
+        self.gemm(B, nin, 512, ptr(dfa), 512, 0, ptr(P["fc.0.weight"]), nin, 0, ptr(dfcin), nin)
+        return dfcin
+
+    # ------------------------------------------------------------------ compat: dense table grads
+    def dense_table_grad(self, key):
+        """Materialise the dense gradient of one embedding table from the compact rows (autograd path)."""
+        a = self.a
+        shp = self.arena.shapes[key]
+        out = torch.zeros(shp, dtype=torch.float32, device=self.device)
+        if key == "dare.emb_att.weight":
+            t, base = self.tg["att"], 0
+        elif key == "dare.emb_rep.weight":
+            t, base = self.tg["rep"], 0
+        else:
+            c = a.cat_names.index(key[len("cat_embs."):-len(".weight")])
+            t, base = self.tg["cat"], int(self.cat_row_base_np[c])
+        call("ctr_scatter_rows", ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["n"], shp[1], t["G"].shape[1],
+             base, shp[0], ptr(out), self.s())
+        return out

@@ -1,0 +1,255 @@
+"""Fused clip_grad_norm_ + AdamW + EMA for the CTRModel parameter arena.
+
+Drop-in for the reference step tail (src/train.py:133-139 construction, :185-199 per step):
+    nn.utils.clip_grad_norm_(model.parameters(), c); opt.step(); ema.update(model, global_step)
+Semantics are torch's dense ones (every element decays / moves each step, untouched table rows see
+grad 0), executed as ONE pass over (p, m, v, ema) by csrc/optim.hip with table grads read from the
+compact row dedup -- no dense table gradient is ever written.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import OptChunk, OptSeg, call
+from .engine import ptr
+
+INVALID_KEY = 0xFFFFFFFF
+
+
+def ema_decay_at(base, warmup_steps, warmup_type, n_updates):
+    """ModelEMA._decay_at (src/utils/ema.py:72-88)."""
+    if warmup_steps <= 0 or warmup_type == "none":
+        return base
+    t = min(1.0, (n_updates + 1) / warmup_steps)
+    if warmup_type == "linear":
+        d = 1.0 - (1.0 - base) * t
+    elif warmup_type == "cosine":
+        d = 1.0 - (1.0 - base) * (0.5 * (1 + math.cos(math.pi * (1 - t))))
+    else:
+        d = base
+    return float(max(0.0, min(1.0, d)))
+
+
+class ArenaEMA:
+    """ModelEMA (src/utils/ema.py:11-198) over the arena: fp32 shadow of every parameter."""
+
+    def __init__(self, model, base_decay=0.999, warmup_steps=0, warmup_type="linear", update_after_step=0,
+                 update_interval=1, ema_on_buffers="copy", offload_to_cpu=False, pin_memory=False, param_filter=None):
+        if offload_to_cpu:
+            raise NotImplementedError("offload_to_cpu EMA is not supported on the fused path")
+        if param_filter:
+            raise NotImplementedError("param_filter is not supported on the fused path")
+        self.model = model
+        self.base_decay = float(base_decay)
+        self.warmup_steps = int(max(0, warmup_steps))
+        self.warmup_type = warmup_type
+        self.update_after_step = int(max(0, update_after_step))
+        self.update_interval = int(max(1, update_interval))
+        self.ema_on_buffers = ema_on_buffers
+        self.offload_to_cpu = False
+        self.pin_memory = bool(pin_memory)
+        self.param_filter = set()
+        self.num_updates = 0
+        self.shadow = model.arena.buf.clone()
+        self._saved = None
+
+    def wants_update(self, global_step):
+        if global_step < self.update_after_step:
+            return False
+        return (global_step - self.update_after_step) % self.update_interval == 0
+
+    def next_decay(self):
+        return ema_decay_at(self.base_decay, self.warmup_steps, self.warmup_type, self.num_updates)
+
+    def update(self, model, global_step):
+        """Standalone update (when not fused into FusedAdamW.step)."""
+        opt = getattr(model, "_fused_opt", None)
+        if opt is None:
+            raise RuntimeError("ArenaEMA.update needs a FusedAdamW bound to the model")
+        opt.ema_only(self, global_step)
+
+    @torch.no_grad()
+    def store(self, model):
+        self._saved = model.arena.buf.clone()
+
+    @torch.no_grad()
+    def copy_to(self, model):
+        model.arena.buf.copy_(self.shadow)
+
+    @torch.no_grad()
+    def restore(self, model):
+        if self._saved is None:
+            return
+        model.arena.buf.copy_(self._saved)
+        self._saved = None
+
+    def shadow_params(self):
+        ar = self.model.arena
+        return {k: ar._view(self.shadow, k) for k in ar.order}
+
+    def state_dict(self):
+        return {"base_decay": self.base_decay, "warmup_steps": self.warmup_steps, "warmup_type": self.warmup_type,
+                "update_after_step": self.update_after_step, "update_interval": self.update_interval,
+                "ema_on_buffers": self.ema_on_buffers, "offload_to_cpu": False, "pin_memory": self.pin_memory,
+                "param_filter": [], "num_updates": self.num_updates,
+                "shadow_params": {k: v.detach().cpu().clone() for k, v in self.shadow_params().items()},
+                "shadow_buffers": {}}
+
+    def load_state_dict(self, state):
+        self.base_decay = float(state["base_decay"])
+        self.warmup_steps = int(state["warmup_steps"])
+        self.warmup_type = state["warmup_type"]
+        self.update_after_step = int(state["update_after_step"])
+        self.update_interval = int(state["update_interval"])
+        self.num_updates = int(state.get("num_updates", 0))
+        for k, v in self.shadow_params().items():
+            v.copy_(state["shadow_params"][k])
+
+
+def build_ema(model, cfg):
+    """src/utils/ema.py:200-216."""
+    if not cfg.get("ema", {}).get("enabled", False):
+        return None
+    ec = cfg["ema"]
+    return ArenaEMA(model, base_decay=float(ec.get("decay", 0.999)), warmup_steps=int(ec.get("warmup_steps", 0)),
+                    warmup_type=str(ec.get("warmup_type", "linear")),
+                    update_after_step=int(ec.get("update_after_step", 0)),
+                    update_interval=int(ec.get("update_interval", 1)),
+                    ema_on_buffers=str(ec.get("ema_on_buffers", "copy")),
+                    offload_to_cpu=bool(ec.get("offload_to_cpu", False)),
+                    pin_memory=bool(ec.get("pin_memory", False)), param_filter=ec.get("param_filter", []))
+
+
+class FusedAdamW:
+    """torch.optim.AdamW(model.parameters(), lr, weight_decay) + clip + EMA as one arena stream."""
+
+    def __init__(self, model, lr, weight_decay=1e-2, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=0.0, ema=None):
+        self.model = model
+        self.arena = ar = model.arena
+        self.engine = model.engine
+        self.param_groups = [{"lr": float(lr), "weight_decay": float(weight_decay), "betas": betas, "eps": eps}]
+        self.max_grad_norm = float(max_grad_norm)
+        self.ema = ema
+        dev = ar.device
+        self.m = torch.zeros(ar.total, dtype=torch.float32, device=dev)
+        self.v = torch.zeros(ar.total, dtype=torch.float32, device=dev)
+        self.step_count = 0
+        self.norm_out = torch.zeros(2, dtype=torch.float32, device=dev)     # [global norm, clip coef]
+        self.nparts_call = _lib.query("ctr_norm_nparts_per_call")
+        self.norm_parts = torch.zeros(4 * self.nparts_call, dtype=torch.float32, device=dev)
+        self._seg_key = None
+        self._segs_dev = None
+        self._build_chunks()
+        object.__setattr__(model, "_fused_opt", self)
+
+    # -------------------------------------------------------------- layout
+    def _segments(self, tg):
+        """Segment table: dense-grad region, no-grad region, then one sparse segment per table."""
+        ar, eng, a = self.arena, self.engine, self.engine.a
+        segs = []
+        if ar.n_dense_grad > 0:
+            segs.append(dict(p_off=0, n=ar.n_dense_grad, width=1, kind=0, g_off=0))
+        lo, hi = ar.nograd_range
+        if hi > lo:
+            segs.append(dict(p_off=lo, n=hi - lo, width=1, kind=2, g_off=0))
+        for key in ["dare.emb_att.weight", "dare.emb_rep.weight"] + [f"cat_embs.{c}.weight" for c in a.cat_names]:
+            shp = ar.shapes[key]
+            if key == "dare.emb_att.weight":
+                name, base = "att", 0
+            elif key == "dare.emb_rep.weight":
+                name, base = "rep", 0
+            else:
+                name, base = "cat", int(eng.cat_row_base_np[a.cat_names.index(key[9:-7])])
+            t = tg.get(name) if tg else None
+            segs.append(dict(p_off=ar.offsets[key], n=int(np.prod(shp)), width=shp[1], kind=1, g_off=0,
+                             keys=ptr(t["keys"]) if t else None, G=ptr(t["G"]) if t else None,
+                             n_uniq=ptr(t["n_uniq"]) if t else None, g_ld=t["G"].shape[1] if t else 0,
+                             key_base=base, name=name))
+        return segs
+
+    def _build_chunks(self):
+        segs = self._segments(None)
+        CH = _lib.query("ctr_opt_chunk_elems")
+        self._chunk_all, self._chunk_adam = [], []
+        for si, sg in enumerate(segs):
+            for e0 in range(0, sg["n"], CH):
+                c = (si, e0, min(sg["n"], e0 + CH))
+                self._chunk_all.append(c)
+                if sg["kind"] != 2:
+                    self._chunk_adam.append(c)
+        self._chunks_dev = {}
+        for name, lst in (("all", self._chunk_all), ("adam", self._chunk_adam)):
+            arr = (OptChunk * max(1, len(lst)))()
+            for i, (si, e0, e1) in enumerate(lst):
+                arr[i].seg, arr[i].pad, arr[i].e0, arr[i].e1 = si, 0, e0, e1
+            raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
+            self._chunks_dev[name] = (torch.from_numpy(raw).to(self.arena.device), len(lst))
+
+    def _segs_device(self, tg):
+        segs = self._segments(tg)
+        key = tuple((s.get("keys"), s.get("G"), s.get("n_uniq")) for s in segs)
+        if key != self._seg_key:
+            arr = (OptSeg * len(segs))()
+            for i, s in enumerate(segs):
+                o = arr[i]
+                o.p_off, o.n, o.width, o.kind, o.g_off = s["p_off"], s["n"], s["width"], s["kind"], s["g_off"]
+                o.keys, o.G, o.n_uniq = s.get("keys"), s.get("G"), s.get("n_uniq")
+                o.g_ld, o.key_base = s.get("g_ld", 0), s.get("key_base", 0)
+            raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
+            self._segs_dev = torch.from_numpy(raw).to(self.arena.device)
+            self._seg_key = key
+        return self._segs_dev
+
+    # -------------------------------------------------------------- step
+    def clip(self, tg):
+        """Global grad L2 norm over dense grads + deduplicated table rows -> (norm, coef) on device."""
+        st = self.engine.s()
+        parts = self.norm_parts
+        n = self.nparts_call
+        call("ctr_sqnorm_dense", ptr(self.arena.grad), self.arena.n_dense_grad, ptr(parts, 0), st)
+        for j, name in enumerate(("att", "rep", "cat")):
+            t = tg[name]
+            call("ctr_sqnorm_rows", ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["width"], t["G"].shape[1],
+                 INVALID_KEY, ptr(parts, (j + 1) * n), st)
+        call("ctr_clip_finalize", ptr(parts), 4 * n, self.max_grad_norm, ptr(self.norm_out), st)
+        return self.norm_out
+
+    def step(self, tg=None, global_step=None):
+        """clip (if max_grad_norm > 0) -> AdamW -> EMA (if bound and due at global_step)."""
+        tg = tg if tg is not None else self.engine.tg
+        g = self.param_groups[0]
+        self.clip(tg)
+        self.step_count += 1
+        do_ema = 0
+        decay = 0.0
+        if self.ema is not None and global_step is not None and self.ema.wants_update(global_step):
+            do_ema = 1
+            decay = self.ema.next_decay()
+        segs = self._segs_device(tg)
+        chunks, n = self._chunks_dev["all" if do_ema else "adam"]
+        b1, b2 = g["betas"]
+        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.arena.buf), ptr(self.m), ptr(self.v),
+             ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf), ptr(self.arena.grad),
+             ptr(self.norm_out, 1) if self.max_grad_norm > 0 else None, float(g["lr"]), float(g["weight_decay"]),
+             float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1, do_ema, self.engine.s())
+        if do_ema:
+            self.ema.num_updates += 1
+
+    def ema_only(self, ema, global_step):
+        if not ema.wants_update(global_step):
+            return
+        decay = ema.next_decay()
+        segs = self._segs_device(None)
+        chunks, n = self._chunks_dev["all"]
+        g = self.param_groups[0]
+        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.arena.buf), ptr(self.m), ptr(self.v),
+             ptr(ema.shadow), ptr(self.arena.grad), None, float(g["lr"]), float(g["weight_decay"]), 0.9, 0.999,
+             1e-8, max(1, self.step_count), float(decay), 0, 1, self.engine.s())
+        ema.num_updates += 1
+
+    def zero_grad(self, set_to_none=True):
+        pass   # grads are overwritten every backward

@@ -1,0 +1,167 @@
+"""CTRModel -- drop-in for src/models/wrapper.py:7-176 on MI355X.
+
+Same constructor signature, same ``forward(batch) -> (logits, prob, aux_logit)`` and the same
+``state_dict`` keys/shapes/order as the reference (parameters are views into one device arena, see
+engine.ParamArena).  The compute is libctrhip.so; there is no torch/CPU fallback.
+
+Two training paths:
+  * reference-style: ``logits, prob, aux = model(batch); loss = f(...); loss.backward()`` works --
+    a custom autograd.Function runs the HIP backward and hands torch ordinary dense ``.grad`` tensors
+    (tables included; fine for tests / small vocabularies);
+  * fused (what tossctr.train and bench.py use): ``model.train_step(...)`` via tossctr.optim --
+    table grads stay compact (sorted unique rows) and clip + AdamW + EMA run as one HBM stream.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .arch import Arch
+from .engine import Engine, ParamArena, ptr
+from . import _lib
+
+
+def _tree_module(root: nn.Module, key: str) -> tuple:
+    parts = key.split(".")
+    mod = root
+    for name in parts[:-1]:
+        if name not in mod._modules:
+            mod.add_module(name, nn.Module())
+        mod = mod._modules[name]
+    return mod, parts[-1]
+
+
+class _Query:
+    """`.dare.query_mode` is read by the reference wrapper (src/models/wrapper.py:154)."""
+
+
+class _CTRFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, inputs, seed, *params):
+        logits, prob, aux, sv = model.engine.forward(*inputs, training=True, seed=seed, save=True)
+        ctx.model, ctx.sv = model, sv
+        ctx.set_materialize_grads(False)
+        return logits.clone(), prob.clone(), aux.clone()
+
+    @staticmethod
+    def backward(ctx, g_logits, g_prob, g_aux):
+        model, sv = ctx.model, ctx.sv
+        eng = model.engine
+        B = sv["B"]
+        dz = torch.zeros(B, device=eng.device) if g_logits is None else g_logits.float().contiguous().clone()
+        if g_prob is not None:   # prob = sigmoid(logits): dz += dprob * p * (1 - p)
+            p = sv["prob"]
+            dz = dz + g_prob * p * (1 - p)
+        daux = None if g_aux is None else g_aux.float().contiguous()
+        eng.backward(sv, dz, daux)
+        grads = []
+        for k in model.arena.order:
+            if model.arena.kind[k] == "table":
+                grads.append(eng.dense_table_grad(k))
+            elif k in model.no_grad and not (k.startswith("dare.aux_head") and daux is not None):
+                grads.append(None)
+            else:
+                grads.append(eng.G[k].clone())
+        return (None, None, None, *grads)
+
+
+class CTRModel(nn.Module):
+    def __init__(self, cfg, seq_vocab: int, num_feat_dim: int, mask_feat_dim: int, cat_cardinals: dict,
+                 cat_cols_order: list, device=None):
+        super().__init__()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+        if device is None or torch.device(device).type != "cuda":
+            raise RuntimeError("tossctr.CTRModel runs only on an MI355X (HIP) device; no CPU fallback")
+        _lib.load()
+        self.cfg = cfg
+        self.arch = Arch.from_cfg(cfg, seq_vocab, num_feat_dim, mask_feat_dim, cat_cardinals, cat_cols_order)
+        self.cat_cols_order = list(cat_cols_order)
+        self.num_dim, self.mask_dim, self.D = num_feat_dim, mask_feat_dim, self.arch.D
+        self.query_key = self.arch.query_key
+        self.aux_weight = self.arch.aux_w
+        self.use_qnn = self.arch.use_qnn
+        object.__setattr__(self, "arena", ParamArena(self.arch, torch.device(device)))
+        object.__setattr__(self, "engine", Engine(self.arch, self.arena))
+        self.no_grad = self.arch.no_grad_keys()
+        for k in self.arena.order:
+            mod, name = _tree_module(self, k)
+            mod.register_parameter(name, nn.Parameter(self.arena.views[k], requires_grad=True))
+        self.dare.query_mode = self.arch.query_mode
+        self.seed = int(cfg.get("seed", 777))
+        self._step = 0
+        self.reset_parameters()
+
+    # the arena is not an nn.Module buffer: keep .to()/.cuda() from re-allocating parameters
+    def _apply(self, fn, recurse=True):
+        return self
+
+    @torch.no_grad()
+    def reset_parameters(self, generator=None):
+        """Reference default init: nn.Embedding N(0,1) (pad row 0), nn.Linear kaiming-uniform /
+        U(+-1/sqrt(fan_in)) biases, RMSNorm w = 1, feature slopes N(0, 0.02^2), U/V N(0, 0.02^2)."""
+        a = self.arch
+        g = generator
+        for k in self.arena.order:
+            t = self.arena.views[k]
+            if k.endswith(".w"):
+                t.fill_(1.0)
+            elif ".emb_" in k or k.startswith("cat_embs.") or "pbias.rel" in k:
+                t.normal_(0.0, 1.0, generator=g)
+                if ".emb_" in k:
+                    t[a.pad_id].zero_()
+            elif k in ("num_embed.weight", "mask_embed.weight", "qnn.U", "qnn.V"):
+                t.normal_(0.0, 0.02, generator=g)
+            elif k == "num_embed.bias":
+                t.zero_()
+            else:
+                fan_in = t.shape[-1] if t.dim() > 1 else self._fan_in_of_bias(k)
+                bound = 1.0 / max(1, fan_in) ** 0.5
+                t.uniform_(-bound, bound, generator=g)
+
+    def _fan_in_of_bias(self, k):
+        wk = k[: -len("bias")] + "weight"
+        if k.endswith("in_proj_bias"):
+            return self.D
+        if wk in self.arena.shapes:
+            return self.arena.shapes[wk][-1]
+        return 1
+
+    # ------------------------------------------------------------------ forward
+    def _stage(self, batch):
+        """X_num/X_mask -> f32, X_cat/seq -> int32 on the model device (src/models/wrapper.py:139-143)."""
+        dev = self.arena.device
+        X_num = batch["X_num"].to(dev, non_blocking=True).float().contiguous()
+        X_mask = batch["X_mask"].to(dev, non_blocking=True).float().contiguous()
+        X_cat = batch["X_cat"].to(dev, non_blocking=True).to(torch.int32).contiguous()
+        seq = batch["seq"].to(dev, non_blocking=True).to(torch.int32).contiguous()
+        return X_num, X_mask, X_cat, seq
+
+    def next_seed(self):
+        self._step += 1
+        return ((self.seed & 0xFFFFFFFF) << 32) | (self._step & 0xFFFFFFFF)
+
+    def forward(self, batch, seed=None):
+        inputs = self._stage(batch)
+        if self.training and torch.is_grad_enabled():
+            seed = self.next_seed() if seed is None else seed
+            return _CTRFunction.apply(self, inputs, seed, *[getattr(*_tree_module(self, k)) for k in self.arena.order])
+        logits, prob, aux, _ = self.engine.forward(*inputs, training=self.training,
+                                                   seed=self.next_seed() if seed is None else seed, save=False)
+        return logits.clone(), prob.clone(), aux.clone()
+
+    # ------------------------------------------------------------------ fused training step
+    def train_step(self, inputs, y, opt, global_step, seed=None):
+        """One reference step (src/train.py:152-199): forward -> bce_wll_style(+aux) -> backward ->
+        clip -> AdamW -> EMA, all on device, no host sync.  ``inputs`` = staged (X_num, X_mask, X_cat,
+        seq) device tensors (see ``stage``), ``y`` float labels on device.  Returns the loss (device)."""
+        seed = self.next_seed() if seed is None else seed
+        eng = self.engine
+        _, _, _, sv = eng.forward(*inputs, training=True, seed=seed, save=True)
+        loss, dz, daux = eng.loss(sv, y)
+        tg = eng.backward(sv, dz, daux)
+        opt.step(tg, global_step)
+        return loss
+
+    def stage(self, batch):
+        return self._stage(batch)
