@@ -197,20 +197,27 @@ typedef struct {
 } ctr_opt_chunk_t;
 
 int ctr_opt_chunk_elems(void);
-int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, float* P, float* M, float* V,
-                  float* E, const float* dgrad, const float* coef, float lr, float wd, float beta1, float beta2,
-                  float eps, int step, float ema_decay, int do_adam, int do_ema, void* stream);
+/* krange: 2*nchunks uint32 scratch (per-chunk key ranges of the sparse segments) */
+int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, uint32_t* krange, float* P,
+                  float* M, float* V, float* E, const float* dgrad, const float* coef, float lr, float wd, float beta1,
+                  float beta2, float eps, int step, float ema_decay, int do_adam, int do_ema, void* stream);
 int ctr_norm_nparts_per_call(void);
 int ctr_sqnorm_dense(const float* x, long n, float* part, void* stream);
 int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int width, int ld,
                     uint32_t invalid_key, float* part, void* stream);
-/* out[0] = global L2 norm, out[1] = min(1, max_norm/(norm+1e-6)) (1 if max_norm <= 0) */
-int ctr_clip_finalize(const float* part, int nparts, float max_norm, float* out, void* stream);
+/* out[0] = global L2 norm of (summed grads * grad_scale); out[1] = grad_scale * min(1, max_norm/(norm+1e-6))
+ * (grad_scale alone if max_norm <= 0) -- the multiplier the AdamW stream applies to raw grads      */
+int ctr_clip_finalize(const float* part, int nparts, float max_norm, float grad_scale, float* out, void* stream);
+/* data parallel: invalidate slots >= counts[r] of each rank's block of n gathered keys */
+int ctr_mask_tail_keys(uint32_t* keys, int n, int world, const uint32_t* counts, void* stream);
 
 
 /* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */
 int ctr_sigmoid(const float* x, int n, float* y, void* stream);
 int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream);
+/* batch assembly from HBM-resident shard columns (replaces ShardedDataset.__getitem__ + collate_sharded,
+ * src/data/dataset.py:77-80,98-124): dst[r, :] = src[idx[r], :], rows of row_words 4-byte words     */
+int ctr_gather_rows(const void* src, long row_words, const long* idx, int n, void* dst, void* stream);
 int ctr_scatter_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int max_uniq, int width, int ld,
                      uint32_t key_base, long n_rows, float* out, void* stream);
 

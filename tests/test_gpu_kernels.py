@@ -107,6 +107,7 @@ def test_rowgrad_dedup_matches_numpy():
     ref = np.zeros((len(ref_k), width))
     pos = np.searchsorted(ref_k, keys)
     np.add.at(ref, pos, vals.astype(np.float64))
+    ref[ref_k == 0xFFFFFFFF] = 0.0          # the dropped (pad) group is not summed
     assert np.abs(ug[:u].cpu().numpy() - ref).max() < 1e-4
     # bitwise reproducible
     ug2 = torch.empty_like(ug)
@@ -202,7 +203,7 @@ def test_topk_select_vs_torch(L_, K, D):
 def test_fused_adamw_matches_torch():
     """ctr_adamw_ema on a dense segment == torch.optim.AdamW + clip + EMA arithmetic."""
     L = _lib()
-    n = 10_000
+    n = 10_240
     p0 = torch.randn(n)
     g = torch.randn(n)
     p_t = p0.clone().requires_grad_(True)
@@ -226,8 +227,11 @@ def test_fused_adamw_matches_torch():
         opt.step()
         with torch.no_grad():
             shadow_ref.mul_(0.9).add_(p_t.detach(), alpha=0.1)
-        L.call("ctr_adamw_ema", ptr(cd), len(chunks), ptr(sd), ptr(P), ptr(Mm), ptr(V), ptr(E), ptr(G), ptr(coef, 1),
+        kr = torch.zeros(2 * len(chunks), dtype=torch.int32, device="cuda")
+        L.call("ctr_adamw_ema", ptr(cd), len(chunks), ptr(sd), ptr(kr), ptr(P), ptr(Mm), ptr(V), ptr(E), ptr(G),
+               ptr(coef, 1),
                3e-3, 1e-2, 0.9, 0.999, 1e-8, step, 0.9, 1, 1, stream())
     torch.cuda.synchronize()
-    assert (P.cpu() - p_t.detach()).abs().max() < 1e-6
-    assert (E.cpu() - shadow_ref).abs().max() < 1e-6
+    # a few ulp: the kernel's fused multiply-adds vs torch's separately rounded CPU ops
+    assert torch.allclose(P.cpu(), p_t.detach(), rtol=1e-6, atol=1e-6)
+    assert torch.allclose(E.cpu(), shadow_ref, rtol=1e-6, atol=1e-6)

@@ -244,15 +244,15 @@ __global__ void pos_bias_mean_kernel(const float* __restrict__ rel, int H, int n
   }
 }
 
-// drel[d, h] = (sum_p part[p, d]) / H
-__global__ void pos_bias_grad_kernel(const float* __restrict__ part, int nparts, int H, int n,
-                                     float* __restrict__ drel) {
-  for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int p = 0; p < nparts; ++p) s += part[(long)p * n + d];
-    const float g = s / (float)H;
-    for (int h = 0; h < H; ++h) drel[(long)d * H + h] = g;
-  }
+// drel[d, h] = (sum_p part[p, d]) / H ; one workgroup per distance d, fixed-order block reduction
+__global__ __launch_bounds__(256) void pos_bias_grad_kernel(const float* __restrict__ part, int nparts, int H, int n,
+                                                            float* __restrict__ drel) {
+  __shared__ float red[4];
+  const int d = blockIdx.x;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < nparts; p += 256) s += part[(long)p * n + d];
+  s = block_sum(s, red);
+  if (threadIdx.x < H) drel[(long)d * H + threadIdx.x] = s / (float)H;
 }
 
 }  // namespace ctr
@@ -321,6 +321,7 @@ extern "C" int ctr_pos_bias_mean(const float* rel, int H, int n, float* out, voi
 }
 
 extern "C" int ctr_pos_bias_grad(const float* part, int nparts, int H, int n, float* drel, void* stream) {
-  pos_bias_grad_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(part, nparts, H, n, drel);
+  CTR_REQUIRE(H <= 256, "H > 256");
+  pos_bias_grad_kernel<<<n, 256, 0, (hipStream_t)stream>>>(part, nparts, H, n, drel);
   return check_launch("pos_bias_grad");
 }

@@ -18,10 +18,10 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
                                                              const float* __restrict__ P, int fe, int D,
                                                              float* __restrict__ out, long out_ld) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* sP = sm;               // [D][fe]
-  float* sW = sm + D * fe;      // [F][fe]
+  float* sP = sm;               // [fe][D]: lanes (consecutive d) read consecutive banks
+  float* sW = sm + D * fe;      // [F][fe] (broadcast across the d lanes)
   float* sB = sW + F * fe;      // [F][fe]
-  for (int i = threadIdx.x; i < D * fe; i += blockDim.x) sP[i] = P[i];
+  for (int i = threadIdx.x; i < D * fe; i += blockDim.x) sP[(i % fe) * D + i / fe] = P[i];
   for (int i = threadIdx.x; i < F * fe; i += blockDim.x) {
     sW[i] = W[i];
     sB[i] = bias ? bias[i] : 0.f;
@@ -38,53 +38,53 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
     for (int k = 0; k < fe; ++k) {
       float e = xv * sW[f * fe + k];
       if (bias) e = e + sB[f * fe + k];
-      acc = fmaf(e, sP[d * fe + k], acc);
+      acc = fmaf(e, sP[k * D + d], acc);
     }
     out[b * out_ld + (long)f * D + d] = acc;
   }
 }
 
-// S1[f,d] = sum_b x[b,f] dout[b,f,d],  S0[f,d] = sum_b dout[b,f,d]   (per row-chunk partials)
-__global__ __launch_bounds__(256) void feat_embed_bwd_partial(const float* __restrict__ x, int B, int F, int D,
-                                                             const float* __restrict__ dout, long dout_ld,
-                                                             int rows_per_chunk, float* __restrict__ part) {
-  const int chunk = blockIdx.y;
-  const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
-  for (int fd = blockIdx.x * blockDim.x + threadIdx.x; fd < F * D; fd += gridDim.x * blockDim.x) {
-    const int f = fd / D;
-    float s1 = 0.f, s0 = 0.f;
-    for (int b = b0; b < b1; ++b) {
-      const float g = dout[(long)b * dout_ld + fd];
+// S1[f,d] = sum_b x[b,f] dout[b,f,d],  S0[f,d] = sum_b dout[b,f,d]: one workgroup per feature f;
+// lanes = d (coalesced dout rows), 256/D row groups stride the batch, combined in fixed order.
+__global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restrict__ x, int B, int F, int D,
+                                                          const float* __restrict__ dout, long dout_ld,
+                                                          float* __restrict__ S) {
+  __shared__ float r1[256], r0[256];
+  const int f = blockIdx.x, t = threadIdx.x;
+  const int RG = 256 / D;
+  const int d = t % D, rg = t / D;
+  float s1 = 0.f, s0 = 0.f;
+  if (rg < RG)
+    for (int b = rg; b < B; b += RG) {
+      const float g = dout[(long)b * dout_ld + (long)f * D + d];
       s1 = fmaf(x[(long)b * F + f], g, s1);
       s0 += g;
     }
-    part[((long)chunk * 2 + 0) * F * D + fd] = s1;
-    part[((long)chunk * 2 + 1) * F * D + fd] = s0;
+  r1[t] = s1;
+  r0[t] = s0;
+  __syncthreads();
+  if (t < D) {
+    float a = 0.f, c = 0.f;
+    for (int g = 0; g < RG; ++g) {
+      a += r1[g * D + t];
+      c += r0[g * D + t];
+    }
+    S[(long)f * D + t] = a;
+    S[(long)F * D + (long)f * D + t] = c;
   }
 }
 
-// reduce chunks -> S1, S0; then dW = S1 @ P, dbias = S0 @ P, dP = sum_f S1^T W + S0^T bias
-__global__ __launch_bounds__(256) void feat_embed_bwd_final(int nchunk, int F, int D, int fe,
-                                                           const float* __restrict__ part,
+// dW = S1 @ P, dbias = S0 @ P, dP = sum_f S1^T W + S0^T bias   (one thread per output element)
+__global__ __launch_bounds__(256) void feat_embed_bwd_final(int F, int D, int fe, const float* __restrict__ S,
                                                            const float* __restrict__ W,
                                                            const float* __restrict__ bias,
                                                            const float* __restrict__ P,
                                                            float* __restrict__ dW, float* __restrict__ dbias,
                                                            float* __restrict__ dP) {
-  extern __shared__ float S[];   // [2][F][D]
-  for (int fd = threadIdx.x; fd < F * D; fd += blockDim.x) {
-    float s1 = 0.f, s0 = 0.f;
-    for (int c = 0; c < nchunk; ++c) {
-      s1 += part[((long)c * 2 + 0) * F * D + fd];
-      s0 += part[((long)c * 2 + 1) * F * D + fd];
-    }
-    S[fd] = s1;
-    S[F * D + fd] = s0;
-  }
-  __syncthreads();
   const float* S1 = S;
   const float* S0 = S + F * D;
-  for (int q = threadIdx.x; q < F * fe; q += blockDim.x) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q < F * fe) {
     const int f = q / fe, k = q % fe;
     float a = 0.f, c = 0.f;
     for (int d = 0; d < D; ++d) {
@@ -93,15 +93,15 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_final(int nchunk, int F, i
     }
     dW[q] = a;
     if (dbias) dbias[q] = c;
-  }
-  for (int q = threadIdx.x; q < D * fe; q += blockDim.x) {
-    const int d = q / fe, k = q % fe;
+  } else if (q < F * fe + D * fe) {
+    const int r = q - F * fe;
+    const int d = r / fe, k = r % fe;
     float a = 0.f;
     for (int f = 0; f < F; ++f) {
       a = fmaf(S1[f * D + d], W[f * fe + k], a);
       if (bias) a = fmaf(S0[f * D + d], bias[f * fe + k], a);
     }
-    dP[q] = a;
+    dP[r] = a;
   }
 }
 
@@ -342,24 +342,16 @@ extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, 
   return check_launch("feat_embed_fwd");
 }
 
-extern "C" size_t ctr_feat_embed_bwd_ws(int B, int F, int D) {
-  int nchunk = (B + 255) / 256;
-  return (size_t)nchunk * 2 * F * D * sizeof(float);
-}
+extern "C" size_t ctr_feat_embed_bwd_ws(int B, int F, int D) { return (size_t)2 * F * D * sizeof(float); }
 
 extern "C" int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, const float* bias, const float* P,
                                   int fe, int D, const float* dout, long dout_ld, float* dW, float* dbias,
                                   float* dP, float* ws, void* stream) {
   if (F == 0) return 0;
+  CTR_REQUIRE(D <= 256, "D > 256");
   hipStream_t s = (hipStream_t)stream;
-  const int rpc = 256;
-  const int nchunk = (B + rpc - 1) / rpc;
-  float* part = ws;
-  const size_t sm = (size_t)2 * F * D * sizeof(float);
-  CTR_REQUIRE(sm <= 64 * 1024, "feat_embed_bwd: 2*F*D exceeds 64 KB LDS");
-  dim3 g1(cdiv((long)F * D, 256), nchunk);
-  feat_embed_bwd_partial<<<g1, 256, 0, s>>>(x, B, F, D, dout, dout_ld, rpc, part);
-  feat_embed_bwd_final<<<1, 256, sm, s>>>(nchunk, F, D, fe, part, W, bias, P, dW, dbias, dP);
+  feat_embed_bwd_sums<<<F, 256, 0, s>>>(x, B, F, D, dout, dout_ld, ws);
+  feat_embed_bwd_final<<<cdiv((long)(F + D) * fe, 256), 256, 0, s>>>(F, D, fe, ws, W, bias, P, dW, dbias, dP);
   return check_launch("feat_embed_bwd");
 }
 

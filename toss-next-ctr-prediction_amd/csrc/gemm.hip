@@ -289,7 +289,15 @@ __global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
   const long MN = (long)g.M * g.N;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < MN; q += (long)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += g.ws[z * MN + q];
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {   // 8 independent loads in flight, summed in slab order
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = g.ws[(z + j) * MN + q];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += a[j];
+    }
+    for (; z < splits; ++z) s += g.ws[z * MN + q];
     const int m = (int)(q / g.N), n = (int)(q % g.N);
     g.C[(long)m * g.ldc + n] = epi_elem(g.epi, s, m, n, g.N, g.ldc);
   }

@@ -40,110 +40,107 @@ __device__ __forceinline__ void adam_ema_elem(const OptScalars& s, float& p, flo
   if (s.do_ema) e = e * s.ema_d + s.ema_omd * p;          // shadow.mul_(d).add_(p, alpha=1-d)
 }
 
+// For every sparse-segment chunk: [lo, hi) = index range of the sorted unique keys that fall in the
+// chunk's rows.  One thread per chunk (binary searches run in parallel, not as a serial prologue of
+// every streaming workgroup).
+__global__ __launch_bounds__(256) void chunk_key_range_kernel(const ctr_opt_chunk_t* __restrict__ chunks, int nchunks,
+                                                              const ctr_opt_seg_t* __restrict__ segs,
+                                                              uint32_t* __restrict__ range) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= nchunks) return;
+  const ctr_opt_chunk_t ch = chunks[c];
+  const ctr_opt_seg_t sg = segs[ch.seg];
+  uint32_t lo = 0, hi = 0;
+  if (sg.kind == 1) {
+    const uint32_t nu = *sg.n_uniq;
+    const uint32_t k0 = sg.key_base + (uint32_t)(ch.e0 / sg.width);
+    const uint32_t k1 = sg.key_base + (uint32_t)((min(ch.e1, sg.n) - 1) / sg.width);   // real rows only
+    uint32_t a = 0, b = nu;
+    while (a < b) { const uint32_t mid = (a + b) >> 1; if (sg.keys[mid] < k0) a = mid + 1; else b = mid; }
+    lo = a;
+    b = nu;
+    while (a < b) { const uint32_t mid = (a + b) >> 1; if (sg.keys[mid] <= k1) a = mid + 1; else b = mid; }
+    hi = a;
+  }
+  range[2 * c] = lo;
+  range[2 * c + 1] = hi;
+}
+
+__device__ __forceinline__ float row_grad(const ctr_opt_seg_t& sg, const int* map, int nrows, int rel, int width,
+                                          float coef) {
+  const int row = rel / width;
+  const int slot = row < nrows ? map[row] : -1;
+  return slot >= 0 ? sg.G[(long)slot * sg.g_ld + (rel - row * width)] * coef : 0.0f;
+}
+
+// Streams one OPT_CHUNK-element chunk of one segment per workgroup, one float4 of each of p, m, v,
+// ema per thread per iteration (registers only -- no address-taken arrays, so nothing spills to
+// scratch).  Segments are streamed in whole float4s: the tail float4 lies inside the param's
+// 64-element arena padding.  Sparse segments: the touched rows of the chunk are mapped into an LDS
+// slot table from the precomputed key range; untouched rows get grad 0 (dense AdamW semantics).
 __global__ __launch_bounds__(256) void adamw_ema_kernel(const ctr_opt_chunk_t* __restrict__ chunks,
                                                         const ctr_opt_seg_t* __restrict__ segs,
+                                                        const uint32_t* __restrict__ krange,
                                                         float* __restrict__ P, float* __restrict__ M,
                                                         float* __restrict__ V, float* __restrict__ E,
                                                         const float* __restrict__ dgrad,
                                                         const float* __restrict__ coef_ptr, OptScalars s) {
   __shared__ int map[OPT_MAXROWS];
-  __shared__ uint32_t lo_s;
   const ctr_opt_chunk_t ch = chunks[blockIdx.x];
   const ctr_opt_seg_t sg = segs[ch.seg];
   const float coef = coef_ptr ? *coef_ptr : 1.0f;
   const bool adam = s.do_adam && sg.kind != 2;
+  const bool sparse = adam && sg.kind == 1;
   const int tid = threadIdx.x;
-  long r0 = 0;
-  if (sg.kind == 1 && adam) {
-    r0 = ch.e0 / sg.width;
-    const long r1 = (ch.e1 - 1) / sg.width;
-    const int nrows = (int)(r1 - r0 + 1);
+  const int width = sg.width;
+  const long r0 = ch.e0 / width;
+  const int off0 = (int)(ch.e0 - r0 * width);     // chunk start inside its first row
+  int nrows = 0;
+  if (sparse) {
+    nrows = (int)((ch.e1 - 1) / width - r0 + 1);
     for (int i = tid; i < nrows; i += 256) map[i] = -1;
-    const uint32_t nu = *sg.n_uniq;
-    const uint32_t k0 = sg.key_base + (uint32_t)r0, k1 = sg.key_base + (uint32_t)r1;
-    if (tid == 0) {
-      uint32_t lo = 0, hi = nu;   // first index with key >= k0
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sg.keys[mid] < k0) lo = mid + 1;
-        else hi = mid;
-      }
-      lo_s = lo;
-    }
     __syncthreads();
-    for (uint32_t i = lo_s + tid; i < nu; i += 256) {
-      const uint32_t k = sg.keys[i];
-      if (k > k1) break;
-      map[k - k0] = (int)i;
-    }
+    const uint32_t lo = krange[2 * blockIdx.x], hi = krange[2 * blockIdx.x + 1];
+    const uint32_t k0 = sg.key_base + (uint32_t)r0;
+    for (uint32_t i = lo + tid; i < hi; i += 256) map[sg.keys[i] - k0] = (int)i;
     __syncthreads();
   }
-  float* p = P + sg.p_off;
-  float* m = M + sg.p_off;
-  float* v = V + sg.p_off;
-  float* e = E + sg.p_off;
-  for (long q = ch.e0 + (long)tid * 4; q < ch.e1; q += 1024) {
-    const int cnt = (int)min((long)4, ch.e1 - q);
-    float4 pv = {0, 0, 0, 0}, mv = {0, 0, 0, 0}, vv = {0, 0, 0, 0}, ev = {0, 0, 0, 0};
-    const bool full = cnt == 4;
-    if (full) {
-      pv = *(const float4*)(p + q);
-      if (adam) {
-        mv = *(const float4*)(m + q);
-        vv = *(const float4*)(v + q);
-      }
-      if (s.do_ema) ev = *(const float4*)(e + q);
-    } else {
-      float* pp = (float*)&pv;
-      float* mp = (float*)&mv;
-      float* vp = (float*)&vv;
-      float* ep = (float*)&ev;
-      for (int j = 0; j < cnt; ++j) {
-        pp[j] = p[q + j];
-        if (adam) {
-          mp[j] = m[q + j];
-          vp[j] = v[q + j];
-        }
-        if (s.do_ema) ep[j] = e[q + j];
-      }
-    }
-    float g[4] = {0.f, 0.f, 0.f, 0.f};
+  float* p = P + sg.p_off + ch.e0;
+  float* m = M + sg.p_off + ch.e0;
+  float* v = V + sg.p_off + ch.e0;
+  float* e = E + sg.p_off + ch.e0;
+  const float* gd = dgrad + sg.g_off + ch.e0;
+  const int n = (int)(ch.e1 - ch.e0);             // multiple of 4
+#pragma unroll 2
+  for (int lq = tid * 4; lq < n; lq += 1024) {
+    float4 pv = *(const float4*)(p + lq);
+    float4 mv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f}, ev = {0.f, 0.f, 0.f, 0.f};
+    float4 g = {0.f, 0.f, 0.f, 0.f};
     if (adam) {
+      mv = *(const float4*)(m + lq);
+      vv = *(const float4*)(v + lq);
       if (sg.kind == 0) {
-        const float* gp = dgrad + sg.g_off + q;
-        for (int j = 0; j < cnt; ++j) g[j] = gp[j] * coef;
+        g = *(const float4*)(gd + lq);
+        g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
       } else {
-        for (int j = 0; j < cnt; ++j) {
-          const long el = q + j;
-          const long row = el / sg.width;
-          const int slot = map[row - r0];
-          if (slot >= 0) g[j] = sg.G[(long)slot * sg.g_ld + (el - row * sg.width)] * coef;
-        }
+        const int rel = off0 + lq;
+        g.x = row_grad(sg, map, nrows, rel, width, coef);
+        g.y = row_grad(sg, map, nrows, rel + 1, width, coef);
+        g.z = row_grad(sg, map, nrows, rel + 2, width, coef);
+        g.w = row_grad(sg, map, nrows, rel + 3, width, coef);
       }
     }
-    float* pp = (float*)&pv;
-    float* mp = (float*)&mv;
-    float* vp = (float*)&vv;
-    float* ep = (float*)&ev;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) adam_ema_elem(s, pp[j], mp[j], vp[j], ep[j], g[j], adam);
-    if (full) {
-      if (adam) {
-        *(float4*)(p + q) = pv;
-        *(float4*)(m + q) = mv;
-        *(float4*)(v + q) = vv;
-      }
-      if (s.do_ema) *(float4*)(e + q) = ev;
-    } else {
-      for (int j = 0; j < cnt; ++j) {
-        if (adam) {
-          p[q + j] = pp[j];
-          m[q + j] = mp[j];
-          v[q + j] = vp[j];
-        }
-        if (s.do_ema) e[q + j] = ep[j];
-      }
+    if (s.do_ema) ev = *(const float4*)(e + lq);
+    adam_ema_elem(s, pv.x, mv.x, vv.x, ev.x, g.x, adam);
+    adam_ema_elem(s, pv.y, mv.y, vv.y, ev.y, g.y, adam);
+    adam_ema_elem(s, pv.z, mv.z, vv.z, ev.z, g.z, adam);
+    adam_ema_elem(s, pv.w, mv.w, vv.w, ev.w, g.w, adam);
+    if (adam) {
+      *(float4*)(p + lq) = pv;
+      *(float4*)(m + lq) = mv;
+      *(float4*)(v + lq) = vv;
     }
+    if (s.do_ema) *(float4*)(e + lq) = ev;
   }
 }
 
@@ -177,16 +174,18 @@ __global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __rest
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// grad_scale = 1/world under data parallelism: grads were summed across ranks, the reference
+// (DDP semantics) clips and steps on their mean.
 __global__ __launch_bounds__(256) void clip_finalize_kernel(const float* __restrict__ part, int nparts, float max_norm,
-                                                            float* __restrict__ out) {
+                                                            float grad_scale, float* __restrict__ out) {
   __shared__ float red[4];
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
   s = block_sum(s, red);
   if (threadIdx.x == 0) {
-    const float norm = sqrtf(s);
+    const float norm = sqrtf(s) * grad_scale;
     out[0] = norm;
-    out[1] = max_norm > 0.f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f;
+    out[1] = (max_norm > 0.f ? fminf(max_norm / (norm + 1e-6f), 1.0f) : 1.0f) * grad_scale;
   }
 }
 
@@ -196,10 +195,10 @@ using namespace ctr;
 
 extern "C" int ctr_opt_chunk_elems(void) { return OPT_CHUNK; }
 
-extern "C" int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, float* P, float* M,
-                             float* V, float* E, const float* dgrad, const float* coef, float lr, float wd,
-                             float beta1, float beta2, float eps, int step, float ema_decay, int do_adam, int do_ema,
-                             void* stream) {
+extern "C" int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, uint32_t* krange,
+                             float* P, float* M, float* V, float* E, const float* dgrad, const float* coef, float lr,
+                             float wd, float beta1, float beta2, float eps, int step, float ema_decay, int do_adam,
+                             int do_ema, void* stream) {
   if (nchunks == 0) return 0;
   OptScalars s;
   // host-side scalar math in double, exactly as torch/optim/adam.py computes it in Python floats
@@ -215,7 +214,9 @@ extern "C" int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const c
   s.ema_omd = (float)(1.0 - (double)ema_decay);
   s.do_adam = do_adam;
   s.do_ema = do_ema;
-  adamw_ema_kernel<<<nchunks, 256, 0, (hipStream_t)stream>>>(chunks, segs, P, M, V, E, dgrad, coef, s);
+  hipStream_t st = (hipStream_t)stream;
+  if (do_adam) chunk_key_range_kernel<<<cdiv(nchunks, 256), 256, 0, st>>>(chunks, nchunks, segs, krange);
+  adamw_ema_kernel<<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);
   return check_launch("adamw_ema");
 }
 
@@ -232,7 +233,8 @@ extern "C" int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint3
   return check_launch("sqnorm_rows");
 }
 
-extern "C" int ctr_clip_finalize(const float* part, int nparts, float max_norm, float* out, void* stream) {
-  clip_finalize_kernel<<<1, 256, 0, (hipStream_t)stream>>>(part, nparts, max_norm, out);
+extern "C" int ctr_clip_finalize(const float* part, int nparts, float max_norm, float grad_scale, float* out,
+                                 void* stream) {
+  clip_finalize_kernel<<<1, 256, 0, (hipStream_t)stream>>>(part, nparts, max_norm, grad_scale, out);
   return check_launch("clip_finalize");
 }

@@ -134,42 +134,48 @@ __global__ __launch_bounds__(256) void se_bwd_partial(const float* __restrict__ 
   }
 }
 
-// one workgroup: dgate -> dz2 -> dW2, db2, dg1 -> dz1 -> dW1, db1, dmean
-__global__ __launch_bounds__(256) void se_mlp_bwd(const float* __restrict__ part, int nparts, int C, int Cr,
-                                                  const float* __restrict__ mean, const float* __restrict__ g1,
-                                                  const float* __restrict__ gate, const float* __restrict__ W1,
-                                                  const float* __restrict__ W2, float* __restrict__ dW1,
-                                                  float* __restrict__ db1, float* __restrict__ dW2,
-                                                  float* __restrict__ db2, float* __restrict__ dmean) {
-  extern __shared__ float sz[];
-  float* dz2 = sz;             // [C]
-  float* dz1 = sz + C;         // [Cr]
+// one workgroup: dgate -> dz2 (sigmoid'), db2; dg1 = W2^T dz2 -> dz1 (relu'), db1.  dz2 / dz1 go to
+// the workspace for the grid-wide outer products below.
+__global__ __launch_bounds__(256) void se_mlp_bwd_vec(const float* __restrict__ part, int nparts, int C, int Cr,
+                                                      const float* __restrict__ g1, const float* __restrict__ gate,
+                                                      const float* __restrict__ W2, float* __restrict__ db1,
+                                                      float* __restrict__ db2, float* __restrict__ dz2g,
+                                                      float* __restrict__ dz1g) {
+  extern __shared__ float sz[];   // dz2 [C]
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float dg = 0.f;
     for (int p = 0; p < nparts; ++p) dg += part[(long)p * C + c];
     const float s = gate[c];
     const float v = dg * (s * (1.f - s));
-    dz2[c] = v;
+    sz[c] = v;
     db2[c] = v;
+    dz2g[c] = v;
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < C * Cr; q += blockDim.x) {
-    const int c = q / Cr, j = q % Cr;
-    dW2[q] = dz2[c] * g1[j];
-  }
   for (int j = threadIdx.x; j < Cr; j += blockDim.x) {
     float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(dz2[c], W2[(long)c * Cr + j], acc);
+    for (int c = 0; c < C; ++c) acc = fmaf(sz[c], W2[(long)c * Cr + j], acc);
     const float v = g1[j] > 0.f ? acc : 0.f;
-    dz1[j] = v;
     db1[j] = v;
+    dz1g[j] = v;
   }
-  __syncthreads();
-  for (int q = threadIdx.x; q < Cr * C; q += blockDim.x) {
-    const int j = q / C, c = q % C;
-    dW1[q] = dz1[j] * mean[c];
-  }
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+}
+
+// grid: dW2 = dz2 (x) g1, dW1 = dz1 (x) mean, dmean = W1^T dz1
+__global__ __launch_bounds__(256) void se_mlp_bwd_outer(int C, int Cr, const float* __restrict__ mean,
+                                                        const float* __restrict__ g1, const float* __restrict__ W1,
+                                                        const float* __restrict__ dz2, const float* __restrict__ dz1,
+                                                        float* __restrict__ dW1, float* __restrict__ dW2,
+                                                        float* __restrict__ dmean) {
+  const long q = blockIdx.x * 256L + threadIdx.x;
+  const long n2 = (long)C * Cr;
+  if (q < n2) {
+    dW2[q] = dz2[q / Cr] * g1[q % Cr];
+  } else if (q < 2 * n2) {
+    const long r = q - n2;
+    dW1[r] = dz1[r / C] * mean[r % C];
+  } else if (q < 2 * n2 + C) {
+    const int c = (int)(q - 2 * n2);
     float acc = 0.f;
     for (int j = 0; j < Cr; ++j) acc = fmaf(dz1[j], W1[(long)j * C + c], acc);
     dmean[c] = acc;
@@ -222,7 +228,7 @@ extern "C" int ctr_scale_drop(const float* x, int B, int C, const float* gate, u
   return check_launch("scale_drop");
 }
 
-extern "C" size_t ctr_se_bwd_ws(int B, int C) { return ((size_t)cdiv(B, 64) * C + C) * sizeof(float); }
+extern "C" size_t ctr_se_bwd_ws(int B, int C) { return ((size_t)cdiv(B, 64) * C + 3 * (size_t)C) * sizeof(float); }
 
 extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, int Cr, const float* gate,
                           const float* g1, const float* mean, const float* W1, const float* W2, uint32_t drop_key,
@@ -238,8 +244,10 @@ extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B
   se_bwd_partial<<<dim3(cdiv(C, 256), np), 256, 0, s>>>(dout, dout_ld, x, B, C, gate, d, rpb, dx,
                                                        gate ? part : nullptr);
   if (gate) {
-    se_mlp_bwd<<<1, 256, (C + Cr) * sizeof(float), s>>>(part, np, C, Cr, mean, g1, gate, W1, W2, dW1, db1, dW2, db2,
-                                                        dmean);
+    float* dz2 = dmean + C;                // [C]
+    float* dz1 = dz2 + C;                  // [Cr <= C]
+    se_mlp_bwd_vec<<<1, 256, C * sizeof(float), s>>>(part, np, C, Cr, g1, gate, W2, db1, db2, dz2, dz1);
+    se_mlp_bwd_outer<<<cdiv(2L * C * Cr + C, 256), 256, 0, s>>>(C, Cr, mean, g1, W1, dz2, dz1, dW1, dW2, dmean);
     long n = (long)B * C;
     int blocks = (int)std::min<long>((n + 255) / 256, 16384);
     add_row_bcast<<<blocks, 256, 0, s>>>(dx, B, C, dmean, (float)B);

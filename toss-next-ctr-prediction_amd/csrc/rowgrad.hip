@@ -23,7 +23,11 @@ __global__ void iota_kernel(uint32_t* v, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = (uint32_t)i;
 }
 
+// one wave per unique key, lane = column; members summed in (stable) contribution order.  The
+// INVALID group (pad tokens: dropped by padding_idx) is skipped -- it is by far the largest group
+// (every short history contributes pads to its top-K) and its sum is never read.
 __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ contrib, int ld, int width,
+                                                     const uint32_t* __restrict__ uniq_keys,
                                                      const uint32_t* __restrict__ sorted_idx,
                                                      const uint32_t* __restrict__ counts,
                                                      const uint32_t* __restrict__ offsets,
@@ -32,10 +36,25 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ c
   const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (u >= *n_uniq) return;
+  if (uniq_keys[u] == 0xFFFFFFFFu) {
+    if (lane < width) out[(long)u * width + lane] = 0.f;
+    return;
+  }
   const uint32_t off = offsets[u], cnt = counts[u];
   if (lane < width) {
     float acc = 0.f;
-    for (uint32_t i = 0; i < cnt; ++i) acc += contrib[(long)sorted_idx[off + i] * ld + lane];
+    uint32_t i = 0;
+    for (; i + 4 <= cnt; i += 4) {   // issue 4 independent row loads, add in order
+      const float a0 = contrib[(long)sorted_idx[off + i] * ld + lane];
+      const float a1 = contrib[(long)sorted_idx[off + i + 1] * ld + lane];
+      const float a2 = contrib[(long)sorted_idx[off + i + 2] * ld + lane];
+      const float a3 = contrib[(long)sorted_idx[off + i + 3] * ld + lane];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; i < cnt; ++i) acc += contrib[(long)sorted_idx[off + i] * ld + lane];
     out[(long)u * width + lane] = acc;
   }
 }
@@ -103,7 +122,8 @@ extern "C" int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, in
   tb = w.temp_bytes;
   e = rocprim::exclusive_scan(base, tb, (const uint32_t*)counts, offsets, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
   CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
-  segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib, ld, width, sidx, counts, offsets, n_uniq, uniq_grad);
+  segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib, ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
+                                           uniq_grad);
   return check_launch("rowgrad");
 }
 
@@ -130,4 +150,23 @@ extern "C" int ctr_scatter_rows(const uint32_t* keys, const float* G, const uint
   int blocks = std::min(cdiv((long)max_uniq * width, 256), 8192);
   scatter_rows_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(keys, G, n_uniq, width, ld, key_base, n_rows, out);
   return check_launch("scatter_rows");
+}
+
+namespace ctr {
+__global__ void mask_tail_keys_kernel(uint32_t* __restrict__ keys, int n, int world, const uint32_t* __restrict__ counts) {
+  const long total = (long)n * world;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / n);
+    if ((uint32_t)(i - (long)r * n) >= counts[r]) keys[i] = 0xFFFFFFFFu;
+  }
+}
+}  // namespace ctr
+
+// data parallel: after all-gathering every rank's compact (keys, rows) buffers (n slots each, the first
+// counts[r] valid), invalidate the unused slots so a second ctr_rowgrad merges them across ranks
+extern "C" int ctr_mask_tail_keys(uint32_t* keys, int n, int world, const uint32_t* counts, void* stream) {
+  if ((long)n * world == 0) return 0;
+  int blocks = std::min(cdiv((long)n * world, 256), 8192);
+  mask_tail_keys_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(keys, n, world, counts);
+  return check_launch("mask_tail_keys");
 }

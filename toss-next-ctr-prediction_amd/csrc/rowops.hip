@@ -111,23 +111,39 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_big(const float* __restrict__
 }
 
 // ---------------- column sums: out[n] = sum_m X[m, n] (two-level, fixed order) ----------------
+// block = (64-column tile) x (row chunk); 4 row groups of 64 lanes stride the chunk, combined in order
 __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ X, long ld, int M, int N,
                                                       int rows_per_block, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + tx;
   const int m0 = blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
-  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
-    float s = 0.f;
-    for (int m = m0; m < m1; ++m) s += X[(long)m * ld + n];
-    part[(long)blockIdx.y * N + n] = s;
+  float s = 0.f;
+  if (n < N) {
+    int m = m0 + ty;
+    for (; m + 12 < m1; m += 16) {
+      const float a0 = X[(long)m * ld + n], a1 = X[(long)(m + 4) * ld + n];
+      const float a2 = X[(long)(m + 8) * ld + n], a3 = X[(long)(m + 12) * ld + n];
+      s += a0;
+      s += a1;
+      s += a2;
+      s += a3;
+    }
+    for (; m < m1; m += 4) s += X[(long)m * ld + n];
   }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && n < N) part[(long)blockIdx.y * N + n] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
 }
 
-__global__ __launch_bounds__(256) void colsum_final(const float* __restrict__ part, int nparts, int N, float div,
-                                                    float* __restrict__ out) {
-  for (int n = blockIdx.x * 256 + threadIdx.x; n < N; n += gridDim.x * 256) {
-    float s = 0.f;
-    for (int p = 0; p < nparts; ++p) s += part[(long)p * N + n];
-    out[n] = div == 1.0f ? s : s / div;
-  }
+// one wave per column: lanes stride the partials, fixed xor-tree combine
+__global__ __launch_bounds__(64) void colsum_final(const float* __restrict__ part, int nparts, int N, float div,
+                                                   float* __restrict__ out) {
+  const int n = blockIdx.x;
+  float s = 0.f;
+  for (int p = threadIdx.x; p < nparts; p += 64) s += part[(long)p * N + n];
+  s = wave_sum(s);
+  if (threadIdx.x == 0) out[n] = div == 1.0f ? s : s / div;
 }
 
 // ---------------- loss: bce_wll_style(logits) + aux_w * bce_wll_style(aux) and d/dz ----------------
@@ -221,16 +237,17 @@ extern "C" int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long l
   return check_launch("rmsnorm_bwd");
 }
 
-extern "C" size_t ctr_colsum_ws_size(int M, int N) { return (size_t)cdiv(M, 256) * N * sizeof(float); }
+extern "C" size_t ctr_colsum_ws_size(int M, int N) { return (size_t)cdiv(M, 64) * N * sizeof(float); }
 
 // out[n] = (sum_m X[m, n]) / div   (div = 1 for plain sums, B for torch .mean(dim=0))
 extern "C" int ctr_colsum(const float* X, long ld, int M, int N, float div, float* out, float* ws, void* stream) {
   if (N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int rpb = 256;
+  const int ctiles = cdiv(N, 64);
+  const int rpb = std::min(4096, std::max(64, cdiv((long)M * ctiles, 1024)));   // ~1024 blocks
   const int np = M > 0 ? cdiv(M, rpb) : 0;
-  if (np > 0) colsum_partial<<<dim3(cdiv(N, 256), np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
-  colsum_final<<<cdiv(N, 256), 256, 0, s>>>(ws, np, N, div, out);
+  if (np > 0) colsum_partial<<<dim3(ctiles, np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
+  colsum_final<<<N, 64, 0, s>>>(ws, np, N, div, out);
   return check_launch("colsum");
 }
 
@@ -261,6 +278,30 @@ extern "C" int ctr_sigmoid(const float* x, int n, float* y, void* stream) {
   if (n == 0) return 0;
   sigmoid_kernel<<<std::min(cdiv(n, 256), 4096), 256, 0, (hipStream_t)stream>>>(x, n, y);
   return check_launch("sigmoid");
+}
+
+namespace ctr {
+// one wave per output row; rows are whole 4-byte words (f32 / i32 shard columns staged in HBM)
+__global__ __launch_bounds__(256) void gather_rows_kernel(const uint32_t* __restrict__ src, long row_words,
+                                                          const long* __restrict__ idx, int n,
+                                                          uint32_t* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  for (long r = blockIdx.x * 4L + (threadIdx.x >> 6); r < n; r += (long)gridDim.x * 4) {
+    const uint32_t* s = src + idx[r] * row_words;
+    uint32_t* d = dst + r * row_words;
+    for (long w = lane; w < row_words; w += 64) d[w] = s[w];
+  }
+}
+}  // namespace ctr
+
+// batch assembly from HBM-resident shards: dst[r] = src[idx[r]] (replaces ShardedDataset.__getitem__
+// + collate_sharded, src/data/dataset.py:77-80, 98-124, for device-staged data)
+extern "C" int ctr_gather_rows(const void* src, long row_words, const long* idx, int n, void* dst, void* stream) {
+  if (n == 0 || row_words == 0) return 0;
+  int blocks = std::min(cdiv(n, 4), 8192);
+  gather_rows_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>((const uint32_t*)src, row_words, idx, n,
+                                                              (uint32_t*)dst);
+  return check_launch("gather_rows");
 }
 
 // strided 2-D copy (feature concatenation for the fc head, src/models/wrapper.py:168-172)

@@ -70,13 +70,15 @@ SIGS = {
     "ctr_rowgrad_ws_size": (z, [i]),
     "ctr_rowgrad": (i, [p, p, i, i, i, i, p, p, p, p, z, p]),
     "ctr_opt_chunk_elems": (i, []),
-    "ctr_adamw_ema": (i, [p, i, p, p, p, p, p, p, p, f, f, f, f, f, i, f, i, i, p]),
+    "ctr_adamw_ema": (i, [p, i, p, p, p, p, p, p, p, p, f, f, f, f, f, i, f, i, i, p]),
     "ctr_norm_nparts_per_call": (i, []),
     "ctr_sqnorm_dense": (i, [p, l, p, p]),
     "ctr_sqnorm_rows": (i, [p, p, p, i, i, u, p, p]),
-    "ctr_clip_finalize": (i, [p, i, f, p, p]),
+    "ctr_clip_finalize": (i, [p, i, f, f, p, p]),
+    "ctr_mask_tail_keys": (i, [p, i, i, p, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
+    "ctr_gather_rows": (i, [p, l, p, i, p, p]),
     "ctr_scatter_rows": (i, [p, p, p, i, i, i, u, l, p, p]),
 }
 

@@ -163,11 +163,15 @@ class Engine:
 
     @staticmethod
     def wgrad_splits(M, N, K):
-        tiles = max(1, math.ceil(M / 128)) * max(1, math.ceil(N / 128))
-        return int(max(1, min(K // 256, math.ceil(1024 / tiles))))
+        """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows): ~512 workgroups,
+        each split >= 512 rows deep (tile shapes as in ctr_gemm's dispatch)."""
+        bn = 32 if N <= 32 else 64 if N <= 64 else 96 if N <= 96 else 128
+        bm = 64 if (M <= 64 and bn == 128) else 128
+        tiles = math.ceil(M / bm) * math.ceil(N / bn)
+        return int(max(1, min(K // 512, math.ceil(512 / tiles))))
 
     def colsum(self, X, ld, M, N, out, div=1.0):
-        w = self.splitk_ws(max(1, math.ceil(max(M, 1) / 256)) * N)
+        w = self.splitk_ws(_lib.query("ctr_colsum_ws_size", M, N) // 4 + 1)
         call("ctr_colsum", X, ld, M, N, float(div), out, ptr(w), self.s())
 
     def wgrad(self, dY, ldy, X, ldx, M_rows, n_out, n_in, dW, lddw=None, bias_grad=None):

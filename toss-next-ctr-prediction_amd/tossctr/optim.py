@@ -127,13 +127,21 @@ def build_ema(model, cfg):
 class FusedAdamW:
     """torch.optim.AdamW(model.parameters(), lr, weight_decay) + clip + EMA as one arena stream."""
 
-    def __init__(self, model, lr, weight_decay=1e-2, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=0.0, ema=None):
+    def __init__(self, model, lr, weight_decay=1e-2, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=0.0, ema=None,
+                 process_group=None):
         self.model = model
         self.arena = ar = model.arena
         self.engine = model.engine
         self.param_groups = [{"lr": float(lr), "weight_decay": float(weight_decay), "betas": betas, "eps": eps}]
         self.max_grad_norm = float(max_grad_norm)
         self.ema = ema
+        self.pg = process_group
+        self.world = 1
+        if process_group is not None:
+            import torch.distributed as dist
+            self.world = dist.get_world_size(process_group)
+        self._timing = False
+        self._events = []
         dev = ar.device
         self.m = torch.zeros(ar.total, dtype=torch.float32, device=dev)
         self.v = torch.zeros(ar.total, dtype=torch.float32, device=dev)
@@ -176,8 +184,9 @@ class FusedAdamW:
         CH = _lib.query("ctr_opt_chunk_elems")
         self._chunk_all, self._chunk_adam = [], []
         for si, sg in enumerate(segs):
-            for e0 in range(0, sg["n"], CH):
-                c = (si, e0, min(sg["n"], e0 + CH))
+            n4 = (sg["n"] + 3) // 4 * 4     # stream whole float4s; the tail sits in the 64-element padding
+            for e0 in range(0, n4, CH):
+                c = (si, e0, min(n4, e0 + CH))
                 self._chunk_all.append(c)
                 if sg["kind"] != 2:
                     self._chunk_adam.append(c)
@@ -188,6 +197,7 @@ class FusedAdamW:
                 arr[i].seg, arr[i].pad, arr[i].e0, arr[i].e1 = si, 0, e0, e1
             raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
             self._chunks_dev[name] = (torch.from_numpy(raw).to(self.arena.device), len(lst))
+        self.krange = torch.zeros(2 * max(1, len(self._chunk_all)), dtype=torch.int32, device=self.arena.device)
 
     def _segs_device(self, tg):
         segs = self._segments(tg)
@@ -215,12 +225,52 @@ class FusedAdamW:
             t = tg[name]
             call("ctr_sqnorm_rows", ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["width"], t["G"].shape[1],
                  INVALID_KEY, ptr(parts, (j + 1) * n), st)
-        call("ctr_clip_finalize", ptr(parts), 4 * n, self.max_grad_norm, ptr(self.norm_out), st)
+        call("ctr_clip_finalize", ptr(parts), 4 * n, self.max_grad_norm, 1.0 / self.world, ptr(self.norm_out), st)
         return self.norm_out
+
+    # -------------------------------------------------------------- data parallel
+    def exchange(self, tg):
+        """DDP semantics over RCCL: dense grads all-reduced (summed; the 1/world mean is folded into the
+        clip multiplier), each table's compact (keys, rows) all-gathered and re-deduplicated so every
+        rank applies the same global row grads (replicated tables stay bitwise identical)."""
+        import torch.distributed as dist
+        eng = self.engine
+        dist.all_reduce(self.arena.grad[:self.arena.n_dense_grad], group=self.pg)
+        out = {}
+        st = eng.s()
+        W = eng.ws(-1, -1)
+        for name in ("att", "rep", "cat"):
+            t = tg[name]
+            n, w = t["n"], t["width"]
+            keys = W.get(f"dp_{name}_keys", (self.world * n,), torch.int32)
+            rows = W.get(f"dp_{name}_rows", (self.world * n, w))
+            cnt = W.get(f"dp_{name}_cnt", (self.world,), torch.int32)
+            dist.all_gather_into_tensor(keys, t["keys"][:n], group=self.pg)
+            dist.all_gather_into_tensor(rows, t["G"][:n], group=self.pg)
+            dist.all_gather_into_tensor(cnt, t["n_uniq"], group=self.pg)
+            call("ctr_mask_tail_keys", ptr(keys), n, self.world, ptr(cnt), st)
+            bits = eng.seq_key_bits if name != "cat" else eng.cat_key_bits
+            out[name] = eng._rowgrad(W, f"dp_{name}", keys, rows, self.world * n, w, w, bits)
+        return out
+
+    def time_kernels(self, on):
+        """Bracket each fused-optimizer launch with HIP events on the stream it runs on."""
+        self._timing = bool(on)
+        if on:
+            self._events = []
+
+    def kernel_ms(self):
+        torch.cuda.synchronize()
+        if not self._events:
+            return float("nan")
+        return sum(a.elapsed_time(b) for a, b in self._events) / len(self._events)
 
     def step(self, tg=None, global_step=None):
         """clip (if max_grad_norm > 0) -> AdamW -> EMA (if bound and due at global_step)."""
         tg = tg if tg is not None else self.engine.tg
+        if self.pg is not None:
+            tg = self.exchange(tg)
+            self.engine.tg = tg
         g = self.param_groups[0]
         self.clip(tg)
         self.step_count += 1
@@ -232,10 +282,16 @@ class FusedAdamW:
         segs = self._segs_device(tg)
         chunks, n = self._chunks_dev["all" if do_ema else "adam"]
         b1, b2 = g["betas"]
-        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.arena.buf), ptr(self.m), ptr(self.v),
-             ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf), ptr(self.arena.grad),
-             ptr(self.norm_out, 1) if self.max_grad_norm > 0 else None, float(g["lr"]), float(g["weight_decay"]),
+        if self._timing:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
+             ptr(self.v), ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf), ptr(self.arena.grad),
+             ptr(self.norm_out, 1), float(g["lr"]), float(g["weight_decay"]),
              float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1, do_ema, self.engine.s())
+        if self._timing:
+            ev[1].record()
+            self._events.append(ev)
         if do_ema:
             self.ema.num_updates += 1
 
@@ -246,8 +302,8 @@ class FusedAdamW:
         segs = self._segs_device(None)
         chunks, n = self._chunks_dev["all"]
         g = self.param_groups[0]
-        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.arena.buf), ptr(self.m), ptr(self.v),
-             ptr(ema.shadow), ptr(self.arena.grad), None, float(g["lr"]), float(g["weight_decay"]), 0.9, 0.999,
+        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
+             ptr(self.v), ptr(ema.shadow), ptr(self.arena.grad), None, float(g["lr"]), float(g["weight_decay"]), 0.9, 0.999,
              1e-8, max(1, self.step_count), float(decay), 0, 1, self.engine.s())
         ema.num_updates += 1
 

@@ -1,7 +1,30 @@
-"""K-fold training loop -- drop-in for src/train.py (main / train_one_fold) on MI355X."""
+"""K-fold training loop -- drop-in for src/train.py (``main(cfg_path)``, ``train_one_fold``) on MI355X.
+
+Same control flow as the reference (src/train.py:92-366): StratifiedGroupKFold(max(5, n_splits)),
+fold-level resume (skip a fold whose ckpt exists), per-step lr = cosine_warmup_lr, the step
+forward -> bce_wll_style (+aux_w * aux) -> backward -> clip -> AdamW -> EMA, per-epoch validation with
+EMA weights, AP/WLL/Score, temperature calibration, early stopping, ``torch.save({"state", "score"})``.
+
+MI355X differences (same results, different mechanics):
+  * batches come from HBM-resident shards (data.DeviceShards) gathered by the fold's permuted index,
+    not DataLoader worker processes;
+  * the step is the fused device step (CTRModel.train_step + optim.FusedAdamW): no per-step host
+    sync -- the reference's ``float(loss.cpu())`` each step (src/train.py:202) becomes an on-device sum;
+  * ``best_state["model"]`` is a detached copy (the reference stores live references, so its "best"
+    checkpoint is really the last epoch's weights);
+  * optional data parallelism: run under torchrun, every rank takes its own stride of each epoch's
+    permutation; grads are synchronised by FusedAdamW (RCCL).
+"""
 from __future__ import annotations
 
+import argparse
+import copy
+import json
 import math
+import os
+
+import numpy as np
+import torch
 
 
 def cosine_warmup_lr(epoch, step, steps_per_epoch, base_lr, warmup_epochs=1, total_epochs=10):
@@ -13,3 +36,184 @@ def cosine_warmup_lr(epoch, step, steps_per_epoch, base_lr, warmup_epochs=1, tot
         return base_lr * (gstep + 1) / max(1, warmup_steps)
     progress = (gstep - warmup_steps) / max(1, total_steps - warmup_steps)
     return 0.5 * base_lr * (1.0 + math.cos(math.pi * progress))
+
+
+def set_seed(seed: int, deterministic: bool = True):
+    """src/utils/seed.py:3-17 (the HIP kernels are deterministic by construction)."""
+    import random
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+    if torch.cuda.is_available():
+        torch.cuda.manual_seed_all(seed)
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def _cardinals(cfg, cat_cols):
+    d = cfg["data"]
+    return {c: int(d["hash_buckets"].get(c, 1000003)) + int(d.get("hash_buckets_margin", 0)) for c in cat_cols}
+
+
+def _feature_dims(manifest_path):
+    with open(manifest_path) as f:
+        man = json.load(f)
+    first = man["shards"][0]
+    return (int(np.load(first["X_num"]["path"], mmap_mode="r").shape[1]),
+            int(np.load(first["X_mask"]["path"], mmap_mode="r").shape[1]))
+
+
+@torch.no_grad()
+def predict_logits(model, store, idx_np, bs):
+    """Eval-mode forward over rows idx (src/train.py:211-225); returns logits (numpy)."""
+    from .engine import ptr  # noqa: F401  (import keeps the HIP library resident)
+    model.eval()
+    dev = store.device
+    out = []
+    idx_all = torch.from_numpy(np.asarray(idx_np, dtype=np.int64)).to(dev)
+    for s in range(0, idx_all.numel(), bs):
+        inputs, _ = store.batch(idx_all[s:s + bs], slot=1)
+        logits, _, _, _ = model.engine.forward(*inputs, training=False, seed=0, save=False)
+        out.append(logits.clone())
+    return torch.cat(out).cpu().numpy() if out else np.zeros(0, np.float32)
+
+
+def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None, device=None):
+    """src/train.py:92-317 (same signature + optional pre-staged ``store``). Returns (best_state, best_score)."""
+    from .configs import cat_cardinals  # noqa: F401
+    from .data import DeviceShards
+    from .metrics import Calibrator, final_score
+    from .optim import FusedAdamW, build_ema
+    from .wrapper import CTRModel
+    dist = _dist()
+    world = dist.get_world_size() if dist else 1
+    rank = dist.get_rank() if dist else 0
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    bs, epochs, warmup = cfg["train"]["batch_size"], cfg["train"]["epochs"], cfg["train"]["warmup_epochs"]
+    cat_cols = cfg["data"]["cat_cols"]
+    store = store or DeviceShards(manifest_path, device)
+    seq_vocab = int(cfg.get("seq_vocab", 10_000_000))              # src/train.py:116
+    cards = _cardinals(cfg, cat_cols)
+    n_num, n_mask = _feature_dims(manifest_path)
+    model = CTRModel(cfg, seq_vocab, n_num, n_mask, cards, cat_cols, device=device)
+    model.reset_parameters(torch.Generator(device=device).manual_seed(int(cfg.get("seed", 777)) + fold))
+    ema = build_ema(model, cfg)
+    opt = FusedAdamW(model, lr=cfg["train"]["lr"], weight_decay=cfg["train"]["weight_decay"],
+                     max_grad_norm=cfg["train"].get("grad_clip_norm", 0.0), ema=ema,
+                     process_group=dist.group.WORLD if dist else None)
+    y_host = store.t["y"].view(-1).cpu().numpy()
+    idx_tr = np.asarray(idx_tr, dtype=np.int64)
+    steps_per_epoch = math.ceil(len(idx_tr) / (bs * world))
+    gen = torch.Generator(device=device).manual_seed(int(cfg.get("seed", 777)) * 1000 + fold)
+    idx_tr_dev = torch.from_numpy(idx_tr).to(device)
+    global_step, best_score, best_state, wait = 0, -1e9, None, 0
+    for epoch in range(1, epochs + 1):
+        model.train()
+        perm = idx_tr_dev[torch.randperm(len(idx_tr), generator=gen, device=device)]
+        loss_sum = torch.zeros((), device=device)
+        for step in range(steps_per_epoch):
+            global_step += 1
+            lo = (step * world + rank) * bs
+            idx = perm[lo:lo + bs]
+            if idx.numel() == 0:
+                idx = perm[:bs]
+            inputs, y = store.batch(idx)
+            opt.param_groups[0]["lr"] = cosine_warmup_lr(epoch - 1, step, steps_per_epoch, cfg["train"]["lr"], warmup,
+                                                         epochs)
+            loss_sum += model.train_step(inputs, y, opt, global_step=global_step)[0]
+        tr_loss = float(loss_sum.item()) / max(1, steps_per_epoch)
+        use_ema_eval = ema is not None and cfg["ema"].get("eval_with_ema", True)
+        if use_ema_eval:
+            ema.store(model)
+            ema.copy_to(model)
+        z_raw = predict_logits(model, store, idx_va, bs)
+        y_true = y_host[np.asarray(idx_va, dtype=np.int64)].astype(np.int64)
+        p_raw = 1.0 / (1.0 + np.exp(-z_raw.astype(np.float64)))
+        ap, wll, score = final_score(y_true, p_raw)
+        cal, score_cal = None, None
+        if cfg.get("calibration", {}).get("enabled", False):
+            cc = cfg["calibration"]
+            cal = Calibrator(method=cc.get("method", "temperature"), lr=float(cc.get("lr", 0.05)),
+                             iters=int(cc.get("iters", 200))).fit(z_raw, y_true)
+            ap_cal, wll_cal, score_cal = final_score(y_true, cal.predict_proba(z_raw))
+        if rank == 0:
+            K, tau = cfg["sequence"]["top_k"], cfg["sequence"]["recency_tau"]
+            lr = opt.param_groups[0]["lr"]
+            logger.row(fold=fold, epoch=epoch, split="val", loss=round(tr_loss, 6), AP=round(ap, 6),
+                       WLL=round(wll, 6), Score=round(score, 6), lr=lr, bs=bs, K=K, tau=tau)
+            logger.csv(fold=fold, epoch=epoch, split="val", loss=tr_loss, AP=ap, WLL=wll, Score=score, lr=lr, bs=bs,
+                       K=K, tau=tau)
+            logger.scalars(f"fold{fold}", epoch, train_loss=tr_loss, val_AP=ap, val_WLL=wll, val_Score=score)
+            if score_cal is not None:
+                logger.row(fold=fold, epoch=epoch, split="val_cal", loss="--", AP=round(ap_cal, 6),
+                           WLL=round(wll_cal, 6), Score=round(score_cal, 6), lr=lr, bs=bs, K=K, tau=tau)
+        if use_ema_eval:
+            ema.restore(model)
+        cur = score_cal if score_cal is not None else score
+        if cur > best_score:
+            best_score = cur
+            best_state = {"model": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
+                          "cfg": cfg, "best_score": best_score, "epoch": epoch,
+                          "calibrator": ({"method": cal.method, "temperature": cal.temperature} if cal else None),
+                          "ema": (ema.state_dict() if ema is not None else None), "global_step": global_step}
+            wait = 0
+        else:
+            wait += 1
+            if wait >= cfg["train"]["early_stop_patience"]:
+                break
+    del model, opt, ema
+    torch.cuda.empty_cache()
+    return best_state, best_score
+
+
+def main(cfg_path_or_dict):
+    """src/train.py:319-352."""
+    from sklearn.model_selection import StratifiedGroupKFold
+    from .data import DeviceShards, load_labels_groups_for_split
+    from .metrics import Logger
+    if isinstance(cfg_path_or_dict, dict):
+        cfg = copy.deepcopy(cfg_path_or_dict)
+    else:
+        import yaml
+        with open(cfg_path_or_dict) as f:
+            cfg = yaml.safe_load(f)
+    os.makedirs(cfg["logging"]["log_dir"], exist_ok=True)
+    set_seed(cfg["seed"], deterministic=cfg.get("deterministic", True))
+    dist = _dist()
+    rank = dist.get_rank() if dist else 0
+    device = torch.device("cuda", torch.cuda.current_device())
+    out_dir = os.path.join(cfg["logging"]["log_dir"], cfg["exp_name"])
+    logger = Logger(out_dir, tb=cfg["logging"].get("tb", False), csv_log=cfg["logging"].get("csv_log", True),
+                    quiet=rank != 0)
+    manifest_path = cfg["data"]["manifest_train"]
+    y, groups = load_labels_groups_for_split(manifest_path)
+    n_splits = int(cfg["cv"]["n_splits"])
+    sgkf = StratifiedGroupKFold(n_splits=max(5, n_splits), shuffle=True, random_state=cfg["seed"])
+    store = DeviceShards(manifest_path, device)
+    results = {}
+    for fold, (tr, va) in enumerate(sgkf.split(np.zeros_like(y), y, groups)):
+        if n_splits == 1 and fold > 0:
+            break
+        ckpt = os.path.join(out_dir, f"ckpt_folds_{fold}.pt")
+        if os.path.exists(ckpt):
+            continue
+        state, score = train_one_fold(cfg, fold, tr, va, manifest_path, logger, store=store, device=device)
+        if rank == 0:
+            os.makedirs(out_dir, exist_ok=True)
+            torch.save({"state": state, "score": score}, ckpt)
+        results[fold] = score
+    return results
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", required=True)
+    args = ap.parse_args()
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as _d
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        _d.init_process_group("nccl")
+    main(args.cfg)
