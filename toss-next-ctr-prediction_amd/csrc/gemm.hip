@@ -58,7 +58,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int SC = BN + 4;
   constexpr int LDS_K = 2 * BK * (SA + SB);
-  constexpr int LDS_E = BM * SC;
+  // only the fused residual+RMSNorm epilogue (BN <= 64 tiles) stages the tile through LDS; every other
+  // epilogue runs straight from the accumulator registers (keeps big tiles at 4 workgroups / CU)
+  constexpr int LDS_E = BN <= 64 ? BM * SC : 0;
   constexpr int LDS = LDS_K > LDS_E ? LDS_K : LDS_E;
   __shared__ __attribute__((aligned(16))) float smem[LDS];
   float* As = smem;
@@ -212,7 +214,40 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
 
-  // ---- stage the accumulator tile through LDS: Cs[i][j], row stride SC ----
+  const ctr_gemm_epi_t& e = g.epi;
+  // accumulator (i, j, r) of this lane holds C[m0 + wm + 16i + 4(lane>>4) + r][n0 + wn + 16j + (lane&15)]
+  const int lrow = wm + (lane >> 4) * 4, lcol = wn + (lane & 15);
+  if (gridDim.z > 1) {  // split-K partial: raw slab, epilogue happens in the reduce kernel
+    float* slab = g.ws + (long)blockIdx.z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + lcol + j * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + lrow + i * 16 + r;
+          if (m < g.M && n < g.N) slab[(long)m * g.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  if constexpr (LDS_E == 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + lcol + j * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + lrow + i * 16 + r;
+          if (m < g.M && n < g.N) g.C[(long)m * g.ldc + n] = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
+        }
+      }
+    return;
+  } else {
+  // ---- fused-norm tiles: stage the accumulator tile through LDS (Cs[i][j], row stride SC) so each
+  // row is visible to one thread group ----
   float* Cs = smem;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -223,15 +258,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         Cs[(wm + i * 16 + (lane >> 4) * 4 + r) * SC + wn + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
 
-  const ctr_gemm_epi_t& e = g.epi;
-  if (gridDim.z > 1) {  // split-K partial: raw slab, epilogue happens in the reduce kernel
-    float* slab = g.ws + (long)blockIdx.z * g.M * g.N;
-    for (int q = tid; q < BM * BN; q += 256) {
-      const int i = q / BN, j = q % BN, m = m0 + i, n = n0 + j;
-      if (m < g.M && n < g.N) slab[(long)m * g.N + n] = Cs[i * SC + j];
-    }
-    return;
-  }
   if (e.norm_w) {  // full row in this tile (host guarantees N <= BN, gridDim.y == 1)
     constexpr int TPR = BN / 4;          // threads per row
     constexpr int RPP = 256 / TPR;       // rows per pass
@@ -282,6 +308,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       for (int j = 0; j < 4; ++j)
         if (n + j < g.N) p[j] = v[j];
     }
+  }
   }
 }
 

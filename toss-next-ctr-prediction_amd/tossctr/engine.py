@@ -154,8 +154,19 @@ class Engine:
             self._splitk = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=self.device)
         return self._splitk
 
+    @staticmethod
+    def _tiles(M, N):
+        bn = 32 if N <= 32 else 64 if N <= 64 else 96 if N <= 96 else 128
+        bm = 64 if (M <= 64 and bn == 128) else 128
+        return math.ceil(M / bm) * math.ceil(N / bn)
+
     def gemm(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, splits=1):
-        """C = op(A) op(B) (+ epilogue); A/B/C are raw pointers."""
+        """C = op(A) op(B) (+ epilogue); A/B/C are raw pointers.  A grid too small to fill the 256 CUs
+        with a deep K (e.g. the QNN MLP's first layer, 32x4 tiles over K = 6400) is split along K."""
+        if splits == 1 and K >= 1024 and not (epi is not None and epi.norm_w):
+            tiles = self._tiles(M, N)
+            if tiles < 192:
+                splits = int(max(1, min(math.ceil(384 / tiles), K // 512)))
         wsp = None
         if splits > 1:
             wsp = ptr(self.splitk_ws(splits * M * N))
@@ -165,10 +176,7 @@ class Engine:
     def wgrad_splits(M, N, K):
         """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows): ~512 workgroups,
         each split >= 512 rows deep (tile shapes as in ctr_gemm's dispatch)."""
-        bn = 32 if N <= 32 else 64 if N <= 64 else 96 if N <= 96 else 128
-        bm = 64 if (M <= 64 and bn == 128) else 128
-        tiles = math.ceil(M / bm) * math.ceil(N / bn)
-        return int(max(1, min(K // 512, math.ceil(512 / tiles))))
+        return int(max(1, min(K // 512, math.ceil(512 / Engine._tiles(M, N)))))
 
     def colsum(self, X, ld, M, N, out, div=1.0):
         w = self.splitk_ws(_lib.query("ctr_colsum_ws_size", M, N) // 4 + 1)

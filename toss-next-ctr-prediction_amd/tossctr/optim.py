@@ -233,9 +233,9 @@ class FusedAdamW:
         """DDP semantics over RCCL: dense grads all-reduced (summed; the 1/world mean is folded into the
         clip multiplier), each table's compact (keys, rows) all-gathered and re-deduplicated so every
         rank applies the same global row grads (replicated tables stay bitwise identical)."""
-        import torch.distributed as dist
+        from . import dist as D
         eng = self.engine
-        dist.all_reduce(self.arena.grad[:self.arena.n_dense_grad], group=self.pg)
+        D.allreduce_sum_(self.arena.grad[:self.arena.n_dense_grad], self.pg)
         out = {}
         st = eng.s()
         W = eng.ws(-1, -1)
@@ -245,9 +245,7 @@ class FusedAdamW:
             keys = W.get(f"dp_{name}_keys", (self.world * n,), torch.int32)
             rows = W.get(f"dp_{name}_rows", (self.world * n, w))
             cnt = W.get(f"dp_{name}_cnt", (self.world,), torch.int32)
-            dist.all_gather_into_tensor(keys, t["keys"][:n], group=self.pg)
-            dist.all_gather_into_tensor(rows, t["G"][:n], group=self.pg)
-            dist.all_gather_into_tensor(cnt, t["n_uniq"], group=self.pg)
+            D.gather_compact(t["keys"][:n], t["G"][:n], t["n_uniq"], keys, rows, cnt, self.pg)
             call("ctr_mask_tail_keys", ptr(keys), n, self.world, ptr(cnt), st)
             bits = eng.seq_key_bits if name != "cat" else eng.cat_key_bits
             out[name] = eng._rowgrad(W, f"dp_{name}", keys, rows, self.world * n, w, w, bits)
