@@ -128,6 +128,24 @@ int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K
                  const float* lrow, float* dqkv, float* drel_part, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Fused position-wise FFN + residual + RMSNorm of DAREEncoderLayer, src/models/dare.py:53-70
+ * (ffn = Linear(D,FF) -> GELU -> Dropout -> Linear(FF,D); x2 = norm2(x1 + ffn(x1)))       (ffn.hip)
+ * The FF-wide activations never reach HBM: the backward recomputes them from x1.
+ * ------------------------------------------------------------------------------------------- */
+int ctr_ffn_supported(int D, int FF);          /* D in {16, 32, 64}, FF % 16 == 0 */
+int ctr_ffn_slab_rows(int M, int D);           /* workgroups of ctr_ffn_bwd = rows of its grad slab */
+/* y = norm_w * h * r, h = x + (gelu(x W1^T + b1) [dropout] W2^T + b2), r = 1/rms(h)               */
+int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
+                const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
+                float drop_scale, float* y, float* h, float* r, void* stream);
+/* dh = grad wrt h (after ctr_rmsnorm_bwd).  dx = dh + (dact W1); per-workgroup weight-grad slab rows
+ * (ld_slab floats): dW1 (FF, D) at 0, db1 (FF) at o_b1, dW2 (D, FF) at o_w2 -- colsum them (the
+ * offsets may match the arena layout so one ctr_colsum lands in the grad buffer).  db2 = colsum(dh). */
+int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
+                const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* dx, float* slab,
+                long ld_slab, int o_b1, int o_w2, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Row / column ops                                                                (rowops.hip)
  * ------------------------------------------------------------------------------------------- */
 /* RMSNorm.forward for long rows (QNN pre_norm, src/models/qnn_alpha.py:110-113) */
@@ -210,6 +228,41 @@ int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq
 int ctr_clip_finalize(const float* part, int nparts, float max_norm, float grad_scale, float* out, void* stream);
 /* data parallel: invalidate slots >= counts[r] of each rank's block of n gathered keys */
 int ctr_mask_tail_keys(uint32_t* keys, int n, int world, const uint32_t* counts, void* stream);
+
+/* ---- exact lazy AdamW/EMA for embedding tables (replaces the table part of the dense
+ * torch.optim.AdamW.step + ModelEMA.update, src/train.py:195-199, src/utils/ema.py:92-131).
+ * Every optimizer tick is recorded in a device history (one 48-byte entry of scalars per tick); each
+ * table row remembers the last tick applied to it (last[row]).  A row is brought current -- the
+ * skipped ticks replayed with grad 0, bit-identical to the dense stream -- when it is read (forward:
+ * ctr_lazy_touch), when it receives a gradient (ctr_lazy_update: replay, then the tick with its grad),
+ * or at ctr_lazy_flush (before parameters / moments / EMA are read as a whole).  Untouched rows cost
+ * nothing per step, instead of 32 B/element of HBM traffic.                                         */
+typedef struct {
+  int64_t p_off;     /* arena offset (floats) of the table                                      */
+  int64_t rows;      /* rows of the table                                                       */
+  int32_t width;     /* row width (floats), 1..64                                               */
+  uint32_t key_base; /* first key of this table in its group's compact key space (update only) */
+  int32_t* last;     /* per-row last applied tick                                               */
+} ctr_lazy_tab_t;
+
+int ctr_opt_hist_entry_bytes(void);
+/* hist[tick] = the scalars of one AdamW(+EMA) tick (same arguments as ctr_adamw_ema)              */
+int ctr_opt_hist_record(void* hist, int tick, float lr, float wd, float beta1, float beta2, float eps, int step,
+                        float ema_decay, int do_adam, int do_ema, void* stream);
+/* bring the rows read by a batch up to tick: X (nx, ncols) int32 row ids; per_column != 0: column c
+ * indexes tabs[c] (ntabs == ncols); else every id is a row of each of the ntabs tables.  E may be NULL
+ * (no EMA).                                                                                         */
+int ctr_lazy_touch(const ctr_lazy_tab_t* tabs, int ntabs, const int32_t* X, long nx, int ncols, int per_column,
+                   float* P, float* M, float* V, float* E, const void* hist, int tick, void* stream);
+/* apply tick to the rows of one compact grad group (sorted unique keys, rows G with leading dim g_ld,
+ * *n_uniq valid of at most cap; INVALID keys skipped), replaying each row's skipped ticks first;
+ * grads are scaled by *coef (clip multiplier).  tabs sorted by key_base.                           */
+int ctr_lazy_update(const ctr_lazy_tab_t* tabs, int ntabs, const uint32_t* keys, const float* G, int g_ld,
+                    const uint32_t* n_uniq, long cap, const float* coef, float* P, float* M, float* V, float* E,
+                    const void* hist, int tick, void* stream);
+/* bring every row of every table up to tick; max_rows = max over tabs of rows                      */
+int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_rows, float* P, float* M, float* V, float* E,
+                   const void* hist, int tick, void* stream);
 
 
 /* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */

@@ -235,3 +235,52 @@ def test_fused_adamw_matches_torch():
     # a few ulp: the kernel's fused multiply-adds vs torch's separately rounded CPU ops
     assert torch.allclose(P.cpu(), p_t.detach(), rtol=1e-6, atol=1e-6)
     assert torch.allclose(E.cpu(), shadow_ref, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,D,FF,p", [(300, 32, 384, 0.1), (1000, 16, 48, 0.1), (130, 64, 384, 0.15),
+                                      (4097, 32, 384, 0.0), (64, 32, 16, 0.5)])
+def test_fused_ffn_vs_torch(M, D, FF, p):
+    """ffn.hip: Linear -> GELU -> Dropout -> Linear -> +x -> RMSNorm forward, and its backward
+    (dx incl. the residual, per-workgroup [dW1 | db1 | dW2] slabs reduced by ctr_colsum) vs autograd."""
+    from oracle.rng import keep_mask
+    from tossctr.rng import drop_args
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M + D + FF)
+    x = torch.randn(M, D, device="cuda", generator=g)
+    W1 = torch.randn(FF, D, device="cuda", generator=g) / math.sqrt(D)
+    b1 = torch.randn(FF, device="cuda", generator=g) * 0.1
+    W2 = torch.randn(D, FF, device="cuda", generator=g) / math.sqrt(FF)
+    b2 = torch.randn(D, device="cuda", generator=g) * 0.1
+    nw = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    seed, site = (5 << 32) | 9, 4
+    key, thresh, scale = drop_args(seed, site, p, True)
+    y, h, r = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
+    L.call("ctr_ffn_fwd", ptr(x), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(nw), 1e-6, key, thresh, scale,
+           ptr(y), ptr(h), ptr(r), stream())
+    mask = torch.from_numpy(keep_mask(seed, site, p, (M, FF)).astype(np.float32)).cuda() if p > 0 else \
+        torch.ones(M, FF, device="cuda")
+    xr, W1r, b1r, W2r = (t.detach().double().requires_grad_() for t in (x, W1, b1, W2))
+    pre = xr @ W1r.t() + b1r
+    fo = torch.nn.functional.gelu(pre) * mask.double() * float(np.float32(scale if p > 0 else 1.0))
+    hr = xr + (fo @ W2r.t() + b2.double())
+    rr = 1.0 / torch.sqrt((hr * hr).mean(1) + 1e-6)
+    assert rel(h.double(), hr) < 1e-5
+    assert rel(r.double(), rr) < 1e-5
+    assert rel(y.double(), nw.double() * hr * rr[:, None]) < 1e-5
+    # backward from a random grad wrt h
+    dh = torch.randn(M, D, device="cuda", generator=g)
+    hr.backward(dh.double())
+    dx = torch.empty(M, D, device="cuda")
+    nb = L.query("ctr_ffn_slab_rows", M, D)
+    o_b1 = FF * D
+    o_w2 = o_b1 + (FF + 63) // 64 * 64
+    ld = o_w2 + D * FF
+    slab = torch.zeros(nb, ld, device="cuda")
+    L.call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(dx), ptr(slab),
+           ld, o_b1, o_w2, stream())
+    red = slab.double().sum(0)
+    assert rel(dx.double(), xr.grad) < 1e-5
+    assert rel(red[:FF * D].view(FF, D), W1r.grad) < 1e-5
+    assert rel(red[o_b1:o_b1 + FF], b1r.grad) < 1e-5
+    assert rel(red[o_w2:o_w2 + D * FF].view(D, FF), W2r.grad) < 1e-5
+    assert float(red[o_b1 + FF:o_w2].abs().max()) == 0.0 if o_w2 > o_b1 + FF else True

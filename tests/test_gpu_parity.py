@@ -55,15 +55,17 @@ def test_autograd_path_step0_matches_reference(case):
             fx.check(f"grad0/{k}", prm.grad, RTOL, 1e-7)
 
 
+@pytest.mark.parametrize("lazy", [True, False], ids=["lazy", "dense"])
 @pytest.mark.parametrize("case", CASES)
-def test_fused_train_steps_match_reference(case):
-    """The fused path (compact table grads + clip/AdamW/EMA stream) over all fixture steps."""
+def test_fused_train_steps_match_reference(case, lazy):
+    """The fused path (compact table grads + clip/AdamW/EMA; tables lazy or in the dense stream) over
+    all fixture steps."""
     from tossctr import FusedAdamW, build_ema
     fx = Fixture(case)
     m, tr = fx.meta, fx.meta["train"]
     model = build(fx)
     ema = build_ema(model, m["cfg"])
-    opt = FusedAdamW(model, lr=tr["lr"], weight_decay=tr["wd"], max_grad_norm=tr["clip"], ema=ema)
+    opt = FusedAdamW(model, lr=tr["lr"], weight_decay=tr["wd"], max_grad_norm=tr["clip"], ema=ema, lazy=lazy)
     for t in range(m["steps"]):
         b = fx.batch(t)
         opt.param_groups[0]["lr"] = m["lrs"][t]
@@ -113,6 +115,7 @@ def test_fused_step_is_deterministic():
         b = fx.batch(0)
         model.train_step(model.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda(), opt, 1,
                          seed=m["seeds"][0])
+        model.sync()
         outs.append(model.arena.buf.clone())
     assert torch.equal(outs[0], outs[1])
 

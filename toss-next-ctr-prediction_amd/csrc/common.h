@@ -109,6 +109,6 @@ __device__ __forceinline__ float softplus_f(float x) {  // torch F.softplus(beta
 
 __device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace ctr

@@ -1,0 +1,358 @@
+// Fused position-wise FFN of the DARE encoder layer (src/models/dare.py:53-70, the ffn Sequential
+// Linear(D, FF) -> GELU -> Dropout -> Linear(FF, D), then residual + RMSNorm), forward and backward.
+//
+// Unfused, each layer writes and re-reads two M x FF fp32 activations (pre-GELU and post-dropout:
+// 2 x 377 MB at M = 245,760, FF = 384) and the backward writes/reads a third (dact) -- ~2.3 GB of HBM
+// traffic per layer.  Here a workgroup owns RT rows, each wave RW = RT/4 of them, and all four waves
+// walk FF in lock-step 16-column chunks; the FF-wide values live only in registers (plus a 16-column
+// wave-private LDS tile).  The backward recomputes pre = x1 W1^T + b1 and the dropout mask
+// (counter-based hash, common.h) instead of reading them.
+//
+// All products are v_mfma_f32_16x16x4_f32 (exact fp32).  Operand layouts (lane l, g = l>>4, c = l&15):
+//   A[i][k] -> lane holds A[c][g],  B[k][j] -> lane holds B[g][c],  C[i][j] -> reg r holds C[4g+r][c].
+// A contraction may visit its k index in any order, which removes transposes:
+//   * D-contractions (x1 W1^T, dh W2) give lane group g the k range [g*D/4, (g+1)*D/4), so each lane
+//     reads its A row segment with ds_read_b128 and its B row segment with 16-byte global loads;
+//   * row-contractions (dW1, dW2) use the C-layout register r of a 16-row block directly as the A / B
+//     operand whose k-set is the rows {4g + r}.
+// Only the FF-contractions (fo W2^T forward, dact W1 backward) stage the chunk through LDS.
+// Weight / bias grads: per chunk the four waves' partials are summed in a fixed order and written to
+// the workgroup's slab; ctr_colsum (rowops.hip) reduces the slabs in a fixed order -- deterministic.
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct FfnArgs {
+  int M, FF;
+  const float* x;      // (M, D) layer input x1 (post-norm1)
+  const float* W1;     // (FF, D)
+  const float* b1;     // (FF)
+  const float* W2;     // (D, FF)
+  const float* b2;     // (D)
+  const float* nw;     // (D) norm2 weight
+  float eps;
+  Drop drop;
+  // forward outputs
+  float* y;            // (M, D) = norm2(x + ffn(x))
+  float* h;            // (M, D) pre-norm sum (saved for the norm backward)
+  float* r;            // (M) 1/rms
+  // backward
+  const float* dh;     // (M, D) grad wrt the pre-norm sum (from ctr_rmsnorm_bwd)
+  float* dx;           // (M, D) grad wrt x1 (ffn path + residual)
+  float* slab;         // (gridDim.x, ld_slab): [dW1 at 0 | db1 at o_b1 | dW2 at o_w2] per workgroup
+  long ld_slab;
+  int o_b1, o_w2;
+};
+
+template <int D>
+struct FfnTile {
+  static constexpr int RT = D >= 64 ? 64 : 128;   // rows per workgroup
+  static constexpr int RW = RT / 4;               // rows per wave
+  static constexpr int NI = RW / 16;              // 16-row blocks per wave
+  static constexpr int NJ = D / 16;               // 16-col blocks of D
+  static constexpr int KQ = D / 4;                // k-steps of a D-contraction
+  static constexpr int S = D + 4;                 // LDS row stride of x / dh tiles (16 B aligned)
+  static constexpr int SS = 20;                   // staging row stride (16 cols + pad)
+  static constexpr int TILE = RT * S;             // floats of one x / dh tile
+  static constexpr int STG = RW * SS;             // one wave's staging tile
+  static constexpr int PW = 32 * D + 16;          // one wave's per-chunk weight-grad partial
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// rows [m0, m0+RT) of a (M, D) matrix -> LDS tile with stride S (zero rows past M)
+template <int D>
+__device__ __forceinline__ void load_tile(const float* __restrict__ src, int M, int m0, float* dst) {
+  using T = FfnTile<D>;
+  for (int q = threadIdx.x; q < T::RT * D / 4; q += 256) {
+    const int i = q / (D / 4), c4 = (q % (D / 4)) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m0 + i < M) v = *(const f32x4*)(src + (long)(m0 + i) * D + c4);
+    *(f32x4*)(dst + i * T::S + c4) = v;
+  }
+}
+
+// acc[i] (C[row][ff], rows 16i.. of the wave's tile rows, ff = this lane's column) += rows x D @ B over
+// D, lane group g covering d in [g*KQ, (g+1)*KQ); bv[kk] = this lane's B value for d = g*KQ + kk.
+template <int D>
+__device__ __forceinline__ void dcontract(const float* tile, const float (&bv)[FfnTile<D>::KQ],
+                                          f32x4 (&acc)[FfnTile<D>::NI], int g, int c) {
+  using T = FfnTile<D>;
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i) {
+    const float* row = tile + (16 * i + c) * T::S + g * T::KQ;
+    acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kq = 0; kq < T::KQ; kq += 4) {
+      const f32x4 a = *(const f32x4*)(row + kq);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[i] = mfma4(a[t], bv[kq + t], acc[i]);
+    }
+  }
+}
+
+// acc[i][j] += st(rows x 16) @ Wslice(16 x D): A from the staging tile, bw[j][t] = B[f0 + 4g + t][16j + c]
+template <int D>
+__device__ __forceinline__ void fcontract(const float* st, const float (&bw)[FfnTile<D>::NJ][4],
+                                          f32x4 (&acc)[FfnTile<D>::NI][FfnTile<D>::NJ], int g, int c) {
+  using T = FfnTile<D>;
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i) {
+    const f32x4 av = *(const f32x4*)(st + (16 * i + c) * T::SS + 4 * g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) acc[i][j] = mfma4(av[t], bw[j][t], acc[i][j]);
+  }
+}
+
+// ---------------------------------------------------------------- forward
+template <int D>
+__global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
+  using T = FfnTile<D>;
+  __shared__ __attribute__((aligned(16))) float smem[T::TILE + 4 * T::STG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int m0 = blockIdx.x * T::RT;
+  load_tile<D>(a.x, a.M, m0, smem);
+  __syncthreads();
+  const float* xw = smem + w * T::RW * T::S;     // this wave's rows
+  float* st = smem + T::TILE + w * T::STG;
+
+  f32x4 yacc[T::NI][T::NJ];
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int f0 = 0; f0 < a.FF; f0 += 16) {
+    const int ff = f0 + c;
+    float bv[T::KQ];
+#pragma unroll
+    for (int kq = 0; kq < T::KQ; kq += 4)
+      *(f32x4*)&bv[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
+    f32x4 pre[T::NI];
+    dcontract<D>(xw, bv, pre, g, c);
+    const float bias = a.b1[ff];
+    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + 4 * g + rr;
+        float v = gelu_f(pre[i][rr] + bias);
+        if (a.drop.thresh) v = drop_apply(a.drop, (uint32_t)((long)(m0 + w * T::RW + row) * a.FF + ff), v);
+        st[row * T::SS + c] = v;
+      }
+    __builtin_amdgcn_wave_barrier();
+    float bw[T::NJ][4];
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) {
+      const f32x4 v = *(const f32x4*)(a.W2 + (long)(16 * j + c) * a.FF + f0 + 4 * g);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bw[j][t] = v[t];
+    }
+    fcontract<D>(st, bw, yacc, g, c);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // h = x + (y + b2); RMSNorm over the row (the row's D values sit in the 16 lanes of one lane group)
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
+      float hv[T::NJ];
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) {
+        const int d = 16 * j + c;
+        hv[j] = xw[row * T::S + d] + (yacc[i][j][rr] + a.b2[d]);
+        ss += hv[j] * hv[j];
+      }
+      ss = group_sum<16>(ss);
+      const float rs = 1.0f / sqrtf(ss / (float)D + a.eps);
+      if (m < a.M) {
+        if (c == 0) a.r[m] = rs;
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) {
+          const int d = 16 * j + c;
+          a.h[(long)m * D + d] = hv[j];
+          a.y[(long)m * D + d] = a.nw[d] * hv[j] * rs;
+        }
+      }
+    }
+}
+
+// ---------------------------------------------------------------- backward
+template <int D>
+__global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
+  using T = FfnTile<D>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::TILE + 4 * T::STG + 4 * T::PW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int m0 = blockIdx.x * T::RT;
+  load_tile<D>(a.x, a.M, m0, smem);
+  load_tile<D>(a.dh, a.M, m0, smem + T::TILE);
+  __syncthreads();
+  const float* xw = smem + w * T::RW * T::S;
+  const float* dw = smem + T::TILE + w * T::RW * T::S;
+  float* st = smem + 2 * T::TILE + w * T::STG;
+  float* red = smem + 2 * T::TILE + 4 * T::STG;
+  float* pw = red + w * T::PW;
+  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
+
+  f32x4 dxacc[T::NI][T::NJ];
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int f0 = 0; f0 < a.FF; f0 += 16) {
+    const int ff = f0 + c;
+    const float bias = a.b1[ff];
+    f32x4 pre[T::NI];
+    {
+      float bv[T::KQ];
+#pragma unroll
+      for (int kq = 0; kq < T::KQ; kq += 4)
+        *(f32x4*)&bv[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
+      dcontract<D>(xw, bv, pre, g, c);
+    }
+    f32x4 dact[T::NI];
+    {
+      float bv[T::KQ];
+#pragma unroll
+      for (int kk = 0; kk < T::KQ; ++kk) bv[kk] = a.W2[(long)(g * T::KQ + kk) * a.FF + ff];
+      dcontract<D>(dw, bv, dact, g, c);
+    }
+    f32x4 dw2[T::NJ], dw1[T::NJ];
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) dw2[j] = dw1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float db = 0.f;
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + 4 * g + rr;
+        const uint32_t di = (uint32_t)((long)(m0 + w * T::RW + row) * a.FF + ff);
+        const float z = pre[i][rr] + bias;
+        const bool keep = a.drop.thresh ? drop_keep(a.drop, di) : true;
+        const float sc = a.drop.thresh ? (keep ? a.drop.scale : 0.f) : 1.f;
+        const float fo = a.drop.thresh ? (keep ? gelu_f(z) * a.drop.scale : 0.f) : gelu_f(z);
+        const float da = dact[i][rr] * sc * gelu_grad(z);
+        dact[i][rr] = da;
+        db += da;
+        // dW2[d][ff] += dh[row][d] fo[row][ff];  dW1[ff][d] += dact[row][ff] x[row][d]   (k-set rows {4g+rr})
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) {
+          dw2[j] = mfma4(dw[row * T::S + 16 * j + c], fo, dw2[j]);
+          dw1[j] = mfma4(da, xw[row * T::S + 16 * j + c], dw1[j]);
+        }
+      }
+    db += __shfl_xor(db, 16);
+    db += __shfl_xor(db, 32);
+    // dx += dact W1 over this chunk (stage dact as [row][16])
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) st[(16 * i + 4 * g + rr) * T::SS + c] = dact[i][rr];
+    __builtin_amdgcn_wave_barrier();
+    float bw[T::NJ][4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) bw[j][t] = a.W1[(long)(f0 + 4 * g + t) * D + 16 * j + c];
+    fcontract<D>(st, bw, dxacc, g, c);
+    // weight-grad partials of this wave -> LDS; fixed-order sum over the 4 waves -> slab
+    __syncthreads();                        // previous chunk's reduction has read `red`
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        pw[(4 * g + rr) * D + 16 * j + c] = dw1[j][rr];                 // C[ff = 4g+rr][d = 16j+c]
+        pw[16 * D + (16 * j + 4 * g + rr) * 16 + c] = dw2[j][rr];       // C[d = 16j+4g+rr][ff = c]
+      }
+    if (g == 0) pw[32 * D + c] = db;
+    __syncthreads();
+    for (int q = tid; q < T::PW; q += 256) {
+      const float s = ((red[q] + red[T::PW + q]) + red[2 * T::PW + q]) + red[3 * T::PW + q];
+      if (q < 16 * D) slab[(long)f0 * D + q] = s;
+      else if (q < 32 * D) {
+        const int u = q - 16 * D;
+        slab[a.o_w2 + (long)(u >> 4) * a.FF + f0 + (u & 15)] = s;
+      } else {
+        slab[a.o_b1 + f0 + (q - 32 * D)] = s;
+      }
+    }
+  }
+
+  // dx = dact W1 (complete over FF in this wave) + dh (residual path)
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
+      if (m < a.M) {
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) {
+          const int d = 16 * j + c;
+          a.dx[(long)m * D + d] = dxacc[i][j][rr] + dw[row * T::S + d];
+        }
+      }
+    }
+}
+
+template <int D>
+static void launch_ffn(const FfnArgs& a, bool bwd, hipStream_t s) {
+  const int blocks = cdiv(a.M, FfnTile<D>::RT);
+  if (bwd) ffn_bwd_kernel<D><<<blocks, 256, 0, s>>>(a);
+  else ffn_fwd_kernel<D><<<blocks, 256, 0, s>>>(a);
+}
+
+static bool ffn_shape_ok(int D, int FF) { return (D == 16 || D == 32 || D == 64) && FF > 0 && FF % 16 == 0; }
+
+static int ffn_dispatch(const FfnArgs& a, int D, bool bwd, hipStream_t s) {
+  switch (D) {
+    case 16: launch_ffn<16>(a, bwd, s); break;
+    case 32: launch_ffn<32>(a, bwd, s); break;
+    default: launch_ffn<64>(a, bwd, s); break;
+  }
+  return check_launch(bwd ? "ffn_bwd" : "ffn_fwd");
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int ctr_ffn_supported(int D, int FF) { return ffn_shape_ok(D, FF) ? 1 : 0; }
+
+extern "C" int ctr_ffn_slab_rows(int M, int D) { return cdiv(M, D >= 64 ? 64 : 128); }
+
+extern "C" int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
+                           const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
+                           float drop_scale, float* y, float* h, float* r, void* stream) {
+  CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_fwd: needs D in {16,32,64} and FF % 16 == 0");
+  if (M <= 0) return 0;
+  FfnArgs a = {};
+  a.M = M; a.FF = FF; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.b2 = b2; a.nw = norm_w; a.eps = eps;
+  a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.y = y; a.h = h; a.r = r;
+  return ffn_dispatch(a, D, false, (hipStream_t)stream);
+}
+
+extern "C" int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
+                           const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* dx,
+                           float* slab, long ld_slab, int o_b1, int o_w2, void* stream) {
+  CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(o_b1 >= FF * D && o_w2 >= o_b1 + FF && ld_slab >= (long)o_w2 + (long)D * FF, "ctr_ffn_bwd: slab layout");
+  if (M <= 0) return 0;
+  FfnArgs a = {};
+  a.M = M; a.FF = FF; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2;
+  a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.dh = dh; a.dx = dx; a.slab = slab; a.ld_slab = ld_slab; a.o_b1 = o_b1; a.o_w2 = o_w2;
+  return ffn_dispatch(a, D, true, (hipStream_t)stream);
+}

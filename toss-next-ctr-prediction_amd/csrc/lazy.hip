@@ -1,0 +1,278 @@
+// Exact lazy AdamW + EMA for the embedding tables.
+//
+// The reference steps every element of every table each step (torch.optim.AdamW over dense
+// nn.Embedding grads, src/train.py:195; ModelEMA.update, src/utils/ema.py:92-131): with 1.24 B
+// table elements that is ~40 GB of HBM traffic per step although a batch touches well under 1% of
+// the rows.  Here a row is only brought up to date when something needs it:
+//   * ctr_lazy_touch   -- rows a batch reads in the forward (hashed categoricals, sequence tokens),
+//   * ctr_lazy_update  -- rows that receive a gradient this tick (replay, then the real tick),
+//   * ctr_lazy_flush   -- all rows, before parameters / moments / EMA are read as a whole.
+// "Brought up to date" = the ticks the row missed are replayed from the device tick history with
+// grad 0, through the same adam.h arithmetic as the dense stream, so the result is bit-identical to
+// stepping the row densely every tick (tests/test_gpu_lazy.py checks that bitwise).
+//
+// Work mapping: a group of lg lanes per row; lane l holds elements l, l+lg, ... (<= 8 per lane, rows
+// are <= 64 wide) in registers across the whole replay, so the history entry of a tick is loaded once
+// per lane and the row's p, m, v, ema are read and written once.
+#include "adam.h"
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+
+constexpr int LQ = 8;           // row elements held per lane (rows are <= 64 wide)
+constexpr int LG = 8;           // lanes per row in touch / update (any table width)
+constexpr int HWIN = 256;       // flush: the last HWIN history entries are staged in LDS
+constexpr int FLUSH_MAXTABS = 64;
+constexpr uint32_t LAZY_INVALID = 0xFFFFFFFFu;
+
+__global__ void opt_hist_record_kernel(OptScalars* hist, int tick, OptScalars s) { hist[tick] = s; }
+
+// History lookup: entries [lo, ..] from LDS when staged, older ones from global memory.
+struct HistView {
+  const OptScalars* g;
+  const OptScalars* lds;
+  int lo;
+  __device__ __forceinline__ OptScalars operator[](int k) const { return (lds && k >= lo) ? lds[k - lo] : g[k]; }
+};
+
+// Brings one row from tick s to tick t_idle with grad 0, then (grow != null) applies tick t_idle+1 with
+// grad grow*coef.  The row is spread over lg lanes: lane l holds elements l, l+lg, ... (nq of them).
+// A row whose moments are all zero (never stepped with a non-zero grad) stays zero under idle ticks:
+// only the decay multiply and the EMA remain.  With m == v == 0, adam_elem(g = 0) gives m = v = +0,
+// denom = eps and p = fmaf(-step, +0, p * decay) == p * decay: bit for bit the same.
+__device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __restrict__ m_row,
+                                           float* __restrict__ v_row, float* __restrict__ e_row, int width, int l,
+                                           int lg, int nq, const HistView& hv, int s, int t_idle,
+                                           const float* __restrict__ grow, float coef) {
+  float p[LQ], m[LQ], v[LQ], e[LQ];
+#pragma unroll
+  for (int q = 0; q < LQ; ++q) {
+    const int j = l + lg * q;
+    p[q] = m[q] = v[q] = e[q] = 0.0f;
+    if (q < nq && j < width) {
+      p[q] = p_row[j];
+      m[q] = m_row[j];
+      v[q] = v_row[j];
+      if (e_row) e[q] = e_row[j];
+    }
+  }
+  bool zero = true;
+#pragma unroll
+  for (int q = 0; q < LQ; ++q) zero = zero && m[q] == 0.0f && v[q] == 0.0f;
+  if (zero) {
+    bool stepped = false;
+    for (int k = s + 1; k <= t_idle; ++k) {
+      const OptScalars sc = hv[k];
+      if (sc.do_adam) {
+        stepped = true;
+#pragma unroll
+        for (int q = 0; q < LQ; ++q)
+          if (q < nq) p[q] = p[q] * sc.decay_mul;
+      }
+      if (sc.do_ema) {
+#pragma unroll
+        for (int q = 0; q < LQ; ++q)
+          if (q < nq) ema_elem(sc, p[q], e[q]);
+      }
+    }
+    if (stepped) {
+#pragma unroll
+      for (int q = 0; q < LQ; ++q) m[q] = v[q] = 0.0f;    // a dense idle tick leaves +0 moments
+    }
+  } else {
+    for (int k = s + 1; k <= t_idle; ++k) {
+      const OptScalars sc = hv[k];
+#pragma unroll
+      for (int q = 0; q < LQ; ++q) {
+        if (q < nq) {
+          if (sc.do_adam) idle_adam_elem(sc, p[q], m[q], v[q]);
+          if (sc.do_ema) ema_elem(sc, p[q], e[q]);
+        }
+      }
+    }
+  }
+  if (grow) {
+    const OptScalars sc = hv[t_idle + 1];
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+      const int j = l + lg * q;
+      if (q < nq && j < width) adam_ema_elem(sc, p[q], m[q], v[q], e[q], grow[j] * coef, sc.do_adam != 0);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < LQ; ++q) {
+    const int j = l + lg * q;
+    if (q < nq && j < width) {
+      p_row[j] = p[q];
+      m_row[j] = m[q];
+      v_row[j] = v[q];
+      if (e_row) e_row[j] = e[q];
+    }
+  }
+}
+
+struct RowPtrs {
+  float *p, *m, *v, *e;
+};
+
+__device__ __forceinline__ RowPtrs row_ptrs(const ctr_lazy_tab_t& tb, long row, float* P, float* M, float* V,
+                                            float* E) {
+  const long o = tb.p_off + row * (long)tb.width;
+  return {P + o, M + o, V + o, E ? E + o : nullptr};
+}
+
+// One 8-lane group per (id, table) item.  The group leader claims the row with a CAS on last[row]
+// (s -> tick); only the winner replays, so a row read many times in a batch is caught up once.
+__global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+                                                         const int32_t* __restrict__ X, long nitems, int ncols,
+                                                         int per_column, float* P, float* M, float* V, float* E,
+                                                         const OptScalars* __restrict__ hist, int tick) {
+  const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
+  const int l8 = threadIdx.x & (LG - 1);
+  int s = tick, win = 0, ti = 0;
+  long row = -1;
+  if (item < nitems) {
+    long xi;
+    if (per_column) {
+      xi = item;
+      ti = (int)(item % ncols);
+    } else {
+      xi = item / ntabs;
+      ti = (int)(item % ntabs);
+    }
+    row = X[xi];
+    if (l8 == 0 && row >= 0 && row < tabs[ti].rows) {
+      int* lp = tabs[ti].last + row;
+      s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s < tick) win = atomicCAS(lp, s, tick) == s;
+    }
+  }
+  const int leader = (threadIdx.x & 63) & ~(LG - 1);
+  win = __shfl(win, leader);
+  s = __shfl(s, leader);
+  if (!win) return;
+  const ctr_lazy_tab_t tb = tabs[ti];
+  const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
+  replay_row(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s, tick,
+             nullptr, 0.0f);
+}
+
+// One 8-lane group per compact grad slot: keys are unique, so no claim is needed.
+__global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+                                                          const uint32_t* __restrict__ keys,
+                                                          const float* __restrict__ G, int g_ld,
+                                                          const uint32_t* __restrict__ n_uniq, long cap,
+                                                          const float* __restrict__ coef_ptr, float* P, float* M,
+                                                          float* V, float* E, const OptScalars* __restrict__ hist,
+                                                          int tick) {
+  const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
+  const int l8 = threadIdx.x & (LG - 1);
+  const long nu = min(cap, (long)*n_uniq);
+  if (item >= nu) return;
+  const uint32_t key = keys[item];
+  if (key == LAZY_INVALID) return;
+  int a = 0, b = ntabs;   // last table with key_base <= key
+  while (b - a > 1) {
+    const int mid = (a + b) >> 1;
+    if (tabs[mid].key_base <= key) a = mid; else b = mid;
+  }
+  const ctr_lazy_tab_t tb = tabs[a];
+  const long row = (long)(key - tb.key_base);
+  if (row >= tb.rows) return;
+  const int s = tb.last[row];
+  const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
+  const float coef = coef_ptr ? *coef_ptr : 1.0f;
+  replay_row(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s, tick - 1,
+             G + item * (long)g_ld, coef);
+  if (l8 == 0) tb.last[row] = tick;
+}
+
+// lanes per row for a table in the flush: enough that a lane holds <= LQ elements, as few as possible
+__device__ __forceinline__ int flush_lg(int width) {
+  const int need = (width + LQ - 1) / LQ;
+  return need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
+}
+
+// Persistent grid over (table, chunk of 256/lg rows) work items; the recent history is staged in LDS
+// once per workgroup.  Per chunk everything (table, lg, nq) is workgroup-uniform.
+__global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+                                                         float* P, float* M, float* V, float* E,
+                                                         const OptScalars* __restrict__ hist, int tick) {
+  __shared__ OptScalars hs[HWIN];
+  __shared__ long chunk0[FLUSH_MAXTABS + 1];
+  const int tid = threadIdx.x;
+  const int lo = max(1, tick - HWIN + 1);
+  for (int k = lo + tid; k <= tick; k += 256) hs[k - lo] = hist[k];
+  if (tid == 0) {
+    long c = 0;
+    for (int t = 0; t < ntabs; ++t) {
+      chunk0[t] = c;
+      c += cdiv(tabs[t].rows, 256 / flush_lg(tabs[t].width));
+    }
+    chunk0[ntabs] = c;
+  }
+  __syncthreads();
+  const HistView hv{hist, hs, lo};
+  const long nchunks = chunk0[ntabs];
+  for (long c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    int a = 0, b = ntabs;
+    while (b - a > 1) {
+      const int mid = (a + b) >> 1;
+      if (chunk0[mid] <= c) a = mid; else b = mid;
+    }
+    const ctr_lazy_tab_t tb = tabs[a];
+    const int lg = flush_lg(tb.width);
+    const long row = (c - chunk0[a]) * (256 / lg) + tid / lg;
+    if (row >= tb.rows) continue;
+    const int s = tb.last[row];
+    if (s >= tick) continue;
+    const int l = tid & (lg - 1);
+    const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
+    replay_row(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), hv, s, tick, nullptr, 0.0f);
+    if (l == 0) tb.last[row] = tick;
+  }
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int ctr_opt_hist_entry_bytes(void) { return (int)sizeof(OptScalars); }
+
+extern "C" int ctr_opt_hist_record(void* hist, int tick, float lr, float wd, float beta1, float beta2, float eps,
+                                   int step, float ema_decay, int do_adam, int do_ema, void* stream) {
+  CTR_REQUIRE(hist != nullptr && tick > 0, "ctr_opt_hist_record: bad history / tick");
+  const OptScalars s = make_opt_scalars(lr, wd, beta1, beta2, eps, step, ema_decay, do_adam, do_ema);
+  opt_hist_record_kernel<<<1, 1, 0, (hipStream_t)stream>>>((OptScalars*)hist, tick, s);
+  return check_launch("opt_hist_record");
+}
+
+extern "C" int ctr_lazy_touch(const ctr_lazy_tab_t* tabs, int ntabs, const int32_t* X, long nx, int ncols,
+                              int per_column, float* P, float* M, float* V, float* E, const void* hist, int tick,
+                              void* stream) {
+  CTR_REQUIRE(ntabs > 0 && (!per_column || ntabs == ncols), "ctr_lazy_touch: per_column needs ntabs == ncols");
+  if (tick <= 0 || nx <= 0 || ncols <= 0) return 0;
+  const long nitems = per_column ? nx * ncols : nx * ncols * ntabs;
+  lazy_touch_kernel<<<(unsigned)cdiv(nitems * LG, 256L), 256, 0, (hipStream_t)stream>>>(
+      tabs, ntabs, X, nitems, ncols, per_column, P, M, V, E, (const OptScalars*)hist, tick);
+  return check_launch("lazy_touch");
+}
+
+extern "C" int ctr_lazy_update(const ctr_lazy_tab_t* tabs, int ntabs, const uint32_t* keys, const float* G, int g_ld,
+                               const uint32_t* n_uniq, long cap, const float* coef, float* P, float* M, float* V,
+                               float* E, const void* hist, int tick, void* stream) {
+  CTR_REQUIRE(ntabs > 0 && tick > 0, "ctr_lazy_update: bad tables / tick");
+  if (cap <= 0) return 0;
+  lazy_update_kernel<<<(unsigned)cdiv(cap * LG, 256L), 256, 0, (hipStream_t)stream>>>(
+      tabs, ntabs, keys, G, g_ld, n_uniq, cap, coef, P, M, V, E, (const OptScalars*)hist, tick);
+  return check_launch("lazy_update");
+}
+
+extern "C" int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_rows, float* P, float* M, float* V,
+                              float* E, const void* hist, int tick, void* stream) {
+  CTR_REQUIRE(ntabs <= FLUSH_MAXTABS, "ctr_lazy_flush: too many tables");
+  if (ntabs <= 0 || tick <= 0 || max_rows <= 0) return 0;
+  lazy_flush_kernel<<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist, tick);
+  return check_launch("lazy_flush");
+}

@@ -9,6 +9,7 @@
 // compact (sorted unique keys, summed rows) produced by rowgrad.hip, and each workgroup maps the
 // touched rows of its chunk into an LDS slot table (binary search + forward scan of the sorted keys).
 // Per element: read p, m, v, ema (+ g) and write p, m, v, ema once -- 32 B/param of HBM traffic.
+#include "adam.h"
 #include "common.h"
 #include "ctr_hip.h"
 
@@ -16,29 +17,6 @@ namespace ctr {
 
 constexpr int OPT_CHUNK = 8192;                 // elements per workgroup
 constexpr int OPT_MAXROWS = OPT_CHUNK / 4 + 2;  // sparse segments need width >= 4
-
-struct OptScalars {
-  float decay_mul;    // 1 - lr*wd
-  float b1w;          // 1 - beta1 (lerp weight)
-  float b2, omb2;     // beta2, 1 - beta2
-  float eps;
-  float step_size;    // lr / (1 - beta1^t)
-  float bc2_sqrt;     // sqrt(1 - beta2^t)
-  float ema_d, ema_omd;
-  int do_adam, do_ema;
-};
-
-__device__ __forceinline__ void adam_ema_elem(const OptScalars& s, float& p, float& m, float& v, float& e, float g,
-                                              bool adam) {
-  if (adam) {
-    p = p * s.decay_mul;                                  // param.mul_(1 - lr*wd)
-    m = m + s.b1w * (g - m);                              // exp_avg.lerp_(grad, 1-beta1)
-    v = v * s.b2 + s.omb2 * g * g;                        // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
-    const float denom = sqrtf(v) / s.bc2_sqrt + s.eps;    // (sqrt(v) / bc2_sqrt).add_(eps)
-    p = p + (-s.step_size) * (m / denom);                 // param.addcdiv_(m, denom, -step_size)
-  }
-  if (s.do_ema) e = e * s.ema_d + s.ema_omd * p;          // shadow.mul_(d).add_(p, alpha=1-d)
-}
 
 // For every sparse-segment chunk: [lo, hi) = index range of the sorted unique keys that fall in the
 // chunk's rows.  One thread per chunk (binary searches run in parallel, not as a serial prologue of
@@ -200,20 +178,7 @@ extern "C" int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const c
                              float wd, float beta1, float beta2, float eps, int step, float ema_decay, int do_adam,
                              int do_ema, void* stream) {
   if (nchunks == 0) return 0;
-  OptScalars s;
-  // host-side scalar math in double, exactly as torch/optim/adam.py computes it in Python floats
-  const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
-  s.decay_mul = (float)(1.0 - (double)lr * (double)wd);
-  s.b1w = (float)(1.0 - (double)beta1);
-  s.b2 = beta2;
-  s.omb2 = (float)(1.0 - (double)beta2);
-  s.eps = eps;
-  s.step_size = (float)((double)lr / bc1);
-  s.bc2_sqrt = (float)std::sqrt(bc2);
-  s.ema_d = ema_decay;
-  s.ema_omd = (float)(1.0 - (double)ema_decay);
-  s.do_adam = do_adam;
-  s.do_ema = do_ema;
+  const OptScalars s = make_opt_scalars(lr, wd, beta1, beta2, eps, step, ema_decay, do_adam, do_ema);
   hipStream_t st = (hipStream_t)stream;
   if (do_adam) chunk_key_range_kernel<<<cdiv(nchunks, 256), 256, 0, st>>>(chunks, nchunks, segs, krange);
   adamw_ema_kernel<<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);

@@ -31,6 +31,11 @@ class OptChunk(C.Structure):
     _fields_ = [("seg", C.c_int32), ("pad", C.c_int32), ("e0", C.c_int64), ("e1", C.c_int64)]
 
 
+class LazyTab(C.Structure):
+    _fields_ = [("p_off", C.c_int64), ("rows", C.c_int64), ("width", C.c_int32), ("key_base", C.c_uint32),
+                ("last", p)]
+
+
 # name: (restype, argtypes) -- keep in the order of include/ctr_hip.h
 SIGS = {
     "ctr_last_error": (C.c_char_p, []),
@@ -54,6 +59,10 @@ SIGS = {
     "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p]),
     "ctr_attn_bwd_nparts": (i, [i, i, i]),
     "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
+    "ctr_ffn_supported": (i, [i, i]),
+    "ctr_ffn_slab_rows": (i, [i, i]),
+    "ctr_ffn_fwd": (i, [p, i, i, i, p, p, p, p, p, f, u, u, f, p, p, p, p]),
+    "ctr_ffn_bwd": (i, [p, p, i, i, i, p, p, p, u, u, f, p, p, l, i, i, p]),
     "ctr_rmsnorm_fwd": (i, [p, l, i, i, p, f, p, l, p, p]),
     "ctr_rmsnorm_bwd_nparts": (i, [i, i]),
     "ctr_rmsnorm_bwd": (i, [p, l, p, l, p, p, i, i, p, l, p, l, p, p]),
@@ -76,6 +85,11 @@ SIGS = {
     "ctr_sqnorm_rows": (i, [p, p, p, i, i, u, p, p]),
     "ctr_clip_finalize": (i, [p, i, f, f, p, p]),
     "ctr_mask_tail_keys": (i, [p, i, i, p, p]),
+    "ctr_opt_hist_entry_bytes": (i, []),
+    "ctr_opt_hist_record": (i, [p, i, f, f, f, f, f, i, f, i, i, p]),
+    "ctr_lazy_touch": (i, [p, i, p, l, i, i, p, p, p, p, p, i, p]),
+    "ctr_lazy_update": (i, [p, i, p, p, i, p, l, p, p, p, p, p, p, i, p]),
+    "ctr_lazy_flush": (i, [p, i, l, p, p, p, p, p, i, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
     "ctr_gather_rows": (i, [p, l, p, i, p, p]),

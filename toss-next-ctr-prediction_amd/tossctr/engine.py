@@ -96,6 +96,15 @@ class Workspace:
             self.t[name] = t
         return t
 
+    def get_zeroed(self, name, shape, dtype=torch.float32):
+        """Like get(), zero-filled when (re)allocated: for buffers whose unwritten entries must read 0."""
+        shape = tuple(int(s) for s in shape)
+        t = self.t.get(name)
+        if t is None or t.shape != shape or t.dtype != dtype:
+            t = torch.zeros(shape, dtype=dtype, device=self.device)
+            self.t[name] = t
+        return t
+
 
 class Engine:
     def __init__(self, arch: Arch, arena: ParamArena):
@@ -129,6 +138,21 @@ class Engine:
         self._splitk = None
         self._gen = 0
         self.stream = None
+        self.lazy = None     # a lazy FusedAdamW: table rows are brought current before they are read
+        # fused FFN kernels (ffn.hip) when the shape allows; the GEMM path otherwise
+        self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden)) and \
+            self._ffn_contiguous()
+
+    def _ffn_contiguous(self):
+        """The fused FFN backward colsums its [dW1 | db1 | dW2] slab straight into the grad arena."""
+        off = self.arena.offsets
+        for li in range(self.a.n_layers):
+            p = f"dare.layers.{li}."
+            if not (off[p + "ffn.0.weight"] < off[p + "ffn.0.bias"] < off[p + "ffn.3.weight"]):
+                return False
+            if self.arena.kind[p + "ffn.0.weight"] != "dense" or self.arena.kind[p + "ffn.3.weight"] != "dense":
+                return False
+        return True
 
     # ------------------------------------------------------------------ helpers
     def s(self):
@@ -214,6 +238,9 @@ class Engine:
                  ptr(P["mask_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, mask_off), FD, st)
         # ---- hashed categorical gather + projection (+ emb dropout into xF) (wrapper.py:106-112,149-150)
         cat_e = W.get("cat_e", (B, a.Fc, D))
+        if self.lazy is not None:
+            self.lazy.touch_rows(X_cat, "cat")
+            self.lazy.touch_rows(seq, "seq")
         dk = drop_args(seed, SITE_EMB, a.p_emb, training)
         call("ctr_cat_embed_fwd", ptr(X_cat), B, a.Fc, ptr(self.arena.buf), ptr(self.cat_tab_off),
              ptr(self.cat_proj_off), ptr(self.cat_dims_t), D, ptr(cat_e), ptr(xF, cat_off), FD, *dk, st)
@@ -260,18 +287,25 @@ class Engine:
                       GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), ld_resid=D,
                               norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1), norm_eps=1e-6))
             FF = a.ffn_hidden
-            act = W.get(f"ffa{li}", (M, FF))
-            fo = W.get(f"ffo{li}", (M, FF))
             dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
-            self.gemm(M, FF, D, ptr(x1), D, 0, ptr(P[pre + "ffn.0.weight"]), D, 1, ptr(fo), FF,
-                      GemmEpi(bias=ptr(P[pre + "ffn.0.bias"]), act=2, pre=ptr(act), drop_key=dfk[0],
-                              drop_thresh=dfk[1], drop_scale=dfk[2]))
             h2 = W.get(f"h2_{li}", (M, D))
             r2 = W.get(f"r2_{li}", (M,))
             x2 = W.get(f"x{li + 1}", (B, K, D))
-            self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(x2), D,
-                      GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
-                              norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
+            act = fo = None
+            if self.ffn_fused:
+                # Linear -> GELU -> Dropout -> Linear -> +x1 -> RMSNorm in one kernel (ffn.hip)
+                call("ctr_ffn_fwd", ptr(x1), M, D, FF, ptr(P[pre + "ffn.0.weight"]), ptr(P[pre + "ffn.0.bias"]),
+                     ptr(P[pre + "ffn.3.weight"]), ptr(P[pre + "ffn.3.bias"]), ptr(P[pre + "norm2.w"]), 1e-6, *dfk,
+                     ptr(x2), ptr(h2), ptr(r2), st)
+            else:
+                act = W.get(f"ffa{li}", (M, FF))
+                fo = W.get(f"ffo{li}", (M, FF))
+                self.gemm(M, FF, D, ptr(x1), D, 0, ptr(P[pre + "ffn.0.weight"]), D, 1, ptr(fo), FF,
+                          GemmEpi(bias=ptr(P[pre + "ffn.0.bias"]), act=2, pre=ptr(act), drop_key=dfk[0],
+                                  drop_thresh=dfk[1], drop_scale=dfk[2]))
+                self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(x2), D,
+                          GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
+                                  norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
             Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, h1=h1, r1=r1, x1=x1, act=act, fo=fo,
                       h2=h2, r2=r2)
             layers.append(Ls)
@@ -508,19 +542,35 @@ class Engine:
         call("ctr_rmsnorm_bwd", ptr(dx2), D, ptr(Ls["h2"]), D, ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]), M, D,
              ptr(dh2), D, None, 0, ptr(dwp), st)
         self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm2.w"]))
-        # ffn.3: f @ W2^T + b2
-        self.wgrad(ptr(dh2), D, ptr(Ls["fo"]), FF, M, D, FF, ptr(G[pre + "ffn.3.weight"]),
-                   bias_grad=ptr(G[pre + "ffn.3.bias"]))
-        dact = W.get("dffa", (M, FF))
         dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
-        self.gemm(M, FF, D, ptr(dh2), D, 0, ptr(P[pre + "ffn.3.weight"]), FF, 0, ptr(dact), FF,
-                  GemmEpi(dact=2, aux=ptr(Ls["act"]), drop_key=dfk[0], drop_thresh=dfk[1], drop_scale=dfk[2]))
-        # ffn.0: x1 @ W1^T + b1
-        self.wgrad(ptr(dact), FF, ptr(Ls["x1"]), D, M, FF, D, ptr(G[pre + "ffn.0.weight"]),
-                   bias_grad=ptr(G[pre + "ffn.0.bias"]))
         dx1 = W.get("dx1", (M, D))
-        self.gemm(M, D, FF, ptr(dact), FF, 0, ptr(P[pre + "ffn.0.weight"]), D, 0, ptr(dx1), D,
-                  GemmEpi(add=ptr(dh2), ld_add=D))
+        if self.ffn_fused:
+            # one kernel: recompute pre/GELU/dropout from x1, dx1 = dh2 + dact W1, per-workgroup slabs
+            # [dW1 | db1 | dW2] laid out like the grad arena from ffn.0.weight on -> one colsum lands them
+            o0 = self.arena.offsets[pre + "ffn.0.weight"]
+            o_b1 = self.arena.offsets[pre + "ffn.0.bias"] - o0
+            o_w2 = self.arena.offsets[pre + "ffn.3.weight"] - o0
+            n_sl = o_w2 + D * FF
+            ld_sl = (n_sl + 3) // 4 * 4
+            nb = _lib.query("ctr_ffn_slab_rows", M, D)
+            slab = W.get_zeroed("ffn_slab", (nb, ld_sl))
+            call("ctr_ffn_bwd", ptr(Ls["x1"]), ptr(dh2), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
+                 ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(dx1), ptr(slab), ld_sl, o_b1,
+                 o_w2, st)
+            self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
+            self.colsum(ptr(dh2), D, M, D, ptr(G[pre + "ffn.3.bias"]))
+        else:
+            # ffn.3: f @ W2^T + b2
+            self.wgrad(ptr(dh2), D, ptr(Ls["fo"]), FF, M, D, FF, ptr(G[pre + "ffn.3.weight"]),
+                       bias_grad=ptr(G[pre + "ffn.3.bias"]))
+            dact = W.get("dffa", (M, FF))
+            self.gemm(M, FF, D, ptr(dh2), D, 0, ptr(P[pre + "ffn.3.weight"]), FF, 0, ptr(dact), FF,
+                      GemmEpi(dact=2, aux=ptr(Ls["act"]), drop_key=dfk[0], drop_thresh=dfk[1], drop_scale=dfk[2]))
+            # ffn.0: x1 @ W1^T + b1
+            self.wgrad(ptr(dact), FF, ptr(Ls["x1"]), D, M, FF, D, ptr(G[pre + "ffn.0.weight"]),
+                       bias_grad=ptr(G[pre + "ffn.0.bias"]))
+            self.gemm(M, D, FF, ptr(dact), FF, 0, ptr(P[pre + "ffn.0.weight"]), D, 0, ptr(dx1), D,
+                      GemmEpi(add=ptr(dh2), ld_add=D))
         # x1 = norm1(x + attn(x))
         dh1 = W.get("dh1", (M, D))
         call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,

@@ -3,8 +3,11 @@
 Drop-in for the reference step tail (src/train.py:133-139 construction, :185-199 per step):
     nn.utils.clip_grad_norm_(model.parameters(), c); opt.step(); ema.update(model, global_step)
 Semantics are torch's dense ones (every element decays / moves each step, untouched table rows see
-grad 0), executed as ONE pass over (p, m, v, ema) by csrc/optim.hip with table grads read from the
-compact row dedup -- no dense table gradient is ever written.
+grad 0).  Dense parameters are ONE pass over (p, m, v, ema) by csrc/optim.hip; the embedding tables
+(1.24 B of the 1.25 B elements at the benchmark config) take the exact lazy path of csrc/lazy.hip:
+a row is replayed to the current tick when read, when it gets a gradient, or at flush() --
+bit-identical to the dense stream, which stays available as lazy=False.  No dense table gradient is
+ever written.
 """
 from __future__ import annotations
 
@@ -54,6 +57,7 @@ class ArenaEMA:
         self.pin_memory = bool(pin_memory)
         self.param_filter = set()
         self.num_updates = 0
+        model.sync()
         self.shadow = model.arena.buf.clone()
         self._saved = None
 
@@ -74,10 +78,12 @@ class ArenaEMA:
 
     @torch.no_grad()
     def store(self, model):
+        model.sync()
         self._saved = model.arena.buf.clone()
 
     @torch.no_grad()
     def copy_to(self, model):
+        model.sync()
         model.arena.buf.copy_(self.shadow)
 
     @torch.no_grad()
@@ -88,6 +94,7 @@ class ArenaEMA:
         self._saved = None
 
     def shadow_params(self):
+        self.model.sync()
         ar = self.model.arena
         return {k: ar._view(self.shadow, k) for k in ar.order}
 
@@ -128,7 +135,7 @@ class FusedAdamW:
     """torch.optim.AdamW(model.parameters(), lr, weight_decay) + clip + EMA as one arena stream."""
 
     def __init__(self, model, lr, weight_decay=1e-2, betas=(0.9, 0.999), eps=1e-8, max_grad_norm=0.0, ema=None,
-                 process_group=None):
+                 process_group=None, lazy=True):
         self.model = model
         self.arena = ar = model.arena
         self.engine = model.engine
@@ -152,7 +159,15 @@ class FusedAdamW:
         self._seg_key = None
         self._segs_dev = None
         self._build_chunks()
+        # exact lazy table update (csrc/lazy.hip): tables leave the dense stream; rows are replayed to
+        # the current tick when read, when they get a gradient, or at flush()
+        self.lazy = bool(lazy)
+        self.tick = 0
+        self._flushed_tick = 0
+        if self.lazy:
+            self._init_lazy()
         object.__setattr__(model, "_fused_opt", self)
+        self.engine.lazy = self if self.lazy else None
 
     # -------------------------------------------------------------- layout
     def _segments(self, tg):
@@ -182,22 +197,86 @@ class FusedAdamW:
     def _build_chunks(self):
         segs = self._segments(None)
         CH = _lib.query("ctr_opt_chunk_elems")
-        self._chunk_all, self._chunk_adam = [], []
+        lists = {"all": [], "adam": [], "all_dense": [], "adam_dense": []}
         for si, sg in enumerate(segs):
             n4 = (sg["n"] + 3) // 4 * 4     # stream whole float4s; the tail sits in the 64-element padding
             for e0 in range(0, n4, CH):
                 c = (si, e0, min(n4, e0 + CH))
-                self._chunk_all.append(c)
+                lists["all"].append(c)
                 if sg["kind"] != 2:
-                    self._chunk_adam.append(c)
+                    lists["adam"].append(c)
+                if sg["kind"] != 1:
+                    lists["all_dense"].append(c)
+                if sg["kind"] == 0:
+                    lists["adam_dense"].append(c)
+        self._chunk_all = lists["all"]
         self._chunks_dev = {}
-        for name, lst in (("all", self._chunk_all), ("adam", self._chunk_adam)):
+        for name, lst in lists.items():
             arr = (OptChunk * max(1, len(lst)))()
             for i, (si, e0, e1) in enumerate(lst):
                 arr[i].seg, arr[i].pad, arr[i].e0, arr[i].e1 = si, 0, e0, e1
             raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
             self._chunks_dev[name] = (torch.from_numpy(raw).to(self.arena.device), len(lst))
         self.krange = torch.zeros(2 * max(1, len(self._chunk_all)), dtype=torch.int32, device=self.arena.device)
+
+    def _init_lazy(self):
+        ar, eng, a = self.arena, self.engine, self.engine.a
+        dev = ar.device
+        keys = ["dare.emb_att.weight", "dare.emb_rep.weight"] + [f"cat_embs.{c}.weight" for c in a.cat_names]
+        total = sum(ar.shapes[k][0] for k in keys)
+        self.last = torch.zeros(total, dtype=torch.int32, device=dev)
+        tabs, r0 = {}, 0
+        for k in keys:
+            rows, width = ar.shapes[k]
+            base = int(eng.cat_row_base_np[a.cat_names.index(k[9:-7])]) if k.startswith("cat_embs.") else 0
+            tabs[k] = (ar.offsets[k], rows, width, base, ptr(self.last, r0))
+            r0 += rows
+        self._lazy_max_rows = max(t[1] for t in tabs.values())
+
+        def dev_tabs(names):
+            arr = (_lib.LazyTab * len(names))()
+            for i, k in enumerate(names):
+                arr[i].p_off, arr[i].rows, arr[i].width, arr[i].key_base, arr[i].last = tabs[k]
+            raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
+            return torch.from_numpy(raw).to(dev), len(names)
+
+        cat = [f"cat_embs.{c}.weight" for c in a.cat_names]     # key_base ascending = X_cat column order
+        self._lazy_tabs = {"att": dev_tabs(keys[:1]), "rep": dev_tabs(keys[1:2]), "seq": dev_tabs(keys[:2]),
+                           "cat": dev_tabs(cat), "all": dev_tabs(keys)}
+        self._hist_entry = _lib.query("ctr_opt_hist_entry_bytes")
+        self.hist = torch.zeros(1024 * self._hist_entry, dtype=torch.uint8, device=dev)
+
+    def _hist_for(self, tick):
+        if (tick + 1) * self._hist_entry > self.hist.numel():
+            h = torch.zeros(2 * self.hist.numel(), dtype=torch.uint8, device=self.arena.device)
+            h[:self.hist.numel()].copy_(self.hist)
+            self.hist = h
+        return self.hist
+
+    def _ema_ptr(self):
+        return ptr(self.ema.shadow) if self.ema is not None else None
+
+    def touch_rows(self, X, group):
+        """Bring the table rows a batch reads up to the current tick (called by Engine.forward):
+        group "cat": X = X_cat (B, Fc), column c indexes table c; "seq": X = seq (B, L), each token a
+        row of both DARE tables."""
+        if self.tick == self._flushed_tick:
+            return
+        tabs, n = self._lazy_tabs[group]
+        call("ctr_lazy_touch", ptr(tabs), n, ptr(X), X.shape[0], X.shape[1], 1 if group == "cat" else 0,
+             ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
+             self.engine.s())
+
+    @torch.no_grad()
+    def flush(self):
+        """Replay every table row to the current tick: afterwards arena, moments and EMA shadow hold
+        exactly what the dense stream would (call before reading them as a whole)."""
+        if not self.lazy or self.tick == self._flushed_tick:
+            return
+        tabs, n = self._lazy_tabs["all"]
+        call("ctr_lazy_flush", ptr(tabs), n, self._lazy_max_rows, ptr(self.arena.buf), ptr(self.m), ptr(self.v),
+             self._ema_ptr(), ptr(self.hist), self.tick, self.engine.s())
+        self._flushed_tick = self.tick
 
     def _segs_device(self, tg):
         segs = self._segments(tg)
@@ -278,15 +357,28 @@ class FusedAdamW:
             do_ema = 1
             decay = self.ema.next_decay()
         segs = self._segs_device(tg)
-        chunks, n = self._chunks_dev["all" if do_ema else "adam"]
+        chunks, n = self._chunks_dev[("all" if do_ema else "adam") + ("_dense" if self.lazy else "")]
         b1, b2 = g["betas"]
+        st = self.engine.s()
         if self._timing:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        if self.lazy:
+            self.tick += 1
+            call("ctr_opt_hist_record", ptr(self._hist_for(self.tick)), self.tick, float(g["lr"]),
+                 float(g["weight_decay"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1,
+                 do_ema, st)
         call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
              ptr(self.v), ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf), ptr(self.arena.grad),
              ptr(self.norm_out, 1), float(g["lr"]), float(g["weight_decay"]),
-             float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1, do_ema, self.engine.s())
+             float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1, do_ema, st)
+        if self.lazy:
+            for name in ("att", "rep", "cat"):
+                t = tg[name]
+                tabs, nt = self._lazy_tabs[name]
+                call("ctr_lazy_update", ptr(tabs), nt, ptr(t["keys"]), ptr(t["G"]), t["G"].shape[1], ptr(t["n_uniq"]),
+                     t["n"], ptr(self.norm_out, 1), ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(),
+                     ptr(self.hist), self.tick, st)
         if self._timing:
             ev[1].record()
             self._events.append(ev)
@@ -298,8 +390,15 @@ class FusedAdamW:
             return
         decay = ema.next_decay()
         segs = self._segs_device(None)
-        chunks, n = self._chunks_dev["all"]
+        chunks, n = self._chunks_dev["all_dense" if self.lazy else "all"]
         g = self.param_groups[0]
+        if self.lazy:
+            if ema is not self.ema:
+                raise RuntimeError("lazy FusedAdamW: the EMA must be the one bound at construction")
+            self.tick += 1
+            call("ctr_opt_hist_record", ptr(self._hist_for(self.tick)), self.tick, float(g["lr"]),
+                 float(g["weight_decay"]), 0.9, 0.999, 1e-8, max(1, self.step_count), float(decay), 0, 1,
+                 self.engine.s())
         call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
              ptr(self.v), ptr(ema.shadow), ptr(self.arena.grad), None, float(g["lr"]), float(g["weight_decay"]), 0.9, 0.999,
              1e-8, max(1, self.step_count), float(decay), 0, 1, self.engine.s())

@@ -92,6 +92,20 @@ class CTRModel(nn.Module):
         self._step = 0
         self.reset_parameters()
 
+    def sync(self):
+        """Bring lazily-updated table rows (FusedAdamW(lazy=True)) up to the current optimizer tick."""
+        opt = self.__dict__.get("_fused_opt")
+        if opt is not None:
+            opt.flush()
+
+    def state_dict(self, *args, **kwargs):
+        self.sync()
+        return super().state_dict(*args, **kwargs)
+
+    def load_state_dict(self, state_dict, strict=True, assign=False):
+        self.sync()     # moments / EMA of lagging rows must be current before their params change
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
     # the arena is not an nn.Module buffer: keep .to()/.cuda() from re-allocating parameters
     def _apply(self, fn, recurse=True):
         return self
