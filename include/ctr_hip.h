@@ -119,13 +119,16 @@ int ctr_pos_bias_grad(const float* part, int nparts, int H, int n, float* drel, 
  * qkv (B*K, 3D) from the in-projection GEMM; o (B*K, D); mrow/lrow (B*H*K) row max / sum saved for
  * the recompute backward; drel_part (B*nparts, 2tk+1) positional-bias grad partials.
  * ------------------------------------------------------------------------------------------- */
+int ctr_attn_mask_words(int B, int K, int H);   /* uint32 words of the dropout keep-bit mask */
+/* mask (nullable without dropout): the forward stores the keep bits of p~, row ((b*H+h)*K + i),
+ * ceil(K/32) words per row; the backward reads them instead of re-evaluating the hash.             */
 int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
-                 uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* o, float* mrow, float* lrow,
-                 void* stream);
+                 uint32_t drop_key, uint32_t drop_thresh, float drop_scale, uint32_t* mask, float* o, float* mrow,
+                 float* lrow, void* stream);
 int ctr_attn_bwd_nparts(int H, int K, int D);
 int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D, const float* relmean,
-                 int tk, float scale, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const float* mrow,
-                 const float* lrow, float* dqkv, float* drel_part, void* stream);
+                 int tk, float scale, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const uint32_t* mask,
+                 const float* mrow, const float* lrow, float* dqkv, float* drel_part, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused position-wise FFN + residual + RMSNorm of DAREEncoderLayer, src/models/dare.py:53-70

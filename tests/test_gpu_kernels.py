@@ -133,8 +133,9 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p):
     mrow = torch.empty(B * H * K, device="cuda")
     lrow = torch.empty(B * H * K, device="cuda")
     scale = float(np.float32(math.sqrt(1.0 / dh)))
-    L.call("ctr_attn_fwd", ptr(qkv), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(o), ptr(mrow), ptr(lrow),
-           stream())
+    mask = torch.zeros(L.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
+    L.call("ctr_attn_fwd", ptr(qkv), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mask), ptr(o), ptr(mrow),
+           ptr(lrow), stream())
     # torch reference (MHA explicit path semantics)
     q, k, v = qkv.view(B, K, 3 * D).split(D, -1)
     q = q.reshape(B, K, H, dh).transpose(1, 2)
@@ -149,14 +150,19 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p):
         keep = torch.from_numpy(orng.keep_mask(1234, 7, p, (B * H, K, K))).cuda().view(B, H, K, K)
         a = a * keep.float() / (1 - p)
     o_ref = (a @ v).transpose(1, 2).reshape(B * K, D)
-    assert rel(o, o_ref.detach()) < 2e-6
+    assert rel(o, o_ref.detach()) < 5e-6
+    if p > 0:   # the stored keep bits are exactly the oracle's mask
+        km = keep.view(B * H * K, K).cpu().numpy()
+        words = mask.view(B * H * K, -1).cpu().numpy().view(np.uint32)
+        bits = (words[:, np.arange(K) // 32] >> (np.arange(K) % 32).astype(np.uint32)) & 1
+        assert np.array_equal(bits.astype(bool), km)
     do = torch.randn(B * K, D, device="cuda")
     o_ref.backward(do)
     dqkv = torch.empty(B * K, 3 * D, device="cuda")
     nparts = L.query("ctr_attn_bwd_nparts", H, K, D) * B
     drp = torch.empty(nparts, 2 * tk + 1, device="cuda")
-    L.call("ctr_attn_bwd", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mrow), ptr(lrow),
-           ptr(dqkv), ptr(drp), stream())
+    L.call("ctr_attn_bwd", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mask), ptr(mrow),
+           ptr(lrow), ptr(dqkv), ptr(drp), stream())
     drel = torch.empty(2 * tk + 1, H, device="cuda")
     L.call("ctr_pos_bias_grad", ptr(drp), nparts, H, 2 * tk + 1, ptr(drel), stream())
     assert rel(dqkv, qkv.grad) < 1e-5

@@ -2,12 +2,15 @@
 // MHA explicit path of torch.nn.functional.multi_head_attention_forward):
 //   s_ij = mean_h rel[j-i+tk] + (q_i * sqrt(1/dh)) . k_j ;  p = softmax_j(s) ; p~ = dropout(p) ;
 //   o_i = sum_j p~_ij v_j
-// One workgroup per (sample, group of G heads); one thread per query row (forward, backward row pass)
-// or key column (backward column pass).  Heads are only dh = D/H = 4..8 wide -- far too thin for an
-// MFMA tile -- so scores are VALU dot products against K/V rows that every lane of a wave reads at
-// the same LDS address (broadcast).  The backward recomputes P from the saved row max / row sum; only
-// dS (K x (K+1), odd stride: conflict-free row reads) is kept in LDS, no K x K tensor reaches HBM.
-// The positional-bias grad is reduced along diagonals in a fixed order (deterministic).
+// One workgroup per (sample, group of G heads).  Heads are only dh = D/H = 2..16 wide -- far too thin
+// for an MFMA tile (a 16x16x4 f32 MFMA would waste 3/4 of its N on a dh = 4 PV product) -- so scores
+// are VALU dot products against K/V/Q rows that a whole wave reads at one LDS address (broadcast).
+// The per-element costs that matter are exp and the counter-hash dropout, so:
+//   * the forward evaluates the hash once and stores the keep bits (B*H*K*ceil(K/32) words: ~15 MB
+//     per layer at the benchmark shape) -- the backward reads bits instead of re-hashing;
+//   * the backward is one pass per key column j (thread = j) that recomputes p_ij once, writes dS_ij
+//     to LDS and accumulates dk_j, dv_j; a second, cheap pass per query row i sums dq_i = dS_i. k.
+// Nothing K x K reaches HBM.  The positional-bias grad is reduced along diagonals in a fixed order.
 #include "common.h"
 #include "ctr_hip.h"
 
@@ -20,6 +23,8 @@ struct AttnArgs {
   int tk;
   float scale;          // sqrt(1/dh) as the reference's python float -> fp32
   Drop drop;            // over ((b*H + h)*K + i)*K + j
+  uint32_t* mask;       // (B*H*K, KW) keep bits of p~ (dropout only)
+  int KW;               // words per mask row = ceil(K/32)
   float* o;             // (B*K, D)
   float* mrow;          // (B*H*K) row max of s
   float* lrow;          // (B*H*K) row sum of exp(s - max)
@@ -36,7 +41,10 @@ __device__ __forceinline__ float dotv(const float (&a)[DH], const float* b) {
   return s;
 }
 
-template <int DH>
+// exp(x) on the hardware exp2 (v_exp_f32, ~1 ulp); forward and backward use the same formula
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+template <int DH, bool BIAS, bool DROP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int K = a.K, D = a.D, G = a.G;
@@ -51,7 +59,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     sk[e] = base[(long)j * 3 * D + D + col];
     sv[e] = base[(long)j * 3 * D + 2 * D + col];
   }
-  if (a.relmean)
+  if (BIAS)
     for (int e = threadIdx.x; e < 2 * a.tk + 1; e += blockDim.x) srel[e] = a.relmean[e];
   __syncthreads();
   const int t = threadIdx.x;
@@ -63,37 +71,49 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const float* kg = sk + g * K * DH;
   const float* vg = sv + g * K * DH;
   const float* rb = srel + a.tk - i;     // rb[j] = relmean[j - i + tk]
-  const bool bias = a.relmean != nullptr;
   float m = -INFINITY;
+#pragma unroll 4
   for (int j = 0; j < K; ++j) {
-    const float s = (bias ? rb[j] : 0.f) + dotv<DH>(qs, kg + j * DH);
+    const float s = (BIAS ? rb[j] : 0.f) + dotv<DH>(qs, kg + j * DH);
     m = fmaxf(m, s);
   }
   float l = 0.f;
   float acc[DH];
 #pragma unroll
   for (int c = 0; c < DH; ++c) acc[c] = 0.f;
-  const uint32_t rowbase = (uint32_t)((((long)b * a.H + h) * K + i) * K);
-  for (int j = 0; j < K; ++j) {
-    const float s = (bias ? rb[j] : 0.f) + dotv<DH>(qs, kg + j * DH);
-    const float e = expf(s - m);
-    l += e;
-    const float w = a.drop.thresh ? (drop_keep(a.drop, rowbase + j) ? e * a.drop.scale : 0.f) : e;
+  const long r = ((long)b * a.H + h) * K + i;
+  const uint32_t rowbase = (uint32_t)(r * K);
+  uint32_t* mrow_bits = a.mask + r * a.KW;
+  for (int j0 = 0; j0 < K; j0 += 32) {          // one keep-bit word per 32 keys
+    const int j1 = min(K, j0 + 32);
+    uint32_t word = 0;
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) {
+      const float s = (BIAS ? rb[j] : 0.f) + dotv<DH>(qs, kg + j * DH);
+      const float e = fexp(s - m);
+      l += e;
+      float w = e;
+      if (DROP) {
+        const bool keep = drop_keep(a.drop, rowbase + j);
+        word |= (uint32_t)keep << (j - j0);
+        w = keep ? e * a.drop.scale : 0.f;
+      }
 #pragma unroll
-    for (int c = 0; c < DH; ++c) acc[c] = fmaf(w, vg[j * DH + c], acc[c]);
+      for (int c = 0; c < DH; ++c) acc[c] = fmaf(w, vg[j * DH + c], acc[c]);
+    }
+    if (DROP) mrow_bits[j0 >> 5] = word;
   }
   const float inv = 1.0f / l;
 #pragma unroll
   for (int c = 0; c < DH; ++c) a.o[((long)b * K + i) * D + h * DH + c] = acc[c] * inv;
-  const long r = ((long)b * a.H + h) * K + i;
   a.mrow[r] = m;
   a.lrow[r] = l;
 }
 
-template <int DH>
+template <int DH, bool BIAS, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int K = a.K, D = a.D, G = a.G;
+  const int K = a.K, D = a.D, G = a.G, KW = a.KW;
   const int KP = K + 1;                    // odd row stride
   const int b = blockIdx.x, hg = blockIdx.y;
   const int nrel = 2 * a.tk + 1;
@@ -101,10 +121,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   float* sk = sq + G * K * DH;
   float* sv = sk + G * K * DH;
   float* sdo = sv + G * K * DH;
-  float* sm_ = sdo + G * K * DH;           // [G][K] row max
-  float* sl = sm_ + G * K;                 // [G][K] row sum
-  float* srel = sl + G * K;                // [nrel]
-  float* dS = srel + ((nrel + 3) & ~3);    // [G][K][KP]
+  float* smx = sdo + G * K * DH;           // [G][K] row max
+  float* sli = smx + G * K;                // [G][K] 1 / row sum
+  float* sD = sli + G * K;                 // [G][K] do_i . o_i
+  float* srel = sD + G * K;                // [nrel]
+  uint32_t* smask = (uint32_t*)(srel + nrel);   // [G][K][KW]
+  float* dS = (float*)(smask + G * K * KW);     // [G][K][KP]
   const float* base = a.qkv + (long)b * K * 3 * D;
   for (int e = threadIdx.x; e < G * K * DH; e += blockDim.x) {
     const int g = e / (K * DH), r = e % (K * DH), j = r / DH, c = r % DH;
@@ -114,74 +136,100 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
     sv[e] = base[(long)j * 3 * D + 2 * D + col];
     sdo[e] = a.dO[((long)b * K + j) * D + col];
   }
-  for (int e = threadIdx.x; e < G * K; e += blockDim.x) {
-    const int g = e / K, i = e % K;
-    const long r = ((long)b * a.H + hg * G + g) * K + i;
-    sm_[e] = a.mrow[r];
-    sl[e] = a.lrow[r];
-  }
-  if (a.relmean)
+  const long r0 = ((long)b * a.H + hg * G) * K;     // first (head, row) of the group
+  if (DROP)
+    for (int e = threadIdx.x; e < G * K * KW; e += blockDim.x) smask[e] = a.mask[r0 * KW + e];
+  if (BIAS)
     for (int e = threadIdx.x; e < nrel; e += blockDim.x) srel[e] = a.relmean[e];
-  __syncthreads();
   const int t = threadIdx.x;
   const bool act = t < G * K;
-  const bool bias = a.relmean != nullptr;
   const int g = act ? t / K : 0, i = act ? t % K : 0, h = hg * G + g;
+  if (act) {
+    smx[t] = a.mrow[r0 + t];
+    sli[t] = 1.0f / a.lrow[r0 + t];
+    float di = 0.f;
+#pragma unroll
+    for (int c = 0; c < DH; ++c)
+      di = fmaf(a.dO[((long)b * K + i) * D + h * DH + c], a.o[((long)b * K + i) * D + h * DH + c], di);
+    sD[t] = di;
+  }
+  __syncthreads();
   const float* qg = sq + g * K * DH;
   const float* kg = sk + g * K * DH;
   const float* vg = sv + g * K * DH;
   const float* dog = sdo + g * K * DH;
+  const float* mg = smx + g * K;
+  const float* lg = sli + g * K;
+  const float* Dg = sD + g * K;
+  const uint32_t* mk = smask + g * K * KW;
   float* dSg = dS + g * K * KP;
-  const uint32_t hbase = (uint32_t)(((long)b * a.H + h) * K * K);
-  // ---- row pass (thread = query row i): P, dP~, dS, dq
+  // ---- column pass (thread = key column j): p_ij, dS_ij -> LDS; dk_j = sum_i dS_ij qs_i, dv_j = sum_i p~_ij do_i
+  // Rows are taken NB at a time: every LDS operand of the NB rows is loaded before any dS store, so the
+  // loads of a batch issue back to back (one latency per batch, not per row).
   if (act) {
-    float qi[DH], di[DH], oi[DH];
-#pragma unroll
-    for (int c = 0; c < DH; ++c) {
-      qi[c] = qg[i * DH + c];
-      di[c] = dog[i * DH + c];
-      oi[c] = a.o[((long)b * K + i) * D + h * DH + c];
-    }
-    const float Di = dotv<DH>(di, oi);
-    const float mi = sm_[g * K + i], li = 1.0f / sl[g * K + i];
-    const float* rb = srel + a.tk - i;
-    float dq[DH];
-#pragma unroll
-    for (int c = 0; c < DH; ++c) dq[c] = 0.f;
-    for (int j = 0; j < K; ++j) {
-      const float s = (bias ? rb[j] : 0.f) + dotv<DH>(qi, kg + j * DH);
-      const float p = expf(s - mi) * li;
-      float dp = dotv<DH>(di, vg + j * DH);
-      if (a.drop.thresh) dp = drop_keep(a.drop, hbase + (uint32_t)(i * K + j)) ? dp * a.drop.scale : 0.f;
-      const float ds = p * (dp - Di);
-      dSg[i * KP + j] = ds;
-#pragma unroll
-      for (int c = 0; c < DH; ++c) dq[c] = fmaf(ds, kg[j * DH + c], dq[c]);
-    }
-#pragma unroll
-    for (int c = 0; c < DH; ++c) a.dqkv[((long)b * K + i) * 3 * D + h * DH + c] = dq[c] * a.scale;
-  }
-  __syncthreads();
-  // ---- column pass (thread = key column j): dk_j = sum_i dS_ij qs_i ; dv_j = sum_i p~_ij do_i
-  if (act) {
+    constexpr int NB = 4;
     const int j = i;
-    float kj[DH], dk[DH], dv[DH];
+    float kj[DH], vj[DH], dk[DH], dv[DH];
 #pragma unroll
     for (int c = 0; c < DH; ++c) {
       kj[c] = kg[j * DH + c];
+      vj[c] = vg[j * DH + c];
       dk[c] = 0.f;
       dv[c] = 0.f;
     }
-    for (int ii = 0; ii < K; ++ii) {
-      const float ds = dSg[ii * KP + j];
-      const float s = (bias ? srel[a.tk + j - ii] : 0.f) + dotv<DH>(kj, qg + ii * DH);
-      float p = expf(s - sm_[g * K + ii]) / sl[g * K + ii];
-      if (a.drop.thresh) p = drop_keep(a.drop, hbase + (uint32_t)(ii * K + j)) ? p * a.drop.scale : 0.f;
+    const float* rb = srel + a.tk + j;   // rb[-ii] = relmean[j - ii + tk]
+    const int jw = j >> 5, jb = j & 31;
+    const float dscale = a.drop.scale;
+    auto row = [&](int ii, const float* qi, const float* doi, float mi, float li, float Di, float rel, uint32_t mw,
+                   float& ds_out) {
+      const float s = rel + dotv<DH>(kj, qi);
+      const float p = fexp(s - mi) * li;
+      float dp = dotv<DH>(vj, doi);
+      float pt = p;
+      if (DROP) {
+        const bool keep = (mw >> jb) & 1u;
+        dp = keep ? dp * dscale : 0.f;
+        pt = keep ? p * dscale : 0.f;
+      }
+      const float ds = p * (dp - Di);
+      ds_out = ds;
 #pragma unroll
       for (int c = 0; c < DH; ++c) {
-        dk[c] = fmaf(ds, qg[ii * DH + c], dk[c]);
-        dv[c] = fmaf(p, dog[ii * DH + c], dv[c]);
+        dk[c] = fmaf(ds, qi[c], dk[c]);
+        dv[c] = fmaf(pt, doi[c], dv[c]);
       }
+    };
+    int ii = 0;
+    for (; ii + NB <= K; ii += NB) {
+      float q[NB][DH], dov[NB][DH], mi[NB], li[NB], Di[NB], rel[NB], ds[NB];
+      uint32_t mw[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+#pragma unroll
+        for (int c = 0; c < DH; ++c) {
+          q[u][c] = qg[(ii + u) * DH + c];
+          dov[u][c] = dog[(ii + u) * DH + c];
+        }
+        mi[u] = mg[ii + u];
+        li[u] = lg[ii + u];
+        Di[u] = Dg[ii + u];
+        rel[u] = BIAS ? rb[-(ii + u)] : 0.f;
+        mw[u] = DROP ? mk[(ii + u) * KW + jw] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) row(ii + u, q[u], dov[u], mi[u], li[u], Di[u], rel[u], mw[u], ds[u]);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) dSg[(ii + u) * KP + j] = ds[u];
+    }
+    for (; ii < K; ++ii) {
+      float q[DH], dov[DH], ds;
+#pragma unroll
+      for (int c = 0; c < DH; ++c) {
+        q[c] = qg[ii * DH + c];
+        dov[c] = dog[ii * DH + c];
+      }
+      row(ii, q, dov, mg[ii], lg[ii], Dg[ii], BIAS ? rb[-ii] : 0.f, DROP ? mk[ii * KW + jw] : 0u, ds);
+      dSg[ii * KP + j] = ds;
     }
 #pragma unroll
     for (int c = 0; c < DH; ++c) {
@@ -189,8 +237,24 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
       a.dqkv[((long)b * K + j) * 3 * D + 2 * D + h * DH + c] = dv[c];
     }
   }
+  __syncthreads();
+  // ---- row pass (thread = query row i): dq_i = scale * sum_j dS_ij k_j
+  if (act) {
+    float dq[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) dq[c] = 0.f;
+    const float* dsr = dSg + i * KP;
+#pragma unroll 4
+    for (int j = 0; j < K; ++j) {
+      const float ds = dsr[j];
+#pragma unroll
+      for (int c = 0; c < DH; ++c) dq[c] = fmaf(ds, kg[j * DH + c], dq[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < DH; ++c) a.dqkv[((long)b * K + i) * 3 * D + h * DH + c] = dq[c] * a.scale;
+  }
   // ---- positional-bias grad: sum of dS along diagonals j - i = o, heads of the group in order
-  if (bias) {
+  if (BIAS) {
     for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
       const int o = e - a.tk;
       float s = 0.f;
@@ -198,6 +262,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
         const int i0 = o >= 0 ? 0 : -o, i1 = o >= 0 ? K - o : K;
         for (int gg = 0; gg < G; ++gg) {
           const float* Pq = dS + gg * K * KP;
+#pragma unroll 4
           for (int ii = i0; ii < i1; ++ii) s += Pq[ii * KP + ii + o];
         }
       }
@@ -214,37 +279,57 @@ static int pick_group(int H, int K, size_t per_head_lds, size_t lds_cap) {
 }
 
 static size_t bwd_lds(int G, int K, int dh, int tk) {
-  const int nrel = 2 * tk + 1;
-  return ((size_t)4 * G * K * dh + 2 * G * K + ((nrel + 3) & ~3) + (size_t)G * K * (K + 1)) * sizeof(float);
+  const int nrel = 2 * tk + 1, KW = (K + 31) / 32;
+  return ((size_t)4 * G * K * dh + 3 * G * K + nrel + (size_t)G * K * KW + (size_t)G * K * (K + 1)) * sizeof(float);
 }
 
 static int bwd_group(int H, int K, int dh) {
-  return pick_group(H, K, (size_t)(K * (K + 1) + 4 * K * dh + 2 * K) * 4, 80 * 1024);
+  return pick_group(H, K, (size_t)(K * (K + 1) + 4 * K * dh + 3 * K + K * ((K + 31) / 32)) * 4, 80 * 1024);
+}
+
+template <int DH, bool BIAS, bool DROP>
+static void launch_fwd3(const AttnArgs& a, size_t sm, hipStream_t s) {
+  attn_fwd_kernel<DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), (a.G * a.K + 63) / 64 * 64, sm, s>>>(a);
 }
 
 template <int DH>
 static void launch_fwd(const AttnArgs& a, size_t sm, hipStream_t s) {
-  attn_fwd_kernel<DH><<<dim3(a.B, a.H / a.G), (a.G * a.K + 63) / 64 * 64, sm, s>>>(a);
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  if (bias && drop) launch_fwd3<DH, true, true>(a, sm, s);
+  else if (bias) launch_fwd3<DH, true, false>(a, sm, s);
+  else if (drop) launch_fwd3<DH, false, true>(a, sm, s);
+  else launch_fwd3<DH, false, false>(a, sm, s);
+}
+
+template <int DH, bool BIAS, bool DROP>
+static void launch_bwd3(const AttnArgs& a, size_t sm, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<DH, BIAS, DROP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  attn_bwd_kernel<DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), (a.G * a.K + 63) / 64 * 64, sm, s>>>(a);
 }
 
 template <int DH>
 static void launch_bwd(const AttnArgs& a, size_t sm, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<DH>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
-  attn_bwd_kernel<DH><<<dim3(a.B, a.H / a.G), (a.G * a.K + 63) / 64 * 64, sm, s>>>(a);
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  if (bias && drop) launch_bwd3<DH, true, true>(a, sm, s);
+  else if (bias) launch_bwd3<DH, true, false>(a, sm, s);
+  else if (drop) launch_bwd3<DH, false, true>(a, sm, s);
+  else launch_bwd3<DH, false, false>(a, sm, s);
 }
 
 }  // namespace ctr
 
 using namespace ctr;
 
+extern "C" int ctr_attn_mask_words(int B, int K, int H) { return B * H * K * ((K + 31) / 32); }
+
 extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
-                            uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* o, float* mrow,
-                            float* lrow, void* stream) {
+                            uint32_t drop_key, uint32_t drop_thresh, float drop_scale, uint32_t* mask, float* o,
+                            float* mrow, float* lrow, void* stream) {
   if (B == 0) return 0;
   const int dh = D / H;
   CTR_REQUIRE(D % H == 0 && (dh == 2 || dh == 4 || dh == 8 || dh == 16), "head dim must be 2, 4, 8 or 16");
@@ -254,6 +339,8 @@ extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const 
   AttnArgs a{};
   a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = G;
   a.relmean = relmean; a.tk = tk; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = mask; a.KW = (K + 31) / 32;
+  CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
   a.o = o; a.mrow = mrow; a.lrow = lrow;
   const size_t sm = ((size_t)2 * G * K * dh + 2 * tk + 1) * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
@@ -270,16 +357,18 @@ extern "C" int ctr_attn_bwd_nparts(int H, int K, int D) { return H / bwd_group(H
 
 extern "C" int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D,
                             const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
-                            float drop_scale, const float* mrow, const float* lrow, float* dqkv, float* drel_part,
-                            void* stream) {
+                            float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow, float* dqkv,
+                            float* drel_part, void* stream) {
   if (B == 0) return 0;
   const int dh = D / H;
   CTR_REQUIRE(D % H == 0 && (dh == 2 || dh == 4 || dh == 8 || dh == 16), "head dim must be 2, 4, 8 or 16");
   CTR_REQUIRE(K <= 256, "K > 256");
+  CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
   const int G = bwd_group(H, K, dh);
   AttnArgs a{};
   a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = G;
   a.relmean = relmean; a.tk = tk; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = const_cast<uint32_t*>(mask); a.KW = (K + 31) / 32;
   a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow); a.lrow = const_cast<float*>(lrow);
   a.dO = dO; a.dqkv = dqkv; a.drel_part = drel_part;
   const size_t sm = bwd_lds(G, K, dh, tk);

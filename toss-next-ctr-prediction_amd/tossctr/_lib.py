@@ -56,9 +56,10 @@ SIGS = {
     "ctr_pool_bwd": (i, [p, p, p, i, i, i, i, u, u, f, p, p, l, p, p, p, p]),
     "ctr_pos_bias_mean": (i, [p, i, i, p, p]),
     "ctr_pos_bias_grad": (i, [p, i, i, i, p, p]),
-    "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p]),
+    "ctr_attn_mask_words": (i, [i, i, i]),
+    "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
     "ctr_attn_bwd_nparts": (i, [i, i, i]),
-    "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
+    "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_ffn_supported": (i, [i, i]),
     "ctr_ffn_slab_rows": (i, [i, i]),
     "ctr_ffn_fwd": (i, [p, i, i, i, p, p, p, p, p, f, u, u, f, p, p, p, p]),

@@ -278,8 +278,10 @@ class Engine:
             mrow = W.get(f"mrow{li}", (B * a.H * K,))
             lrow = W.get(f"lrow{li}", (B * a.H * K,))
             da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
-            call("ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean), a.top_k, scale, *da, ptr(o), ptr(mrow),
-                 ptr(lrow), st)
+            amask = W.get(f"amask{li}", (_lib.query("ctr_attn_mask_words", B, K, a.H),), torch.int32) \
+                if da[1] else None
+            call("ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean), a.top_k, scale, *da, ptr(amask), ptr(o),
+                 ptr(mrow), ptr(lrow), st)
             h1 = W.get(f"h1_{li}", (M, D))
             r1 = W.get(f"r1_{li}", (M,))
             x1 = W.get(f"x1_{li}", (M, D))
@@ -306,7 +308,8 @@ class Engine:
                 self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(x2), D,
                           GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
                                   norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
-            Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, h1=h1, r1=r1, x1=x1, act=act, fo=fo,
+            Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, amask=amask, h1=h1, r1=r1, x1=x1,
+                      act=act, fo=fo,
                       h2=h2, r2=r2)
             layers.append(Ls)
             xs.append(x2)
@@ -589,7 +592,7 @@ class Engine:
         da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
         scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
         call("ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale,
-             *da, ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
+             *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
         if a.add_pos:
             call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), st)
         # in_proj
