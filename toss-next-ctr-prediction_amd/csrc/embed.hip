@@ -12,50 +12,43 @@ namespace ctr {
 // ------------------------------------------------------------------------------------------------
 // numeric / binary feature embedding
 // ------------------------------------------------------------------------------------------------
+// out[b, f, d] = sum_k (x[b,f] W[f,k] + bias[f,k]) P[d,k] = x[b,f] * A[f,d] + Bv[f,d] with
+// A[f,d] = W[f,:].P[d,:], Bv[f,d] = bias[f,:].P[d,:] formed once per workgroup: the stream is then one
+// FMA per output (the reference's per-k rounding differs by a few ulp).  Workgroup = (feature f, chunk
+// of FE_ROWS samples); lanes = d, so each sample's D outputs are one contiguous store.
+constexpr int FE_ROWS = 64;
+
 __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __restrict__ x, int B, int F,
                                                              const float* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ P, int fe, int D,
                                                              float* __restrict__ out, long out_ld) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* sP = sm;               // [fe][D]: lanes (consecutive d) read consecutive banks
-  float* sW = sm + D * fe;      // [F][fe] (broadcast across the d lanes)
-  float* sB = sW + F * fe;      // [F][fe]
-  for (int i = threadIdx.x; i < D * fe; i += blockDim.x) sP[(i % fe) * D + i / fe] = P[i];
-  for (int i = threadIdx.x; i < F * fe; i += blockDim.x) {
-    sW[i] = W[i];
-    sB[i] = bias ? bias[i] : 0.f;
+  const int f = blockIdx.y, b0 = blockIdx.x * FE_ROWS;
+  const int RG = 256 / D, d = threadIdx.x % D, rg = threadIdx.x / D;
+  if (rg >= RG) return;
+  float A = 0.f, Bv = 0.f;
+  for (int k = 0; k < fe; ++k) {
+    const float pk = P[(long)d * fe + k];
+    A = fmaf(W[(long)f * fe + k], pk, A);
+    if (bias) Bv = fmaf(bias[(long)f * fe + k], pk, Bv);
   }
-  __syncthreads();
-  const long total = (long)B * F * D;
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
-    const int d = (int)(q % D);
-    const long bf = q / D;
-    const int f = (int)(bf % F);
-    const long b = bf / F;
-    const float xv = x[b * F + f];
-    float acc = 0.f;
-    for (int k = 0; k < fe; ++k) {
-      float e = xv * sW[f * fe + k];
-      if (bias) e = e + sB[f * fe + k];
-      acc = fmaf(e, sP[k * D + d], acc);
-    }
-    out[b * out_ld + (long)f * D + d] = acc;
-  }
+  const int b1 = min(B, b0 + FE_ROWS);
+  for (int b = b0 + rg; b < b1; b += RG) out[(long)b * out_ld + (long)f * D + d] = fmaf(x[(long)b * F + f], A, Bv);
 }
 
-// S1[f,d] = sum_b x[b,f] dout[b,f,d],  S0[f,d] = sum_b dout[b,f,d]: one workgroup per feature f;
-// lanes = d (coalesced dout rows), 256/D row groups stride the batch, combined in fixed order.
+// per (feature f, sample chunk): S1[f,d] = sum_b x[b,f] dout[b,f,d], S0[f,d] = sum_b dout[b,f,d]
+// lanes = d, 256/D row groups stride the chunk, combined in fixed order -> part[chunk][2][F][D]
 __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restrict__ x, int B, int F, int D,
                                                           const float* __restrict__ dout, long dout_ld,
-                                                          float* __restrict__ S) {
+                                                          int rows_per_chunk, float* __restrict__ part) {
   __shared__ float r1[256], r0[256];
-  const int f = blockIdx.x, t = threadIdx.x;
+  const int f = blockIdx.x, chunk = blockIdx.y, t = threadIdx.x;
   const int RG = 256 / D;
   const int d = t % D, rg = t / D;
+  const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
   float s1 = 0.f, s0 = 0.f;
   if (rg < RG)
-    for (int b = rg; b < B; b += RG) {
+    for (int b = b0 + rg; b < b1; b += RG) {
       const float g = dout[(long)b * dout_ld + (long)f * D + d];
       s1 = fmaf(x[(long)b * F + f], g, s1);
       s0 += g;
@@ -69,39 +62,51 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restri
       a += r1[g * D + t];
       c += r0[g * D + t];
     }
-    S[(long)f * D + t] = a;
-    S[(long)F * D + (long)f * D + t] = c;
+    float* o = part + (long)chunk * 2 * F * D;
+    o[(long)f * D + t] = a;
+    o[(long)F * D + (long)f * D + t] = c;
   }
 }
 
-// dW = S1 @ P, dbias = S0 @ P, dP = sum_f S1^T W + S0^T bias   (one thread per output element)
-__global__ __launch_bounds__(256) void feat_embed_bwd_final(int F, int D, int fe, const float* __restrict__ S,
-                                                           const float* __restrict__ W,
-                                                           const float* __restrict__ bias,
-                                                           const float* __restrict__ P,
-                                                           float* __restrict__ dW, float* __restrict__ dbias,
-                                                           float* __restrict__ dP) {
-  const float* S1 = S;
-  const float* S0 = S + F * D;
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q < F * fe) {
-    const int f = q / fe, k = q % fe;
-    float a = 0.f, c = 0.f;
-    for (int d = 0; d < D; ++d) {
-      a = fmaf(S1[f * D + d], P[d * fe + k], a);
-      c = fmaf(S0[f * D + d], P[d * fe + k], c);
+// one workgroup: S = sum over chunks (fixed order) into LDS, then
+// dW = S1 @ P, dbias = S0 @ P, dP = sum_f S1^T W + S0^T bias
+__global__ __launch_bounds__(1024) void feat_embed_bwd_final(int nchunk, int F, int D, int fe,
+                                                            const float* __restrict__ part,
+                                                            const float* __restrict__ W,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ P,
+                                                            float* __restrict__ dW, float* __restrict__ dbias,
+                                                            float* __restrict__ dP) {
+  extern __shared__ float sS[];          // [2][F][D]
+  const int n2 = 2 * F * D;
+  for (int q = threadIdx.x; q < n2; q += blockDim.x) {
+    float v = 0.f;
+    for (int c = 0; c < nchunk; ++c) v += part[(long)c * n2 + q];
+    sS[q] = v;
+  }
+  __syncthreads();
+  const float* S1 = sS;
+  const float* S0 = sS + F * D;
+  for (int q = threadIdx.x; q < (F + D) * fe; q += blockDim.x) {
+    if (q < F * fe) {
+      const int f = q / fe, k = q % fe;
+      float a = 0.f, c = 0.f;
+      for (int d = 0; d < D; ++d) {
+        a = fmaf(S1[f * D + d], P[d * fe + k], a);
+        c = fmaf(S0[f * D + d], P[d * fe + k], c);
+      }
+      dW[q] = a;
+      if (dbias) dbias[q] = c;
+    } else {
+      const int r = q - F * fe;
+      const int d = r / fe, k = r % fe;
+      float a = 0.f;
+      for (int f = 0; f < F; ++f) {
+        a = fmaf(S1[f * D + d], W[f * fe + k], a);
+        if (bias) a = fmaf(S0[f * D + d], bias[f * fe + k], a);
+      }
+      dP[r] = a;
     }
-    dW[q] = a;
-    if (dbias) dbias[q] = c;
-  } else if (q < F * fe + D * fe) {
-    const int r = q - F * fe;
-    const int d = r / fe, k = r % fe;
-    float a = 0.f;
-    for (int f = 0; f < F; ++f) {
-      a = fmaf(S1[f * D + d], W[f * fe + k], a);
-      if (bias) a = fmaf(S0[f * D + d], bias[f * fe + k], a);
-    }
-    dP[r] = a;
   }
 }
 
@@ -118,20 +123,20 @@ __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restric
                                                             const float* __restrict__ arena, CatMeta cm, int D,
                                                             float* __restrict__ cat_e, float* __restrict__ xf,
                                                             long xf_ld, Drop drop) {
-  const long total = (long)B * Fc * D;
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
-    const int d = (int)(q % D);
-    const long bc = q / D;
-    const int c = (int)(bc % Fc);
-    const long b = bc / Fc;
+  const uint32_t total = (uint32_t)B * Fc * D;   // host checks < 2^32; 32-bit index math
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
+    const uint32_t bc = q / (uint32_t)D;
+    const int d = (int)(q - bc * D);
+    const uint32_t b = bc / (uint32_t)Fc;
+    const int c = (int)(bc - b * Fc);
     const int dc = cm.dims[c];
-    const long row = xcat[b * Fc + c];
+    const long row = xcat[(long)b * Fc + c];
     const float* t = arena + cm.tab_off[c] + row * dc;
     const float* p = arena + cm.proj_off[c] + (long)d * dc;
     float acc = 0.f;
     for (int k = 0; k < dc; ++k) acc = fmaf(t[k], p[k], acc);
     cat_e[q] = acc;
-    if (xf) xf[b * xf_ld + (long)c * D + d] = drop_apply(drop, (uint32_t)q, acc);
+    if (xf) xf[(long)b * xf_ld + (long)c * D + d] = drop_apply(drop, q, acc);
   }
 }
 
@@ -142,42 +147,70 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_rows(const int* __restrict_
                                                           const float* __restrict__ dcat,
                                                           const uint32_t* __restrict__ row_base,
                                                           float* __restrict__ contrib, uint32_t* __restrict__ keys) {
-  const long total = (long)B * Fc * 64;
-  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+  const uint32_t total = (uint32_t)B * Fc * 64;
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
     const int k = (int)(q & 63);
-    const long bc = q >> 6;
-    const int c = (int)(bc % Fc);
-    const long b = bc / Fc;
+    const uint32_t bc = q >> 6;
+    const uint32_t b = bc / (uint32_t)Fc;
+    const int c = (int)(bc - b * Fc);
     const int dc = cm.dims[c];
     float acc = 0.f;
     if (k < dc) {
       const float* p = arena + cm.proj_off[c] + k;
-      const float* g = dcat + bc * D;
+      const float* g = dcat + (long)bc * D;
       for (int d = 0; d < D; ++d) acc = fmaf(g[d], p[(long)d * dc], acc);
     }
     contrib[q] = acc;
-    if (k == 0) keys[bc] = row_base[c] + (uint32_t)xcat[b * Fc + c];
+    if (k == 0) keys[bc] = row_base[c] + (uint32_t)xcat[(long)b * Fc + c];
   }
 }
 
-// dP_c[d,k] = sum_b dcat[b,c,d] * T_c[row_b, k]   -- block (c, chunk) partials over a row chunk
+// dP_c[d,k] = sum_b dcat[b,c,d] * T_c[row_b, k]   -- block (c, chunk) partials over a row chunk.
+// The chunk's gathered table rows and dcat rows are staged in LDS 64 samples at a time (the gather is
+// the latency-bound part), then each thread reduces its (d, k) outputs from LDS.
+constexpr int CP_SUB = 64;
+
 __global__ __launch_bounds__(256) void cat_embed_bwd_proj_partial(const int* __restrict__ xcat, int B, int Fc,
                                                                   const float* __restrict__ arena, CatMeta cm,
                                                                   int D, const float* __restrict__ dcat,
                                                                   int rows_per_chunk, float* __restrict__ part) {
+  __shared__ float sT[CP_SUB][65];
+  __shared__ float sG[CP_SUB][65];
   const int c = blockIdx.x, chunk = blockIdx.y;
   const int dc = cm.dims[c];
   const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
   const float* T = arena + cm.tab_off[c];
   float* out = part + ((long)chunk * Fc + c) * (64 * 64);
-  for (int q = threadIdx.x; q < D * dc; q += blockDim.x) {
-    const int d = q / dc, k = q % dc;
-    float acc = 0.f;
-    for (int b = b0; b < b1; ++b) {
-      const long row = xcat[(long)b * Fc + c];
-      acc = fmaf(dcat[((long)b * Fc + c) * D + d], T[row * dc + k], acc);
+  const int nq = D * dc;                 // <= 4096 outputs: up to 16 per thread
+  float acc[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) acc[u] = 0.f;
+  for (int s0 = b0; s0 < b1; s0 += CP_SUB) {
+    const int ns = min(CP_SUB, b1 - s0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < ns * 64; e += 256) {
+      const int i = e >> 6, k = e & 63;
+      const long b = s0 + i;
+      const long row = xcat[b * Fc + c];
+      sT[i][k] = k < dc ? T[row * dc + k] : 0.f;
+      sG[i][k] = k < D ? dcat[(b * Fc + c) * D + k] : 0.f;
     }
-    out[q] = acc;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = threadIdx.x + 256 * u;
+      if (q < nq) {
+        const int d = q / dc, k = q - d * dc;
+        float a = acc[u];
+        for (int i = 0; i < ns; ++i) a = fmaf(sG[i][d], sT[i][k], a);
+        acc[u] = a;
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int q = threadIdx.x + 256 * u;
+    if (q < nq) out[q] = acc[u];
   }
 }
 
@@ -334,24 +367,30 @@ using namespace ctr;
 extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, const float* bias, const float* P,
                                   int fe, int D, float* out, long out_ld, void* stream) {
   if (B == 0 || F == 0) return 0;
-  size_t sm = (size_t)(D * fe + 2 * F * fe) * sizeof(float);
-  CTR_REQUIRE(sm <= 64 * 1024, "feat_embed weights exceed 64 KB LDS staging");
-  long total = (long)B * F * D;
-  int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-  feat_embed_fwd_kernel<<<blocks, 256, sm, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D, out, out_ld);
+  CTR_REQUIRE(D <= 256, "D > 256");
+  feat_embed_fwd_kernel<<<dim3(cdiv(B, FE_ROWS), F), 256, 0, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D, out,
+                                                                                     out_ld);
   return check_launch("feat_embed_fwd");
 }
 
-extern "C" size_t ctr_feat_embed_bwd_ws(int B, int F, int D) { return (size_t)2 * F * D * sizeof(float); }
+static int fe_chunks(int B) { return std::max(1, std::min(16, cdiv(B, 256))); }
+
+extern "C" size_t ctr_feat_embed_bwd_ws(int B, int F, int D) {
+  return (size_t)fe_chunks(B) * 2 * F * D * sizeof(float);
+}
 
 extern "C" int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, const float* bias, const float* P,
                                   int fe, int D, const float* dout, long dout_ld, float* dW, float* dbias,
                                   float* dP, float* ws, void* stream) {
   if (F == 0) return 0;
   CTR_REQUIRE(D <= 256, "D > 256");
+  CTR_REQUIRE((size_t)2 * F * D * sizeof(float) <= 64 * 1024, "feat_embed_bwd: 2*F*D exceeds LDS");
   hipStream_t s = (hipStream_t)stream;
-  feat_embed_bwd_sums<<<F, 256, 0, s>>>(x, B, F, D, dout, dout_ld, ws);
-  feat_embed_bwd_final<<<cdiv((long)(F + D) * fe, 256), 256, 0, s>>>(F, D, fe, ws, W, bias, P, dW, dbias, dP);
+  const int nch = fe_chunks(B);
+  const int rpc = cdiv(B, nch);
+  feat_embed_bwd_sums<<<dim3(F, nch), 256, 0, s>>>(x, B, F, D, dout, dout_ld, rpc, ws);
+  feat_embed_bwd_final<<<1, 1024, (size_t)2 * F * D * sizeof(float), s>>>(nch, F, D, fe, ws, W, bias, P, dW, dbias,
+                                                                          dP);
   return check_launch("feat_embed_bwd");
 }
 
@@ -359,6 +398,7 @@ extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* ar
                                  const long* proj_off, const int* dims, int D, float* cat_e, float* xf, long xf_ld,
                                  uint32_t drop_key, uint32_t drop_thresh, float drop_scale, void* stream) {
   if (B == 0 || Fc == 0) return 0;
+  CTR_REQUIRE((long)B * Fc * 64 < (1L << 32), "cat_embed: B*Fc*64 must fit 32-bit indexing");
   CatMeta cm{tab_off, proj_off, dims};
   long total = (long)B * Fc * D;
   int blocks = (int)std::min<long>((total + 255) / 256, 16384);
@@ -368,7 +408,7 @@ extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* ar
 }
 
 extern "C" size_t ctr_cat_embed_bwd_ws(int B, int Fc) {
-  int nchunk = (B + 127) / 128;
+  int nchunk = (B + 255) / 256;
   return (size_t)nchunk * Fc * 64 * 64 * sizeof(float);
 }
 
@@ -378,12 +418,13 @@ extern "C" int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* ar
                                  const long* proj_goff, float* ws, void* stream) {
   if (B == 0 || Fc == 0) return 0;
   CTR_REQUIRE(D <= 64, "D > 64");
+  CTR_REQUIRE((long)B * Fc * 64 < (1L << 32), "cat_embed: B*Fc*64 must fit 32-bit indexing");
   hipStream_t s = (hipStream_t)stream;
   CatMeta cm{tab_off, proj_off, dims};
   long total = (long)B * Fc * 64;
   int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   cat_embed_bwd_rows<<<blocks, 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, row_base, contrib, keys);
-  const int rpc = 128;
+  const int rpc = 256;
   const int nchunk = (B + rpc - 1) / rpc;
   cat_embed_bwd_proj_partial<<<dim3(Fc, nchunk), 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, rpc, ws);
   cat_embed_bwd_proj_final<<<Fc, 256, 0, s>>>(nchunk, Fc, D, cm, proj_goff, ws, grad_arena);

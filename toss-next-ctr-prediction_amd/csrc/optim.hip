@@ -134,19 +134,33 @@ __global__ __launch_bounds__(256) void sqnorm_dense_kernel(const float* __restri
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// Compact row grads: rows are sorted by key and the INVALID group (if any) is the last row, so the
+// valid rows are one contiguous prefix -- summed as a flat float4 stream (padding columns are zero).
 __global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __restrict__ keys,
                                                           const float* __restrict__ G,
                                                           const uint32_t* __restrict__ n_uniq, int width, int ld,
                                                           uint32_t invalid_key, float* __restrict__ part) {
   __shared__ float red[4];
   const uint32_t nu = *n_uniq;
+  const uint32_t nv = (nu > 0 && keys[nu - 1] == invalid_key) ? nu - 1 : nu;
   float s = 0.f;
-  const long total = (long)nu * width;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const long u = i / width;
-    if (keys[u] == invalid_key) continue;
-    const float g = G[u * ld + (i - u * width)];
-    s = fmaf(g, g, s);
+  if ((ld & 3) == 0) {
+    const long total4 = (long)nv * ld / 4;
+    const float4* G4 = (const float4*)G;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
+      const float4 g = G4[i];
+      s = fmaf(g.x, g.x, s);
+      s = fmaf(g.y, g.y, s);
+      s = fmaf(g.z, g.z, s);
+      s = fmaf(g.w, g.w, s);
+    }
+  } else {
+    const long total = (long)nv * width;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+      const long u = i / width;
+      const float g = G[u * ld + (i - u * width)];
+      s = fmaf(g, g, s);
+    }
   }
   s = block_sum(s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;

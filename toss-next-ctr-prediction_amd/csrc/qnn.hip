@@ -77,23 +77,42 @@ __global__ __launch_bounds__(256) void qnn_reduce_bwd_kernel(const float* __rest
 
 // ---------------- SE block ----------------
 // tiny vector MLP, one workgroup: g1 = relu(W1 m + b1) (Cr), gate = sigmoid(W2 g1 + b2) (C)
-__global__ __launch_bounds__(256) void se_mlp_fwd(const float* __restrict__ mean, int C, int Cr,
-                                                  const float* __restrict__ W1, const float* __restrict__ b1,
-                                                  const float* __restrict__ W2, const float* __restrict__ b2,
-                                                  float* __restrict__ g1, float* __restrict__ gate) {
-  extern __shared__ float sg[];
-  for (int j = threadIdx.x; j < Cr; j += blockDim.x) {
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(mean[c], W1[(long)j * C + c], acc);
-    const float v = acc + b1[j];
-    sg[j] = v > 0.f ? v : 0.f;
-    g1[j] = sg[j];
+// y[r] = act(A[r, :] . x + bias[r]) for row-major A (R x N): one wave per row (coalesced row reads,
+// fixed-order wave reduction); act 0 none, 1 relu, 2 sigmoid.  The SE gate's two tiny matvecs
+// (src/models/qnn_alpha.py:44-52) run as two such grids instead of one serial workgroup.
+__global__ __launch_bounds__(256) void matvec_rows_kernel(const float* __restrict__ A, int R, int N,
+                                                          const float* __restrict__ x, const float* __restrict__ bias,
+                                                          int act, float* __restrict__ y) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= R) return;
+  float s = 0.f;
+  for (int c = lane; c < N; c += 64) s = fmaf(A[(long)r * N + c], x[c], s);
+  s = wave_sum(s);
+  if (lane == 0) {
+    float v = s + (bias ? bias[r] : 0.f);
+    if (act == 1) v = v > 0.f ? v : 0.f;
+    else if (act == 2) v = sigmoid_f(v);
+    y[r] = v;
   }
+}
+
+// y[n] = sum_r x[r] * A[r][n] for row-major A (R x N): 64 columns x 4 row groups per workgroup, the four
+// partials summed in a fixed order.  mask (nullable): y[n] = 0 where mask[n] <= 0 (relu').  y2: copy.
+__global__ __launch_bounds__(256) void matvec_cols_kernel(const float* __restrict__ A, int R, int N,
+                                                          const float* __restrict__ x, const float* __restrict__ mask,
+                                                          float* __restrict__ y, float* __restrict__ y2) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6, n = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (n < N)
+    for (int r = rg; r < R; r += 4) s = fmaf(x[r], A[(long)r * N + n], s);
+  red[rg][cl] = s;
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float acc = 0.f;
-    for (int j = 0; j < Cr; ++j) acc = fmaf(sg[j], W2[(long)c * Cr + j], acc);
-    gate[c] = sigmoid_f(acc + b2[c]);
+  if (rg == 0 && n < N) {
+    float v = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+    if (mask) v = mask[n] > 0.f ? v : 0.f;
+    y[n] = v;
+    if (y2) y2[n] = v;
   }
 }
 
@@ -134,39 +153,25 @@ __global__ __launch_bounds__(256) void se_bwd_partial(const float* __restrict__ 
   }
 }
 
-// one workgroup: dgate -> dz2 (sigmoid'), db2; dg1 = W2^T dz2 -> dz1 (relu'), db1.  dz2 / dz1 go to
-// the workspace for the grid-wide outer products below.
-__global__ __launch_bounds__(256) void se_mlp_bwd_vec(const float* __restrict__ part, int nparts, int C, int Cr,
-                                                      const float* __restrict__ g1, const float* __restrict__ gate,
-                                                      const float* __restrict__ W2, float* __restrict__ db1,
-                                                      float* __restrict__ db2, float* __restrict__ dz2g,
-                                                      float* __restrict__ dz1g) {
-  extern __shared__ float sz[];   // dz2 [C]
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float dg = 0.f;
-    for (int p = 0; p < nparts; ++p) dg += part[(long)p * C + c];
-    const float s = gate[c];
-    const float v = dg * (s * (1.f - s));
-    sz[c] = v;
-    db2[c] = v;
-    dz2g[c] = v;
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < Cr; j += blockDim.x) {
-    float acc = 0.f;
-    for (int c = 0; c < C; ++c) acc = fmaf(sz[c], W2[(long)c * Cr + j], acc);
-    const float v = g1[j] > 0.f ? acc : 0.f;
-    db1[j] = v;
-    dz1g[j] = v;
-  }
+// dgate[c] = sum of the row-block partials (fixed order); dz2 = dgate * sigmoid'(.)  -> db2, dz2
+__global__ __launch_bounds__(256) void se_dgate_kernel(const float* __restrict__ part, int nparts, int C,
+                                                       const float* __restrict__ gate, float* __restrict__ db2,
+                                                       float* __restrict__ dz2) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float dg = 0.f;
+  for (int p = 0; p < nparts; ++p) dg += part[(long)p * C + c];
+  const float s = gate[c];
+  const float v = dg * (s * (1.f - s));
+  db2[c] = v;
+  dz2[c] = v;
 }
 
-// grid: dW2 = dz2 (x) g1, dW1 = dz1 (x) mean, dmean = W1^T dz1
+// grid: dW2 = dz2 (x) g1, dW1 = dz1 (x) mean
 __global__ __launch_bounds__(256) void se_mlp_bwd_outer(int C, int Cr, const float* __restrict__ mean,
-                                                        const float* __restrict__ g1, const float* __restrict__ W1,
-                                                        const float* __restrict__ dz2, const float* __restrict__ dz1,
-                                                        float* __restrict__ dW1, float* __restrict__ dW2,
-                                                        float* __restrict__ dmean) {
+                                                        const float* __restrict__ g1, const float* __restrict__ dz2,
+                                                        const float* __restrict__ dz1, float* __restrict__ dW1,
+                                                        float* __restrict__ dW2) {
   const long q = blockIdx.x * 256L + threadIdx.x;
   const long n2 = (long)C * Cr;
   if (q < n2) {
@@ -174,11 +179,6 @@ __global__ __launch_bounds__(256) void se_mlp_bwd_outer(int C, int Cr, const flo
   } else if (q < 2 * n2) {
     const long r = q - n2;
     dW1[r] = dz1[r / C] * mean[r % C];
-  } else if (q < 2 * n2 + C) {
-    const int c = (int)(q - 2 * n2);
-    float acc = 0.f;
-    for (int j = 0; j < Cr; ++j) acc = fmaf(dz1[j], W1[(long)j * C + c], acc);
-    dmean[c] = acc;
   }
 }
 
@@ -214,7 +214,9 @@ extern "C" int ctr_qnn_reduce_bwd(const float* A, int B, int F, int H, int R, co
 
 extern "C" int ctr_se_fwd_gate(const float* mean, int C, int Cr, const float* W1, const float* b1, const float* W2,
                                const float* b2, float* g1, float* gate, void* stream) {
-  se_mlp_fwd<<<1, 256, Cr * sizeof(float), (hipStream_t)stream>>>(mean, C, Cr, W1, b1, W2, b2, g1, gate);
+  hipStream_t s = (hipStream_t)stream;
+  matvec_rows_kernel<<<cdiv(Cr, 4), 256, 0, s>>>(W1, Cr, C, mean, b1, 1, g1);
+  matvec_rows_kernel<<<cdiv(C, 4), 256, 0, s>>>(W2, C, Cr, g1, b2, 2, gate);
   return check_launch("se_fwd_gate");
 }
 
@@ -246,8 +248,10 @@ extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B
   if (gate) {
     float* dz2 = dmean + C;                // [C]
     float* dz1 = dz2 + C;                  // [Cr <= C]
-    se_mlp_bwd_vec<<<1, 256, C * sizeof(float), s>>>(part, np, C, Cr, g1, gate, W2, db1, db2, dz2, dz1);
-    se_mlp_bwd_outer<<<cdiv(2L * C * Cr + C, 256), 256, 0, s>>>(C, Cr, mean, g1, W1, dz2, dz1, dW1, dW2, dmean);
+    se_dgate_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, np, C, gate, db2, dz2);
+    matvec_cols_kernel<<<cdiv(Cr, 64), 256, 0, s>>>(W2, C, Cr, dz2, g1, db1, dz1);     // dz1 = relu'(W2^T dz2)
+    matvec_cols_kernel<<<cdiv(C, 64), 256, 0, s>>>(W1, Cr, C, dz1, nullptr, dmean, nullptr);   // W1^T dz1
+    se_mlp_bwd_outer<<<cdiv(2L * C * Cr, 256), 256, 0, s>>>(C, Cr, mean, g1, dz2, dz1, dW1, dW2);
     long n = (long)B * C;
     int blocks = (int)std::min<long>((n + 255) / 256, 16384);
     add_row_bcast<<<blocks, 256, 0, s>>>(dx, B, C, dmean, (float)B);

@@ -85,12 +85,59 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_small(const float* __restrict
   }
 }
 
-// big rows: one workgroup per row (QNN pre-norm); dw partial per row-chunk of rows_per_block rows
+// big rows (QNN pre-norm, N = F*D = 6400): a workgroup takes rows_per_block rows; each thread keeps its
+// NPT columns of w*dy and h in registers, so dy and h are read once, and accumulates its columns'
+// dw partials across the rows in registers (dw_part: one row per workgroup).
+template <int NPT>
 __global__ __launch_bounds__(256) void rmsnorm_bwd_big(const float* __restrict__ dy, long ldy,
                                                        const float* __restrict__ h, long ldh,
                                                        const float* __restrict__ r, const float* __restrict__ w,
                                                        int M, int N, float* __restrict__ dh, long lddh,
                                                        int rows_per_block, float* __restrict__ dw_part) {
+  __shared__ float red[4];
+  const int m0 = blockIdx.x * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  float wv[NPT], acc[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int n = threadIdx.x + 256 * k;
+    wv[k] = n < N ? w[n] : 0.f;
+    acc[k] = 0.f;
+  }
+  for (int m = m0; m < m1; ++m) {
+    const float* gy = dy + (long)m * ldy;
+    const float* hv = h + (long)m * ldh;
+    const float rm = r[m];
+    float g[NPT], hh[NPT];
+    float dot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int n = threadIdx.x + 256 * k;
+      g[k] = n < N ? gy[n] : 0.f;
+      hh[k] = n < N ? hv[n] : 0.f;
+      dot = fmaf(wv[k] * g[k], hh[k], dot);
+      acc[k] = fmaf(g[k] * hh[k], rm, acc[k]);
+    }
+    dot = block_sum(dot, red);
+    const float coef = rm * rm * rm / (float)N * dot;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int n = threadIdx.x + 256 * k;
+      if (n < N) dh[(long)m * lddh + n] = wv[k] * g[k] * rm - hh[k] * coef;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int n = threadIdx.x + 256 * k;
+    if (n < N) dw_part[(long)blockIdx.x * N + n] = acc[k];
+  }
+}
+
+// fallback for rows wider than 32 * 256: two passes over the row
+__global__ __launch_bounds__(256) void rmsnorm_bwd_huge(const float* __restrict__ dy, long ldy,
+                                                        const float* __restrict__ h, long ldh,
+                                                        const float* __restrict__ r, const float* __restrict__ w,
+                                                        int M, int N, float* __restrict__ dh, long lddh,
+                                                        int rows_per_block, float* __restrict__ dw_part) {
   __shared__ float red[4];
   const int m0 = blockIdx.x * rows_per_block, m1 = min(M, m0 + rows_per_block);
   for (int m = m0; m < m1; ++m) {
@@ -213,9 +260,12 @@ extern "C" int ctr_rmsnorm_fwd(const float* x, long ldx, int M, int N, const flo
   return check_launch("rmsnorm_fwd");
 }
 
+// big rows: ~512 workgroups (2 per CU), at least 2 rows each
+static int big_rows_per_block(int M) { return std::max(2, cdiv(M, 512)); }
+
 extern "C" int ctr_rmsnorm_bwd_nparts(int M, int N) {
   if (N <= 64) return cdiv(M, 256);
-  return cdiv(M, 16);
+  return cdiv(M, big_rows_per_block(M));
 }
 
 extern "C" int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long ldh, const float* r, const float* w,
@@ -231,8 +281,12 @@ extern "C" int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long l
     else rmsnorm_bwd_small<16><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, add, ld_add, rpb, dw_part);
   } else {
     CTR_REQUIRE(add == nullptr, "big-row rmsnorm bwd: add unsupported");
-    const int rpb = 16;
-    rmsnorm_bwd_big<<<cdiv(M, rpb), 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
+    const int rpb = big_rows_per_block(M);
+    const int nb = cdiv(M, rpb);
+    if (N <= 256 * 8) rmsnorm_bwd_big<8><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
+    else if (N <= 256 * 16) rmsnorm_bwd_big<16><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
+    else if (N <= 256 * 32) rmsnorm_bwd_big<32><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
+    else rmsnorm_bwd_huge<<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
   }
   return check_launch("rmsnorm_bwd");
 }
