@@ -137,16 +137,18 @@ int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K
  * ------------------------------------------------------------------------------------------- */
 int ctr_ffn_supported(int D, int FF);          /* D in {16, 32, 64}, FF % 16 == 0 */
 int ctr_ffn_slab_rows(int M, int D);           /* workgroups of ctr_ffn_bwd = rows of its grad slab */
-/* y = norm_w * h * r, h = x + (gelu(x W1^T + b1) [dropout] W2^T + b2), r = 1/rms(h)               */
+int ctr_ffn_mask_words(int M, int FF);         /* uint32 words of the dropout keep-bit mask (16 bits per 16 cols) */
+/* y = norm_w * h * r, h = x + (gelu(x W1^T + b1) [dropout] W2^T + b2), r = 1/rms(h).  mask (nullable
+ * without dropout) receives the keep bits, row-major (M, FF/16) uint16.                            */
 int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
                 const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
-                float drop_scale, float* y, float* h, float* r, void* stream);
+                float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* stream);
 /* dh = grad wrt h (after ctr_rmsnorm_bwd).  dx = dh + (dact W1); per-workgroup weight-grad slab rows
  * (ld_slab floats): dW1 (FF, D) at 0, db1 (FF) at o_b1, dW2 (D, FF) at o_w2 -- colsum them (the
  * offsets may match the arena layout so one ctr_colsum lands in the grad buffer).  db2 = colsum(dh). */
 int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
-                const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* dx, float* slab,
-                long ld_slab, int o_b1, int o_w2, void* stream);
+                const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const uint32_t* mask,
+                float* dx, float* slab, long ld_slab, int o_b1, int o_w2, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Row / column ops                                                                (rowops.hip)

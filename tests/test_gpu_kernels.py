@@ -261,8 +261,9 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     seed, site = (5 << 32) | 9, 4
     key, thresh, scale = drop_args(seed, site, p, True)
     y, h, r = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
+    fmask = torch.zeros(L.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
     L.call("ctr_ffn_fwd", ptr(x), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(nw), 1e-6, key, thresh, scale,
-           ptr(y), ptr(h), ptr(r), stream())
+           ptr(fmask), ptr(y), ptr(h), ptr(r), stream())
     mask = torch.from_numpy(keep_mask(seed, site, p, (M, FF)).astype(np.float32)).cuda() if p > 0 else \
         torch.ones(M, FF, device="cuda")
     xr, W1r, b1r, W2r = (t.detach().double().requires_grad_() for t in (x, W1, b1, W2))
@@ -273,6 +274,10 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     assert rel(h.double(), hr) < 1e-5
     assert rel(r.double(), rr) < 1e-5
     assert rel(y.double(), nw.double() * hr * rr[:, None]) < 1e-5
+    if p > 0:   # stored keep bits == the oracle mask
+        words = fmask.cpu().numpy().view(np.uint16)[:M * (FF // 16)].reshape(M, FF // 16)
+        bits = (words[:, np.arange(FF) // 16] >> (np.arange(FF) % 16).astype(np.uint16)) & 1
+        assert np.array_equal(bits.astype(bool), mask.cpu().numpy().astype(bool))
     # backward from a random grad wrt h
     dh = torch.randn(M, D, device="cuda", generator=g)
     hr.backward(dh.double())
@@ -282,8 +287,8 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     o_w2 = o_b1 + (FF + 63) // 64 * 64
     ld = o_w2 + D * FF
     slab = torch.zeros(nb, ld, device="cuda")
-    L.call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(dx), ptr(slab),
-           ld, o_b1, o_w2, stream())
+    L.call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask),
+           ptr(dx), ptr(slab), ld, o_b1, o_w2, stream())
     red = slab.double().sum(0)
     assert rel(dx.double(), xr.grad) < 1e-5
     assert rel(red[:FF * D].view(FF, D), W1r.grad) < 1e-5

@@ -23,14 +23,25 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ P, int fe, int D,
                                                              float* __restrict__ out, long out_ld) {
+  extern __shared__ float sfe[];         // P [D][fe+1] | W row [fe] | bias row [fe]
   const int f = blockIdx.y, b0 = blockIdx.x * FE_ROWS;
   const int RG = 256 / D, d = threadIdx.x % D, rg = threadIdx.x / D;
+  const int FP = fe + 1;
+  float* sP = sfe;
+  float* sW = sfe + D * FP;
+  float* sB = sW + fe;
+  for (int q = threadIdx.x; q < D * fe; q += 256) sP[(q / fe) * FP + q % fe] = P[q];
+  for (int q = threadIdx.x; q < fe; q += 256) {
+    sW[q] = W[(long)f * fe + q];
+    sB[q] = bias ? bias[(long)f * fe + q] : 0.f;
+  }
+  __syncthreads();
   if (rg >= RG) return;
   float A = 0.f, Bv = 0.f;
   for (int k = 0; k < fe; ++k) {
-    const float pk = P[(long)d * fe + k];
-    A = fmaf(W[(long)f * fe + k], pk, A);
-    if (bias) Bv = fmaf(bias[(long)f * fe + k], pk, Bv);
+    const float pk = sP[d * FP + k];
+    A = fmaf(sW[k], pk, A);
+    Bv = fmaf(sB[k], pk, Bv);
   }
   const int b1 = min(B, b0 + FE_ROWS);
   for (int b = b0 + rg; b < b1; b += RG) out[(long)b * out_ld + (long)f * D + d] = fmaf(x[(long)b * F + f], A, Bv);
@@ -71,20 +82,30 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restri
 // one workgroup: S = sum over chunks (fixed order) into LDS, then
 // dW = S1 @ P, dbias = S0 @ P, dP = sum_f S1^T W + S0^T bias
 __global__ __launch_bounds__(1024) void feat_embed_bwd_final(int nchunk, int F, int D, int fe,
-                                                            const float* __restrict__ part,
-                                                            const float* __restrict__ W,
-                                                            const float* __restrict__ bias,
-                                                            const float* __restrict__ P,
+                                                            const float* __restrict__ part, const float* W,
+                                                            const float* bias, const float* P,
                                                             float* __restrict__ dW, float* __restrict__ dbias,
                                                             float* __restrict__ dP) {
-  extern __shared__ float sS[];          // [2][F][D]
+  extern __shared__ float sS[];          // [2][F][D] | P [D][fe] | W [F][fe] | bias [F][fe]
   const int n2 = 2 * F * D;
   for (int q = threadIdx.x; q < n2; q += blockDim.x) {
     float v = 0.f;
+#pragma unroll 4
     for (int c = 0; c < nchunk; ++c) v += part[(long)c * n2 + q];
     sS[q] = v;
   }
+  float* sPm = sS + n2;
+  float* sWm = sPm + D * fe;
+  float* sBm = sWm + F * fe;
+  for (int q = threadIdx.x; q < D * fe; q += blockDim.x) sPm[q] = P[q];
+  for (int q = threadIdx.x; q < F * fe; q += blockDim.x) {
+    sWm[q] = W[q];
+    sBm[q] = bias ? bias[q] : 0.f;
+  }
   __syncthreads();
+  P = sPm;
+  W = sWm;
+  bias = bias ? sBm : nullptr;
   const float* S1 = sS;
   const float* S0 = sS + F * D;
   for (int q = threadIdx.x; q < (F + D) * fe; q += blockDim.x) {
@@ -134,6 +155,7 @@ __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restric
     const float* t = arena + cm.tab_off[c] + row * dc;
     const float* p = arena + cm.proj_off[c] + (long)d * dc;
     float acc = 0.f;
+#pragma unroll 8
     for (int k = 0; k < dc; ++k) acc = fmaf(t[k], p[k], acc);
     cat_e[q] = acc;
     if (xf) xf[(long)b * xf_ld + (long)c * D + d] = drop_apply(drop, q, acc);
@@ -158,6 +180,7 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_rows(const int* __restrict_
     if (k < dc) {
       const float* p = arena + cm.proj_off[c] + k;
       const float* g = dcat + (long)bc * D;
+#pragma unroll 8
       for (int d = 0; d < D; ++d) acc = fmaf(g[d], p[(long)d * dc], acc);
     }
     contrib[q] = acc;
@@ -249,6 +272,7 @@ __global__ __launch_bounds__(64) void context_fwd_kernel(CtxArgs a) {
   if (d < D) {
     if (a.Fn > 0) {
       float s = 0.f;
+#pragma unroll 8
       for (int f = 0; f < a.Fn; ++f) s += a.num_e[(long)b * a.num_ld + (long)f * D + d];
       sctx[nctx * D + d] = s / (float)a.Fn;
     }
@@ -256,12 +280,14 @@ __global__ __launch_bounds__(64) void context_fwd_kernel(CtxArgs a) {
   if (a.Fn > 0) ++nctx;
   if (d < D && a.Fm > 0) {
     float s = 0.f;
+#pragma unroll 8
     for (int f = 0; f < a.Fm; ++f) s += a.mask_e[(long)b * a.mask_ld + (long)f * D + d];
     sctx[nctx * D + d] = s / (float)a.Fm;
   }
   if (a.Fm > 0) ++nctx;
   if (d < D) {
     float s = 0.f;
+#pragma unroll 8
     for (int c = 0; c < a.Fc; ++c) s += a.cat_e[((long)b * a.Fc + c) * D + d];
     sctx[nctx * D + d] = a.Fc > 0 ? s / (float)a.Fc : 0.f;
   }
@@ -274,6 +300,7 @@ __global__ __launch_bounds__(64) void context_fwd_kernel(CtxArgs a) {
     float h = 0.f;
     if (a.mode != 0) {
       float acc = 0.f;
+#pragma unroll 8
       for (int j = 0; j < W; ++j) acc = fmaf(sctx[j], a.Wc[(long)d * W + j], acc);
       h = acc + a.bc[d];
       h = h > 0.f ? h : 0.f;
@@ -321,6 +348,7 @@ __global__ __launch_bounds__(64) void context_bwd_kernel(CtxBwdArgs a) {
   for (int j = d; j < W; j += 64) {
     float acc = 0.f;
     if (f.mode != 0)
+#pragma unroll 8
       for (int i = 0; i < D; ++i) acc = fmaf(sdp[i], f.Wc[(long)i * W + j], acc);
     sdctx[j] = acc;
   }
@@ -333,6 +361,7 @@ __global__ __launch_bounds__(64) void context_bwd_kernel(CtxBwdArgs a) {
     float g = sdctx[slot * D + d];
     if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fcslot * D + d];
     g = g / (float)f.Fn;
+#pragma unroll 8
     for (int k = 0; k < f.Fn; ++k) a.dnum[(long)b * f.num_ld + (long)k * D + d] += g;
     ++slot;
     ++fcslot;
@@ -341,6 +370,7 @@ __global__ __launch_bounds__(64) void context_bwd_kernel(CtxBwdArgs a) {
     float g = sdctx[slot * D + d];
     if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fcslot * D + d];
     g = g / (float)f.Fm;
+#pragma unroll 8
     for (int k = 0; k < f.Fm; ++k) a.dmask[(long)b * f.mask_ld + (long)k * D + d] += g;
     ++slot;
     ++fcslot;
@@ -368,8 +398,10 @@ extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, 
                                   int fe, int D, float* out, long out_ld, void* stream) {
   if (B == 0 || F == 0) return 0;
   CTR_REQUIRE(D <= 256, "D > 256");
-  feat_embed_fwd_kernel<<<dim3(cdiv(B, FE_ROWS), F), 256, 0, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D, out,
-                                                                                     out_ld);
+  const size_t sm = ((size_t)D * (fe + 1) + 2 * fe) * sizeof(float);
+  CTR_REQUIRE(sm <= 64 * 1024, "feat_embed: D x fe projection exceeds LDS");
+  feat_embed_fwd_kernel<<<dim3(cdiv(B, FE_ROWS), F), 256, sm, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D, out,
+                                                                                      out_ld);
   return check_launch("feat_embed_fwd");
 }
 
@@ -384,13 +416,19 @@ extern "C" int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, 
                                   float* dP, float* ws, void* stream) {
   if (F == 0) return 0;
   CTR_REQUIRE(D <= 256, "D > 256");
-  CTR_REQUIRE((size_t)2 * F * D * sizeof(float) <= 64 * 1024, "feat_embed_bwd: 2*F*D exceeds LDS");
+  const size_t sm = ((size_t)2 * F * D + (size_t)D * fe + (size_t)2 * F * fe) * sizeof(float);
+  CTR_REQUIRE(sm <= 160 * 1024, "feat_embed_bwd: sums + weights exceed LDS");
   hipStream_t s = (hipStream_t)stream;
   const int nch = fe_chunks(B);
   const int rpc = cdiv(B, nch);
   feat_embed_bwd_sums<<<dim3(F, nch), 256, 0, s>>>(x, B, F, D, dout, dout_ld, rpc, ws);
-  feat_embed_bwd_final<<<1, 1024, (size_t)2 * F * D * sizeof(float), s>>>(nch, F, D, fe, ws, W, bias, P, dW, dbias,
-                                                                          dP);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)feat_embed_bwd_final, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  feat_embed_bwd_final<<<1, 1024, sm, s>>>(nch, F, D, fe, ws, W, bias, P, dW, dbias, dP);
   return check_launch("feat_embed_bwd");
 }
 

@@ -35,6 +35,7 @@ struct FfnArgs {
   const float* nw;     // (D) norm2 weight
   float eps;
   Drop drop;
+  uint16_t* mask;      // (M, FF/16) dropout keep bits: written by the forward, read by the backward
   // forward outputs
   float* y;            // (M, D) = norm2(x + ffn(x))
   float* h;            // (M, D) pre-norm sum (saved for the norm backward)
@@ -129,35 +130,55 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int f0 = 0; f0 < a.FF; f0 += 16) {
+  // W slices of chunk f0 are prefetched one chunk ahead (global latency overlaps the chunk's MFMAs)
+  float bv[T::KQ], bw[T::NJ][4], bias;
+  auto load_w = [&](int f0, float (&v1)[T::KQ], float (&v2)[T::NJ][4], float& b) {
     const int ff = f0 + c;
-    float bv[T::KQ];
 #pragma unroll
-    for (int kq = 0; kq < T::KQ; kq += 4)
-      *(f32x4*)&bv[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
-    f32x4 pre[T::NI];
-    dcontract<D>(xw, bv, pre, g, c);
-    const float bias = a.b1[ff];
-    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]
-#pragma unroll
-    for (int i = 0; i < T::NI; ++i)
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = 16 * i + 4 * g + rr;
-        float v = gelu_f(pre[i][rr] + bias);
-        if (a.drop.thresh) v = drop_apply(a.drop, (uint32_t)((long)(m0 + w * T::RW + row) * a.FF + ff), v);
-        st[row * T::SS + c] = v;
-      }
-    __builtin_amdgcn_wave_barrier();
-    float bw[T::NJ][4];
+    for (int kq = 0; kq < T::KQ; kq += 4) *(f32x4*)&v1[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) {
       const f32x4 v = *(const f32x4*)(a.W2 + (long)(16 * j + c) * a.FF + f0 + 4 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) bw[j][t] = v[t];
+      for (int t = 0; t < 4; ++t) v2[j][t] = v[t];
     }
+    b = a.b1[ff];
+  };
+  load_w(0, bv, bw, bias);
+  const int FW = a.FF / 16;
+  for (int f0 = 0; f0 < a.FF; f0 += 16) {
+    const int ff = f0 + c;
+    float bvn[T::KQ], bwn[T::NJ][4], biasn;
+    if (f0 + 16 < a.FF) load_w(f0 + 16, bvn, bwn, biasn);
+    f32x4 pre[T::NI];
+    dcontract<D>(xw, bv, pre, g, c);
+    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]; keep bits -> mask (16 per row and chunk)
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
+        float v = gelu_f(pre[i][rr] + bias);
+        if (a.drop.thresh) {
+          const bool keep = drop_keep(a.drop, (uint32_t)((long)m * a.FF + ff));
+          v = keep ? v * a.drop.scale : 0.f;
+          const unsigned long long bal = __ballot(keep);
+          if (c == 0 && a.mask && m < a.M) a.mask[(long)m * FW + (f0 >> 4)] = (uint16_t)(bal >> (16 * g));
+        }
+        st[row * T::SS + c] = v;
+      }
+    __builtin_amdgcn_wave_barrier();
     fcontract<D>(st, bw, yacc, g, c);
     __builtin_amdgcn_wave_barrier();
+    if (f0 + 16 < a.FF) {
+#pragma unroll
+      for (int kq = 0; kq < T::KQ; ++kq) bv[kq] = bvn[kq];
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bw[j][t] = bwn[j][t];
+      bias = biasn;
+    }
   }
 
   // h = x + (y + b2); RMSNorm over the row (the row's D values sit in the 16 lanes of one lane group)
@@ -211,24 +232,29 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // W slices of chunk f0 are prefetched one chunk ahead
+  float bv1[T::KQ], bv2[T::KQ], bw[T::NJ][4], bias;
+  auto load_w = [&](int f0, float (&v1)[T::KQ], float (&v2)[T::KQ], float (&v3)[T::NJ][4], float& b) {
+    const int ff = f0 + c;
+#pragma unroll
+    for (int kq = 0; kq < T::KQ; kq += 4) *(f32x4*)&v1[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
+#pragma unroll
+    for (int kk = 0; kk < T::KQ; ++kk) v2[kk] = a.W2[(long)(g * T::KQ + kk) * a.FF + ff];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) v3[j][t] = a.W1[(long)(f0 + 4 * g + t) * D + 16 * j + c];
+    b = a.b1[ff];
+  };
+  load_w(0, bv1, bv2, bw, bias);
+  const int FW = a.FF / 16;
   for (int f0 = 0; f0 < a.FF; f0 += 16) {
     const int ff = f0 + c;
-    const float bias = a.b1[ff];
-    f32x4 pre[T::NI];
-    {
-      float bv[T::KQ];
-#pragma unroll
-      for (int kq = 0; kq < T::KQ; kq += 4)
-        *(f32x4*)&bv[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
-      dcontract<D>(xw, bv, pre, g, c);
-    }
-    f32x4 dact[T::NI];
-    {
-      float bv[T::KQ];
-#pragma unroll
-      for (int kk = 0; kk < T::KQ; ++kk) bv[kk] = a.W2[(long)(g * T::KQ + kk) * a.FF + ff];
-      dcontract<D>(dw, bv, dact, g, c);
-    }
+    float bv1n[T::KQ], bv2n[T::KQ], bwn[T::NJ][4], biasn;
+    if (f0 + 16 < a.FF) load_w(f0 + 16, bv1n, bv2n, bwn, biasn);
+    f32x4 pre[T::NI], dact[T::NI];
+    dcontract<D>(xw, bv1, pre, g, c);
+    dcontract<D>(dw, bv2, dact, g, c);
     f32x4 dw2[T::NJ], dw1[T::NJ];
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) dw2[j] = dw1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -237,13 +263,17 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
     for (int i = 0; i < T::NI; ++i)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int row = 16 * i + 4 * g + rr;
-        const uint32_t di = (uint32_t)((long)(m0 + w * T::RW + row) * a.FF + ff);
+        const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
         const float z = pre[i][rr] + bias;
-        const bool keep = a.drop.thresh ? drop_keep(a.drop, di) : true;
+        // gelu and gelu' share erf; exp on the hardware exp2 (a few ulp on gelu' only)
+        const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+        const float gz = z * cdf;
+        const float gg = cdf + z * (__builtin_amdgcn_exp2f(-0.72134752044448170f * z * z) * 0.39894228040143268f);
+        bool keep = true;
+        if (a.drop.thresh) keep = m < a.M && ((a.mask[(long)m * FW + (f0 >> 4)] >> c) & 1u);
         const float sc = a.drop.thresh ? (keep ? a.drop.scale : 0.f) : 1.f;
-        const float fo = a.drop.thresh ? (keep ? gelu_f(z) * a.drop.scale : 0.f) : gelu_f(z);
-        const float da = dact[i][rr] * sc * gelu_grad(z);
+        const float fo = (m < a.M) ? gz * sc : 0.f;
+        const float da = dact[i][rr] * sc * gg;
         dact[i][rr] = da;
         db += da;
         // dW2[d][ff] += dh[row][d] fo[row][ff];  dW1[ff][d] += dact[row][ff] x[row][d]   (k-set rows {4g+rr})
@@ -261,11 +291,6 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) st[(16 * i + 4 * g + rr) * T::SS + c] = dact[i][rr];
     __builtin_amdgcn_wave_barrier();
-    float bw[T::NJ][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j) bw[j][t] = a.W1[(long)(f0 + 4 * g + t) * D + 16 * j + c];
     fcontract<D>(st, bw, dxacc, g, c);
     // weight-grad partials of this wave -> LDS; fixed-order sum over the 4 waves -> slab
     __syncthreads();                        // previous chunk's reduction has read `red`
@@ -279,14 +304,26 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
     if (g == 0) pw[32 * D + c] = db;
     __syncthreads();
     for (int q = tid; q < T::PW; q += 256) {
-      const float s = ((red[q] + red[T::PW + q]) + red[2 * T::PW + q]) + red[3 * T::PW + q];
-      if (q < 16 * D) slab[(long)f0 * D + q] = s;
+      const float sum = ((red[q] + red[T::PW + q]) + red[2 * T::PW + q]) + red[3 * T::PW + q];
+      if (q < 16 * D) slab[(long)f0 * D + q] = sum;
       else if (q < 32 * D) {
         const int u = q - 16 * D;
-        slab[a.o_w2 + (long)(u >> 4) * a.FF + f0 + (u & 15)] = s;
+        slab[a.o_w2 + (long)(u >> 4) * a.FF + f0 + (u & 15)] = sum;
       } else {
-        slab[a.o_b1 + f0 + (q - 32 * D)] = s;
+        slab[a.o_b1 + f0 + (q - 32 * D)] = sum;
       }
+    }
+    if (f0 + 16 < a.FF) {
+#pragma unroll
+      for (int kq = 0; kq < T::KQ; ++kq) {
+        bv1[kq] = bv1n[kq];
+        bv2[kq] = bv2n[kq];
+      }
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bw[j][t] = bwn[j][t];
+      bias = biasn;
     }
   }
 
@@ -332,27 +369,33 @@ extern "C" int ctr_ffn_supported(int D, int FF) { return ffn_shape_ok(D, FF) ? 1
 
 extern "C" int ctr_ffn_slab_rows(int M, int D) { return cdiv(M, D >= 64 ? 64 : 128); }
 
+extern "C" int ctr_ffn_mask_words(int M, int FF) { return (int)(((long)M * (FF / 16) + 1) / 2); }
+
 extern "C" int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
                            const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
-                           float drop_scale, float* y, float* h, float* r, void* stream) {
+                           float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* stream) {
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_fwd: needs D in {16,32,64} and FF % 16 == 0");
   if (M <= 0) return 0;
   FfnArgs a = {};
   a.M = M; a.FF = FF; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.b2 = b2; a.nw = norm_w; a.eps = eps;
   a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = (uint16_t*)mask;
   a.y = y; a.h = h; a.r = r;
   return ffn_dispatch(a, D, false, (hipStream_t)stream);
 }
 
 extern "C" int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
-                           const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, float* dx,
-                           float* slab, long ld_slab, int o_b1, int o_w2, void* stream) {
+                           const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale,
+                           const uint32_t* mask, float* dx, float* slab, long ld_slab, int o_b1, int o_w2,
+                           void* stream) {
+  CTR_REQUIRE(!drop_thresh || mask, "ctr_ffn_bwd with dropout needs the forward's keep bits");
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd: needs D in {16,32,64} and FF % 16 == 0");
   CTR_REQUIRE(o_b1 >= FF * D && o_w2 >= o_b1 + FF && ld_slab >= (long)o_w2 + (long)D * FF, "ctr_ffn_bwd: slab layout");
   if (M <= 0) return 0;
   FfnArgs a = {};
   a.M = M; a.FF = FF; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2;
   a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = (uint16_t*)const_cast<uint32_t*>(mask);
   a.dh = dh; a.dx = dx; a.slab = slab; a.ld_slab = ld_slab; a.o_b1 = o_b1; a.o_w2 = o_w2;
   return ffn_dispatch(a, D, true, (hipStream_t)stream);
 }

@@ -37,24 +37,53 @@ struct HistView {
 };
 
 // Brings one row from tick s to tick t_idle with grad 0, then (grow != null) applies tick t_idle+1 with
-// grad grow*coef.  The row is spread over lg lanes: lane l holds elements l, l+lg, ... (nq of them).
+// grad grow*coef.  The row is spread over lg lanes.  Element of register slot q in lane l:
+//   strided (any width):          j = l + lg*q, q < nq
+//   contiguous (width % 8 == 0):  j = 8l + q   -- two 16-byte loads / stores per array per lane
 // A row whose moments are all zero (never stepped with a non-zero grad) stays zero under idle ticks:
 // only the decay multiply and the EMA remain.  With m == v == 0, adam_elem(g = 0) gives m = v = +0,
 // denom = eps and p = fmaf(-step, +0, p * decay) == p * decay: bit for bit the same.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool VEC>
 __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __restrict__ m_row,
                                            float* __restrict__ v_row, float* __restrict__ e_row, int width, int l,
                                            int lg, int nq, const HistView& hv, int s, int t_idle,
                                            const float* __restrict__ grow, float coef) {
   float p[LQ], m[LQ], v[LQ], e[LQ];
+  const bool vlane = VEC && 8 * l < width;
+  auto elem = [&](int q) { return VEC ? 8 * l + q : l + lg * q; };
+  auto live = [&](int q) { return VEC ? vlane : (q < nq && l + lg * q < width); };
+  if (VEC) {
 #pragma unroll
-  for (int q = 0; q < LQ; ++q) {
-    const int j = l + lg * q;
-    p[q] = m[q] = v[q] = e[q] = 0.0f;
-    if (q < nq && j < width) {
-      p[q] = p_row[j];
-      m[q] = m_row[j];
-      v[q] = v_row[j];
-      if (e_row) e[q] = e_row[j];
+    for (int q = 0; q < LQ; ++q) p[q] = m[q] = v[q] = e[q] = 0.0f;
+    if (vlane) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 pv = *(const f32x4*)(p_row + 8 * l + 4 * h), mv = *(const f32x4*)(m_row + 8 * l + 4 * h);
+        const f32x4 vv = *(const f32x4*)(v_row + 8 * l + 4 * h);
+        const f32x4 ev = e_row ? *(const f32x4*)(e_row + 8 * l + 4 * h) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          p[4 * h + t] = pv[t];
+          m[4 * h + t] = mv[t];
+          v[4 * h + t] = vv[t];
+          e[4 * h + t] = ev[t];
+        }
+      }
+    }
+    nq = LQ;
+  } else {
+#pragma unroll
+    for (int q = 0; q < LQ; ++q) {
+      const int j = l + lg * q;
+      p[q] = m[q] = v[q] = e[q] = 0.0f;
+      if (q < nq && j < width) {
+        p[q] = p_row[j];
+        m[q] = m_row[j];
+        v[q] = v_row[j];
+        if (e_row) e[q] = e_row[j];
+      }
     }
   }
   bool zero = true;
@@ -95,19 +124,29 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
   if (grow) {
     const OptScalars sc = hv[t_idle + 1];
 #pragma unroll
+    for (int q = 0; q < LQ; ++q)
+      if (live(q)) adam_ema_elem(sc, p[q], m[q], v[q], e[q], grow[elem(q)] * coef, sc.do_adam != 0);
+  }
+  if (VEC) {
+    if (vlane) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        *(f32x4*)(p_row + 8 * l + 4 * h) = f32x4{p[4 * h], p[4 * h + 1], p[4 * h + 2], p[4 * h + 3]};
+        *(f32x4*)(m_row + 8 * l + 4 * h) = f32x4{m[4 * h], m[4 * h + 1], m[4 * h + 2], m[4 * h + 3]};
+        *(f32x4*)(v_row + 8 * l + 4 * h) = f32x4{v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
+        if (e_row) *(f32x4*)(e_row + 8 * l + 4 * h) = f32x4{e[4 * h], e[4 * h + 1], e[4 * h + 2], e[4 * h + 3]};
+      }
+    }
+  } else {
+#pragma unroll
     for (int q = 0; q < LQ; ++q) {
       const int j = l + lg * q;
-      if (q < nq && j < width) adam_ema_elem(sc, p[q], m[q], v[q], e[q], grow[j] * coef, sc.do_adam != 0);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < LQ; ++q) {
-    const int j = l + lg * q;
-    if (q < nq && j < width) {
-      p_row[j] = p[q];
-      m_row[j] = m[q];
-      v_row[j] = v[q];
-      if (e_row) e_row[j] = e[q];
+      if (q < nq && j < width) {
+        p_row[j] = p[q];
+        m_row[j] = m[q];
+        v_row[j] = v[q];
+        if (e_row) e_row[j] = e[q];
+      }
     }
   }
 }
@@ -154,8 +193,8 @@ __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* _
   if (!win) return;
   const ctr_lazy_tab_t tb = tabs[ti];
   const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
-  replay_row(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s, tick,
-             nullptr, 0.0f);
+  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s, tick,
+                    nullptr, 0.0f);
 }
 
 // One 8-lane group per compact grad slot: keys are unique, so no claim is needed.
@@ -183,8 +222,8 @@ __global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* 
   const int s = tb.last[row];
   const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
   const float coef = coef_ptr ? *coef_ptr : 1.0f;
-  replay_row(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s, tick - 1,
-             G + item * (long)g_ld, coef);
+  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s,
+                    tick - 1, G + item * (long)g_ld, coef);
   if (l8 == 0) tb.last[row] = tick;
 }
 
@@ -229,7 +268,10 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
     if (s >= tick) continue;
     const int l = tid & (lg - 1);
     const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
-    replay_row(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), hv, s, tick, nullptr, 0.0f);
+    if ((tb.width & 7) == 0 && (tb.p_off & 3) == 0)     // block-uniform
+      replay_row<true>(r.p, r.m, r.v, r.e, tb.width, l, lg, LQ, hv, s, tick, nullptr, 0.0f);
+    else
+      replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), hv, s, tick, nullptr, 0.0f);
     if (l == 0) tb.last[row] = tick;
   }
 }

@@ -96,20 +96,20 @@ __global__ __launch_bounds__(256) void matvec_rows_kernel(const float* __restric
   }
 }
 
-// y[n] = sum_r x[r] * A[r][n] for row-major A (R x N): 64 columns x 4 row groups per workgroup, the four
-// partials summed in a fixed order.  mask (nullable): y[n] = 0 where mask[n] <= 0 (relu').  y2: copy.
+// y[n] = sum_r x[r] * A[r][n] for row-major A (R x N): one wave per output column, lanes stride the
+// rows (strided reads of a small, L2-resident matrix), fixed-order wave reduction.
+// mask (nullable): y[n] = 0 where mask[n] <= 0 (relu').  y2: copy.
 __global__ __launch_bounds__(256) void matvec_cols_kernel(const float* __restrict__ A, int R, int N,
                                                           const float* __restrict__ x, const float* __restrict__ mask,
                                                           float* __restrict__ y, float* __restrict__ y2) {
-  __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6, n = blockIdx.x * 64 + cl;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (n >= N) return;
   float s = 0.f;
-  if (n < N)
-    for (int r = rg; r < R; r += 4) s = fmaf(x[r], A[(long)r * N + n], s);
-  red[rg][cl] = s;
-  __syncthreads();
-  if (rg == 0 && n < N) {
-    float v = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+#pragma unroll 4
+  for (int r = lane; r < R; r += 64) s = fmaf(x[r], A[(long)r * N + n], s);
+  s = wave_sum(s);
+  if (lane == 0) {
+    float v = s;
     if (mask) v = mask[n] > 0.f ? v : 0.f;
     y[n] = v;
     if (y2) y2[n] = v;
@@ -249,8 +249,8 @@ extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B
     float* dz2 = dmean + C;                // [C]
     float* dz1 = dz2 + C;                  // [Cr <= C]
     se_dgate_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, np, C, gate, db2, dz2);
-    matvec_cols_kernel<<<cdiv(Cr, 64), 256, 0, s>>>(W2, C, Cr, dz2, g1, db1, dz1);     // dz1 = relu'(W2^T dz2)
-    matvec_cols_kernel<<<cdiv(C, 64), 256, 0, s>>>(W1, Cr, C, dz1, nullptr, dmean, nullptr);   // W1^T dz1
+    matvec_cols_kernel<<<cdiv(Cr, 4), 256, 0, s>>>(W2, C, Cr, dz2, g1, db1, dz1);     // dz1 = relu'(W2^T dz2)
+    matvec_cols_kernel<<<cdiv(C, 4), 256, 0, s>>>(W1, Cr, C, dz1, nullptr, dmean, nullptr);   // W1^T dz1
     se_mlp_bwd_outer<<<cdiv(2L * C * Cr, 256), 256, 0, s>>>(C, Cr, mean, g1, dz2, dz1, dW1, dW2);
     long n = (long)B * C;
     int blocks = (int)std::min<long>((n + 255) / 256, 16384);

@@ -293,12 +293,14 @@ class Engine:
             h2 = W.get(f"h2_{li}", (M, D))
             r2 = W.get(f"r2_{li}", (M,))
             x2 = W.get(f"x{li + 1}", (B, K, D))
-            act = fo = None
+            act = fo = fmask = None
             if self.ffn_fused:
                 # Linear -> GELU -> Dropout -> Linear -> +x1 -> RMSNorm in one kernel (ffn.hip)
+                fmask = W.get(f"fmask{li}", (_lib.query("ctr_ffn_mask_words", M, FF),), torch.int32) \
+                    if dfk[1] else None
                 call("ctr_ffn_fwd", ptr(x1), M, D, FF, ptr(P[pre + "ffn.0.weight"]), ptr(P[pre + "ffn.0.bias"]),
                      ptr(P[pre + "ffn.3.weight"]), ptr(P[pre + "ffn.3.bias"]), ptr(P[pre + "norm2.w"]), 1e-6, *dfk,
-                     ptr(x2), ptr(h2), ptr(r2), st)
+                     ptr(fmask), ptr(x2), ptr(h2), ptr(r2), st)
             else:
                 act = W.get(f"ffa{li}", (M, FF))
                 fo = W.get(f"ffo{li}", (M, FF))
@@ -309,7 +311,7 @@ class Engine:
                           GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
                                   norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
             Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, amask=amask, h1=h1, r1=r1, x1=x1,
-                      act=act, fo=fo,
+                      act=act, fo=fo, fmask=fmask,
                       h2=h2, r2=r2)
             layers.append(Ls)
             xs.append(x2)
@@ -558,8 +560,8 @@ class Engine:
             nb = _lib.query("ctr_ffn_slab_rows", M, D)
             slab = W.get_zeroed("ffn_slab", (nb, ld_sl))
             call("ctr_ffn_bwd", ptr(Ls["x1"]), ptr(dh2), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
-                 ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(dx1), ptr(slab), ld_sl, o_b1,
-                 o_w2, st)
+                 ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dx1),
+                 ptr(slab), ld_sl, o_b1, o_w2, st)
             self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
             self.colsum(ptr(dh2), D, M, D, ptr(G[pre + "ffn.3.bias"]))
         else:
