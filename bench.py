@@ -52,6 +52,20 @@ def synth_batches(nb, B, L, Fn, Fm, cards, vocab, device, seed):
     return out
 
 
+MFMA_F32_PEAK_TFS = 157.3   # MI355X dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md
+
+
+def kernel_work(name, a, B, ffn_M):
+    """(bound, algorithmic units per launch, unit) of the timed entry points -- SURVEY §8(d) per-unit
+    figures x the units one launch processes ("Roofline accounting")."""
+    D, FF = a.D, a.ffn_hidden
+    if name == "ctr_ffn_bwd":     # dfo = dh W2, dW2 = dh^T fo, dW1 = dact^T x, dx = dact W1 (pre recompute excluded)
+        return "mfma", 8.0 * ffn_M * FF * D, "flop"
+    if name == "ctr_ffn_fwd":     # pre = x W1^T, y = fo W2^T
+        return "mfma", 4.0 * ffn_M * FF * D, "flop"
+    return None
+
+
 def opt_algorithmic_bytes(opt, with_ema):
     """HBM bytes one fused clip/AdamW/EMA launch must move (per element: read+write p, m, v (+ema) = 24
     (+8) B; dense grads read 4 B; no-grad params EMA-only: read p, e, write e = 12 B; plus the touched
@@ -69,6 +83,32 @@ def opt_algorithmic_bytes(opt, with_ema):
         t = tg[name]
         b += int(t["n_uniq"].item()) * t["width"] * 4
     return b
+
+
+def pmc_traffic(name):
+    """HBM bytes per launch of the entry point's kernel from the committed rocprofv3 PMC summaries
+    (profiles/r01/pmc_{fetch,write}.csv: separate --pmc FETCH_SIZE / WRITE_SIZE passes of this bench),
+    corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE counts half of wide streaming reads:
+    x2).  None when the summaries are absent."""
+    import csv
+    kern = {"ctr_ffn_bwd": "ffn_bwd_kernel", "ctr_ffn_fwd": "ffn_fwd_kernel"}.get(name)
+    base = os.path.join(REPO, "profiles", "r01")
+    if kern is None:
+        return None
+    vals = {}
+    for ctr, fn in (("FETCH_SIZE", "pmc_fetch.csv"), ("WRITE_SIZE", "pmc_write.csv")):
+        path = os.path.join(base, fn)
+        if not os.path.exists(path):
+            return None
+        xs = []
+        with open(path) as fh:
+            for r in csv.DictReader(fh):
+                if kern in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
+                    xs.append(float(r["Counter_Value"]))
+        if not xs:
+            return None
+        vals[ctr] = sum(xs) / len(xs) * 1024.0      # rocprofv3 reports KB
+    return round(2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"])
 
 
 def cpu_baseline(cfg, B, L, seed=0):
@@ -166,6 +206,10 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     opt.time_kernels(True)
+    from tossctr import _lib
+    timed = ("ctr_ffn_bwd", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_touch",
+             "ctr_lazy_update", "ctr_adamw_ema")
+    _lib.time_calls(timed)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = run(g, g)
@@ -183,6 +227,8 @@ def main():
     opt_ms = opt.kernel_ms()
     flush_ms = fl[0].elapsed_time(fl[1])
     opt.time_kernels(False)
+    kstats = _lib.timed_ms()
+    _lib.time_calls(())
     if pg is not None:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -192,8 +238,25 @@ def main():
     if rank == 0:
         ms = elapsed / args.steps * 1e3
         samples = args.batch * world * args.steps / elapsed
-        nbytes = opt_algorithmic_bytes(opt, ema is not None)
-        achieved = nbytes / (opt_ms * 1e-3) / 1e9
+        # dominant timed kernel (by device time per step) and its roofline
+        a = model.arch
+        ffn_M = args.batch * a.K_eff(args.seq_len)
+        per_step = {n: c * ms / args.steps for n, (c, ms) in kstats.items()}
+        kernels = {n: {"calls_per_step": round(kstats[n][0] / args.steps, 2), "avg_launch_ms": round(kstats[n][1], 4),
+                       "ms_per_step": round(per_step[n], 4)} for n in kstats}
+        roof = None
+        for n in sorted(per_step, key=per_step.get, reverse=True):
+            w = kernel_work(n, a, args.batch, ffn_M)
+            if w is None:
+                continue
+            bound, work, unit = w
+            ach = work / (kstats[n][1] * 1e-3) / 1e12
+            roof = {"bound": bound, "kernel": n, "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": round(ach / MFMA_F32_PEAK_TFS, 4),
+                    "traffic": pmc_traffic(n), "work_per_launch": work, "work_unit": unit,
+                    "avg_launch_ms": round(kstats[n][1], 4), "ms_per_step": round(per_step[n], 4),
+                    "share_of_step": round(per_step[n] / ms, 4)}
+            break
         rec = {
             "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref",
             "value": round(samples, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
@@ -203,10 +266,8 @@ def main():
                                    "bs=4096 per GPU, full train step incl. clip+AdamW+EMA over 1.24B params",
                        "global_batch": args.batch * world, "seq_len": args.seq_len,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "hbm", "kernel": "adamw_ema_kernel (fused clip+AdamW+EMA stream)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_per_launch": nbytes, "avg_launch_ms": round(opt_ms, 4)},
+            "roofline": roof,
+            "kernels": kernels,
             "opt_ms_per_step": round(opt_ms, 3),
             "table_update": "dense stream" if args.dense_opt else "exact lazy (replay on read/grad; final flush timed)",
             "flush_ms": round(flush_ms, 3),

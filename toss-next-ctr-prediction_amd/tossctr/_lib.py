@@ -121,9 +121,39 @@ class CtrError(RuntimeError):
     pass
 
 
+_timed = {}     # entry name -> list of (start, end) torch.cuda.Event pairs, while timing is on
+
+
+def time_calls(names):
+    """Bracket every call of the named entry points with HIP events on the current stream (the stream
+    the library launches on); ``timed_ms()`` reads the per-call averages.  ``time_calls(())`` stops."""
+    _timed.clear()
+    for n in names:
+        _timed[n] = []
+
+
+def timed_ms():
+    """{name: (calls, average ms per call)} of the calls bracketed since time_calls()."""
+    import torch
+    torch.cuda.synchronize()
+    out = {}
+    for n, evs in _timed.items():
+        if evs:
+            out[n] = (len(evs), sum(a.elapsed_time(b) for a, b in evs) / len(evs))
+    return out
+
+
 def call(name, *args):
     lib = load()
+    ev = None
+    if name in _timed:
+        import torch
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        ev[0].record()
     rc = getattr(lib, name)(*args)
+    if ev is not None:
+        ev[1].record()
+        _timed[name].append(ev)
     if rc != 0:
         raise CtrError(f"{name} failed ({rc}): {lib.ctr_last_error().decode()}")
     return rc
