@@ -170,13 +170,22 @@ int ctr_loss(const float* z, const float* za, const float* y, int B, float aux_w
 /* ---------------------------------------------------------------------------------------------
  * QNN-alpha, src/models/qnn_alpha.py                                                  (qnn.hip)
  * ------------------------------------------------------------------------------------------- */
-/* U (H,D,R) <-> Ucat (D,H*R) so all heads' A = z @ U_h is one GEMM */
+/* U (H,D,R) <-> Ucat (D,H*R) (all heads side by side) */
 int ctr_qnn_ucat(const float* src, int H, int D, int R, float* dst, int inverse, void* stream);
-/* _pair_interaction_all reduction (l.86-97): S = sum_F A, quad = S^2 - sum_F A^2, inter = quad @ V_h */
-int ctr_qnn_reduce_fwd(const float* A, int B, int F, int H, int R, const float* V, int P, float* S, float* quad,
-                       float* inter, void* stream);
-int ctr_qnn_reduce_bwd(const float* A, int B, int F, int H, int R, const float* V, int P, const float* S,
-                       const float* dinter, float* dA, void* stream);
+/* V (H,R,P) -> block-diagonal Vfull (H*R, H*P) (inverse: extract the diagonal blocks), so the per-head
+ * products quad_h @ V_h and their grads are GEMMs                                                    */
+int ctr_qnn_vfull(const float* V, int H, int R, int P, float* vfull, int inverse, void* stream);
+/* _pair_interaction_all (l.86-97) without forming A = z @ Ucat: per sample b (z rows (F, D)):
+ * zsum = sum_f z_f, G = z^T z (D x D), S = zsum @ Ucat, quad = S*S - diag(Ucat^T G Ucat) (QR wide) */
+int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int QR, float* zsum, float* G,
+                     float* S, float* quad, void* stream);
+/* backward to z: dz_f = 2 Ucat (dquad o S) - 2 (Ucat diag(dquad) Ucat^T) z_f (+ dz_add, nullable);
+ * DS = dquad o S (for dUcat)                                                                       */
+int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
+                     const float* dquad, const float* dz_add, float* dz, float* DS, void* stream);
+/* dUcat = 2 (T1 - sum_e Ucat[e,c] T[d*D+e, c]) with T1 = zsum^T DS (D x QR), T = G^T dquad (D*D x QR) */
+int ctr_qnn_du_combine(const float* T1, const float* T, const float* ucat, int D, int QR, float* ducat,
+                       void* stream);
 /* SEBlock (l.17-26): gate from the batch mean; scale + QNN dropout (l.120-121) */
 int ctr_se_fwd_gate(const float* mean, int C, int Cr, const float* W1, const float* b1, const float* W2,
                     const float* b2, float* g1, float* gate, void* stream);

@@ -295,3 +295,48 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     assert rel(red[o_b1:o_b1 + FF], b1r.grad) < 1e-5
     assert rel(red[o_w2:o_w2 + D * FF].view(D, FF), W2r.grad) < 1e-5
     assert float(red[o_b1 + FF:o_w2].abs().max()) == 0.0 if o_w2 > o_b1 + FF else True
+
+
+@pytest.mark.parametrize("B,F,D,QR", [(37, 23, 16, 8), (64, 200, 32, 96), (9, 27, 64, 96), (5, 3, 32, 20)])
+def test_qnn_gram_vs_torch(B, F, D, QR):
+    """qnn.hip Gram form of _pair_interaction_all (src/models/qnn_alpha.py:86-97) vs the A = z @ U
+    formulation with autograd: S, quad, dz (incl. the added residual grad) and dUcat."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(B * F + D)
+    z = torch.randn(B, F, D, device="cuda", generator=g)
+    U = torch.randn(D, QR, device="cuda", generator=g) * 0.1
+    zsum, G = torch.empty(B, D, device="cuda"), torch.empty(B, D * D, device="cuda")
+    S, quad = torch.empty(B, QR, device="cuda"), torch.empty(B, QR, device="cuda")
+    L.call("ctr_qnn_gram_fwd", ptr(z), B, F, D, ptr(U), QR, ptr(zsum), ptr(G), ptr(S), ptr(quad), stream())
+    zr, Ur = z.double().requires_grad_(), U.double().requires_grad_()
+    A = zr @ Ur
+    s_ref = A.sum(1)
+    q_ref = s_ref * s_ref - (A * A).sum(1)
+    assert rel(S.double(), s_ref.detach()) < 1e-5
+    assert rel(quad.double(), q_ref.detach()) < 1e-5
+    assert rel(G.double().view(B, D, D), (zr.transpose(1, 2) @ zr).detach()) < 1e-5
+    dquad = torch.randn(B, QR, device="cuda", generator=g)
+    dz_add = torch.randn(B, F, D, device="cuda", generator=g)
+    q_ref.backward(dquad.double())
+    dz, DS = torch.empty(B, F, D, device="cuda"), torch.empty(B, QR, device="cuda")
+    L.call("ctr_qnn_gram_bwd", ptr(z), B, F, D, ptr(U), QR, ptr(S), ptr(dquad), ptr(dz_add), ptr(dz), ptr(DS),
+           stream())
+    assert rel(dz.double(), zr.grad + dz_add.double()) < 1e-5
+    T1 = (zsum.t() @ DS).contiguous()
+    T = (G.t() @ dquad).contiguous()
+    du = torch.empty(D, QR, device="cuda")
+    L.call("ctr_qnn_du_combine", ptr(T1), ptr(T), ptr(U), D, QR, ptr(du), stream())
+    assert rel(du.double(), Ur.grad) < 1e-5
+
+
+def test_qnn_vfull_roundtrip():
+    L = _lib()
+    H, R, P = 3, 4, 5
+    V = torch.randn(H, R, P, device="cuda")
+    vf = torch.full((H * R, H * P), 7.0, device="cuda")
+    L.call("ctr_qnn_vfull", ptr(V), H, R, P, ptr(vf), 0, stream())
+    ref = torch.block_diag(*[V[h] for h in range(H)])
+    assert torch.equal(vf, ref)
+    back = torch.empty_like(V)
+    L.call("ctr_qnn_vfull", ptr(vf), H, R, P, ptr(back), 1, stream())
+    assert torch.equal(back, V)

@@ -1,13 +1,26 @@
 // QNN-alpha feature interaction (src/models/qnn_alpha.py):
 //   pair_interaction_all (l.86-97): per head h, A = z @ U_h (B,F,r); s = sum_F A; quad = s*s - sum_F A*A;
-//                                   out_h = quad @ V_h.   A for all heads comes from ONE MFMA GEMM
-//                                   (B*F, D) x (D, H*r) (gemm.hip) on the head-concatenated U; this file
-//                                   holds the F-reduction + block-diagonal V product and their backward.
+//                                   out_h = quad @ V_h.
 //   SEBlock (l.17-26): gate = sigmoid(W2 relu(W1 mean_B(x) + b1) + b2); x * gate  (batch-coupled).
+//
+// The (B*F) x (H*r) tensor A is never formed.  With Ucat = [U_1 .. U_H] (D x QR) and per-sample
+// Gram matrices G_b = z_b^T z_b (D x D) and zsum_b = sum_f z_bf:
+//   s    = zsum_b @ Ucat,                 sum_f A^2 = diag(Ucat^T G_b Ucat)
+//   dz_f = sum_c dA_fc U_c = 2 U (dquad o s) - 2 (U diag(dquad) U^T) z_f      (dA = 2 dquad (s - A))
+//   dU   = 2 [ zsum^T (dquad o s) - sum_b G_b U diag(dquad_b) ]               (batched GEMMs)
+// i.e. the same sums re-associated (fp32 rounding differs at the 1e-7 level): the interaction costs
+// two passes over z (105 MB at cfg2) instead of a 315 MB A tensor written, read and its gradient
+// written and read twice.  The head-block-diagonal V products are plain GEMMs on Vfull (QR x H*P).
 #include "common.h"
 #include "ctr_hip.h"
 
 namespace ctr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 mfma4q(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
 // U (H, D, R) <-> Ucat (D, H*R)
 __global__ void ucat_kernel(const float* __restrict__ src, int H, int D, int R, float* __restrict__ dst, int inverse) {
@@ -20,59 +33,218 @@ __global__ void ucat_kernel(const float* __restrict__ src, int H, int D, int R, 
   }
 }
 
-// one workgroup per sample: S[c] = sum_f A[f,c], quad[c] = S^2 - sum_f A^2, inter[h*P+p] = sum_r quad[h*R+r] V[h,r,p]
-__global__ __launch_bounds__(256) void qnn_reduce_fwd_kernel(const float* __restrict__ A, int F, int H, int R,
-                                                             const float* __restrict__ V, int P,
-                                                             float* __restrict__ S, float* __restrict__ quad,
-                                                             float* __restrict__ inter) {
-  extern __shared__ float sq[];
-  const int b = blockIdx.x, C = H * R;
-  const float* Ab = A + (long)b * F * C;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = 0.f, s2 = 0.f;
-    for (int f = 0; f < F; ++f) {
-      const float a = Ab[(long)f * C + c];
-      s += a;
-      s2 += a * a;
+// V (H, R, P) <-> block-diagonal Vfull (H*R, H*P); forward expand writes the zeros too
+__global__ void vfull_kernel(const float* __restrict__ src, int H, int R, int P, float* __restrict__ dst,
+                             int inverse) {
+  const long QR = (long)H * R, C = (long)H * P;
+  if (!inverse) {
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < QR * C; q += (long)gridDim.x * blockDim.x) {
+      const long row = q / C, col = q % C;
+      const long h = row / R, hc = col / P;
+      dst[q] = (h == hc) ? src[(h * R + row % R) * P + col % P] : 0.f;
     }
-    const float qd = s * s - s2;
-    S[(long)b * C + c] = s;
-    quad[(long)b * C + c] = qd;
-    sq[c] = qd;
-  }
-  __syncthreads();
-  for (int o = threadIdx.x; o < H * P; o += blockDim.x) {
-    const int h = o / P, p = o % P;
-    float acc = 0.f;
-    for (int r = 0; r < R; ++r) acc = fmaf(sq[h * R + r], V[((long)h * R + r) * P + p], acc);
-    inter[(long)b * H * P + o] = acc;
+  } else {
+    for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < QR * P; q += (long)gridDim.x * blockDim.x) {
+      const long h = q / ((long)R * P), rp = q % ((long)R * P), r = rp / P, pp = rp % P;
+      dst[q] = src[(h * R + r) * C + h * P + pp];
+    }
   }
 }
 
-// dquad[c] = sum_p dinter[h*P+p] V[h,r,p]; dA[f,c] = 2*dquad[c]*(S[c] - A[f,c])
-__global__ __launch_bounds__(256) void qnn_reduce_bwd_kernel(const float* __restrict__ A, int F, int H, int R,
-                                                             const float* __restrict__ V, int P,
-                                                             const float* __restrict__ S,
-                                                             const float* __restrict__ dinter,
-                                                             float* __restrict__ dA) {
-  extern __shared__ float sd[];
-  const int b = blockIdx.x, C = H * R;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const int h = c / R, r = c % R;
-    float acc = 0.f;
-    for (int p = 0; p < P; ++p) acc = fmaf(dinter[(long)b * H * P + h * P + p], V[((long)h * R + r) * P + p], acc);
-    sd[c] = acc;
+// Ucat staged in LDS, zero-padded to QRp = 16*ceil(QR/16) columns, row stride QRp + 1
+template <int D>
+__device__ __forceinline__ void stage_ucat(const float* __restrict__ ucat, int QR, int QRp, float* sU) {
+  for (int q = threadIdx.x; q < D * QRp; q += blockDim.x) {
+    const int d = q / QRp, c = q % QRp;
+    sU[d * (QRp + 1) + c] = c < QR ? ucat[d * QR + c] : 0.f;
   }
+}
+
+// One wave per sample.  G = z^T z by MFMA with the F rows as the contraction (A and B operands are the
+// same loaded values: lane (g, c) holds z[4s+g][16i+c]); then H = G Ucat using the symmetric G's
+// C-layout registers directly as A operands (k-set {16i + 4g + r}), and sum_f A^2 = sum_d U o H.
+template <int D>
+__global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restrict__ z, int B, int F,
+                                                           const float* __restrict__ ucat, int QR,
+                                                           float* __restrict__ zsum_out, float* __restrict__ G_out,
+                                                           float* __restrict__ S_out, float* __restrict__ quad_out) {
+  constexpr int NT = D / 16;
+  extern __shared__ float sU[];
+  const int QRp = (QR + 15) / 16 * 16, US = QRp + 1;
+  float* szs = sU + D * US;                      // [4 waves][D] zsum
+  stage_ucat<D>(ucat, QR, QRp, sU);
   __syncthreads();
-  const float* Ab = A + (long)b * F * C;
-  float* dAb = dA + (long)b * F * C;
-  for (int q = threadIdx.x; q < F * C; q += blockDim.x) {
-    const int c = q % C;
-    const float g = sd[c];
-    // autograd of s*s - sum(A*A): ds = g*s + g*s ; dA = ds - (g*A + g*A)
-    const float s = S[(long)b * C + c];
-    dAb[q] = (g * s + g * s) - (g * Ab[q] + g * Ab[q]);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int b = blockIdx.x * 4 + w;
+  if (b >= B) return;
+  const float* zb = z + (long)b * F * D;
+  f32x4 acc[NT][NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float zs[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) zs[i] = 0.f;
+  for (int f0 = 0; f0 < F; f0 += 4) {
+    const int f = f0 + g;
+    float v[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      v[i] = f < F ? zb[(long)f * D + 16 * i + c] : 0.f;
+      zs[i] += v[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = mfma4q(v[i], v[j], acc[i][j]);
   }
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    zs[i] += __shfl_xor(zs[i], 16);
+    zs[i] += __shfl_xor(zs[i], 32);
+  }
+  float* zw = szs + w * D;
+  if (g == 0) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      zw[16 * i + c] = zs[i];
+      zsum_out[(long)b * D + 16 * i + c] = zs[i];
+    }
+  }
+  // G (row-major D x D per sample): reg r of tile (i, j) = G[16i + 4g + r][16j + c]
+  float* Gb = G_out + (long)b * D * D;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Gb[(16 * i + 4 * g + r) * D + 16 * j + c] = acc[i][j][r];
+  __builtin_amdgcn_wave_barrier();
+  for (int t = 0; t < QRp / 16; ++t) {
+    const int cc = 16 * t + c;
+    // S[cc] = zsum . U[:, cc]
+    float sv = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < D; ++d) sv = fmaf(zw[d], sU[d * US + cc], sv);
+    // H[:, t-block] = G U[:, t-block]; sa2 = sum_d U[d][cc] H[d][cc]
+    float sa2 = 0.f;
+#pragma unroll
+    for (int jd = 0; jd < NT; ++jd) {
+      f32x4 h = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h = mfma4q(acc[i][jd][r], sU[(16 * i + 4 * g + r) * US + cc], h);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sa2 = fmaf(h[r], sU[(16 * jd + 4 * g + r) * US + cc], sa2);
+    }
+    sa2 += __shfl_xor(sa2, 16);
+    sa2 += __shfl_xor(sa2, 32);
+    if (g == 0 && cc < QR) {
+      S_out[(long)b * QR + cc] = sv;
+      quad_out[(long)b * QR + cc] = sv * sv - sa2;
+    }
+  }
+}
+
+// One wave per sample: M = U diag(dquad) U^T (MFMA over the QR columns), w = U (dquad o S);
+// dz_f = 2 w - 2 M z_f (+ dz_add) with M's C-layout registers as the B operand (k-set {16i+4g+r}).
+template <int D>
+__global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restrict__ z, int B, int F,
+                                                           const float* __restrict__ ucat, int QR,
+                                                           const float* __restrict__ S,
+                                                           const float* __restrict__ dquad,
+                                                           const float* __restrict__ dz_add, float* __restrict__ dz,
+                                                           float* __restrict__ DS) {
+  constexpr int NT = D / 16;
+  extern __shared__ float sU[];
+  const int QRp = (QR + 15) / 16 * 16, US = QRp + 1;
+  float* sdq = sU + D * US;                      // [4 waves][QRp] dquad, then [QRp] dquad*S
+  stage_ucat<D>(ucat, QR, QRp, sU);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int b = blockIdx.x * 4 + w;
+  if (b >= B) return;
+  float* dq = sdq + w * 2 * QRp;
+  float* dqs = dq + QRp;
+  for (int q = lane; q < QRp; q += 64) {
+    const float d = q < QR ? dquad[(long)b * QR + q] : 0.f;
+    const float sv = q < QR ? S[(long)b * QR + q] : 0.f;
+    dq[q] = d;
+    dqs[q] = d * sv;
+    if (q < QR) DS[(long)b * QR + q] = d * sv;
+  }
+  __builtin_amdgcn_wave_barrier();
+  // M[d][e] = sum_c U[d][c] dq[c] U[e][c]
+  f32x4 M[NT][NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) M[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < QRp; k0 += 4) {
+    const int k = k0 + g;
+    float av[NT], bv[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      bv[i] = sU[(16 * i + c) * US + k];
+      av[i] = bv[i] * dq[k];
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) M[i][j] = mfma4q(av[i], bv[j], M[i][j]);
+  }
+  // w[e] for e = 16j + c
+  float wv[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    float a = 0.f;
+#pragma unroll 8
+    for (int q = 0; q < QRp; ++q) a = fmaf(sU[(16 * j + c) * US + q], dqs[q], a);
+    wv[j] = 2.f * a;
+  }
+  const float* zb = z + (long)b * F * D;
+  const float* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
+  float* ob = dz + (long)b * F * D;
+  for (int f0 = 0; f0 < F; f0 += 16) {
+    const int fa = f0 + c;                       // A-operand row of this lane
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float av = fa < F ? zb[(long)fa * D + 16 * i + 4 * g + r] : 0.f;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[j] = mfma4q(av, M[i][j][r], acc[j]);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = f0 + 4 * g + r;
+      if (f < F) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int e = 16 * j + c;
+          float v = wv[j] - 2.f * acc[j][r];
+          if (ab) v += ab[(long)f * D + e];
+          ob[(long)f * D + e] = v;
+        }
+      }
+    }
+  }
+}
+
+// dUcat[d][c] = 2 (T1[d][c] - sum_e U[e][c] T[d*D + e][c])
+__global__ void qnn_du_combine_kernel(const float* __restrict__ T1, const float* __restrict__ T,
+                                      const float* __restrict__ ucat, int D, int QR, float* __restrict__ du) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= D * QR) return;
+  const int d = q / QR, c = q % QR;
+  float s = 0.f;
+  for (int e = 0; e < D; ++e) s = fmaf(ucat[e * QR + c], T[((long)d * D + e) * QR + c], s);
+  du[q] = 2.f * (T1[q] - s);
 }
 
 // ---------------- SE block ----------------
@@ -198,18 +370,50 @@ extern "C" int ctr_qnn_ucat(const float* src, int H, int D, int R, float* dst, i
   return check_launch("qnn_ucat");
 }
 
-extern "C" int ctr_qnn_reduce_fwd(const float* A, int B, int F, int H, int R, const float* V, int P, float* S,
-                                  float* quad, float* inter, void* stream) {
-  if (B == 0) return 0;
-  qnn_reduce_fwd_kernel<<<B, 256, H * R * sizeof(float), (hipStream_t)stream>>>(A, F, H, R, V, P, S, quad, inter);
-  return check_launch("qnn_reduce_fwd");
+extern "C" int ctr_qnn_vfull(const float* V, int H, int R, int P, float* vfull, int inverse, void* stream) {
+  const long n = inverse ? (long)H * R * P : (long)H * R * H * P;
+  vfull_kernel<<<(unsigned)std::min<long>(cdiv(n, 256L), 4096L), 256, 0, (hipStream_t)stream>>>(V, H, R, P, vfull,
+                                                                                              inverse);
+  return check_launch("qnn_vfull");
 }
 
-extern "C" int ctr_qnn_reduce_bwd(const float* A, int B, int F, int H, int R, const float* V, int P, const float* S,
-                                  const float* dinter, float* dA, void* stream) {
+static size_t gram_lds(int D, int QR) {
+  const int QRp = (QR + 15) / 16 * 16;
+  return ((size_t)D * (QRp + 1) + 8 * (size_t)std::max(D, QRp)) * sizeof(float);
+}
+
+extern "C" int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int QR, float* zsum,
+                                float* G, float* S, float* quad, void* stream) {
+  CTR_REQUIRE(D == 16 || D == 32 || D == 64, "qnn gram: D must be 16, 32 or 64");
   if (B == 0) return 0;
-  qnn_reduce_bwd_kernel<<<B, 256, H * R * sizeof(float), (hipStream_t)stream>>>(A, F, H, R, V, P, S, dinter, dA);
-  return check_launch("qnn_reduce_bwd");
+  const size_t sm = gram_lds(D, QR);
+  CTR_REQUIRE(sm <= 64 * 1024, "qnn gram: U exceeds LDS");
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = cdiv(B, 4);
+  if (D == 16) qnn_gram_fwd_kernel<16><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, zsum, G, S, quad);
+  else if (D == 32) qnn_gram_fwd_kernel<32><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, zsum, G, S, quad);
+  else qnn_gram_fwd_kernel<64><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, zsum, G, S, quad);
+  return check_launch("qnn_gram_fwd");
+}
+
+extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
+                                const float* dquad, const float* dz_add, float* dz, float* DS, void* stream) {
+  CTR_REQUIRE(D == 16 || D == 32 || D == 64, "qnn gram: D must be 16, 32 or 64");
+  if (B == 0) return 0;
+  const size_t sm = gram_lds(D, QR);
+  CTR_REQUIRE(sm <= 64 * 1024, "qnn gram: U exceeds LDS");
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = cdiv(B, 4);
+  if (D == 16) qnn_gram_bwd_kernel<16><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else if (D == 32) qnn_gram_bwd_kernel<32><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else qnn_gram_bwd_kernel<64><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  return check_launch("qnn_gram_bwd");
+}
+
+extern "C" int ctr_qnn_du_combine(const float* T1, const float* T, const float* ucat, int D, int QR, float* ducat,
+                                  void* stream) {
+  qnn_du_combine_kernel<<<cdiv((long)D * QR, 256L), 256, 0, (hipStream_t)stream>>>(T1, T, ucat, D, QR, ducat);
+  return check_launch("qnn_du_combine");
 }
 
 extern "C" int ctr_se_fwd_gate(const float* mean, int C, int Cr, const float* W1, const float* b1, const float* W2,

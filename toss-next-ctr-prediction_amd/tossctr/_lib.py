@@ -72,8 +72,10 @@ SIGS = {
     "ctr_colsum": (i, [p, l, i, i, f, p, p, p]),
     "ctr_loss": (i, [p, p, p, i, f, p, p, p, p]),
     "ctr_qnn_ucat": (i, [p, i, i, i, p, i, p]),
-    "ctr_qnn_reduce_fwd": (i, [p, i, i, i, i, p, i, p, p, p, p]),
-    "ctr_qnn_reduce_bwd": (i, [p, i, i, i, i, p, i, p, p, p, p]),
+    "ctr_qnn_vfull": (i, [p, i, i, i, p, i, p]),
+    "ctr_qnn_gram_fwd": (i, [p, i, i, i, p, i, p, p, p, p, p]),
+    "ctr_qnn_gram_bwd": (i, [p, i, i, i, p, i, p, p, p, p, p, p]),
+    "ctr_qnn_du_combine": (i, [p, p, p, i, i, p, p]),
     "ctr_se_fwd_gate": (i, [p, i, i, p, p, p, p, p, p, p]),
     "ctr_scale_drop": (i, [p, i, i, p, u, u, f, p, l, p]),
     "ctr_se_bwd_ws": (z, [i, i]),

@@ -352,13 +352,16 @@ class Engine:
         call("ctr_rmsnorm_fwd", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq), st)
         ucat = W.get("ucat", (D, QR))
         call("ctr_qnn_ucat", ptr(P["qnn.U"]), a.qh, D, a.qr, ptr(ucat), 0, st)
-        A = W.get("qA", (B * F, QR))
-        self.gemm(B * F, QR, D, ptr(z), D, 0, ptr(ucat), QR, 0, ptr(A), QR)
+        # pair interaction through per-sample Gram matrices: A = z @ Ucat is never formed (qnn.hip)
+        zsum = W.get("qzsum", (B, D))
+        gram = W.get("qgram", (B, D * D))
         S = W.get("qS", (B, QR))
         quad = W.get("qquad", (B, QR))
+        call("ctr_qnn_gram_fwd", ptr(z), B, F, D, ptr(ucat), QR, ptr(zsum), ptr(gram), ptr(S), ptr(quad), st)
+        vfull = W.get("qvfull", (QR, C))
+        call("ctr_qnn_vfull", ptr(P["qnn.V"]), a.qh, a.qr, a.qP, ptr(vfull), 0, st)
         inter_pre = W.get("inter_pre", (B, C))
-        call("ctr_qnn_reduce_fwd", ptr(A), B, F, a.qh, a.qr, ptr(P["qnn.V"]), a.qP, ptr(S), ptr(quad),
-             ptr(inter_pre), st)
+        self.gemm(B, C, QR, ptr(quad), QR, 0, ptr(vfull), C, 0, ptr(inter_pre), C)
         gate = g1 = mean = None
         if a.use_se:
             mean = W.get("se_mean", (C,))
@@ -397,8 +400,8 @@ class Engine:
             if not last:
                 hs.append(out)
                 acts.append(pre)
-        return dict(z=z, rq=rq, ucat=ucat, A=A, S=S, quad=quad, inter_pre=inter_pre, mean=mean, g1=g1, gate=gate,
-                    inter=inter, hs=hs, acts=acts)
+        return dict(z=z, rq=rq, ucat=ucat, zsum=zsum, gram=gram, vfull=vfull, S=S, quad=quad, inter_pre=inter_pre,
+                    mean=mean, g1=g1, gate=gate, inter=inter, hs=hs, acts=acts)
 
     def _fc_forward(self, W, fcin, ctx, cat_e, B, seed, training, logits):
         """QNN disabled: fc head on [u, mean(num_e), mean(mask_e), cat_embs] (wrapper.py:95-100,167-173)."""
@@ -641,8 +644,6 @@ class Engine:
         dz_mlp = W.get("dz_mlp", (B, FD))
         if a.use_residual:
             self.gemm(B, FD, ncur, ptr(dcur), ncur, 0, ptr(W0), din, 0, ptr(dz_mlp), FD)
-        else:
-            dz_mlp.zero_()
         # SE + dropout
         dinter_pre = W.get("dinter_pre", (B, C))
         dq_ = drop_args(seed, SITE_QNN, a.qnn_p, training)
@@ -652,20 +653,26 @@ class Engine:
              ptr(q["mean"]), ptr(P.get("qnn.se.fc.0.weight")), ptr(P.get("qnn.se.fc.2.weight")), *dq_, ptr(dinter_pre),
              ptr(G.get("qnn.se.fc.0.weight")), ptr(G.get("qnn.se.fc.0.bias")), ptr(G.get("qnn.se.fc.2.weight")),
              ptr(G.get("qnn.se.fc.2.bias")), ptr(sws), st)
-        # pair interaction
-        dA = W.get("qdA", (B * F, QR))
-        call("ctr_qnn_reduce_bwd", ptr(q["A"]), B, F, a.qh, a.qr, ptr(P["qnn.V"]), a.qP, ptr(q["S"]),
-             ptr(dinter_pre), ptr(dA), st)
-        for h in range(a.qh):   # dV_h = quad_h^T @ dinter_h
-            self.gemm(a.qr, a.qP, B, ptr(q["quad"], h * a.qr), QR, 1, ptr(dinter_pre, h * a.qP), C, 0,
-                      ptr(G["qnn.V"], h * a.qr * a.qP), a.qP, None, self.wgrad_splits(a.qr, a.qP, B))
-        ducat = W.get("ducat", (D, QR))
-        self.gemm(D, QR, B * F, ptr(q["z"]), D, 1, ptr(dA), QR, 0, ptr(ducat), QR, None,
-                  self.wgrad_splits(D, QR, B * F))
-        call("ctr_qnn_ucat", ptr(ducat), a.qh, D, a.qr, ptr(G["qnn.U"]), 1, st)
+        # pair interaction (Gram form, qnn.hip): dquad = dinter Vfull^T; dV = blockdiag(quad^T dinter)
+        dquad = W.get("qdquad", (B, QR))
+        self.gemm(B, QR, C, ptr(dinter_pre), C, 0, ptr(q["vfull"]), C, 1, ptr(dquad), QR)
+        dvfull = W.get("qdvfull", (QR, C))
+        self.gemm(QR, C, B, ptr(q["quad"]), QR, 1, ptr(dinter_pre), C, 0, ptr(dvfull), C, None,
+                  self.wgrad_splits(QR, C, B))
+        call("ctr_qnn_vfull", ptr(dvfull), a.qh, a.qr, a.qP, ptr(G["qnn.V"]), 1, st)
         dz = W.get("dz", (B, FD))
-        self.gemm(B * F, D, QR, ptr(dA), QR, 0, ptr(q["ucat"]), QR, 1, ptr(dz), D,
-                  GemmEpi(add=ptr(dz_mlp), ld_add=D))
+        DS = W.get("qDS", (B, QR))
+        call("ctr_qnn_gram_bwd", ptr(q["z"]), B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]), ptr(dquad),
+             ptr(dz_mlp) if a.use_residual else None, ptr(dz), ptr(DS), st)
+        # dUcat = 2 (zsum^T DS - sum_b G_b Ucat diag(dquad_b))
+        T1 = W.get("qT1", (D, QR))
+        self.gemm(D, QR, B, ptr(q["zsum"]), D, 1, ptr(DS), QR, 0, ptr(T1), QR, None, self.wgrad_splits(D, QR, B))
+        T = W.get("qT", (D * D, QR))
+        self.gemm(D * D, QR, B, ptr(q["gram"]), D * D, 1, ptr(dquad), QR, 0, ptr(T), QR, None,
+                  self.wgrad_splits(D * D, QR, B))
+        ducat = W.get("ducat", (D, QR))
+        call("ctr_qnn_du_combine", ptr(T1), ptr(T), ptr(q["ucat"]), D, QR, ptr(ducat), st)
+        call("ctr_qnn_ucat", ptr(ducat), a.qh, D, a.qr, ptr(G["qnn.U"]), 1, st)
         # pre-norm
         npart = _lib.query("ctr_rmsnorm_bwd_nparts", B, FD)
         dwp = W.get("dwq_part", (npart, FD))
