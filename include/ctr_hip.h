@@ -69,16 +69,19 @@ size_t ctr_feat_embed_bwd_ws(int B, int F, int D);
 int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, const float* bias, const float* P, int fe, int D,
                        const float* dout, long dout_ld, float* dW, float* dbias, float* dP, float* ws, void* stream);
 /* CTRModel._embed_cats + emb_dropout, src/models/wrapper.py:106-112,149-150: hashed-bucket gather of
- * X_cat[b,c] from table c (arena + tab_off[c], row width dims[c]) projected by P_c (arena + proj_off[c]).
+ * X_cat[b,c] from table c (tab_base + tab_off[c], row stride row_ld, or dims[c] when row_ld == 0;
+ * tab_base NULL = arena) projected by P_c (arena + proj_off[c]).  Row-sharded tables pass the
+ * batch's fetched rows as tab_base (tab_off 0, row_ld 64) and X_cat remapped to fetched-row ids.
  * cat_e = pre-dropout (B, Fc, D); xf (nullable) receives the dropped copy at row stride xf_ld.      */
-int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const long* tab_off, const long* proj_off,
-                      const int* dims, int D, float* cat_e, float* xf, long xf_ld, uint32_t drop_key,
-                      uint32_t drop_thresh, float drop_scale, void* stream);
+int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const float* tab_base, const long* tab_off,
+                      const long* proj_off, const int* dims, int row_ld, int D, float* cat_e, float* xf, long xf_ld,
+                      uint32_t drop_key, uint32_t drop_thresh, float drop_scale, void* stream);
 size_t ctr_cat_embed_bwd_ws(int B, int Fc);
 /* backward: row-grad contributions (B*Fc rows x 64, zero-padded) keyed row_base[c] + X_cat[b,c] for
  * ctr_rowgrad, and dP_c written into grad_arena + proj_goff[c].                                    */
-int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* arena, const long* tab_off, const long* proj_off,
-                      const int* dims, int D, const float* dcat, const uint32_t* row_base, float* contrib,
+int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* arena, const float* tab_base, const long* tab_off,
+                      const long* proj_off, const int* dims, int row_ld, int D, const float* dcat,
+                      const uint32_t* row_base, float* contrib,
                       uint32_t* keys, float* grad_arena, const long* proj_goff, float* ws, void* stream);
 /* CTRModel._context_vector / _make_query, src/models/wrapper.py:114-136; mode 0 S1, 1 S2, 2 concat */
 int ctr_context_fwd(const float* num_e, long num_ld, int Fn, const float* mask_e, long mask_ld, int Fm,
@@ -263,9 +266,10 @@ int ctr_opt_hist_entry_bytes(void);
 /* hist[tick] = the scalars of one AdamW(+EMA) tick (same arguments as ctr_adamw_ema)              */
 int ctr_opt_hist_record(void* hist, int tick, float lr, float wd, float beta1, float beta2, float eps, int step,
                         float ema_decay, int do_adam, int do_ema, void* stream);
-/* bring the rows read by a batch up to tick: X (nx, ncols) int32 row ids; per_column != 0: column c
- * indexes tabs[c] (ntabs == ncols); else every id is a row of each of the ntabs tables.  E may be NULL
- * (no EMA).                                                                                         */
+/* bring the rows read by a batch up to tick: X (nx, ncols) int32 row ids; per_column == 1: column c
+ * indexes tabs[c] (ntabs == ncols); == 2: every entry is a key of the tables' key space (table = last
+ * with key_base <= key, row = key - key_base; tabs sorted by key_base); 0: every id is a row of each
+ * of the ntabs tables.  E may be NULL (no EMA).                                                     */
 int ctr_lazy_touch(const ctr_lazy_tab_t* tabs, int ntabs, const int32_t* X, long nx, int ncols, int per_column,
                    float* P, float* M, float* V, float* E, const void* hist, int tick, void* stream);
 /* apply tick to the rows of one compact grad group (sorted unique keys, rows G with leading dim g_ld,
@@ -278,6 +282,31 @@ int ctr_lazy_update(const ctr_lazy_tab_t* tabs, int ntabs, const uint32_t* keys,
 int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_rows, float* P, float* M, float* V, float* E,
                    const void* hist, int tick, void* stream);
 
+
+/* ---- row-sharded embedding tables (BASELINE config 5): row r of a table lives on rank
+ * r % world at local row r / world.  Replaces, for tables larger than one GPU, the reference's
+ * in-memory nn.Embedding gathers (src/models/dare.py:118-119,138, src/models/wrapper.py:106-112) and
+ * embedding_dense_backward with an owner exchange (all-to-alls issued by tossctr/shard.py).
+ * Owner-major keys: okey = (id % world) << lbits | local_key; local_key = id / world (sequence) or
+ * lbase[c] + id / world (categorical column c).  Valid okeys must be < 2^key_bits - 1.            */
+size_t ctr_shard_plan_ws_size(long n);
+/* ids X (n = rows*ncols int32; mode 0 sequence tokens, pad_id excluded; mode 1 categorical) -> sorted
+ * unique okeys uniq[0, *n_uniq) (INVALID last if a pad was present), remap[i] = 1 + unique index of
+ * X[i] (0 for pads), send_counts[w] = unique valid okeys owned by rank w (contiguous runs)          */
+int ctr_shard_plan(const int32_t* X, long n, int ncols, int mode, int pad_id, const uint32_t* lbase, int world,
+                   int lbits, int key_bits, uint32_t* uniq, uint32_t* n_uniq, int32_t* remap, long long* send_counts,
+                   void* ws, size_t ws_bytes, void* stream);
+/* owner side: local[i] = okeys[i] & mask                                                            */
+int ctr_shard_strip(const uint32_t* okeys, long n, uint32_t mask, int32_t* local, void* stream);
+/* owner side: rows of the requested local keys.  mode 0: tabs = {att, rep} (width out_ld), rows to
+ * out0 / out1; mode 1: tabs sorted by key_base, row zero-padded to out_ld floats into out0          */
+int ctr_shard_gather(const int32_t* local, long n, int mode, const ctr_lazy_tab_t* tabs, int ntabs, const float* P,
+                     float* out0, float* out1, int out_ld, void* stream);
+/* backward: sorted unique fetched-row ids uk[0, *nu) (INVALID last) -> out_local[i] = the owner's local
+ * key; counts[w] = entries owned by rank w (runs in rank order; fwd_counts = the plan's send_counts) */
+int ctr_shard_route(const uint32_t* uk, const uint32_t* nu, long cap, const uint32_t* uniq_okeys,
+                    const long long* fwd_counts, int world, uint32_t mask, uint32_t* out_local, long long* counts,
+                    void* stream);
 
 /* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */
 int ctr_sigmoid(const float* x, int n, float* y, void* stream);

@@ -78,3 +78,69 @@ def test_dp_exchange_gloo_world2():
     # union of both ranks' valid keys, summed where they overlap
     allk = sorted(set(datas[0][0][:datas[0][2]]) | set(datas[1][0][:datas[1][2]]))
     assert list(k0) == allk
+
+
+# ---------------------------------------------------------------- row-sharded tables (tossctr/shard.py)
+def a2a_worker(rank, world, port, out):
+    """Each rank requests a ragged set of rows from every owner and receives them back: the two
+    all-to-alls of TableShards.fetch (keys out, rows back) with host-known split sizes."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tossctr import dist as D
+    from tossctr.shard import full_to_local
+    table = torch.arange(40 * 3, dtype=torch.float32).view(40, 3)      # full table, row r owned by r % world
+    local = full_to_local(table, rank, world)
+    g = np.random.default_rng(7 + rank)
+    want = np.unique(g.integers(0, 40, 17))
+    owner = want % world
+    order = np.lexsort((want // world, owner))                         # owner-major, as ctr_shard_plan sorts
+    want, owner = want[order], owner[order]
+    send = [int((owner == w).sum()) for w in range(world)]
+    cnt = torch.empty(world, dtype=torch.int64)
+    D.all_to_all_var(cnt, torch.tensor(send, dtype=torch.int64), [1] * world, [1] * world)
+    recv = cnt.tolist()
+    req = torch.empty(sum(recv), dtype=torch.int32)
+    D.all_to_all_var(req, torch.from_numpy((want // world).astype(np.int32)), recv, send)
+    rows = local[req.long()]                                           # owner gathers its local rows
+    back = torch.empty(len(want), 3)
+    D.all_to_all_var(back, rows, send, recv)
+    out[rank] = (want, back.numpy().copy(), table.numpy())
+    dist.destroy_process_group()
+
+
+def test_shard_all_to_all_roundtrip_gloo_world2():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(a2a_worker, args=(world, free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        want, back, table = out[r]
+        np.testing.assert_array_equal(back, table[want])
+
+
+def test_shard_layout_helpers_and_cfg5_key_widths():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "toss-next-ctr-prediction_amd"))
+    from tossctr.arch import Arch
+    from tossctr.configs import N_NUM_NEXT, cat_cardinals, dare_qnn_next_k100_s1
+    from tossctr.shard import TableShards, full_to_local, locals_to_full, shard_rows
+    full = torch.randn(23, 5)
+    for world in (1, 2, 3, 8):
+        parts = torch.stack([full_to_local(full, r, world) for r in range(world)])
+        assert parts.shape == (world, shard_rows(23, world), 5)
+        assert torch.equal(locals_to_full(parts, 23), full)
+    # BASELINE config 5: every hash_buckets = 1e8, emb_dim 64, 8 ranks -> owner-major keys fit 32 bits
+    cfg = dare_qnn_next_k100_s1(emb_dim=64, hash_buckets=100_000_000)
+    cards = cat_cardinals(cfg)
+    arch = Arch.from_cfg(cfg, 10_000_000, N_NUM_NEXT, N_NUM_NEXT, cards, list(cfg["data"]["cat_cols"]))
+    for world in (2, 4, 8):
+        sh = TableShards(arch, None, 0, world, torch.device("cpu"))
+        assert sh.seq_kbits <= 32 and sh.cat_kbits <= 32
+        assert sum(sh.cat_local_rows) * world >= sum(cards.values())
+        # every valid owner-major key stays below the INVALID sentinel's truncated value
+        top = ((world - 1) << sh.cat_lbits) | (sum(sh.cat_local_rows) - 1)
+        assert top < (1 << sh.cat_kbits) - 1
+        top = ((world - 1) << sh.seq_lbits) | (sh.seq_rows - 1)
+        assert top < (1 << sh.seq_kbits) - 1

@@ -1,0 +1,72 @@
+"""Row-sharded embedding tables (tossctr/shard.py, csrc/shard.hip) vs replicated tables, world 2.
+
+Each configuration runs as a child process (tests/dist_shard_worker.py) whose two ranks share cuda:0
+over gloo.  Checks:
+  * world 2 with the SAME batch on both ranks = the single-GPU run (DDP mean of equal grads);
+  * sharded = replicated with DIFFERENT batches per rank: losses, eval logits, every parameter (full
+    tables gathered from the shards) and the EMA shadow -- equal up to the summation order of the
+    global grad norm (per-owner partial sums vs one sum);
+  * sharded lazy = sharded dense optimizer stream, bit for bit;
+  * each rank holds ceil(vocab / 2) rows of a sequence table.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import close_enough
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_cache = {}
+
+
+def _run(tmp_path_factory, mode, same, lazy=1):
+    key = (mode, same, lazy)
+    if key not in _cache:
+        out = str(tmp_path_factory.mktemp("shard") / f"{mode}_{same}_{lazy}.pt")
+        r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", mode,
+                            "--same-batch", str(same), "--lazy", str(lazy), "--out", out],
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        _cache[key] = torch.load(out, weights_only=True)
+    return _cache[key]
+
+
+def _compare(a, b, rtol, atol=1e-6, what=""):
+    close_enough(np.asarray(a["losses"], np.float64), np.asarray(b["losses"], np.float64), rtol, atol, what + "loss")
+    close_enough(a["logits"].double().numpy(), b["logits"].double().numpy(), rtol, atol, what + "logits")
+    assert a["sd"].keys() == b["sd"].keys()
+    for k in a["sd"]:
+        assert a["sd"][k].shape == b["sd"][k].shape, k
+        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), rtol, atol, what + k)
+        close_enough(a["ema"][k].double().numpy().ravel(), b["ema"][k].double().numpy().ravel(), rtol, atol,
+                     what + "ema:" + k)
+
+
+def test_world2_same_batch_matches_single(tmp_path_factory):
+    single = _run(tmp_path_factory, "single", 1)
+    rep = _run(tmp_path_factory, "replicated", 1)
+    sh = _run(tmp_path_factory, "sharded", 1)
+    _compare(rep, single, 1e-5, what="replicated vs single: ")
+    _compare(sh, single, 1e-5, what="sharded vs single: ")
+
+
+def test_sharded_matches_replicated(tmp_path_factory):
+    rep = _run(tmp_path_factory, "replicated", 0)
+    sh = _run(tmp_path_factory, "sharded", 0)
+    assert sh["local_rows"] == (sh["vocab"] + 1) // 2 and rep["local_rows"] == rep["vocab"]
+    _compare(sh, rep, 1e-5, what="sharded vs replicated: ")
+
+
+def test_sharded_lazy_equals_dense_stream(tmp_path_factory):
+    lazy = _run(tmp_path_factory, "sharded", 0, 1)
+    dense = _run(tmp_path_factory, "sharded", 0, 0)
+    assert lazy["losses"] == dense["losses"]
+    for k in lazy["sd"]:
+        assert torch.equal(lazy["sd"][k], dense["sd"][k]), k
+        assert torch.equal(lazy["ema"][k], dense["ema"][k]), k

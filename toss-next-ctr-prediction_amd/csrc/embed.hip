@@ -135,9 +135,11 @@ __global__ __launch_bounds__(1024) void feat_embed_bwd_final(int nchunk, int F, 
 // hashed categorical embeddings: one thread per (b, c, d); the D threads of a (b, c) share the row
 // ------------------------------------------------------------------------------------------------
 struct CatMeta {
-  const long* tab_off;    // element offset of table c in the arena
+  const float* tabs;      // table storage: the arena, or (row-sharded tables) the batch's fetched rows
+  const long* tab_off;    // element offset of table c in tabs
   const long* proj_off;   // element offset of proj c ([D][d_c]) in the arena
   const int* dims;        // d_c
+  int row_ld;             // row stride of every table in tabs (0: d_c)
 };
 
 __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restrict__ xcat, int B, int Fc,
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restric
     const int c = (int)(bc - b * Fc);
     const int dc = cm.dims[c];
     const long row = xcat[(long)b * Fc + c];
-    const float* t = arena + cm.tab_off[c] + row * dc;
+    const float* t = cm.tabs + cm.tab_off[c] + row * (cm.row_ld ? cm.row_ld : dc);
     const float* p = arena + cm.proj_off[c] + (long)d * dc;
     float acc = 0.f;
 #pragma unroll 8
@@ -202,7 +204,8 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_proj_partial(const int* __r
   const int c = blockIdx.x, chunk = blockIdx.y;
   const int dc = cm.dims[c];
   const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
-  const float* T = arena + cm.tab_off[c];
+  const float* T = cm.tabs + cm.tab_off[c];
+  const long tld = cm.row_ld ? cm.row_ld : dc;
   float* out = part + ((long)chunk * Fc + c) * (64 * 64);
   const int nq = D * dc;                 // <= 4096 outputs: up to 16 per thread
   float acc[16];
@@ -215,7 +218,7 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_proj_partial(const int* __r
       const int i = e >> 6, k = e & 63;
       const long b = s0 + i;
       const long row = xcat[b * Fc + c];
-      sT[i][k] = k < dc ? T[row * dc + k] : 0.f;
+      sT[i][k] = k < dc ? T[row * tld + k] : 0.f;
       sG[i][k] = k < D ? dcat[(b * Fc + c) * D + k] : 0.f;
     }
     __syncthreads();
@@ -432,12 +435,14 @@ extern "C" int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, 
   return check_launch("feat_embed_bwd");
 }
 
-extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const long* tab_off,
-                                 const long* proj_off, const int* dims, int D, float* cat_e, float* xf, long xf_ld,
+extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const float* tab_base,
+                                 const long* tab_off, const long* proj_off, const int* dims, int row_ld, int D,
+                                 float* cat_e, float* xf, long xf_ld,
                                  uint32_t drop_key, uint32_t drop_thresh, float drop_scale, void* stream) {
   if (B == 0 || Fc == 0) return 0;
   CTR_REQUIRE((long)B * Fc * 64 < (1L << 32), "cat_embed: B*Fc*64 must fit 32-bit indexing");
-  CatMeta cm{tab_off, proj_off, dims};
+  CTR_REQUIRE(row_ld >= 0 && row_ld <= 64, "cat_embed: row_ld must be in [0, 64]");
+  CatMeta cm{tab_base ? tab_base : arena, tab_off, proj_off, dims, row_ld};
   long total = (long)B * Fc * D;
   int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   cat_embed_fwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(xcat, B, Fc, arena, cm, D, cat_e, xf, xf_ld,
@@ -450,15 +455,17 @@ extern "C" size_t ctr_cat_embed_bwd_ws(int B, int Fc) {
   return (size_t)nchunk * Fc * 64 * 64 * sizeof(float);
 }
 
-extern "C" int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* arena, const long* tab_off,
-                                 const long* proj_off, const int* dims, int D, const float* dcat,
+extern "C" int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* arena, const float* tab_base,
+                                 const long* tab_off, const long* proj_off, const int* dims, int row_ld, int D,
+                                 const float* dcat,
                                  const uint32_t* row_base, float* contrib, uint32_t* keys, float* grad_arena,
                                  const long* proj_goff, float* ws, void* stream) {
   if (B == 0 || Fc == 0) return 0;
   CTR_REQUIRE(D <= 64, "D > 64");
   CTR_REQUIRE((long)B * Fc * 64 < (1L << 32), "cat_embed: B*Fc*64 must fit 32-bit indexing");
+  CTR_REQUIRE(row_ld >= 0 && row_ld <= 64, "cat_embed: row_ld must be in [0, 64]");
   hipStream_t s = (hipStream_t)stream;
-  CatMeta cm{tab_off, proj_off, dims};
+  CatMeta cm{tab_base ? tab_base : arena, tab_off, proj_off, dims, row_ld};
   long total = (long)B * Fc * 64;
   int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   cat_embed_bwd_rows<<<blocks, 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, row_base, contrib, keys);

@@ -173,14 +173,25 @@ __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* _
   long row = -1;
   if (item < nitems) {
     long xi;
-    if (per_column) {
+    if (per_column == 1) {
       xi = item;
       ti = (int)(item % ncols);
+    } else if (per_column == 2) {
+      xi = item;
     } else {
       xi = item / ntabs;
       ti = (int)(item % ntabs);
     }
     row = X[xi];
+    if (per_column == 2 && row >= 0) {   // X holds keys: the last table with key_base <= key
+      int a = 0, b = ntabs;
+      while (b - a > 1) {
+        const int mid = (a + b) >> 1;
+        if (tabs[mid].key_base <= (uint32_t)row) a = mid; else b = mid;
+      }
+      ti = a;
+      row -= (long)tabs[a].key_base;
+    }
     if (l8 == 0 && row >= 0 && row < tabs[ti].rows) {
       int* lp = tabs[ti].last + row;
       s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -293,7 +304,8 @@ extern "C" int ctr_opt_hist_record(void* hist, int tick, float lr, float wd, flo
 extern "C" int ctr_lazy_touch(const ctr_lazy_tab_t* tabs, int ntabs, const int32_t* X, long nx, int ncols,
                               int per_column, float* P, float* M, float* V, float* E, const void* hist, int tick,
                               void* stream) {
-  CTR_REQUIRE(ntabs > 0 && (!per_column || ntabs == ncols), "ctr_lazy_touch: per_column needs ntabs == ncols");
+  CTR_REQUIRE(per_column >= 0 && per_column <= 2, "ctr_lazy_touch: per_column must be 0, 1 or 2");
+  CTR_REQUIRE(ntabs > 0 && (per_column != 1 || ntabs == ncols), "ctr_lazy_touch: per_column needs ntabs == ncols");
   if (tick <= 0 || nx <= 0 || ncols <= 0) return 0;
   const long nitems = per_column ? nx * ncols : nx * ncols * ntabs;
   lazy_touch_kernel<<<(unsigned)cdiv(nitems * LG, 256L), 256, 0, (hipStream_t)stream>>>(

@@ -45,9 +45,9 @@ SIGS = {
     "ctr_feat_embed_fwd": (i, [p, i, i, p, p, p, i, i, p, l, p]),
     "ctr_feat_embed_bwd_ws": (z, [i, i, i]),
     "ctr_feat_embed_bwd": (i, [p, i, i, p, p, p, i, i, p, l, p, p, p, p, p]),
-    "ctr_cat_embed_fwd": (i, [p, i, i, p, p, p, p, i, p, p, l, u, u, f, p]),
+    "ctr_cat_embed_fwd": (i, [p, i, i, p, p, p, p, p, i, i, p, p, l, u, u, f, p]),
     "ctr_cat_embed_bwd_ws": (z, [i, i]),
-    "ctr_cat_embed_bwd": (i, [p, i, i, p, p, p, p, i, p, p, p, p, p, p, p, p]),
+    "ctr_cat_embed_bwd": (i, [p, i, i, p, p, p, p, p, i, i, p, p, p, p, p, p, p, p]),
     "ctr_context_fwd": (i, [p, l, i, p, l, i, p, i, i, i, i, i, p, p, p, p, p, p]),
     "ctr_context_bwd": (i, [p, l, i, p, l, i, p, i, i, i, i, i, p, p, p, p, l, u, u, f, p, l, p, p, p, p, p]),
     "ctr_dare_topk_fwd": (i, [p, i, i, p, p, p, i, p, i, i, p, p, p, p, p]),
@@ -94,6 +94,11 @@ SIGS = {
     "ctr_lazy_touch": (i, [p, i, p, l, i, i, p, p, p, p, p, i, p]),
     "ctr_lazy_update": (i, [p, i, p, p, i, p, l, p, p, p, p, p, p, i, p]),
     "ctr_lazy_flush": (i, [p, i, l, p, p, p, p, p, i, p]),
+    "ctr_shard_plan_ws_size": (z, [l]),
+    "ctr_shard_plan": (i, [p, l, i, i, i, p, i, i, i, p, p, p, p, p, z, p]),
+    "ctr_shard_strip": (i, [p, l, u, p, p]),
+    "ctr_shard_gather": (i, [p, l, i, p, i, p, p, p, i, p]),
+    "ctr_shard_route": (i, [p, p, l, p, p, i, u, p, p, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
     "ctr_gather_rows": (i, [p, l, p, i, p, p]),

@@ -47,3 +47,15 @@ def gather_compact(keys, rows, count, keys_out, rows_out, count_out, group=None)
     all_gather_into(keys_out, keys, group)
     all_gather_into(rows_out, rows, group)
     all_gather_into(count_out, count, group)
+
+
+def all_to_all_var(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None):
+    """out = concat over source ranks of what each sent here; inp's first in_splits[w] rows (dim 0) go
+    to rank w.  Splits are host lists (the row-sharded exchange reads its counts back once per phase)."""
+    if _needs_host_staging(group, inp):
+        ho = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(ho, inp.cpu().contiguous(), list(out_splits), list(in_splits), group=group)
+        out.copy_(ho)
+    else:
+        dist.all_to_all_single(out, inp.contiguous(), list(out_splits), list(in_splits), group=group)
+    return out

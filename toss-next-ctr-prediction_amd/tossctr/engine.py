@@ -43,8 +43,12 @@ class ParamArena:
     The dense-with-grad region is mirrored 1:1 by the dense grad buffer ``grad``.
     """
 
-    def __init__(self, arch: Arch, device):
+    def __init__(self, arch: Arch, device, shards=None):
         shapes = arch.param_shapes()
+        if shards is not None:     # row-sharded tables: this rank's rows only (tossctr/shard.py)
+            local = {"dare.emb_att.weight": shards.seq_rows, "dare.emb_rep.weight": shards.seq_rows}
+            local.update({f"cat_embs.{c}.weight": r for c, r in zip(arch.cat_names, shards.cat_local_rows)})
+            shapes = [(k, (local[k],) + tuple(shp[1:]) if kind == "table" else shp, kind) for k, shp, kind in shapes]
         ng = arch.no_grad_keys()
         groups = ([x for x in shapes if x[2] == "dense" and x[0] not in ng],
                   [x for x in shapes if x[2] == "dense" and x[0] in ng],
@@ -107,9 +111,10 @@ class Workspace:
 
 
 class Engine:
-    def __init__(self, arch: Arch, arena: ParamArena):
+    def __init__(self, arch: Arch, arena: ParamArena, shards=None):
         self.a = arch
         self.arena = arena
+        self.shards = shards
         self.P = arena.views
         self.G = arena.grad_views
         self.device = arena.device
@@ -128,6 +133,13 @@ class Engine:
         self.cat_row_base = torch.from_numpy(self.cat_row_base_np.view(np.int32)).to(dev)
         self.cat_key_bits = _key_bits(int(sum(a.cat_cards)))
         self.seq_key_bits = _key_bits(a.seq_vocab)
+        if shards is not None:
+            # the optimizer addresses table rows by LOCAL keys; the forward/backward by fetched-row ids
+            self.cat_row_base_np = shards.cat_lbase_np.copy()
+            shards.arena_buf = arena.buf
+            shards.tabs_seq = self._tab_array(["dare.emb_att.weight", "dare.emb_rep.weight"], [0, 0])
+            shards.tabs_cat = self._tab_array([f"cat_embs.{c}.weight" for c in a.cat_names],
+                                              [int(x) for x in shards.cat_lbase_np])
         # query column index in the X_cat column order (src/models/wrapper.py:130)
         self.qi = a.cat_cols.index(a.query_key) if a.query_mode != "S2" else 0
         # column order of X_cat = cat_cols; tables are in cardinals order -> must coincide
@@ -142,6 +154,16 @@ class Engine:
         # fused FFN kernels (ffn.hip) when the shape allows; the GEMM path otherwise
         self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden)) and \
             self._ffn_contiguous()
+
+    def _tab_array(self, keys, bases):
+        """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
+        arr = (_lib.LazyTab * len(keys))()
+        for i, (k, kb) in enumerate(zip(keys, bases)):
+            rows, width = self.arena.shapes[k]
+            arr[i].p_off, arr[i].rows, arr[i].width, arr[i].key_base, arr[i].last = \
+                self.arena.offsets[k], rows, width, kb, None
+        raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
+        return torch.from_numpy(raw).to(self.device), len(keys)
 
     def _ffn_contiguous(self):
         """The fused FFN backward colsums its [dW1 | db1 | dW2] slab straight into the grad arena."""
@@ -238,12 +260,11 @@ class Engine:
                  ptr(P["mask_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, mask_off), FD, st)
         # ---- hashed categorical gather + projection (+ emb dropout into xF) (wrapper.py:106-112,149-150)
         cat_e = W.get("cat_e", (B, a.Fc, D))
-        if self.lazy is not None:
-            self.lazy.touch_rows(X_cat, "cat")
-            self.lazy.touch_rows(seq, "seq")
+        tv = self._table_views(X_cat, seq)
+        sv["tv"] = tv
         dk = drop_args(seed, SITE_EMB, a.p_emb, training)
-        call("ctr_cat_embed_fwd", ptr(X_cat), B, a.Fc, ptr(self.arena.buf), ptr(self.cat_tab_off),
-             ptr(self.cat_proj_off), ptr(self.cat_dims_t), D, ptr(cat_e), ptr(xF, cat_off), FD, *dk, st)
+        call("ctr_cat_embed_fwd", ptr(tv["xcat"]), B, a.Fc, ptr(self.arena.buf), tv["cat_tab"], tv["cat_off"],
+             ptr(self.cat_proj_off), ptr(self.cat_dims_t), tv["cat_ld"], D, ptr(cat_e), ptr(xF, cat_off), FD, *dk, st)
         # ---- context + query (wrapper.py:114-136)
         ctx = W.get("ctx", (B, a.nctx * D))
         hq = W.get("hq", (B, D))
@@ -256,9 +277,8 @@ class Engine:
         tok = W.get("topk_tok", (B, K), torch.int32)
         vals = W.get("topk_vals", (B, K))
         xs = [W.get("x0", (B, K, D))]
-        call("ctr_dare_topk_fwd", ptr(seq), B, L, ptr(query), ptr(P["dare.emb_att.weight"]),
-             ptr(P["dare.emb_rep.weight"]), D, ptr(self.decay_log(L)), K, a.pad_id, ptr(idx), ptr(tok), ptr(vals),
-             ptr(xs[0]), st)
+        call("ctr_dare_topk_fwd", ptr(tv["seq"]), B, L, ptr(query), tv["att"], tv["rep"], D, ptr(self.decay_log(L)), K,
+             tv["pad"], ptr(idx), ptr(tok), ptr(vals), ptr(xs[0]), st)
         # ---- encoder layers (dare.py:53-70)
         layers = []
         M = B * K
@@ -341,6 +361,24 @@ class Engine:
             sv.update(gen=self._gen, xF=xF, cat_e=cat_e, ctx=ctx, hq=hq, query=query, idx=idx, tok=tok, vals=vals,
                       xs=xs, layers=layers, w=w, u=u, aux=aux, logits=logits, prob=prob, fcin=fcin, qnn=q, W=W)
         return logits, prob, aux, (sv if save else None)
+
+    def _table_views(self, X_cat, seq):
+        """Where the forward / backward read table rows.  Replicated tables: the arena, indexed by the
+        batch ids (lazy rows brought current first).  Row-sharded tables: the rows fetched from their
+        owners (tossctr/shard.py), indexed by the batch remapped to fetched-row ids (0 = pad)."""
+        a, P = self.a, self.P
+        if self.shards is None:
+            if self.lazy is not None:
+                self.lazy.touch_rows(X_cat, "cat")
+                self.lazy.touch_rows(seq, "seq")
+            return dict(fx=None, xcat=X_cat, seq=seq, pad=a.pad_id, cat_tab=None, cat_off=ptr(self.cat_tab_off),
+                        cat_ld=0, att=ptr(P["dare.emb_att.weight"]), rep=ptr(P["dare.emb_rep.weight"]),
+                        row_base=ptr(self.cat_row_base), seq_bits=self.seq_key_bits, cat_bits=self.cat_key_bits)
+        fx = self.shards.fetch(X_cat, seq)
+        return dict(fx=fx, xcat=fx["xcat"], seq=fx["seq"], pad=0, cat_tab=ptr(fx["cat"]),
+                    cat_off=ptr(self.shards.cat_zero_off), cat_ld=self.shards.CAT_LD, att=ptr(fx["att"]),
+                    rep=ptr(fx["rep"]), row_base=ptr(self.shards.cat_zero_base),
+                    seq_bits=_key_bits(1 + fx["n_seq"]), cat_bits=_key_bits(1 + fx["n_cat"]))
 
     def _qnn_forward(self, W, xF, B, seed, training, logits):
         """QNNAlphaDetailed.forward (qnn_alpha.py:109-130)."""
@@ -482,10 +520,12 @@ class Engine:
         att_c = W.get("att_contrib", (M, D))
         att_k = W.get("att_keys", (M,), torch.int32)
         rep_k = W.get("rep_keys", (M,), torch.int32)
-        call("ctr_dare_topk_bwd", ptr(sv["tok"]), B, K, ptr(sv["query"]), ptr(P["dare.emb_att.weight"]), D,
-             ptr(dvals), a.pad_id, ptr(dq), ptr(att_c), ptr(att_k), ptr(rep_k), st)
-        tg["att"] = self._rowgrad(W, "att", att_k, att_c, M, D, D, self.seq_key_bits)
-        tg["rep"] = self._rowgrad(W, "rep", rep_k, dx, M, D, D, self.seq_key_bits)
+        tv = sv["tv"]
+        tg["fx"] = tv["fx"]
+        call("ctr_dare_topk_bwd", ptr(sv["tok"]), B, K, ptr(sv["query"]), tv["att"], D, ptr(dvals), tv["pad"], ptr(dq),
+             ptr(att_c), ptr(att_k), ptr(rep_k), st)
+        tg["att"] = self._rowgrad(W, "att", att_k, att_c, M, D, D, tv["seq_bits"])
+        tg["rep"] = self._rowgrad(W, "rep", rep_k, dx, M, D, D, tv["seq_bits"])
         # ---------------- context / query
         mode = QUERY_MODES[a.query_mode]
         dcat = W.get("dcat", (B, a.Fc, D))
@@ -517,10 +557,10 @@ class Engine:
         cat_c = W.get("cat_contrib", (n_cat, 64))
         cat_k = W.get("cat_keys", (n_cat,), torch.int32)
         cws = W.get("cat_ws", (_lib.query("ctr_cat_embed_bwd_ws", B, a.Fc) // 4 + 1,))
-        call("ctr_cat_embed_bwd", ptr(sv["X_cat"]), B, a.Fc, ptr(self.arena.buf), ptr(self.cat_tab_off),
-             ptr(self.cat_proj_off), ptr(self.cat_dims_t), D, ptr(dcat), ptr(self.cat_row_base), ptr(cat_c),
+        call("ctr_cat_embed_bwd", ptr(tv["xcat"]), B, a.Fc, ptr(self.arena.buf), tv["cat_tab"], tv["cat_off"],
+             ptr(self.cat_proj_off), ptr(self.cat_dims_t), tv["cat_ld"], D, ptr(dcat), tv["row_base"], ptr(cat_c),
              ptr(cat_k), ptr(self.arena.grad), ptr(self.cat_proj_off), ptr(cws), st)
-        tg["cat"] = self._rowgrad(W, "cat", cat_k, cat_c, n_cat, 64, 64, self.cat_key_bits)
+        tg["cat"] = self._rowgrad(W, "cat", cat_k, cat_c, n_cat, 64, 64, tv["cat_bits"])
         return tg
 
     def _rowgrad(self, W, name, keys, contrib, n, width, ld, key_bits):
@@ -699,6 +739,8 @@ class Engine:
     # ------------------------------------------------------------------ compat: dense table grads
     def dense_table_grad(self, key):
         """Materialise the dense gradient of one embedding table from the compact rows (autograd path)."""
+        if self.shards is not None:
+            raise NotImplementedError("row-sharded tables train through the fused step (model.train_step)")
         a = self.a
         shp = self.arena.shapes[key]
         out = torch.zeros(shp, dtype=torch.float32, device=self.device)

@@ -94,9 +94,10 @@ class ArenaEMA:
         self._saved = None
 
     def shadow_params(self):
+        """{key: shadow tensor}; row-sharded tables come back whole (collective)."""
         self.model.sync()
         ar = self.model.arena
-        return {k: ar._view(self.shadow, k) for k in ar.order}
+        return {k: self.model.full_table(self.shadow, k) for k in ar.order}
 
     def state_dict(self):
         return {"base_decay": self.base_decay, "warmup_steps": self.warmup_steps, "warmup_type": self.warmup_type,
@@ -113,8 +114,14 @@ class ArenaEMA:
         self.update_after_step = int(state["update_after_step"])
         self.update_interval = int(state["update_interval"])
         self.num_updates = int(state.get("num_updates", 0))
-        for k, v in self.shadow_params().items():
-            v.copy_(state["shadow_params"][k])
+        self.model.sync()
+        ar, sh = self.model.arena, self.model.shards
+        for k in ar.order:
+            src = torch.as_tensor(state["shadow_params"][k])
+            if sh is not None and ar.kind[k] == "table":
+                from .shard import full_to_local
+                src = full_to_local(src, sh.rank, sh.world)
+            ar._view(self.shadow, k).copy_(src)
 
 
 def build_ema(model, cfg):
@@ -168,6 +175,11 @@ class FusedAdamW:
             self._init_lazy()
         object.__setattr__(model, "_fused_opt", self)
         self.engine.lazy = self if self.lazy else None
+        self.shards = self.engine.shards
+        if self.shards is not None:
+            if process_group is None:
+                raise ValueError("row-sharded tables need the process_group they are sharded over")
+            self.shards.lazy = self if self.lazy else None
 
     # -------------------------------------------------------------- layout
     def _segments(self, tg):
@@ -267,6 +279,19 @@ class FusedAdamW:
              ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
              self.engine.s())
 
+    def touch_local(self, loc_seq, loc_cat):
+        """Row-sharded tables: bring the local rows other ranks requested this step current (owner side
+        of TableShards.fetch): loc_seq rows of both DARE shards, loc_cat local categorical keys."""
+        if self.tick == self._flushed_tick:
+            return
+        st = self.engine.s()
+        for X, group, mode in ((loc_seq, "seq", 0), (loc_cat, "cat", 2)):
+            if X.numel() == 0:
+                continue
+            tabs, n = self._lazy_tabs[group]
+            call("ctr_lazy_touch", ptr(tabs), n, ptr(X), X.numel(), 1, mode, ptr(self.arena.buf), ptr(self.m),
+                 ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
+
     @torch.no_grad()
     def flush(self):
         """Replay every table row to the current tick: afterwards arena, moments and EMA shadow hold
@@ -304,6 +329,9 @@ class FusedAdamW:
             t = tg[name]
             call("ctr_sqnorm_rows", ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["width"], t["G"].shape[1],
                  INVALID_KEY, ptr(parts, (j + 1) * n), st)
+        if self.shards is not None:     # each rank holds its own rows' grads: sum the table partials
+            from . import dist as D
+            D.allreduce_sum_(parts[n:], self.pg)
         call("ctr_clip_finalize", ptr(parts), 4 * n, self.max_grad_norm, 1.0 / self.world, ptr(self.norm_out), st)
         return self.norm_out
 
@@ -345,7 +373,12 @@ class FusedAdamW:
     def step(self, tg=None, global_step=None):
         """clip (if max_grad_norm > 0) -> AdamW -> EMA (if bound and due at global_step)."""
         tg = tg if tg is not None else self.engine.tg
-        if self.pg is not None:
+        if self.shards is not None:
+            from . import dist as D
+            D.allreduce_sum_(self.arena.grad[:self.arena.n_dense_grad], self.pg)
+            tg = self.shards.route(tg, tg["fx"])
+            self.engine.tg = tg
+        elif self.pg is not None:
             tg = self.exchange(tg)
             self.engine.tg = tg
         g = self.param_groups[0]

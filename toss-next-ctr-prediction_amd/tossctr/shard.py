@@ -1,0 +1,238 @@
+"""Row-sharded embedding tables across the data-parallel ranks (BASELINE config 5).
+
+Replicated tables (tossctr/optim.py ``FusedAdamW.exchange``) all-gather every rank's row grads and
+repeat the table optimizer work on every GPU; with ``hash_buckets=1e8, emb_dim=64`` the tables alone
+(60 B params, 240 GB fp32 before Adam moments) do not fit one GPU at all.  Here row r of a table lives
+on rank ``r % world`` at local row ``r // world`` (tables, moments, EMA shadow and lazy-update state
+are all 1/world per GPU), and a step exchanges only the rows a batch uses:
+
+  forward  ``fetch``:  plan (dedup the batch's ids, owner-major) -> all-to-all of requested keys ->
+           owners bring the rows current (exact lazy AdamW) and gather them -> all-to-all of rows back.
+           The batch is remapped to fetched-row ids, so the forward kernels read a compact table.
+  backward ``route``:  the row-grad dedup runs on fetched-row ids; its sorted unique ids map back to
+           owner runs -> all-to-all of (local key, grad row) -> the owner's second dedup merges the
+           ranks' contributions in rank order (deterministic) -> clip / AdamW / EMA on local rows.
+
+Per rank and step that is the batch's unique rows twice (rows out, grads back) instead of
+world x (all ranks' grads) for the replicated all-gather.  Two host reads of per-owner counts per
+step (forward and backward) size the all-to-alls.
+
+The pad token's rows are never fetched: fetched row 0 is zero, which is what ``padding_idx`` keeps
+the pad rows at (zero init, zero grad, so AdamW/EMA leave them at zero).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import dist as D
+from ._lib import call
+
+INVALID = 0xFFFFFFFF
+
+
+def _ptr(t, elems=0):
+    return t.data_ptr() + elems * t.element_size() if t is not None else None
+
+
+def shard_rows(rows: int, world: int) -> int:
+    """Local rows of a table of ``rows`` rows: ceil(rows / world) (the last ranks may own one fewer)."""
+    return (int(rows) + world - 1) // world
+
+
+def full_to_local(full: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """Rows ``rank, rank + world, ...`` of a full table, padded to shard_rows() rows."""
+    n = shard_rows(full.shape[0], world)
+    out = full.new_zeros((n,) + tuple(full.shape[1:]))
+    loc = full[rank::world]
+    out[:loc.shape[0]] = loc
+    return out
+
+
+def locals_to_full(parts: torch.Tensor, rows: int) -> torch.Tensor:
+    """parts (world, local_rows, width) of every rank -> the full (rows, width) table."""
+    w, n = parts.shape[0], parts.shape[1]
+    return parts.transpose(0, 1).reshape(n * w, *parts.shape[2:])[:rows]
+
+
+class _Grow:
+    """Device buffers that only grow (exchange sizes vary per step)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.t = {}
+
+    def get(self, name, n, width=None, dtype=torch.float32, zero=False):
+        shape = (n,) if width is None else (n, width)
+        t = self.t.get(name)
+        if t is None or t.shape[0] < n or t.dtype != dtype or (width is not None and t.shape[1] != width):
+            cap = max(n, 1) if t is None else max(n, int(t.shape[0] * 1.25))
+            cshape = (cap,) if width is None else (cap, width)
+            t = torch.zeros(cshape, dtype=dtype, device=self.device) if zero else \
+                torch.empty(cshape, dtype=dtype, device=self.device)
+            self.t[name] = t
+        return t[:n] if width is None else t[:n]
+
+
+class TableShards:
+    """Owner map, fetch (forward) and grad routing (backward) for one CTRModel's tables."""
+
+    CAT_LD = 64    # fetched categorical rows are zero-padded to 64 floats (d_c <= 64)
+
+    def __init__(self, arch, group, rank: int, world: int, device):
+        self.a = arch
+        self.group = group
+        self.rank, self.world = int(rank), int(world)
+        self.device = device
+        W = self.world
+        obits = (W - 1).bit_length()
+        # sequence tokens: local key = token // W
+        self.seq_rows = shard_rows(arch.seq_vocab, W)
+        self.seq_lbits = self.seq_rows.bit_length()           # local keys < 2^lbits - 1
+        self.seq_kbits = self.seq_lbits + obits
+        # hashed categoricals: local key = lbase[c] + x // W
+        loc = [shard_rows(c, W) for c in arch.cat_cards]
+        self.cat_local_rows = loc
+        self.cat_lbase_np = np.concatenate([[0], np.cumsum(loc)[:-1]]).astype(np.uint32)
+        total = int(sum(loc))
+        self.cat_lbits = total.bit_length()
+        self.cat_kbits = self.cat_lbits + obits
+        if self.seq_kbits > 32 or self.cat_kbits > 32:
+            raise ValueError(f"row-sharded keys need {max(self.seq_kbits, self.cat_kbits)} bits (> 32): "
+                             f"use more ranks per table or smaller tables")
+        self.cat_lbase = torch.from_numpy(self.cat_lbase_np.view(np.int32)).to(device)
+        self.cat_zero_off = torch.zeros(arch.Fc, dtype=torch.int64, device=device)
+        self.cat_zero_base = torch.zeros(arch.Fc, dtype=torch.int32, device=device)
+        self.buf = _Grow(device)
+        self.lazy = None        # FusedAdamW (lazy) bound by the optimizer: owners bring rows current
+        self.tabs_seq = None    # device ctr_lazy_tab_t arrays of the local shards (set by the engine)
+        self.tabs_cat = None
+        self.arena_buf = None   # the rank's parameter arena (local table shards)
+
+    # ------------------------------------------------------------------ helpers
+    @staticmethod
+    def _mask(bits):
+        return (1 << bits) - 1
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _plan(self, name, X, ncols, mode):
+        n = X.numel()
+        uniq = self.buf.get(f"{name}_uniq", n, dtype=torch.int32)
+        nu = self.buf.get(f"{name}_nu", 1, dtype=torch.int32)
+        remap = self.buf.get(f"{name}_remap", n, dtype=torch.int32)
+        cnt = self.buf.get(f"{name}_cnt", self.world, dtype=torch.int64)
+        wsz = _lib.query("ctr_shard_plan_ws_size", n)
+        ws = self.buf.get("plan_ws", wsz, dtype=torch.uint8)
+        if mode == 0:
+            call("ctr_shard_plan", _ptr(X), n, 1, 0, self.a.pad_id, None, self.world, self.seq_lbits, self.seq_kbits,
+                 _ptr(uniq), _ptr(nu), _ptr(remap), _ptr(cnt), _ptr(ws), wsz, self._stream())
+        else:
+            call("ctr_shard_plan", _ptr(X), n, ncols, 1, 0, _ptr(self.cat_lbase), self.world, self.cat_lbits,
+                 self.cat_kbits, _ptr(uniq), _ptr(nu), _ptr(remap), _ptr(cnt), _ptr(ws), wsz, self._stream())
+        return uniq, remap.view(X.shape), cnt
+
+    def _counts(self, name, a, b):
+        """All-to-all of two per-owner count vectors; one host read returns (send_a, send_b, recv_a, recv_b)."""
+        W = self.world
+        send = self.buf.get(f"{name}_csend", 2 * W, dtype=torch.int64).view(W, 2)
+        send[:, 0].copy_(a)
+        send[:, 1].copy_(b)
+        recv = self.buf.get(f"{name}_crecv", 2 * W, dtype=torch.int64)
+        D.all_to_all_var(recv, send.view(-1), [2] * W, [2] * W, self.group)
+        h = torch.cat([send.view(-1), recv]).cpu().tolist()      # the phase's one host sync
+        return h[0:2 * W:2], h[1:2 * W:2], h[2 * W::2], h[2 * W + 1::2]
+
+    # ------------------------------------------------------------------ forward
+    def fetch(self, X_cat, seq):
+        """Rows the batch reads, fetched from their owners.  Returns the remapped batch (fetched-row
+        ids; 0 = pad) and the compact tables: att/rep (1 + n_uniq, D) with row 0 zero, cat (1 + n, 64)."""
+        a, st = self.a, self._stream()
+        Dm = a.D
+        uniq_s, seq_c, cnt_s = self._plan("seq", seq, 1, 0)
+        uniq_c, xcat_c, cnt_c = self._plan("cat", X_cat, X_cat.shape[1], 1)
+        send_s, send_c, recv_s, recv_c = self._counts("fwd", cnt_s, cnt_c)
+        ns, nc = sum(send_s), sum(send_c)
+        rs, rc = sum(recv_s), sum(recv_c)
+        # requested keys -> owners
+        req_s = self.buf.get("req_s", rs, dtype=torch.int32)
+        req_c = self.buf.get("req_c", rc, dtype=torch.int32)
+        D.all_to_all_var(req_s, uniq_s[:ns], recv_s, send_s, self.group)
+        D.all_to_all_var(req_c, uniq_c[:nc], recv_c, send_c, self.group)
+        # owner side: local keys, rows brought current, rows gathered
+        loc_s = self.buf.get("loc_s", rs, dtype=torch.int32)
+        loc_c = self.buf.get("loc_c", rc, dtype=torch.int32)
+        call("ctr_shard_strip", _ptr(req_s), rs, self._mask(self.seq_lbits), _ptr(loc_s), st)
+        call("ctr_shard_strip", _ptr(req_c), rc, self._mask(self.cat_lbits), _ptr(loc_c), st)
+        if self.lazy is not None:
+            self.lazy.touch_local(loc_s, loc_c)
+        arena = self.arena_buf
+        out_att = self.buf.get("out_att", rs, Dm)
+        out_rep = self.buf.get("out_rep", rs, Dm)
+        out_cat = self.buf.get("out_cat", rc, self.CAT_LD)
+        tabs, nt = self.tabs_seq
+        call("ctr_shard_gather", _ptr(loc_s), rs, 0, _ptr(tabs), nt, _ptr(arena), _ptr(out_att), _ptr(out_rep), Dm, st)
+        tabs, nt = self.tabs_cat
+        call("ctr_shard_gather", _ptr(loc_c), rc, 1, _ptr(tabs), nt, _ptr(arena), _ptr(out_cat), None, self.CAT_LD, st)
+        # rows back, in the requester's unique-key order (fetched row u + 1 = unique key u)
+        att = self.buf.get("att", 1 + seq.numel(), Dm, zero=True)
+        rep = self.buf.get("rep", 1 + seq.numel(), Dm, zero=True)
+        cat = self.buf.get("cat", 1 + X_cat.numel(), self.CAT_LD, zero=True)
+        D.all_to_all_var(att[1:1 + ns], out_att, send_s, recv_s, self.group)
+        D.all_to_all_var(rep[1:1 + ns], out_rep, send_s, recv_s, self.group)
+        D.all_to_all_var(cat[1:1 + nc], out_cat, send_c, recv_c, self.group)
+        return dict(seq=seq_c, xcat=xcat_c, att=att, rep=rep, cat=cat, uniq_s=uniq_s, uniq_c=uniq_c, cnt_s=cnt_s,
+                    cnt_c=cnt_c, n_seq=seq.numel(), n_cat=X_cat.numel())
+
+    # ------------------------------------------------------------------ backward
+    def _rowgrad(self, name, keys, rows, n, width, bits):
+        uk = self.buf.get(f"{name}_uk", n, dtype=torch.int32)
+        ug = self.buf.get(f"{name}_ug", n, width)
+        nu = self.buf.get(f"{name}_nu", 1, dtype=torch.int32)
+        wsz = _lib.query("ctr_rowgrad_ws_size", n)
+        ws = self.buf.get("rowgrad_ws", wsz, dtype=torch.uint8)
+        call("ctr_rowgrad", _ptr(keys), _ptr(rows), n, width, width, bits, _ptr(uk), _ptr(ug), _ptr(nu), _ptr(ws), wsz,
+             self._stream())
+        return dict(keys=uk, G=ug, n_uniq=nu, width=width, n=n)
+
+    def route(self, tg, fx):
+        """Compact grads on fetched-row ids (tg from Engine.backward) -> the owners' merged grads on
+        local keys: {"att", "rep", "cat"} in the layout the optimizer consumes."""
+        st = self._stream()
+        W = self.world
+        ta, tr, tc = tg["att"], tg["rep"], tg["cat"]
+        # att and rep were deduplicated from the same keys (top-K tokens): one key order for both
+        ks = self.buf.get("rk_s", ta["n"], dtype=torch.int32)
+        kc = self.buf.get("rk_c", tc["n"], dtype=torch.int32)
+        cs = self.buf.get("rcnt_s", W, dtype=torch.int64)
+        cc = self.buf.get("rcnt_c", W, dtype=torch.int64)
+        call("ctr_shard_route", _ptr(ta["keys"]), _ptr(ta["n_uniq"]), ta["n"], _ptr(fx["uniq_s"]), _ptr(fx["cnt_s"]), W,
+             self._mask(self.seq_lbits), _ptr(ks), _ptr(cs), st)
+        call("ctr_shard_route", _ptr(tc["keys"]), _ptr(tc["n_uniq"]), tc["n"], _ptr(fx["uniq_c"]), _ptr(fx["cnt_c"]), W,
+             self._mask(self.cat_lbits), _ptr(kc), _ptr(cc), st)
+        send_s, send_c, recv_s, recv_c = self._counts("bwd", cs, cc)
+        ns, nc, rs, rc = sum(send_s), sum(send_c), sum(recv_s), sum(recv_c)
+        Dm = ta["width"]
+        rk_s = self.buf.get("gk_s", rs, dtype=torch.int32)
+        rg_a = self.buf.get("ga_s", rs, Dm)
+        rg_r = self.buf.get("gr_s", rs, Dm)
+        rk_c = self.buf.get("gk_c", rc, dtype=torch.int32)
+        rg_c = self.buf.get("gc_c", rc, tc["width"])
+        D.all_to_all_var(rk_s, ks[:ns], recv_s, send_s, self.group)
+        D.all_to_all_var(rg_a, ta["G"][:ns], recv_s, send_s, self.group)
+        D.all_to_all_var(rg_r, tr["G"][:ns], recv_s, send_s, self.group)
+        D.all_to_all_var(rk_c, kc[:nc], recv_c, send_c, self.group)
+        D.all_to_all_var(rg_c, tc["G"][:nc], recv_c, send_c, self.group)
+        return {"att": self._rowgrad("sh_att", rk_s, rg_a, rs, Dm, self.seq_lbits),
+                "rep": self._rowgrad("sh_rep", rk_s, rg_r, rs, Dm, self.seq_lbits),
+                "cat": self._rowgrad("sh_cat", rk_c, rg_c, rc, tc["width"], self.cat_lbits)}
+
+    # ------------------------------------------------------------------ full-table views (checkpoints)
+    def gather_full(self, local: torch.Tensor, rows: int) -> torch.Tensor:
+        """Every rank's shard of one table -> the full table (collective; result on this device)."""
+        parts = torch.empty((self.world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        D.all_gather_into(parts.view(-1), local.contiguous().view(-1), self.group)
+        return locals_to_full(parts, rows)
+

@@ -67,7 +67,12 @@ class _CTRFunction(torch.autograd.Function):
 
 class CTRModel(nn.Module):
     def __init__(self, cfg, seq_vocab: int, num_feat_dim: int, mask_feat_dim: int, cat_cardinals: dict,
-                 cat_cols_order: list, device=None):
+                 cat_cols_order: list, device=None, process_group=None, shard_tables=False):
+        """Reference constructor (src/models/wrapper.py:8-9) plus MI355X placement: ``device`` (default:
+        the current HIP device) and, for data parallelism, ``shard_tables=True`` with ``process_group``:
+        every embedding table is row-sharded over the group's ranks (tossctr/shard.py) -- each rank
+        holds rows r with r % world == rank.  Collective from then on: every rank runs forward /
+        train_step / state_dict / load_state_dict together."""
         super().__init__()
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
@@ -81,8 +86,17 @@ class CTRModel(nn.Module):
         self.query_key = self.arch.query_key
         self.aux_weight = self.arch.aux_w
         self.use_qnn = self.arch.use_qnn
-        object.__setattr__(self, "arena", ParamArena(self.arch, torch.device(device)))
-        object.__setattr__(self, "engine", Engine(self.arch, self.arena))
+        shards = None
+        if shard_tables:
+            import torch.distributed as dist
+            from .shard import TableShards
+            if process_group is None:
+                process_group = dist.group.WORLD
+            shards = TableShards(self.arch, process_group, dist.get_rank(process_group),
+                                 dist.get_world_size(process_group), torch.device(device))
+        object.__setattr__(self, "shards", shards)
+        object.__setattr__(self, "arena", ParamArena(self.arch, torch.device(device), shards))
+        object.__setattr__(self, "engine", Engine(self.arch, self.arena, shards))
         self.no_grad = self.arch.no_grad_keys()
         for k in self.arena.order:
             mod, name = _tree_module(self, k)
@@ -100,11 +114,38 @@ class CTRModel(nn.Module):
 
     def state_dict(self, *args, **kwargs):
         self.sync()
-        return super().state_dict(*args, **kwargs)
+        sd = super().state_dict(*args, **kwargs)
+        if self.shards is not None:     # full tables, as the reference's state_dict has them (collective)
+            prefix = kwargs.get("prefix", args[1] if len(args) > 1 else "")
+            for k in self.arena.order:
+                if self.arena.kind[k] == "table":
+                    sd[prefix + k] = self.full_table(self.arena.buf, k)
+        return sd
 
     def load_state_dict(self, state_dict, strict=True, assign=False):
         self.sync()     # moments / EMA of lagging rows must be current before their params change
+        if self.shards is not None:     # full tables in, this rank's rows kept
+            from .shard import full_to_local
+            sh = self.shards
+            state_dict = dict(state_dict)
+            for k in self.arena.order:
+                if self.arena.kind[k] == "table" and k in state_dict:
+                    state_dict[k] = full_to_local(torch.as_tensor(state_dict[k]), sh.rank, sh.world)
         return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    def full_table(self, buf, key):
+        """Parameter ``key`` viewed in an arena-layout buffer (parameters, a moment, the EMA shadow);
+        row-sharded tables are gathered from every rank (collective)."""
+        v = self.arena._view(buf, key)
+        if self.shards is None or self.arena.kind[key] != "table":
+            return v
+        return self.shards.gather_full(v, self.arch_rows(key))
+
+    def arch_rows(self, key):
+        for k, shp, _ in self.arch.param_shapes():
+            if k == key:
+                return shp[0]
+        raise KeyError(key)
 
     # the arena is not an nn.Module buffer: keep .to()/.cuda() from re-allocating parameters
     def _apply(self, fn, recurse=True):
@@ -123,7 +164,10 @@ class CTRModel(nn.Module):
             elif ".emb_" in k or k.startswith("cat_embs.") or "pbias.rel" in k:
                 t.normal_(0.0, 1.0, generator=g)
                 if ".emb_" in k:
-                    t[a.pad_id].zero_()
+                    if self.shards is None:
+                        t[a.pad_id].zero_()
+                    elif a.pad_id % self.shards.world == self.shards.rank:
+                        t[a.pad_id // self.shards.world].zero_()
             elif k in ("num_embed.weight", "mask_embed.weight", "qnn.U", "qnn.V"):
                 t.normal_(0.0, 0.02, generator=g)
             elif k == "num_embed.bias":
@@ -158,6 +202,8 @@ class CTRModel(nn.Module):
     def forward(self, batch, seed=None):
         inputs = self._stage(batch)
         if self.training and torch.is_grad_enabled():
+            if self.shards is not None:
+                raise NotImplementedError("row-sharded tables train through the fused step (model.train_step)")
             seed = self.next_seed() if seed is None else seed
             return _CTRFunction.apply(self, inputs, seed, *[getattr(*_tree_module(self, k)) for k in self.arena.order])
         logits, prob, aux, _ = self.engine.forward(*inputs, training=self.training,
