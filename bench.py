@@ -6,7 +6,9 @@ A step = one full reference training step (src/train.py:152-199): forward -> bce
 -> backward -> clip_grad_norm_(0.5) -> AdamW -> EMA(0.999), over the full model (1.24 B params incl.
 the 10M x 32 DARE tables and 35 x 1e6-row hashed tables).  Inputs are synthetic (SURVEY §8(d)
 distributions) and already resident in HBM.  Multi-GPU: one process per GPU (torchrun), data-parallel
-(per-GPU batch 4096, weak scaling): dense grads all-reduced and table row-grads all-gathered over RCCL.
+(per-GPU batch 4096, weak scaling): dense grads all-reduced over RCCL; embedding tables row-sharded
+over the ranks (rows fetched from / grads routed to their owners with RCCL all-to-alls; --tables
+replicated all-gathers row grads instead).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 """
@@ -169,17 +171,21 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense-opt", action="store_true",
                     help="step the tables in the dense AdamW/EMA stream instead of the exact lazy path")
+    ap.add_argument("--tables", choices=("sharded", "replicated"), default="sharded",
+                    help="N > 1: row-shard the embedding tables over the ranks (all-to-all row fetch / grad "
+                         "routing) or replicate them (all-gather of row grads)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())   # ranks > cards: rehearsal
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("CTR_DIST_BACKEND", "nccl")    # gloo: functional rehearsal on one card
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
         pg = dist.group.WORLD
 
     from tossctr import CTRModel, FusedAdamW, build_ema
@@ -191,7 +197,9 @@ def main():
     cols = list(cfg["data"]["cat_cols"])
     vocab = 10_000_000                                   # src/train.py:116
     torch.manual_seed(cfg["seed"])
-    model = CTRModel(cfg, vocab, N_NUM_NEXT, N_NUM_NEXT, cards, cols, device=dev)
+    shard = pg is not None and args.tables == "sharded"
+    model = CTRModel(cfg, vocab, N_NUM_NEXT, N_NUM_NEXT, cards, cols, device=dev, process_group=pg,
+                     shard_tables=shard)
     model.reset_parameters(torch.Generator(device=dev).manual_seed(cfg["seed"]))
     ema = build_ema(model, cfg)
     tr = cfg["train"]
@@ -277,7 +285,8 @@ def main():
             "config": {"workload": "cfgs/dare_qnn_next.yaml + hash_buckets=1e6, emb_dim=32, seq_len=100, "
                                    "bs=4096 per GPU, full train step incl. clip+AdamW+EMA over 1.24B params",
                        "global_batch": args.batch * world, "seq_len": args.seq_len,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}" + ("" if world == 1 else
+                                                     f", tables {'row-sharded' if shard else 'replicated'}")},
             "roofline": roof,
             "step_roofline": {"mode": "dense-equivalent bytes of the reference-semantics step (SURVEY §8(d) formula)",
                               "bytes_per_step": step_bytes_dense_equiv(a, args.batch, args.seq_len, ema is not None),

@@ -56,3 +56,44 @@ def test_kfold_loop_end_to_end(tmp_path, variant):
     assert sum(1 for _ in open(csv_path)) >= 2
     # resume: a second main() skips the finished fold
     assert main(cfg) == {}
+
+
+def test_kfold_loop_world2_sharded_tables(tmp_path):
+    """main() under two ranks (gloo on one card, tables row-sharded): the checkpoint holds full tables,
+    and its recorded validation score is what a single-GPU evaluation of those weights gives (the DP
+    validation spreads batches over the ranks and all-gathers the logits)."""
+    import json
+    import subprocess
+    import sys
+    from sklearn.model_selection import StratifiedGroupKFold
+    from tossctr import CTRModel
+    from tossctr.data import DeviceShards, load_labels_groups_for_split, synth_rows, write_shard_cache
+    from tossctr.metrics import final_score
+    from tossctr.train import predict_logits
+    cols = ["c0", "c1", "c2", "c3"]
+    arr = synth_rows(3000, 6, 6, [203] * 4, 24, 3000, seed=6, pos_rate=0.2)
+    man = write_shard_cache(str(tmp_path / "cache"), arr, shard_rows=1100, num_cols=[f"n{i}" for i in range(6)],
+                            cat_cols=cols, group_key="c0")
+    cfg = tiny_run_cfg(str(tmp_path), man, ema=False)
+    cfg["calibration"]["enabled"] = False
+    cfg["train"]["epochs"] = 1
+    cfg_path, out = str(tmp_path / "cfg.json"), str(tmp_path / "res.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg, f)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "dist_train_worker.py"), cfg_path, out],
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    with open(out) as f:
+        score = json.load(f)["0"]
+    st = torch.load(os.path.join(cfg["logging"]["log_dir"], "tiny", "ckpt_folds_0.pt"), weights_only=False)
+    assert st["state"]["model"]["dare.emb_att.weight"].shape == (3000, 16)
+    m = CTRModel(cfg, 3000, 6, 6, {c: 203 for c in cols}, cols, device="cuda:0")
+    m.load_state_dict(st["state"]["model"], strict=True)
+    y, groups = load_labels_groups_for_split(man)
+    _, va = next(StratifiedGroupKFold(n_splits=5, shuffle=True, random_state=cfg["seed"]).split(
+        np.zeros_like(y), y, groups))
+    store = DeviceShards(man, torch.device("cuda", 0))
+    z = predict_logits(m, store, va, cfg["train"]["batch_size"])
+    _, _, ref = final_score(y[va].astype(np.int64), 1.0 / (1.0 + np.exp(-z.astype(np.float64))))
+    assert abs(ref - score) < 1e-6 * max(1.0, abs(ref)), (ref, score)

@@ -13,7 +13,9 @@ MI355X differences (same results, different mechanics):
   * ``best_state["model"]`` is a detached copy (the reference stores live references, so its "best"
     checkpoint is really the last epoch's weights, SURVEY §5);
   * optional data parallelism: run under torchrun, every rank takes its own stride of each epoch's
-    permutation; grads are synchronised by FusedAdamW (RCCL).
+    permutation; dense grads are all-reduced and the embedding tables row-sharded over the ranks
+    (tossctr/shard.py; ``dist: {shard_tables: false}`` in the yaml keeps them replicated); validation
+    batches are spread over the ranks and their logits all-gathered.
 """
 from __future__ import annotations
 
@@ -68,17 +70,37 @@ def _feature_dims(manifest_path):
 
 @torch.no_grad()
 def predict_logits(model, store, idx_np, bs):
-    """Eval-mode forward over rows idx (src/train.py:211-225); returns logits (numpy)."""
-    from .engine import ptr  # noqa: F401  (import keeps the HIP library resident)
+    """Eval-mode forward over rows idx (src/train.py:211-225); returns logits (numpy).
+
+    The batches are the reference's (consecutive bs-row slices of idx, which matters: the SE gate uses
+    the batch mean).  Data parallel: rank r runs batches r, r + world, ... and the logits are
+    all-gathered, so every rank returns all of them; ranks short of a batch re-run their last one
+    (row-sharded tables make every forward collective) and drop the result."""
     model.eval()
     dev = store.device
-    out = []
+    dist = _dist()
+    world = dist.get_world_size() if dist else 1
+    rank = dist.get_rank() if dist else 0
     idx_all = torch.from_numpy(np.asarray(idx_np, dtype=np.int64)).to(dev)
-    for s in range(0, idx_all.numel(), bs):
-        inputs, _ = store.batch(idx_all[s:s + bs], slot=1)
+    n = idx_all.numel()
+    nb = (n + bs - 1) // bs
+    if nb == 0:
+        return np.zeros(0, np.float32)
+    per_rank = (nb + world - 1) // world
+    mine = torch.zeros(per_rank * bs, dtype=torch.float32, device=dev)
+    for i in range(per_rank):
+        j = min(i * world + rank, nb - 1)
+        sl = idx_all[j * bs:(j + 1) * bs]
+        inputs, _ = store.batch(sl, slot=1)
         logits, _, _, _ = model.engine.forward(*inputs, training=False, seed=0, save=False)
-        out.append(logits.clone())
-    return torch.cat(out).cpu().numpy() if out else np.zeros(0, np.float32)
+        mine[i * bs:i * bs + sl.numel()] = logits
+    if world == 1:
+        return mine[:n].cpu().numpy()
+    from . import dist as D
+    allr = torch.empty(world * per_rank * bs, dtype=torch.float32, device=dev)
+    D.all_gather_into(allr, mine, dist.group.WORLD)
+    out = allr.view(world, per_rank, bs).transpose(0, 1).reshape(-1)     # batch j = (i, r), j = i*world + r
+    return out[:n].cpu().numpy()
 
 
 def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None, device=None):
@@ -98,7 +120,10 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
     seq_vocab = int(cfg.get("seq_vocab", 10_000_000))              # src/train.py:116
     cards = _cardinals(cfg, cat_cols)
     n_num, n_mask = _feature_dims(manifest_path)
-    model = CTRModel(cfg, seq_vocab, n_num, n_mask, cards, cat_cols, device=device)
+    # data parallel: embedding tables row-sharded over the ranks unless dist.shard_tables is false
+    shard = bool(dist) and world > 1 and bool(cfg.get("dist", {}).get("shard_tables", True))
+    model = CTRModel(cfg, seq_vocab, n_num, n_mask, cards, cat_cols, device=device,
+                     process_group=dist.group.WORLD if dist else None, shard_tables=shard)
     model.reset_parameters(torch.Generator(device=device).manual_seed(int(cfg.get("seed", 777)) + fold))
     ema = build_ema(model, cfg)
     opt = FusedAdamW(model, lr=cfg["train"]["lr"], weight_decay=cfg["train"]["weight_decay"],
@@ -214,6 +239,6 @@ if __name__ == "__main__":
     args = ap.parse_args()
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         import torch.distributed as _d
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        _d.init_process_group("nccl")
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+        _d.init_process_group(os.environ.get("CTR_DIST_BACKEND", "nccl"))
     main(args.cfg)

@@ -157,17 +157,24 @@ class CTRModel(nn.Module):
         U(+-1/sqrt(fan_in)) biases, RMSNorm w = 1, feature slopes N(0, 0.02^2), U/V N(0, 0.02^2)."""
         a = self.arch
         g = generator
+        gt = g     # row-sharded tables: every rank draws its own rows (dense params stay identical)
+        if self.shards is not None:
+            base = g.initial_seed() if g is not None else torch.initial_seed()
+            gt = torch.Generator(device=self.arena.device).manual_seed(
+                (base * 1000003 + 7919 * (self.shards.rank + 1)) % (1 << 63))
         for k in self.arena.order:
             t = self.arena.views[k]
             if k.endswith(".w"):
                 t.fill_(1.0)
-            elif ".emb_" in k or k.startswith("cat_embs.") or "pbias.rel" in k:
-                t.normal_(0.0, 1.0, generator=g)
+            elif ".emb_" in k or k.startswith("cat_embs."):
+                t.normal_(0.0, 1.0, generator=gt)
                 if ".emb_" in k:
                     if self.shards is None:
                         t[a.pad_id].zero_()
                     elif a.pad_id % self.shards.world == self.shards.rank:
                         t[a.pad_id // self.shards.world].zero_()
+            elif "pbias.rel" in k:
+                t.normal_(0.0, 1.0, generator=g)
             elif k in ("num_embed.weight", "mask_embed.weight", "qnn.U", "qnn.V"):
                 t.normal_(0.0, 0.02, generator=g)
             elif k == "num_embed.bias":
