@@ -54,6 +54,16 @@ def synth_batches(nb, B, L, Fn, Fm, cards, vocab, device, seed):
     return out
 
 
+WORKLOADS = {
+    "cfg2": "cfgs/dare_qnn_next.yaml + hash_buckets=1e6, emb_dim=32, seq_len={L}, bs={B} per GPU, full train step "
+            "incl. clip+AdamW+EMA over {P:.2f}B params",
+    "cfg3": "cfgs/dare_qnn_next_k100_s1.yaml (K=100, S1) + hash_buckets=1e6, emb_dim=32, seq_len={L}, bs={B} per GPU, "
+            "full train step incl. clip+AdamW+EMA over {P:.2f}B params",
+    "cfg4": "cfgs/v3_k148_s1.yaml (D=64, K=148, 4 layers, EMA off), seq_len={L}, bs={B} per GPU, full train step "
+            "incl. clip+AdamW over {P:.2f}B params",
+    "cfg5": "k100_s1 shape + hash_buckets=1e8, emb_dim=64 (row-sharded tables), seq_len={L}, bs={B} per GPU, "
+            "full train step incl. clip+AdamW+EMA over {P:.2f}B params",
+}
 MFMA_F32_PEAK_TFS = 157.3   # MI355X dense fp32 MFMA (v_mfma_f32_16x16x4_f32), MI355X_MICROARCH.md
 
 
@@ -167,7 +177,9 @@ def main():
     ap.add_argument("--steps", type=int, default=100)    # 20 warm-up, >= 100 timed steps
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--seq-len", type=int, default=100)
+    ap.add_argument("--seq-len", type=int, default=None, help="default: the config's (100; cfg4 400)")
+    ap.add_argument("--config", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2",
+                    help="BASELINE.json config (the metric is quoted on cfg2; cfg5 needs 8 GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dense-opt", action="store_true",
                     help="step the tables in the dense AdamW/EMA stream instead of the exact lazy path")
@@ -192,7 +204,11 @@ def main():
     from tossctr.configs import N_NUM_NEXT, cat_cardinals, dare_qnn_next
     from tossctr.train import cosine_warmup_lr
 
-    cfg = dare_qnn_next(emb_dim=32, max_len=args.seq_len, batch_size=args.batch)
+    from tossctr.configs import BENCH_CONFIGS
+    cfg = BENCH_CONFIGS[args.config](batch_size=args.batch)
+    if args.seq_len is None:
+        args.seq_len = int(cfg["sequence"]["max_len"])
+    cfg["sequence"]["max_len"] = args.seq_len
     cards = cat_cardinals(cfg)
     cols = list(cfg["data"]["cat_cols"])
     vocab = 10_000_000                                   # src/train.py:116
@@ -273,17 +289,20 @@ def main():
             ach = work / (kstats[n][1] * 1e-3) / 1e12
             roof = {"bound": bound, "kernel": n, "achieved": round(ach, 2), "peak": MFMA_F32_PEAK_TFS,
                     "unit": "TFLOP/s", "frac": round(ach / MFMA_F32_PEAK_TFS, 4),
-                    "traffic": pmc_traffic(n), "work_per_launch": work, "work_unit": unit,
+                    "traffic": pmc_traffic(n) if args.config == "cfg2" else None, "work_per_launch": work,
+                    "work_unit": unit,
                     "avg_launch_ms": round(kstats[n][1], 4), "ms_per_step": round(per_step[n], 4),
                     "share_of_step": round(per_step[n] / ms, 4)}
             break
         rec = {
-            "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref",
+            "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref"
+                      + ("" if args.config == "cfg2" else f" [{args.config}: not the headline config]"),
             "value": round(samples, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY 8(d) distributions), HBM-resident",
-            "config": {"workload": "cfgs/dare_qnn_next.yaml + hash_buckets=1e6, emb_dim=32, seq_len=100, "
-                                   "bs=4096 per GPU, full train step incl. clip+AdamW+EMA over 1.24B params",
+            "config": {"workload": WORKLOADS[args.config].format(B=args.batch, L=args.seq_len,
+                                                                 P=sum(int(np.prod(sh)) for _, sh, _ in
+                                                                       a.param_shapes()) / 1e9),
                        "global_batch": args.batch * world, "seq_len": args.seq_len,
                        "parallelism": f"dp{world}" + ("" if world == 1 else
                                                      f", tables {'row-sharded' if shard else 'replicated'}")},
@@ -299,7 +318,7 @@ def main():
         sr = rec["step_roofline"]
         sr["achieved"] = round(sr["bytes_per_step"] / (ms * 1e-3) / 1e9, 1)
         sr["frac"] = round(sr["achieved"] / HBM_PEAK_GBS, 4)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.config == "cfg2":
             del data
             rec["cpu_baseline"] = cpu_baseline(cfg, args.batch, args.seq_len)
         else:

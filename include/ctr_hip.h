@@ -209,6 +209,11 @@ int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, in
 size_t ctr_rowgrad_ws_size(int n);
 int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, int width, int ld, int key_bits,
                 uint32_t* uniq_keys, float* uniq_grad, uint32_t* n_uniq, void* ws, size_t ws_bytes, void* stream);
+/* two contribution arrays with the SAME keys (DARE att and rep rows: both keyed by the top-K tokens)
+ * share one sort: uniq_a / uniq_b are their per-key sums                                          */
+int ctr_rowgrad2(const uint32_t* keys, const float* contrib_a, const float* contrib_b, int n, int width, int ld,
+                 int key_bits, uint32_t* uniq_keys, float* uniq_a, float* uniq_b, uint32_t* n_uniq, void* ws,
+                 size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused clip_grad_norm_ + AdamW + EMA over the parameter arena                      (optim.hip)

@@ -93,10 +93,10 @@ using namespace ctr;
 
 extern "C" size_t ctr_rowgrad_ws_size(int n) { return n > 0 ? rowgrad_layout(n).total : 0; }
 
-extern "C" int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, int width, int ld, int key_bits,
-                           uint32_t* uniq_keys, float* uniq_grad, uint32_t* n_uniq, void* ws, size_t ws_bytes,
-                           void* stream) {
-  hipStream_t s = (hipStream_t)stream;
+// sort + run-length encode + offsets shared by every contribution array keyed by `keys`
+static int rowgrad_core(const uint32_t* keys, const float* const* contrib, float* const* uniq_grad, int ncontrib,
+                        int n, int width, int ld, int key_bits, uint32_t* uniq_keys, uint32_t* n_uniq, void* ws,
+                        size_t ws_bytes, hipStream_t s) {
   if (n == 0) {
     (void)hipMemsetAsync(n_uniq, 0, sizeof(uint32_t), s);
     return check_launch("rowgrad");
@@ -122,9 +122,25 @@ extern "C" int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, in
   tb = w.temp_bytes;
   e = rocprim::exclusive_scan(base, tb, (const uint32_t*)counts, offsets, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
   CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
-  segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib, ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
-                                           uniq_grad);
+  for (int q = 0; q < ncontrib; ++q)
+    segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
+                                             uniq_grad[q]);
   return check_launch("rowgrad");
+}
+
+extern "C" int ctr_rowgrad(const uint32_t* keys, const float* contrib, int n, int width, int ld, int key_bits,
+                           uint32_t* uniq_keys, float* uniq_grad, uint32_t* n_uniq, void* ws, size_t ws_bytes,
+                           void* stream) {
+  return rowgrad_core(keys, &contrib, &uniq_grad, 1, n, width, ld, key_bits, uniq_keys, n_uniq, ws, ws_bytes,
+                      (hipStream_t)stream);
+}
+
+extern "C" int ctr_rowgrad2(const uint32_t* keys, const float* contrib_a, const float* contrib_b, int n, int width,
+                            int ld, int key_bits, uint32_t* uniq_keys, float* uniq_a, float* uniq_b, uint32_t* n_uniq,
+                            void* ws, size_t ws_bytes, void* stream) {
+  const float* c[2] = {contrib_a, contrib_b};
+  float* u[2] = {uniq_a, uniq_b};
+  return rowgrad_core(keys, c, u, 2, n, width, ld, key_bits, uniq_keys, n_uniq, ws, ws_bytes, (hipStream_t)stream);
 }
 
 namespace ctr {

@@ -82,6 +82,7 @@ SIGS = {
     "ctr_se_bwd": (i, [p, l, p, i, i, i, p, p, p, p, p, u, u, f, p, p, p, p, p, p, p]),
     "ctr_rowgrad_ws_size": (z, [i]),
     "ctr_rowgrad": (i, [p, p, i, i, i, i, p, p, p, p, z, p]),
+    "ctr_rowgrad2": (i, [p, p, p, i, i, i, i, p, p, p, p, p, z, p]),
     "ctr_opt_chunk_elems": (i, []),
     "ctr_adamw_ema": (i, [p, i, p, p, p, p, p, p, p, p, f, f, f, f, f, i, f, i, i, p]),
     "ctr_norm_nparts_per_call": (i, []),

@@ -55,6 +55,47 @@ def dare_qnn_next_k100_s1(**kw):
     return cfg
 
 
+# cfgs/v3_k148_s1.yaml:137-171 (hash_buckets; margin 500 at l.172)
+HB_V3 = {
+    "gender": 1005, "age_group": 1011, "day_of_week": 1009, "hour": 1026, "inventory_id": 1020, "l_feat_1": 1004,
+    "l_feat_2": 1005, "l_feat_3": 1005, "l_feat_4": 1028, "l_feat_5": 2078, "l_feat_6": 1902, "l_feat_7": 1315,
+    "l_feat_8": 1005, "l_feat_9": 1478, "l_feat_10": 1264, "l_feat_11": 2526, "l_feat_12": 6052, "l_feat_13": 1004,
+    "l_feat_14": 4239, "l_feat_15": 3584, "l_feat_16": 1004, "l_feat_17": 1478, "l_feat_18": 1010, "l_feat_19": 1005,
+    "l_feat_20": 1004, "l_feat_21": 1005, "l_feat_22": 1005, "l_feat_23": 1004, "l_feat_24": 1005, "l_feat_25": 2790,
+    "l_feat_26": 1020, "l_feat_27": 1007, "feat_a_2": 1008, "feat_a_8": 1010, "feat_a_9": 1012,
+}
+
+
+def v3_k148_s1(batch_size=4096, max_len=400):
+    """BASELINE config 4: cfgs/v3_k148_s1.yaml as-is -- D=64 (l.199), L=400, K=148, S1 (l.181-184),
+    4 layers x 8 heads, ffn 384, ffn dropout 0.15 (l.186-194), dare dropout 0.25 (l.200),
+    inventory_id dim 32 (l.205), EMA off (l.294), buckets l.137-172."""
+    cfg = dare_qnn_next(emb_dim=64, max_len=max_len, batch_size=batch_size)
+    cfg["exp_name"] = "v3_k132_s1"
+    cfg["data"]["hash_buckets"] = dict(HB_V3)
+    cfg["data"]["hash_buckets_margin"] = 500
+    sq = cfg["sequence"]
+    sq.update(top_k=148, query_mode="S1")
+    sq["tfm"].update(n_layers=4, ffn_dropout=0.15)
+    cfg["model"]["dare_dropout"] = 0.25
+    cfg["model"]["cat_embedding_dims"]["inventory_id"] = 32
+    cfg["ema"]["enabled"] = False
+    return cfg
+
+
+def hb1e8_d64(**kw):
+    """BASELINE config 5: the k100_s1 shape with every hash_buckets = 1e8 and emb_dim = 64 (tables of
+    60 B parameters: row-sharded over 8 GPUs)."""
+    kw.setdefault("emb_dim", 64)
+    kw.setdefault("hash_buckets", 100_000_000)
+    cfg = dare_qnn_next_k100_s1(**kw)
+    cfg["exp_name"] = "hb1e8_d64"
+    return cfg
+
+
+BENCH_CONFIGS = {"cfg2": dare_qnn_next, "cfg3": dare_qnn_next_k100_s1, "cfg4": v3_k148_s1, "cfg5": hb1e8_d64}
+
+
 def cat_cardinals(cfg):
     """src/train.py:119: hash_buckets.get(c, 1000003) + hash_buckets_margin."""
     d = cfg["data"]

@@ -524,8 +524,8 @@ class Engine:
         tg["fx"] = tv["fx"]
         call("ctr_dare_topk_bwd", ptr(sv["tok"]), B, K, ptr(sv["query"]), tv["att"], D, ptr(dvals), tv["pad"], ptr(dq),
              ptr(att_c), ptr(att_k), ptr(rep_k), st)
-        tg["att"] = self._rowgrad(W, "att", att_k, att_c, M, D, D, tv["seq_bits"])
-        tg["rep"] = self._rowgrad(W, "rep", rep_k, dx, M, D, D, tv["seq_bits"])
+        # att and rep contributions share their keys (the top-K tokens): one sort for both
+        tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"])
         # ---------------- context / query
         mode = QUERY_MODES[a.query_mode]
         dcat = W.get("dcat", (B, a.Fc, D))
@@ -573,6 +573,18 @@ class Engine:
         call("ctr_rowgrad", ptr(keys), ptr(contrib), n, width, ld, key_bits, ptr(uk), ptr(ug), ptr(nu), ptr(rws),
              rws.numel(), self.s())
         return dict(keys=uk, G=ug, n_uniq=nu, width=width, n=n)
+
+    def _rowgrad2(self, W, keys, contrib_a, contrib_b, n, width, key_bits):
+        uk = W.get("seq_uk", (n,), torch.int32)
+        ua = W.get("att_ug", (n, width))
+        ub = W.get("rep_ug", (n, width))
+        nu = W.get("seq_nu", (1,), torch.int32)
+        wsz = _lib.query("ctr_rowgrad_ws_size", n)
+        rws = W.get("rowgrad_ws", (max(wsz, W.t["rowgrad_ws"].numel() if "rowgrad_ws" in W.t else 0),),
+                    torch.uint8)
+        call("ctr_rowgrad2", ptr(keys), ptr(contrib_a), ptr(contrib_b), n, width, width, key_bits, ptr(uk), ptr(ua),
+             ptr(ub), ptr(nu), ptr(rws), rws.numel(), self.s())
+        return (dict(keys=uk, G=ua, n_uniq=nu, width=width, n=n), dict(keys=uk, G=ub, n_uniq=nu, width=width, n=n))
 
     def _layer_backward(self, sv, li, dx2, dout_buf):
         """DAREEncoderLayer backward (dare.py:53-70). dx2: grad wrt layer output. Returns grad wrt input."""
