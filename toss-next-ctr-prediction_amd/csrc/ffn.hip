@@ -60,6 +60,9 @@ struct FfnTile {
   static constexpr int TILE = RT * S;             // floats of one x / dh tile
   static constexpr int STG = RW * SS;             // one wave's staging tile
   static constexpr int PW = 32 * D + 16;          // one wave's per-chunk weight-grad partial
+  static constexpr int RG = PW > STG ? PW : STG;  // backward: per-wave region (staging, then partial)
+  // backward: double-buffered regions (one barrier per chunk) when two workgroups still fit a CU
+  static constexpr int NBUF = (2 * TILE + 8 * RG) * 4 <= 80 * 1024 ? 2 : 1;
 };
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
@@ -85,15 +88,17 @@ __device__ __forceinline__ void dcontract(const float* tile, const float (&bv)[F
                                           f32x4 (&acc)[FfnTile<D>::NI], int g, int c) {
   using T = FfnTile<D>;
 #pragma unroll
-  for (int i = 0; i < T::NI; ++i) {
-    const float* row = tile + (16 * i + c) * T::S + g * T::KQ;
-    acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < T::NI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // k-step outer, row blocks inner: the NI accumulation chains interleave (no dependent-MFMA stall)
 #pragma unroll
-    for (int kq = 0; kq < T::KQ; kq += 4) {
-      const f32x4 a = *(const f32x4*)(row + kq);
+  for (int kq = 0; kq < T::KQ; kq += 4) {
+    f32x4 av[T::NI];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[i] = mfma4(a[t], bv[kq + t], acc[i]);
-    }
+    for (int i = 0; i < T::NI; ++i) av[i] = *(const f32x4*)(tile + (16 * i + c) * T::S + g * T::KQ + kq);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i) acc[i] = mfma4(av[i][t], bv[kq + t], acc[i]);
   }
 }
 
@@ -213,7 +218,11 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
 template <int D>
 __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   using T = FfnTile<D>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * T::TILE + 4 * T::STG + 4 * T::PW];
+  // [x tile | dh tile | two buffers of 4 per-wave regions]; chunk k uses buffer k & 1 for its dact
+  // staging tile and then (same wave, same region) its weight-grad partial, so one barrier per chunk
+  // separates the partial writes from the cross-wave sum, and the alternate buffer keeps the next
+  // chunk's writes clear of a slower wave's sum.
+  __shared__ __attribute__((aligned(16))) float smem[2 * T::TILE + 4 * T::NBUF * T::RG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   const int m0 = blockIdx.x * T::RT;
   load_tile<D>(a.x, a.M, m0, smem);
@@ -221,9 +230,6 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   __syncthreads();
   const float* xw = smem + w * T::RW * T::S;
   const float* dw = smem + T::TILE + w * T::RW * T::S;
-  float* st = smem + 2 * T::TILE + w * T::STG;
-  float* red = smem + 2 * T::TILE + 4 * T::STG;
-  float* pw = red + w * T::PW;
   float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
 
   f32x4 dxacc[T::NI][T::NJ];
@@ -232,9 +238,14 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // W slices of chunk f0 are prefetched one chunk ahead
+  // W slices and dropout keep words of chunk f0 are prefetched one chunk ahead
+  constexpr int NR = 4 * T::NI;         // rows of this lane: 16 i + 4 g + rr
+  const int FW = a.FF / 16;
+  const bool drop = a.drop.thresh != 0;
   float bv1[T::KQ], bv2[T::KQ], bw[T::NJ][4], bias;
-  auto load_w = [&](int f0, float (&v1)[T::KQ], float (&v2)[T::KQ], float (&v3)[T::NJ][4], float& b) {
+  uint32_t mw[NR];
+  auto load_w = [&](int f0, float (&v1)[T::KQ], float (&v2)[T::KQ], float (&v3)[T::NJ][4], float& b,
+                    uint32_t (&mk)[NR]) {
     const int ff = f0 + c;
 #pragma unroll
     for (int kq = 0; kq < T::KQ; kq += 4) *(f32x4*)&v1[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
@@ -245,13 +256,19 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
       for (int j = 0; j < T::NJ; ++j) v3[j][t] = a.W1[(long)(f0 + 4 * g + t) * D + 16 * j + c];
     b = a.b1[ff];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const int m = m0 + w * T::RW + 16 * (q >> 2) + 4 * g + (q & 3);
+      mk[q] = (drop && m < a.M) ? (uint32_t)a.mask[(long)m * FW + (f0 >> 4)] : 0u;
+    }
   };
-  load_w(0, bv1, bv2, bw, bias);
-  const int FW = a.FF / 16;
+  load_w(0, bv1, bv2, bw, bias, mw);
   for (int f0 = 0; f0 < a.FF; f0 += 16) {
-    const int ff = f0 + c;
+    const int buf = T::NBUF == 2 ? ((f0 >> 4) & 1) : 0;
+    float* rg = smem + 2 * T::TILE + (buf * 4 + w) * T::RG;
     float bv1n[T::KQ], bv2n[T::KQ], bwn[T::NJ][4], biasn;
-    if (f0 + 16 < a.FF) load_w(f0 + 16, bv1n, bv2n, bwn, biasn);
+    uint32_t mwn[NR];
+    if (f0 + 16 < a.FF) load_w(f0 + 16, bv1n, bv2n, bwn, biasn, mwn);
     f32x4 pre[T::NI], dact[T::NI];
     dcontract<D>(xw, bv1, pre, g, c);
     dcontract<D>(dw, bv2, dact, g, c);
@@ -269,9 +286,8 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
         const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
         const float gz = z * cdf;
         const float gg = cdf + z * (__builtin_amdgcn_exp2f(-0.72134752044448170f * z * z) * 0.39894228040143268f);
-        bool keep = true;
-        if (a.drop.thresh) keep = m < a.M && ((a.mask[(long)m * FW + (f0 >> 4)] >> c) & 1u);
-        const float sc = a.drop.thresh ? (keep ? a.drop.scale : 0.f) : 1.f;
+        const bool keep = !drop || ((mw[4 * i + rr] >> c) & 1u);
+        const float sc = drop ? (keep ? a.drop.scale : 0.f) : 1.f;
         const float fo = (m < a.M) ? gz * sc : 0.f;
         const float da = dact[i][rr] * sc * gg;
         dact[i][rr] = da;
@@ -285,26 +301,27 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
       }
     db += __shfl_xor(db, 16);
     db += __shfl_xor(db, 32);
-    // dx += dact W1 over this chunk (stage dact as [row][16])
+    // dx += dact W1 over this chunk (stage dact as [row][16] in this wave's region)
 #pragma unroll
     for (int i = 0; i < T::NI; ++i)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) st[(16 * i + 4 * g + rr) * T::SS + c] = dact[i][rr];
+      for (int rr = 0; rr < 4; ++rr) rg[(16 * i + 4 * g + rr) * T::SS + c] = dact[i][rr];
     __builtin_amdgcn_wave_barrier();
-    fcontract<D>(st, bw, dxacc, g, c);
-    // weight-grad partials of this wave -> LDS; fixed-order sum over the 4 waves -> slab
-    __syncthreads();                        // previous chunk's reduction has read `red`
+    fcontract<D>(rg, bw, dxacc, g, c);
+    __builtin_amdgcn_wave_barrier();
+    // this wave's weight-grad partial over its rows -> the same region; fixed-order 4-wave sum -> slab
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        pw[(4 * g + rr) * D + 16 * j + c] = dw1[j][rr];                 // C[ff = 4g+rr][d = 16j+c]
-        pw[16 * D + (16 * j + 4 * g + rr) * 16 + c] = dw2[j][rr];       // C[d = 16j+4g+rr][ff = c]
+        rg[(4 * g + rr) * D + 16 * j + c] = dw1[j][rr];                 // C[ff = 4g+rr][d = 16j+c]
+        rg[16 * D + (16 * j + 4 * g + rr) * 16 + c] = dw2[j][rr];       // C[d = 16j+4g+rr][ff = c]
       }
-    if (g == 0) pw[32 * D + c] = db;
+    if (g == 0) rg[32 * D + c] = db;
     __syncthreads();
+    const float* red = smem + 2 * T::TILE + buf * 4 * T::RG;
     for (int q = tid; q < T::PW; q += 256) {
-      const float sum = ((red[q] + red[T::PW + q]) + red[2 * T::PW + q]) + red[3 * T::PW + q];
+      const float sum = ((red[q] + red[T::RG + q]) + red[2 * T::RG + q]) + red[3 * T::RG + q];
       if (q < 16 * D) slab[(long)f0 * D + q] = sum;
       else if (q < 32 * D) {
         const int u = q - 16 * D;
@@ -313,6 +330,7 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
         slab[a.o_b1 + f0 + (q - 32 * D)] = sum;
       }
     }
+    if (T::NBUF == 1) __syncthreads();     // single buffer: the sum must finish before the next staging
     if (f0 + 16 < a.FF) {
 #pragma unroll
       for (int kq = 0; kq < T::KQ; ++kq) {
@@ -324,6 +342,8 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
         for (int t = 0; t < 4; ++t) bw[j][t] = bwn[j][t];
       bias = biasn;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) mw[q] = mwn[q];
     }
   }
 
