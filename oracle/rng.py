@@ -13,7 +13,7 @@ follows the reference: ``y = x * (mask / (1 - p))`` (``_dropout_impl``).
 Spec (all u32 arithmetic, wrapping):
     mix32(x)      = lowbias32 finaliser
     site_key      = mix32(lo(seed) ^ mix32(hi(seed) + site * 0x9E3779B9))
-    bits(key, i)  = mix32(mix32(i ^ key) + key)
+    bits(key, i)  = mix32(i ^ key)
     keep(i)       = (bits >> 8) >= round(p * 2^24)
 """
 from __future__ import annotations
@@ -57,7 +57,7 @@ def keep_mask(seed: int, site: int, p: float, shape) -> np.ndarray:
     n = int(np.prod(shape))
     key = np.uint32(site_key(seed, site))
     idx = np.arange(n, dtype=np.uint32)
-    b = mix32_np(mix32_np(idx ^ key) + key)
+    b = mix32_np(idx ^ key)
     return ((b >> np.uint32(8)) >= np.uint32(thresh24(p))).reshape(shape)
 
 

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--D", type=int, default=32)
     ap.add_argument("--FF", type=int, default=384)
     ap.add_argument("--H", type=int, default=8)
+    ap.add_argument("--p", type=float, default=0.1, help="dropout probability (0: no dropout)")
     args = ap.parse_args()
     torch.manual_seed(0)
     st = torch.cuda.current_stream().cuda_stream
@@ -55,7 +56,7 @@ def main():
         W2 = torch.randn(D, FF, device="cuda") / math.sqrt(FF)
         b2 = torch.randn(D, device="cuda") * 0.1
         nw = torch.ones(D, device="cuda")
-        thr = int(round(0.1 * (1 << 24)))
+        thr = int(round(args.p * (1 << 24)))
         mask = torch.zeros(_lib.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
         y, h, r = torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda")
         dh, dx = torch.randn(M, D, device="cuda"), torch.empty(M, D, device="cuda")
@@ -74,7 +75,7 @@ def main():
     if "attn" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1
-        thr = int(round(0.1 * (1 << 24)))
+        thr = int(round(args.p * (1 << 24)))
         scale = 1.0 / math.sqrt(D // H)
         amask = torch.zeros(_lib.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
         o = torch.empty(M, D, device="cuda")

@@ -28,7 +28,8 @@ constexpr int WAVE = 64;
 // ----------------------------------------------------------------------------------------------
 // dropout RNG: counter-based, identical to oracle/rng.py (lowbias32 finaliser)
 //   key  = per (step seed, site), computed on the host (tossctr/rng.py)
-//   bits = mix32(mix32(idx ^ key) + key);  keep = (bits >> 8) >= thresh24
+//   bits = mix32(idx ^ key);  keep = (bits >> 8) >= thresh24   (one lowbias32 round per element: the
+//   key is already a mixed per-(step, site) value; 2 quarter-rate integer multiplies per element)
 // ----------------------------------------------------------------------------------------------
 struct Drop {
   uint32_t key;
@@ -46,7 +47,7 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 }
 
 __device__ __forceinline__ bool drop_keep(const Drop& d, uint32_t idx) {
-  uint32_t b = mix32(mix32(idx ^ d.key) + d.key);
+  uint32_t b = mix32(idx ^ d.key);
   return (b >> 8) >= d.thresh;
 }
 
