@@ -58,6 +58,22 @@ int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* 
              float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, void* stream);
 
 
+/* Row-streaming GEMMs of the DARE encoder layer (MHA in_proj / out_proj, src/models/dare.py:53-62, and
+ * their backward) for D in {16, 32}: M rows x a few-KB weight, HBM-bound           (rowgemm.hip)
+ * C = A W^T (tb = 1, W (N, K)) or A W (tb = 0, W (K, N)); epilogue: + bias, + add, or the fused
+ * residual + RMSNorm (h = resid + (acc + bias), C = norm_w h rsqrt(mean h^2 + eps), h / r saved).
+ * Supported (K, N): (16,16) (16,48) (48,16) (32,32) (32,96) (96,32).                             */
+int ctr_rowgemm_supported(int K, int N);
+int ctr_rowgemm(int M, int K, int N, const float* A, int lda, const float* W, int tb, float* C, int ldc,
+                const float* bias, const float* add, int ld_add, const float* resid, int ld_resid,
+                const float* norm_w, float* norm_h, float* norm_r, float eps, void* stream);
+/* weight + bias grad of one nn.Linear over M rows: slab row w (of ctr_rowgemm_wgrad_rows(M)) =
+ * [dW (NO x NIN) | ... | db (NO) at o_db] partial over wave w's rows; ctr_colsum of the slab rows
+ * (fixed order) lands them in the grad arena.  (NO, NIN): (16,16) (48,16) (32,32) (96,32).        */
+int ctr_rowgemm_wgrad_rows(int M);
+int ctr_rowgemm_wgrad(const float* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN, float* slab,
+                      long ld_slab, int o_db, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Feature embeddings / context                                                    (embed.hip)
  * ------------------------------------------------------------------------------------------- */

@@ -340,3 +340,57 @@ def test_qnn_vfull_roundtrip():
     back = torch.empty_like(V)
     L.call("ctr_qnn_vfull", ptr(vf), H, R, P, ptr(back), 1, stream())
     assert torch.equal(back, V)
+
+
+@pytest.mark.parametrize("K,N", [(32, 96), (32, 32), (96, 32), (16, 48), (48, 16), (16, 16)])
+@pytest.mark.parametrize("M", [1000, 77])
+def test_rowgemm_vs_torch(K, N, M):
+    """rowgemm.hip: C = A W^T (+bias) / A W (+add) / fused residual + RMSNorm, vs torch fp64."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(K * 1000 + N + M)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    Wt = torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)      # nn.Linear layout (tb = 1)
+    Wn = torch.randn(K, N, device="cuda", generator=g) / math.sqrt(K)      # (K, N) layout (tb = 0)
+    b = torch.randn(N, device="cuda", generator=g)
+    add = torch.randn(M, N, device="cuda", generator=g)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    st = stream()
+    L.call("ctr_rowgemm", M, K, N, ptr(A), K, ptr(Wt), 1, ptr(C), N, ptr(b), None, 0, None, 0, None, None, None, 0.0, st)
+    assert rel(C.double(), A.double() @ Wt.double().t() + b.double()) < 1e-6
+    L.call("ctr_rowgemm", M, K, N, ptr(A), K, ptr(Wn), 0, ptr(C), N, None, ptr(add), N, None, 0, None, None, None, 0.0,
+           st)
+    assert rel(C.double(), A.double() @ Wn.double() + add.double()) < 1e-6
+    if K == N:      # out_proj: residual + RMSNorm epilogue
+        res = torch.randn(M, N, device="cuda", generator=g)
+        w = torch.rand(N, device="cuda", generator=g) + 0.5
+        h, r = torch.empty(M, N, device="cuda"), torch.empty(M, device="cuda")
+        L.call("ctr_rowgemm", M, K, N, ptr(A), K, ptr(Wt), 1, ptr(C), N, ptr(b), None, 0, ptr(res), N, ptr(w), ptr(h),
+               ptr(r), 1e-6, st)
+        h_ref = res.double() + (A.double() @ Wt.double().t() + b.double())
+        r_ref = torch.rsqrt(h_ref.pow(2).mean(-1) + 1e-6)
+        assert rel(h.double(), h_ref) < 1e-6 and rel(r.double(), r_ref) < 1e-6
+        assert rel(C.double(), w.double() * h_ref * r_ref[:, None]) < 1e-6
+
+
+@pytest.mark.parametrize("NO,NIN", [(96, 32), (32, 32), (48, 16), (16, 16)])
+@pytest.mark.parametrize("M", [245760, 1001, 5])
+def test_rowgemm_wgrad_vs_torch(NO, NIN, M):
+    """dW = dY^T X and db = colsum(dY) in one pass, slab rows reduced by ctr_colsum, vs torch fp64."""
+    L = _lib()
+    if M == 245760 and NO != 96:
+        pytest.skip("full size checked once")
+    g = torch.Generator(device="cuda").manual_seed(NO + NIN + M)
+    dY = torch.randn(M, NO, device="cuda", generator=g)
+    X = torch.randn(M, NIN, device="cuda", generator=g)
+    o_db = NO * NIN + 8                     # a padding gap before the bias, as in the grad arena
+    n_sl = o_db + NO
+    ld = (n_sl + 3) // 4 * 4
+    rows = L.query("ctr_rowgemm_wgrad_rows", M)
+    slab = torch.zeros(rows, ld, device="cuda")
+    L.call("ctr_rowgemm_wgrad", ptr(dY), NO, ptr(X), NIN, M, NO, NIN, ptr(slab), ld, o_db, stream())
+    out = torch.full((n_sl,), float("nan"), device="cuda")
+    ws = torch.empty(L.query("ctr_colsum_ws_size", rows, n_sl) // 4 + 1, device="cuda")
+    L.call("ctr_colsum", ptr(slab), ld, rows, n_sl, 1.0, ptr(out), ptr(ws), stream())
+    assert rel(out[:NO * NIN].double().view(NO, NIN), dY.double().t() @ X.double()) < 1e-6
+    assert rel(out[o_db:].double(), dY.double().sum(0)) < 1e-6
+    assert float(out[NO * NIN:o_db].abs().max()) == 0.0

@@ -161,12 +161,26 @@ __device__ __forceinline__ RowPtrs row_ptrs(const ctr_lazy_tab_t& tb, long row, 
   return {P + o, M + o, V + o, E ? E + o : nullptr};
 }
 
+// The history entries a workgroup's rows replay, [lo, tick], are staged in LDS once per workgroup
+// (lo = 1 + the smallest last-applied tick among its rows, at most HWIN back): the replay loop then
+// reads each tick's scalars from LDS instead of a dependent global load per tick.
+__device__ __forceinline__ int stage_hist(OptScalars* hs, int* smin, const OptScalars* __restrict__ hist, int tick) {
+  __syncthreads();                       // every row's start tick is in *smin
+  const int lo = max(max(1, *smin + 1), tick - HWIN + 1);
+  for (int k = lo + (int)threadIdx.x; k <= tick; k += 256) hs[k - lo] = hist[k];
+  __syncthreads();
+  return lo;
+}
+
 // One 8-lane group per (id, table) item.  The group leader claims the row with a CAS on last[row]
 // (s -> tick); only the winner replays, so a row read many times in a batch is caught up once.
 __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
                                                          const int32_t* __restrict__ X, long nitems, int ncols,
                                                          int per_column, float* P, float* M, float* V, float* E,
                                                          const OptScalars* __restrict__ hist, int tick) {
+  __shared__ OptScalars hs[HWIN];
+  __shared__ int smin;
+  if (threadIdx.x == 0) smin = tick;
   const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
   const int l8 = threadIdx.x & (LG - 1);
   int s = tick, win = 0, ti = 0;
@@ -192,19 +206,22 @@ __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* _
       ti = a;
       row -= (long)tabs[a].key_base;
     }
-    if (l8 == 0 && row >= 0 && row < tabs[ti].rows) {
-      int* lp = tabs[ti].last + row;
-      s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s < tick) win = atomicCAS(lp, s, tick) == s;
-    }
+  }
+  __syncthreads();                       // smin initialised
+  if (item < nitems && l8 == 0 && row >= 0 && row < tabs[ti].rows) {
+    int* lp = tabs[ti].last + row;
+    s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (s < tick) win = atomicCAS(lp, s, tick) == s;
+    if (win) atomicMin(&smin, s);
   }
   const int leader = (threadIdx.x & 63) & ~(LG - 1);
   win = __shfl(win, leader);
   s = __shfl(s, leader);
+  const int lo = stage_hist(hs, &smin, hist, tick);
   if (!win) return;
   const ctr_lazy_tab_t tb = tabs[ti];
   const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
-  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s, tick,
+  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, hs, lo}, s, tick,
                     nullptr, 0.0f);
 }
 
@@ -216,25 +233,37 @@ __global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* 
                                                           const float* __restrict__ coef_ptr, float* P, float* M,
                                                           float* V, float* E, const OptScalars* __restrict__ hist,
                                                           int tick) {
+  __shared__ OptScalars hs[HWIN];
+  __shared__ int smin;
+  if (threadIdx.x == 0) smin = tick - 1;
   const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
   const int l8 = threadIdx.x & (LG - 1);
   const long nu = min(cap, (long)*n_uniq);
-  if (item >= nu) return;
-  const uint32_t key = keys[item];
-  if (key == LAZY_INVALID) return;
-  int a = 0, b = ntabs;   // last table with key_base <= key
-  while (b - a > 1) {
-    const int mid = (a + b) >> 1;
-    if (tabs[mid].key_base <= key) a = mid; else b = mid;
+  bool live = item < nu;
+  uint32_t key = live ? keys[item] : LAZY_INVALID;
+  live = live && key != LAZY_INVALID;
+  int a = 0;
+  long row = 0;
+  int s = tick - 1;
+  if (live) {
+    int b = ntabs;   // last table with key_base <= key
+    while (b - a > 1) {
+      const int mid = (a + b) >> 1;
+      if (tabs[mid].key_base <= key) a = mid; else b = mid;
+    }
+    row = (long)(key - tabs[a].key_base);
+    live = row < tabs[a].rows;
+    if (live) s = tabs[a].last[row];
   }
+  __syncthreads();                       // smin initialised
+  if (live && l8 == 0) atomicMin(&smin, s);
+  const int lo = stage_hist(hs, &smin, hist, tick);
+  if (!live) return;
   const ctr_lazy_tab_t tb = tabs[a];
-  const long row = (long)(key - tb.key_base);
-  if (row >= tb.rows) return;
-  const int s = tb.last[row];
   const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
   const float coef = coef_ptr ? *coef_ptr : 1.0f;
-  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, nullptr, 0}, s,
-                    tick - 1, G + item * (long)g_ld, coef);
+  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, hs, lo}, s, tick - 1,
+                    G + item * (long)g_ld, coef);
   if (l8 == 0) tb.last[row] = tick;
 }
 

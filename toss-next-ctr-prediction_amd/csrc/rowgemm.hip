@@ -1,0 +1,246 @@
+// Row-streaming GEMMs of the DARE encoder layer (src/models/dare.py:53-62: MHA in_proj / out_proj and
+// their backward, D = 16 or 32): M = B*K rows (245,760 at cfg2) against a weight of a few KB.  These
+// products are HBM-bound (K, N <= 96: ~2-3 flop per byte), so the kernels are shaped for streaming,
+// not for MFMA tiles:
+//
+//   ctr_rowgemm       C[m, :] = epi(A[m, :] W^T or A[m, :] W)   (epilogues: bias, add, residual+RMSNorm)
+//     No LDS and no barrier: every wave keeps its B operand (the whole weight, K*N/64 floats per lane)
+//     in registers and walks 32-row blocks.  The A operand uses the k-order freedom of a contraction:
+//     lane group g (16 lanes) takes k in [g*K/4, (g+1)*K/4), so lane (g, c) reads row 16i + c's segment
+//     with 16-byte loads straight into MFMA operand registers; the C layout (rows 4g + r, column c)
+//     holds whole 16-column strips of a row per lane group -> the RMSNorm row sum is a 16-lane
+//     reduction.
+//   ctr_rowgemm_wgrad dW = dY^T X over all rows, plus db = colsum(dY), for one nn.Linear
+//     Each wave owns a contiguous row range; a k-step of the MFMA is 4 rows (lane group g = row), the
+//     bias grad is one more 16-column block whose B operand is the ones column.  Each wave writes its
+//     partial [dW | db] slab row laid out like the gradient arena (weight, then the bias at o_db);
+//     ctr_colsum reduces the slab rows in a fixed order -- deterministic, no atomics.
+// f32-input MFMA = an exact fmaf chain per lane: results differ from torch's sgemm only in summation
+// order.
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 rg_mfma(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+struct RowGemmArgs {
+  int M;
+  const float* A;
+  int lda;
+  const float* W;          // tb: (N, K) (nn.Linear weight: C = A W^T); else (K, N) (C = A W)
+  int tb;
+  float* C;
+  int ldc;
+  const float* bias;       // (N) or null
+  const float* add;        // C += add[m, :] (after the bias) or null
+  int ld_add;
+  const float* resid;      // fused RMSNorm: h = resid + (acc + bias), C = norm_w * h * rsqrt(mean(h^2) + eps)
+  int ld_resid;
+  const float* norm_w;
+  float* norm_h;           // (M, N) saved h, row stride ldc (nullable)
+  float* norm_r;           // (M) saved rsqrt (nullable)
+  float eps;
+};
+
+template <int K, int N>
+__global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
+  constexpr int KQ = K / 4, NJ = N / 16, NI = 2;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+  float w[NJ][KQ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int kk = 0; kk < KQ; ++kk) {
+      const int n = 16 * j + c, k = g * KQ + kk;
+      w[j][kk] = a.tb ? a.W[n * K + k] : a.W[k * N + n];
+    }
+  float bj[NJ], nw[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    bj[j] = a.bias ? a.bias[16 * j + c] : 0.f;
+    nw[j] = a.norm_w ? a.norm_w[16 * j + c] : 0.f;
+  }
+  const int nblk = (a.M + 16 * NI - 1) / (16 * NI);
+  for (int blk = wave; blk < nblk; blk += nwaves) {
+    const int r0 = blk * 16 * NI;
+    f32x4 av[NI][KQ / 4];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int row = r0 + 16 * i + c;
+#pragma unroll
+      for (int q = 0; q < KQ / 4; ++q)
+        av[i][q] = row < a.M ? *(const f32x4*)(a.A + (long)row * a.lda + g * KQ + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    f32x4 acc[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KQ; ++kk)
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = rg_mfma(av[i][kk >> 2][kk & 3], w[j][kk], acc[i][j]);
+    // epilogue: lane holds C[r0 + 16i + 4g + rr][16j + c]
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = r0 + 16 * i + 4 * g + rr;
+        const bool live = row < a.M;
+        float v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          v[j] = acc[i][j][rr] + bj[j];
+          if (a.add && live) v[j] += a.add[(long)row * a.ld_add + 16 * j + c];
+        }
+        if (a.norm_w) {
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            v[j] = (live ? a.resid[(long)row * a.ld_resid + 16 * j + c] : 0.f) + v[j];
+            ss += v[j] * v[j];
+          }
+          ss = group_sum<16>(ss);
+          const float r = 1.0f / sqrtf(ss / (float)N + a.eps);
+          if (live) {
+            if (c == 0 && a.norm_r) a.norm_r[row] = r;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              if (a.norm_h) a.norm_h[(long)row * a.ldc + 16 * j + c] = v[j];
+              a.C[(long)row * a.ldc + 16 * j + c] = nw[j] * v[j] * r;
+            }
+          }
+        } else if (live) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) a.C[(long)row * a.ldc + 16 * j + c] = v[j];
+        }
+      }
+  }
+}
+
+// dW[NO x NIN] partial of one wave over rows [m_begin, m_end): C tile (I, J) = dY[:, 16I..]^T X[:, 16J..]
+template <int NO, int NIN>
+__global__ __launch_bounds__(64) void rowgemm_wgrad_kernel(const float* __restrict__ dY, int ldy,
+                                                           const float* __restrict__ X, int ldx, int M,
+                                                           int rows_per_wave, float* __restrict__ slab,
+                                                           long ld_slab, int o_db) {
+  constexpr int IO = NO / 16, JW = NIN / 16;
+  constexpr int U = 4;                                       // k-steps (4 rows each) loaded together
+  const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+  const int m_begin = blockIdx.x * rows_per_wave, m_end = min(M, m_begin + rows_per_wave);
+  f32x4 acc[IO][JW + 1];                                     // + the ones block (bias grad)
+#pragma unroll
+  for (int i = 0; i < IO; ++i)
+#pragma unroll
+    for (int j = 0; j <= JW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float one = c == 0 ? 1.f : 0.f;
+  for (int m0 = m_begin; m0 < m_end; m0 += 4 * U) {
+    float ay[U][IO], bx[U][JW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int m = m0 + 4 * u + g;
+      const bool ok = m < m_end;
+#pragma unroll
+      for (int i = 0; i < IO; ++i) ay[u][i] = ok ? dY[(long)m * ldy + 16 * i + c] : 0.f;
+#pragma unroll
+      for (int j = 0; j < JW; ++j) bx[u][j] = ok ? X[(long)m * ldx + 16 * j + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < IO; ++i) {
+#pragma unroll
+        for (int j = 0; j < JW; ++j) acc[i][j] = rg_mfma(ay[u][i], bx[u][j], acc[i][j]);
+        acc[i][JW] = rg_mfma(ay[u][i], one, acc[i][JW]);
+      }
+  }
+  float* out = slab + (long)blockIdx.x * ld_slab;
+#pragma unroll
+  for (int i = 0; i < IO; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int o = 16 * i + 4 * g + rr;
+#pragma unroll
+      for (int j = 0; j < JW; ++j) out[(long)o * NIN + 16 * j + c] = acc[i][j][rr];
+      if (c == 0) out[o_db + o] = acc[i][JW][rr];
+    }
+}
+
+static int rowgemm_grid(int M) {
+  const int nblk = (M + 31) / 32;
+  return std::max(1, std::min((nblk + 3) / 4, 256 * 8));
+}
+
+template <int K, int N>
+static void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
+  rowgemm_kernel<K, N><<<rowgemm_grid(a.M), 256, 0, s>>>(a);
+}
+
+static bool rowgemm_shape(int K, int N) {
+  return (K == 16 && (N == 16 || N == 48)) || (K == 48 && N == 16) || (K == 32 && (N == 32 || N == 96)) ||
+         (K == 96 && N == 32);
+}
+
+static bool wgrad_shape(int NO, int NIN) {
+  return (NIN == 16 && (NO == 16 || NO == 48)) || (NIN == 32 && (NO == 32 || NO == 96));
+}
+
+// wave w of the weight-grad kernel owns rows [w*rpw, (w+1)*rpw): ~2048 waves, rpw a multiple of 16
+static void wgrad_split(int M, int* rpw, int* waves) {
+  const int target = std::max(1, std::min(2048, (M + 63) / 64));
+  *rpw = ((M + target - 1) / target + 15) / 16 * 16;
+  *waves = (M + *rpw - 1) / *rpw;
+}
+
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int ctr_rowgemm_supported(int K, int N) { return rowgemm_shape(K, N) ? 1 : 0; }
+
+extern "C" int ctr_rowgemm(int M, int K, int N, const float* A, int lda, const float* W, int tb, float* C, int ldc,
+                           const float* bias, const float* add, int ld_add, const float* resid, int ld_resid,
+                           const float* norm_w, float* norm_h, float* norm_r, float eps, void* stream) {
+  CTR_REQUIRE(rowgemm_shape(K, N), "ctr_rowgemm: unsupported (K, N)");
+  CTR_REQUIRE((lda & 3) == 0 && (((uintptr_t)A) & 15) == 0, "ctr_rowgemm: A rows must be 16-byte aligned");
+  CTR_REQUIRE(!norm_w || resid, "ctr_rowgemm: the fused RMSNorm needs the residual");
+  if (M <= 0) return 0;
+  RowGemmArgs a{M, A, lda, W, tb, C, ldc, bias, add, ld_add, resid, ld_resid, norm_w, norm_h, norm_r, eps};
+  hipStream_t s = (hipStream_t)stream;
+  if (K == 16 && N == 16) launch_rowgemm<16, 16>(a, s);
+  else if (K == 16) launch_rowgemm<16, 48>(a, s);
+  else if (K == 48) launch_rowgemm<48, 16>(a, s);
+  else if (K == 32 && N == 32) launch_rowgemm<32, 32>(a, s);
+  else if (K == 32) launch_rowgemm<32, 96>(a, s);
+  else launch_rowgemm<96, 32>(a, s);
+  return check_launch("rowgemm");
+}
+
+extern "C" int ctr_rowgemm_wgrad_rows(int M) {
+  int rpw, waves;
+  wgrad_split(std::max(M, 1), &rpw, &waves);
+  return waves;
+}
+
+extern "C" int ctr_rowgemm_wgrad(const float* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN,
+                                 float* slab, long ld_slab, int o_db, void* stream) {
+  CTR_REQUIRE(wgrad_shape(NO, NIN), "ctr_rowgemm_wgrad: unsupported (NO, NIN)");
+  CTR_REQUIRE(o_db >= NO * NIN && ld_slab >= (long)o_db + NO, "ctr_rowgemm_wgrad: slab layout");
+  if (M <= 0) return 0;
+  int rpw, grid;
+  wgrad_split(M, &rpw, &grid);
+  hipStream_t s = (hipStream_t)stream;
+  if (NIN == 16 && NO == 16) rowgemm_wgrad_kernel<16, 16><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  else if (NIN == 16) rowgemm_wgrad_kernel<48, 16><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  else if (NO == 32) rowgemm_wgrad_kernel<32, 32><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  else rowgemm_wgrad_kernel<96, 32><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  return check_launch("rowgemm_wgrad");
+}

@@ -152,6 +152,9 @@ class Engine:
         self.stream = None
         self.lazy = None     # a lazy FusedAdamW: table rows are brought current before they are read
         # fused FFN kernels (ffn.hip) when the shape allows; the GEMM path otherwise
+        # row-streaming in/out-projection kernels (rowgemm.hip) for the D they are built for
+        self.rowgemm = a.n_layers > 0 and all(bool(_lib.query("ctr_rowgemm_supported", k, n))
+                                              for k, n in ((a.D, 3 * a.D), (a.D, a.D), (3 * a.D, a.D)))
         self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden)) and \
             self._ffn_contiguous()
 
@@ -224,6 +227,24 @@ class Engine:
         each split >= 512 rows deep (tile shapes as in ctr_gemm's dispatch)."""
         return int(max(1, min(K // 512, math.ceil(512 / Engine._tiles(M, N)))))
 
+    def rowgemm_call(self, M, K, N, A, W, tb, C, bias=None, add=None, resid=None, norm_w=None, norm_h=None,
+                     norm_r=None):
+        """C (M, N) = A (M, K) W^T (tb) or A W, + bias / + add / residual + RMSNorm (rowgemm.hip)."""
+        call("ctr_rowgemm", M, K, N, A, K, W, tb, C, N, bias, add, N if add else 0, resid, N if resid else 0, norm_w,
+             norm_h, norm_r, 1e-6, self.s())
+
+    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey):
+        """dW = dY^T X and db = colsum(dY) of one nn.Linear in one pass (rowgemm.hip): per-wave partial
+        slab rows laid out like the grad arena from the weight on, reduced by one fixed-order colsum."""
+        o0 = self.arena.offsets[wkey]
+        o_db = self.arena.offsets[bkey] - o0
+        n_sl = o_db + n_out
+        ld = (n_sl + 3) // 4 * 4
+        rows = _lib.query("ctr_rowgemm_wgrad_rows", M)
+        slab = W.get_zeroed(f"wg_slab_{n_out}x{n_in}", (rows, ld))     # padding columns stay zero
+        call("ctr_rowgemm_wgrad", dY, n_out, X, n_in, M, n_out, n_in, ptr(slab), ld, o_db, self.s())
+        self.colsum(ptr(slab), ld, rows, n_sl, ptr(self.arena.grad, o0))
+
     def colsum(self, X, ld, M, N, out, div=1.0):
         w = self.splitk_ws(_lib.query("ctr_colsum_ws_size", M, N) // 4 + 1)
         call("ctr_colsum", X, ld, M, N, float(div), out, ptr(w), self.s())
@@ -288,8 +309,12 @@ class Engine:
             Ls = {}
             x = xs[-1]
             qkv = W.get(f"qkv{li}", (M, 3 * D))
-            self.gemm(M, 3 * D, D, ptr(x), D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 1, ptr(qkv), 3 * D,
-                      GemmEpi(bias=ptr(P[pre + "mha.in_proj_bias"])))
+            if self.rowgemm:
+                self.rowgemm_call(M, D, 3 * D, ptr(x), ptr(P[pre + "mha.in_proj_weight"]), 1, ptr(qkv),
+                                  bias=ptr(P[pre + "mha.in_proj_bias"]))
+            else:
+                self.gemm(M, 3 * D, D, ptr(x), D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 1, ptr(qkv), 3 * D,
+                          GemmEpi(bias=ptr(P[pre + "mha.in_proj_bias"])))
             relmean = None
             if a.add_pos:
                 relmean = W.get(f"relmean{li}", (2 * a.top_k + 1,))
@@ -305,9 +330,14 @@ class Engine:
             h1 = W.get(f"h1_{li}", (M, D))
             r1 = W.get(f"r1_{li}", (M,))
             x1 = W.get(f"x1_{li}", (M, D))
-            self.gemm(M, D, D, ptr(o), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 1, ptr(x1), D,
-                      GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), ld_resid=D,
-                              norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1), norm_eps=1e-6))
+            if self.rowgemm:
+                self.rowgemm_call(M, D, D, ptr(o), ptr(P[pre + "mha.out_proj.weight"]), 1, ptr(x1),
+                                  bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), norm_w=ptr(P[pre + "norm1.w"]),
+                                  norm_h=ptr(h1), norm_r=ptr(r1))
+            else:
+                self.gemm(M, D, D, ptr(o), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 1, ptr(x1), D,
+                          GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), ld_resid=D,
+                                  norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1), norm_eps=1e-6))
             FF = a.ffn_hidden
             dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
             h2 = W.get(f"h2_{li}", (M, D))
@@ -637,10 +667,14 @@ class Engine:
              ptr(dh1), D, None, 0, ptr(dwp), st)
         self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
         # out_proj
-        self.wgrad(ptr(dh1), D, ptr(Ls["o"]), D, M, D, D, ptr(G[pre + "mha.out_proj.weight"]),
-                   bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
         do = W.get("do", (M, D))
-        self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
+        if self.rowgemm:
+            self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight", pre + "mha.out_proj.bias")
+            self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
+        else:
+            self.wgrad(ptr(dh1), D, ptr(Ls["o"]), D, M, D, D, ptr(G[pre + "mha.out_proj.weight"]),
+                       bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
+            self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
         # attention core
         dqkv = W.get("dqkv", (M, 3 * D))
         nparts = _lib.query("ctr_attn_bwd_nparts", a.H, K, D) * B
@@ -654,10 +688,15 @@ class Engine:
             call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), st)
         # in_proj
         x_in = sv["xs"][li]
-        self.wgrad(ptr(dqkv), 3 * D, ptr(x_in), D, M, 3 * D, D, ptr(G[pre + "mha.in_proj_weight"]),
-                   bias_grad=ptr(G[pre + "mha.in_proj_bias"]))
-        self.gemm(M, D, 3 * D, ptr(dqkv), 3 * D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 0, ptr(dout_buf), D,
-                  GemmEpi(add=ptr(dh1), ld_add=D))
+        if self.rowgemm:
+            self.wgrad_rows(W, ptr(dqkv), ptr(x_in), M, 3 * D, D, pre + "mha.in_proj_weight", pre + "mha.in_proj_bias")
+            self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
+                              add=ptr(dh1))
+        else:
+            self.wgrad(ptr(dqkv), 3 * D, ptr(x_in), D, M, 3 * D, D, ptr(G[pre + "mha.in_proj_weight"]),
+                       bias_grad=ptr(G[pre + "mha.in_proj_bias"]))
+            self.gemm(M, D, 3 * D, ptr(dqkv), 3 * D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 0, ptr(dout_buf), D,
+                      GemmEpi(add=ptr(dh1), ld_add=D))
         return dout_buf
 
     def _qnn_backward(self, sv, dlogits, dxF):
