@@ -72,6 +72,35 @@ def main():
         tb = timeit(bwd, args.iters)
         print(f"ffn_fwd M={M} D={D} FF={FF}: {tf * 1e3:.1f} us  {4.0 * M * FF * D / tf / 1e9:.1f} TF/s")
         print(f"ffn_bwd M={M} D={D} FF={FF}: {tb * 1e3:.1f} us  {8.0 * M * FF * D / tb / 1e9:.1f} TF/s")
+    if "rowgemm" in which:
+        x = torch.randn(M, D, device="cuda")
+        Win, bin_ = torch.randn(3 * D, D, device="cuda"), torch.randn(3 * D, device="cuda")
+        Wout, bout = torch.randn(D, D, device="cuda"), torch.randn(D, device="cuda")
+        qkv, o, x1 = torch.empty(M, 3 * D, device="cuda"), torch.randn(M, D, device="cuda"), torch.empty(M, D, device="cuda")
+        h1, r1, nw = torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"), torch.ones(D, device="cuda")
+        dh1, do, dq, dx = (torch.randn(M, D, device="cuda"), torch.empty(M, D, device="cuda"),
+                           torch.randn(M, 3 * D, device="cuda"), torch.empty(M, D, device="cuda"))
+        cases = {
+            "qkv": lambda: call("ctr_rowgemm", M, D, 3 * D, ptr(x), D, ptr(Win), 1, ptr(qkv), 3 * D, ptr(bin_), None, 0,
+                                None, 0, None, None, None, 0.0, st),
+            "out+norm": lambda: call("ctr_rowgemm", M, D, D, ptr(o), D, ptr(Wout), 1, ptr(x1), D, ptr(bout), None, 0,
+                                     ptr(x), D, ptr(nw), ptr(h1), ptr(r1), 1e-6, st),
+            "do": lambda: call("ctr_rowgemm", M, D, D, ptr(dh1), D, ptr(Wout), 0, ptr(do), D, None, None, 0, None, 0,
+                               None, None, None, 0.0, st),
+            "dx": lambda: call("ctr_rowgemm", M, 3 * D, D, ptr(dq), 3 * D, ptr(Win), 0, ptr(dx), D, None, ptr(dh1), D,
+                               None, 0, None, None, None, 0.0, st),
+        }
+        mb = {"qkv": 4 * M * 4 * D, "out+norm": 4 * M * (5 * D + 1), "do": 8 * M * D, "dx": 4 * M * 5 * D}
+        for n, fn in cases.items():
+            t = timeit(fn, args.iters)
+            print(f"rowgemm {n} M={M} D={D}: {t * 1e3:.1f} us  {mb[n] / t / 1e6:.0f} GB/s")
+        for no, ni, dy, xx in ((3 * D, D, dq, x), (D, D, dh1, o)):
+            rows = _lib.query("ctr_rowgemm_wgrad_rows", M)
+            ld = (no * ni + 64 + no + 3) // 4 * 4
+            slab = torch.zeros(rows, ld, device="cuda")
+            fn = lambda: call("ctr_rowgemm_wgrad", ptr(dy), no, ptr(xx), ni, M, no, ni, ptr(slab), ld, no * ni + 64, st)
+            t = timeit(fn, args.iters)
+            print(f"rowgemm_wgrad {no}x{ni} M={M}: {t * 1e3:.1f} us  {4 * M * (no + ni) / t / 1e6:.0f} GB/s")
     if "attn" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1

@@ -47,36 +47,59 @@ struct RowGemmArgs {
   float eps;
 };
 
-template <int K, int N>
+template <int K, int N, bool SIDE>
 __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
   constexpr int KQ = K / 4, NJ = N / 16, NI = 2;
+  constexpr int NS = SIDE ? NJ : 1;      // per-row epilogue operand (add / residual) slots
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
   float w[NJ][KQ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j)
+  for (int j = 0; j < NJ; ++j) {
+    const int n = 16 * j + c;
+    if (a.tb) {         // W[n][g*KQ .. +KQ) is contiguous: 16-byte loads
 #pragma unroll
-    for (int kk = 0; kk < KQ; ++kk) {
-      const int n = 16 * j + c, k = g * KQ + kk;
-      w[j][kk] = a.tb ? a.W[n * K + k] : a.W[k * N + n];
+      for (int q = 0; q < KQ / 4; ++q) {
+        const f32x4 v = *(const f32x4*)(a.W + n * K + g * KQ + 4 * q);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) w[j][4 * q + t] = v[t];
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KQ; ++kk) w[j][kk] = a.W[(g * KQ + kk) * N + n];
     }
+  }
   float bj[NJ], nw[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     bj[j] = a.bias ? a.bias[16 * j + c] : 0.f;
     nw[j] = a.norm_w ? a.norm_w[16 * j + c] : 0.f;
   }
-  const int nblk = (a.M + 16 * NI - 1) / (16 * NI);
-  for (int blk = wave; blk < nblk; blk += nwaves) {
-    const int r0 = blk * 16 * NI;
-    f32x4 av[NI][KQ / 4];
+  const float* side = a.norm_w ? a.resid : a.add;     // per-row epilogue operand (nullable)
+  const int ld_side = a.norm_w ? a.ld_resid : a.ld_add;
+  // the next block's A rows and epilogue operand are loaded while this block computes and stores
+  f32x4 av[NI][KQ / 4];
+  float sv[NI][4][NS];
+  auto load_blk = [&](int blk, f32x4 (&A)[NI][KQ / 4], float (&S)[NI][4][NS]) {
+    const int b0 = blk * 16 * NI;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int row = r0 + 16 * i + c;
+      const int row = b0 + 16 * i + c;
 #pragma unroll
       for (int q = 0; q < KQ / 4; ++q)
-        av[i][q] = row < a.M ? *(const f32x4*)(a.A + (long)row * a.lda + g * KQ + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+        A[i][q] = row < a.M ? *(const f32x4*)(a.A + (long)row * a.lda + g * KQ + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int orow = b0 + 16 * i + 4 * g + rr;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) S[i][rr][j] = (SIDE && orow < a.M) ? side[(long)orow * ld_side + 16 * j + c] : 0.f;
+      }
     }
+  };
+  const int nblk = (a.M + 16 * NI - 1) / (16 * NI);
+  if (wave < nblk) load_blk(wave, av, sv);
+  for (int blk = wave; blk < nblk; blk += nwaves) {
+    const int r0 = blk * 16 * NI;
     f32x4 acc[NI][NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -88,6 +111,14 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
       for (int i = 0; i < NI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = rg_mfma(av[i][kk >> 2][kk & 3], w[j][kk], acc[i][j]);
+    float cur[NI][4][NS];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+#pragma unroll
+        for (int j = 0; j < NS; ++j) cur[i][rr][j] = sv[i][rr][j];
+    if (blk + nwaves < nblk) load_blk(blk + nwaves, av, sv);
     // epilogue: lane holds C[r0 + 16i + 4g + rr][16j + c]
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -99,13 +130,13 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           v[j] = acc[i][j][rr] + bj[j];
-          if (a.add && live) v[j] += a.add[(long)row * a.ld_add + 16 * j + c];
+          if (SIDE && a.add) v[j] += cur[i][rr][SIDE ? j : 0];
         }
         if (a.norm_w) {
           float ss = 0.f;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
-            v[j] = (live ? a.resid[(long)row * a.ld_resid + 16 * j + c] : 0.f) + v[j];
+            v[j] = (SIDE ? cur[i][rr][SIDE ? j : 0] : 0.f) + v[j];
             ss += v[j] * v[j];
           }
           ss = group_sum<16>(ss);
@@ -174,14 +205,24 @@ __global__ __launch_bounds__(64) void rowgemm_wgrad_kernel(const float* __restri
     }
 }
 
-static int rowgemm_grid(int M) {
+// persistent grid: as many workgroups as fit the chip at once (register-limited occupancy)
+template <int K, int N, bool SIDE>
+static int resident_grid(int M) {
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rowgemm_kernel<K, N, SIDE>, 256, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    per_cu = std::min(nb, 4);
+  }
   const int nblk = (M + 31) / 32;
-  return std::max(1, std::min((nblk + 3) / 4, 256 * 8));
+  return std::max(1, std::min((nblk + 3) / 4, 256 * per_cu));
 }
 
 template <int K, int N>
 static void launch_rowgemm(const RowGemmArgs& a, hipStream_t s) {
-  rowgemm_kernel<K, N><<<rowgemm_grid(a.M), 256, 0, s>>>(a);
+  if (a.add || a.norm_w) rowgemm_kernel<K, N, true><<<resident_grid<K, N, true>(a.M), 256, 0, s>>>(a);
+  else rowgemm_kernel<K, N, false><<<resident_grid<K, N, false>(a.M), 256, 0, s>>>(a);
 }
 
 static bool rowgemm_shape(int K, int N) {
