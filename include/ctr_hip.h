@@ -329,6 +329,16 @@ int ctr_shard_route(const uint32_t* uk, const uint32_t* nu, long cap, const uint
                     const long long* fwd_counts, int world, uint32_t mask, uint32_t* out_local, long long* counts,
                     void* stream);
 
+/* ---- fold-ensemble inference tail (src/infer.py:102-158)                                (infer.hip)
+ * p = clip(iso(clip(sigmoid(clip(z/T, +-50))))) with the checkpoint's calibrator (has_T: temperature,
+ * n_iso > 0: isotonic thresholds iso_x/iso_y), else clip(sigmoid(z)); clip = [1e-7, 1 - 1e-7]
+ * (src/utils/calibration.py:102-110, src/infer.py:108-122)                                        */
+int ctr_calibrate(const float* z, int n, float T, int has_T, const float* iso_x, const float* iso_y, int n_iso,
+                  float* p, void* stream);
+/* ensemble_probs (src/utils/metrics.py:48-86) over P (M models x B): method 0 mean, 1 geom_mean,
+ * 2 logit_mean, 3 median, 4 trim_mean (k cut per side), 5 weighted; w (M, nullable) normalised    */
+int ctr_ensemble(const float* P, int M, int B, int method, const float* w, int k, float* out, void* stream);
+
 /* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */
 int ctr_sigmoid(const float* x, int n, float* y, void* stream);
 int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream);

@@ -104,6 +104,8 @@ SIGS = {
     "ctr_shard_strip": (i, [p, l, u, p, p]),
     "ctr_shard_gather": (i, [p, l, i, p, i, p, p, p, i, p]),
     "ctr_shard_route": (i, [p, p, l, p, p, i, u, p, p, p]),
+    "ctr_calibrate": (i, [p, i, f, i, p, p, i, p, p]),
+    "ctr_ensemble": (i, [p, i, i, i, p, i, p, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
     "ctr_gather_rows": (i, [p, l, p, i, p, p]),

@@ -68,6 +68,16 @@ def _feature_dims(manifest_path):
             int(np.load(first["X_mask"]["path"], mmap_mode="r").shape[1]))
 
 
+def _cal_state(cal):
+    """The fitted calibrator as plain data (temperature, isotonic thresholds) for the checkpoint;
+    tossctr.infer applies it on device."""
+    out = {"method": cal.method, "temperature": cal.temperature}
+    if cal.iso is not None:
+        out["iso_x"] = [float(v) for v in cal.iso.X_thresholds_]
+        out["iso_y"] = [float(v) for v in cal.iso.y_thresholds_]
+    return out
+
+
 @torch.no_grad()
 def predict_logits(model, store, idx_np, bs):
     """Eval-mode forward over rows idx (src/train.py:211-225); returns logits (numpy).
@@ -182,7 +192,7 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
             best_score = cur
             best_state = {"model": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
                           "cfg": cfg, "best_score": best_score, "epoch": epoch,
-                          "calibrator": ({"method": cal.method, "temperature": cal.temperature} if cal else None),
+                          "calibrator": (_cal_state(cal) if cal else None),
                           "ema": (ema.state_dict() if ema is not None else None), "global_step": global_step}
             wait = 0
         else:
