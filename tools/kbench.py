@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--FF", type=int, default=384)
     ap.add_argument("--H", type=int, default=8)
     ap.add_argument("--p", type=float, default=0.1, help="dropout probability (0: no dropout)")
+    ap.add_argument("--shapes", default="", help="gemm: comma-separated indices of the shape list")
     args = ap.parse_args()
     torch.manual_seed(0)
     st = torch.cuda.current_stream().cuda_stream
@@ -101,6 +102,27 @@ def main():
             fn = lambda: call("ctr_rowgemm_wgrad", ptr(dy), no, ptr(xx), ni, M, no, ni, ptr(slab), ld, no * ni + 64, st)
             t = timeit(fn, args.iters)
             print(f"rowgemm_wgrad {no}x{ni} M={M}: {t * 1e3:.1f} us  {4 * M * (no + ni) / t / 1e6:.0f} GB/s")
+    if "gemm" in which:        # the QNN MLP's big GEMMs at each split-K factor
+        shapes = [(4096, 512, 6400, 0, 1), (512, 6400, 4096, 1, 0), (4096, 6400, 512, 0, 0),
+                  (4096, 1152, 512, 0, 0), (4096, 512, 1152, 0, 1), (512, 1152, 4096, 1, 0),
+                  (32, 96, 4096, 1, 0), (1, 256, 4096, 1, 0), (1, 32, 4096, 1, 0), (96, 1152, 4096, 1, 0),
+                  (256, 512, 4096, 1, 0), (1024, 96, 4096, 1, 0), (32, 96, 245760, 1, 0)]
+        if args.shapes:
+            shapes = [shapes[int(i)] for i in args.shapes.split(",")]
+        for (Mg, Ng, Kg, ta, tb) in shapes:
+            Ag = torch.randn((Kg, Mg) if ta else (Mg, Kg), device="cuda")
+            Bg = torch.randn((Ng, Kg) if tb else (Kg, Ng), device="cuda")
+            Cg = torch.empty(Mg, Ng, device="cuda")
+            res = []
+            for sp in (1, 2, 4, 6, 8, 16, 32, 64):
+                if sp > max(1, Kg // 64):
+                    continue
+                ws = torch.empty(sp * Mg * Ng + 16, device="cuda")
+                fn = lambda: call("ctr_gemm", Mg, Ng, Kg, ptr(Ag), Ag.shape[1], ta, ptr(Bg), Bg.shape[1], tb, ptr(Cg), Ng,
+                                  None, sp, ptr(ws), st)
+                t = timeit(fn, args.iters)
+                res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
+            print(f"gemm M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
     if "attn" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1

@@ -330,6 +330,21 @@ __global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
   }
 }
 
+// K <= 4 (e.g. the outer product of the logit grad with the last MLP weight): one thread per C element
+__global__ void gemm_smallk_kernel(GemmArgs g, int ta, int tb) {
+  const long MN = (long)g.M * g.N;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < MN; q += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(q / g.N), n = (int)(q % g.N);
+    float acc = 0.f;
+    for (int k = 0; k < g.K; ++k) {
+      const float a = ta ? g.A[(long)k * g.lda + m] : g.A[(long)m * g.lda + k];
+      const float b = tb ? g.B[(long)n * g.ldb + k] : g.B[(long)k * g.ldb + n];
+      acc = fmaf(a, b, acc);
+    }
+    g.C[(long)m * g.ldc + n] = epi_elem(g.epi, acc, m, n, g.N, g.ldc);
+  }
+}
+
 template <int BM, int BN>
 static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s) {
   dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), splits);
@@ -370,6 +385,11 @@ extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, co
   }
   g.klen = klen > 0 ? klen : 1;
   g.ws = ws;
+  if (K <= 4 && !g.epi.norm_w && splits == 1) {
+    const long MN = (long)M * N;
+    gemm_smallk_kernel<<<(int)std::min<long>((MN + 255) / 256, 8192), 256, 0, s>>>(g, ta, tb);
+    return check_launch("ctr_gemm");
+  }
   if (g.epi.norm_w) {
     if (N <= 32) launch_tile<128, 32>(g, ta, tb, 1, s);
     else launch_tile<128, 64>(g, ta, tb, 1, s);
@@ -381,6 +401,8 @@ extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, co
     launch_tile<128, 96>(g, ta, tb, splits, s);
   } else if (M <= 64) {
     launch_tile<64, 128>(g, ta, tb, splits, s);
+  } else if ((long)((M + 127) / 128) * ((N + 127) / 128) * splits < 512) {
+    launch_tile<64, 64>(g, ta, tb, splits, s);     // too few 128x128 tiles to fill the chip
   } else {
     launch_tile<128, 128>(g, ta, tb, splits, s);
   }

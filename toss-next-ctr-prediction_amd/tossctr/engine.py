@@ -205,6 +205,7 @@ class Engine:
 
     @staticmethod
     def _tiles(M, N):
+        """Workgroup tiles of ctr_gemm's dispatch before split-K (128x128 tiles)."""
         bn = 32 if N <= 32 else 64 if N <= 64 else 96 if N <= 96 else 128
         bm = 64 if (M <= 64 and bn == 128) else 128
         return math.ceil(M / bm) * math.ceil(N / bn)
@@ -212,10 +213,10 @@ class Engine:
     def gemm(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, splits=1):
         """C = op(A) op(B) (+ epilogue); A/B/C are raw pointers.  A grid too small to fill the 256 CUs
         with a deep K (e.g. the QNN MLP's first layer, 32x4 tiles over K = 6400) is split along K."""
-        if splits == 1 and K >= 1024 and not (epi is not None and epi.norm_w):
+        if splits == 1 and K >= 512 and not (epi is not None and epi.norm_w):
             tiles = self._tiles(M, N)
-            if tiles < 192:
-                splits = int(max(1, min(math.ceil(384 / tiles), K // 512)))
+            if tiles < 512:     # ~1200 workgroups (tools/kbench.py --which gemm sweeps)
+                splits = int(max(1, min(round(1200 / tiles), K // 256)))
         wsp = None
         if splits > 1:
             wsp = ptr(self.splitk_ws(splits * M * N))
@@ -223,9 +224,9 @@ class Engine:
 
     @staticmethod
     def wgrad_splits(M, N, K):
-        """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows): ~512 workgroups,
-        each split >= 512 rows deep (tile shapes as in ctr_gemm's dispatch)."""
-        return int(max(1, min(K // 512, math.ceil(512 / Engine._tiles(M, N)))))
+        """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows): ~1024 workgroups,
+        each split >= 64 rows deep (tile shapes as in ctr_gemm's dispatch)."""
+        return int(max(1, min(K // 64, math.ceil(1024 / Engine._tiles(M, N)))))
 
     def rowgemm_call(self, M, K, N, A, W, tb, C, bias=None, add=None, resid=None, norm_w=None, norm_h=None,
                      norm_r=None):
