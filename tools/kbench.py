@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--FF", type=int, default=384)
     ap.add_argument("--H", type=int, default=8)
     ap.add_argument("--p", type=float, default=0.1, help="dropout probability (0: no dropout)")
+    ap.add_argument("--nobias", action="store_true", help="attn: no positional bias")
     ap.add_argument("--shapes", default="", help="gemm: comma-separated indices of the shape list")
     args = ap.parse_args()
     torch.manual_seed(0)
@@ -135,6 +136,7 @@ def main():
         dqkv = torch.empty(M, 3 * D, device="cuda")
         nparts = _lib.query("ctr_attn_bwd_nparts", H, K, D) * B
         drp = torch.empty(nparts, 2 * K + 1, device="cuda")
+        rel = None if args.nobias else rel
         fwd = lambda: call("ctr_attn_fwd", ptr(qkv), B, K, H, D, ptr(rel), K, scale, 777, thr, 1.0 / 0.9, ptr(amask),
                            ptr(o), ptr(mrow), ptr(lrow), st)
         bwd = lambda: call("ctr_attn_bwd", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(rel), K, scale, 777, thr,

@@ -253,19 +253,32 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int c = 0; c < DH; ++c) a.dqkv[((long)b * K + i) * 3 * D + h * DH + c] = dq[c] * a.scale;
   }
-  // ---- positional-bias grad: sum of dS along diagonals j - i = o, heads of the group in order
+  // ---- positional-bias grad: sum of dS along diagonals j - i = o.  Each (diagonal, head, half of the
+  // diagonal) is one work item (2G items per diagonal spread over the block instead of one thread
+  // walking all G heads), the 2G partials are then added in a fixed order.
   if (BIAS) {
-    for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
+    __syncthreads();                               // row pass done: the tiles before dS are free
+    const int per = 2 * G;
+    const long prefix = (long)4 * G * K * DH + 3 * G * K + nrel + (long)G * K * KW;
+    float* part = prefix >= (long)nrel * per ? sq : dS + G * K * KP;   // [nrel][2G] (ctr_attn_bwd sizes LDS)
+    for (int q = threadIdx.x; q < nrel * per; q += blockDim.x) {
+      const int e = q / per, gg = (q % per) >> 1, half = q & 1;
       const int o = e - a.tk;
       float s = 0.f;
       if (o > -K && o < K) {
         const int i0 = o >= 0 ? 0 : -o, i1 = o >= 0 ? K - o : K;
-        for (int gg = 0; gg < G; ++gg) {
-          const float* Pq = dS + gg * K * KP;
+        const int im = (i0 + i1) >> 1;
+        const int lo = half ? im : i0, hi = half ? i1 : im;
+        const float* Pq = dS + gg * K * KP;
 #pragma unroll 4
-          for (int ii = i0; ii < i1; ++ii) s += Pq[ii * KP + ii + o];
-        }
+        for (int ii = lo; ii < hi; ++ii) s += Pq[ii * KP + ii + o];
       }
+      part[q] = s;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
+      float s = 0.f;
+      for (int u = 0; u < per; ++u) s += part[e * per + u];
       a.drel_part[((long)b * gridDim.y + hg) * nrel + e] = s;
     }
   }
@@ -280,7 +293,9 @@ static int pick_group(int H, int K, size_t per_head_lds, size_t lds_cap) {
 
 static size_t bwd_lds(int G, int K, int dh, int tk) {
   const int nrel = 2 * tk + 1, KW = (K + 31) / 32;
-  return ((size_t)4 * G * K * dh + 3 * G * K + nrel + (size_t)G * K * KW + (size_t)G * K * (K + 1)) * sizeof(float);
+  const size_t prefix = (size_t)4 * G * K * dh + 3 * G * K + nrel + (size_t)G * K * KW;
+  const size_t part = (size_t)2 * G * nrel;     // positional-bias partials: in the prefix when they fit
+  return (prefix + (size_t)G * K * (K + 1) + (prefix >= part ? 0 : part)) * sizeof(float);
 }
 
 static int bwd_group(int H, int K, int dh) {
