@@ -243,8 +243,8 @@ def main():
     torch.cuda.synchronize()
     opt.time_kernels(True)
     from tossctr import _lib
-    timed = ("ctr_ffn_bwd", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_touch",
-             "ctr_lazy_update", "ctr_adamw_ema")
+    timed = ("ctr_ffn_bwd", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
+             "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_update", "ctr_lazy_update_pair", "ctr_adamw_ema")
     _lib.time_calls(timed)
     t0 = time.perf_counter()
     for _ in range(args.steps):

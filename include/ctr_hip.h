@@ -302,6 +302,17 @@ int ctr_lazy_update(const ctr_lazy_tab_t* tabs, int ntabs, const uint32_t* keys,
 /* bring every row of every table up to tick; max_rows = max over tabs of rows                      */
 int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_rows, float* P, float* M, float* V, float* E,
                    const void* hist, int tick, void* stream);
+/* the DARE table pair {emb_att, emb_rep} (tabs[0], tabs[1], same rows and width): a token's two rows
+ * share their last tick, so one wave replays both (att elements in lanes [0, W), rep in [W, 2W)) --
+ * no divergence between rows, wave-uniform history loads.  touch: tokens X[0, n); update: unique
+ * keys with att grads Ga and rep grads Gb (same keys, as ctr_rowgrad2 produces); flush: all rows.   */
+int ctr_lazy_touch_pair(const ctr_lazy_tab_t* tabs, int width, const int32_t* X, long n, float* P, float* M, float* V,
+                        float* E, const void* hist, int tick, void* stream);
+int ctr_lazy_update_pair(const ctr_lazy_tab_t* tabs, int width, const uint32_t* keys, const float* Ga, const float* Gb,
+                         int g_ld, const uint32_t* n_uniq, long cap, const float* coef, float* P, float* M, float* V,
+                         float* E, const void* hist, int tick, void* stream);
+int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long rows, float* P, float* M, float* V, float* E,
+                        const void* hist, int tick, void* stream);
 
 
 /* ---- row-sharded embedding tables (BASELINE config 5): row r of a table lives on rank

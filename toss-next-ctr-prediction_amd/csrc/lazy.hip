@@ -316,6 +316,178 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// DARE table pair (emb_att, emb_rep): both are read for the same tokens and get gradients for the
+// same keys, so a token's att row and rep row always share their last-applied tick.  One WAVE per
+// token: lanes [0, W) hold the att row's elements, [W, 2W) the rep row's (2 per lane when W = 64),
+// so every lane replays the same tick range -- no divergence between row groups -- and each tick's
+// scalars are a wave-uniform (scalar) load.
+constexpr int PAIR_EPL = 2;     // elements per lane (W <= 64)
+
+struct PairRow {
+  float p[PAIR_EPL], m[PAIR_EPL], v[PAIR_EPL], e[PAIR_EPL];
+  long o[PAIR_EPL];             // arena offsets; -1 = lane slot unused
+};
+
+__device__ __forceinline__ void pair_load(PairRow& r, const ctr_lazy_tab_t& ta, const ctr_lazy_tab_t& tb, long row,
+                                          const float* P, const float* M, const float* V, const float* E) {
+  const int W = ta.width, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < PAIR_EPL; ++q) {
+    const int el = lane + 64 * q;
+    r.o[q] = el < W ? ta.p_off + row * W + el : el < 2 * W ? tb.p_off + row * W + (el - W) : -1;
+    r.p[q] = r.m[q] = r.v[q] = r.e[q] = 0.f;
+    if (r.o[q] >= 0) {
+      r.p[q] = P[r.o[q]];
+      r.m[q] = M[r.o[q]];
+      r.v[q] = V[r.o[q]];
+      if (E) r.e[q] = E[r.o[q]];
+    }
+  }
+}
+
+__device__ __forceinline__ void pair_store(const PairRow& r, float* P, float* M, float* V, float* E) {
+#pragma unroll
+  for (int q = 0; q < PAIR_EPL; ++q)
+    if (r.o[q] >= 0) {
+      P[r.o[q]] = r.p[q];
+      M[r.o[q]] = r.m[q];
+      V[r.o[q]] = r.v[q];
+      if (E) E[r.o[q]] = r.e[q];
+    }
+}
+
+// ticks (s, t_idle] with grad 0, then (g != null) tick t_idle + 1 with grad g[q] * coef; same
+// arithmetic as replay_row (adam.h), decided per wave (s and the zero test are wave-uniform)
+__device__ __forceinline__ void pair_replay(PairRow& r, bool has_e, const OptScalars* __restrict__ hist, int s,
+                                            int t_idle, const float* g, float coef) {
+  bool nz = false;
+#pragma unroll
+  for (int q = 0; q < PAIR_EPL; ++q) nz = nz || r.m[q] != 0.0f || r.v[q] != 0.0f;
+  const bool zero = __ballot(nz) == 0;      // every element of both rows never stepped with a grad
+  if (zero) {
+    bool stepped = false;
+    for (int k = s + 1; k <= t_idle; ++k) {
+      const OptScalars sc = hist[k];
+      if (sc.do_adam) {
+        stepped = true;
+#pragma unroll
+        for (int q = 0; q < PAIR_EPL; ++q) r.p[q] = r.p[q] * sc.decay_mul;
+      }
+      if (sc.do_ema) {
+#pragma unroll
+        for (int q = 0; q < PAIR_EPL; ++q) ema_elem(sc, r.p[q], r.e[q]);
+      }
+    }
+    if (stepped) {
+#pragma unroll
+      for (int q = 0; q < PAIR_EPL; ++q) r.m[q] = r.v[q] = 0.0f;
+    }
+  } else {
+    for (int k = s + 1; k <= t_idle; ++k) {
+      const OptScalars sc = hist[k];
+#pragma unroll
+      for (int q = 0; q < PAIR_EPL; ++q) {
+        if (sc.do_adam) idle_adam_elem(sc, r.p[q], r.m[q], r.v[q]);
+        if (sc.do_ema) ema_elem(sc, r.p[q], r.e[q]);
+      }
+    }
+  }
+  if (g) {
+    const OptScalars sc = hist[t_idle + 1];
+#pragma unroll
+    for (int q = 0; q < PAIR_EPL; ++q)
+      if (r.o[q] >= 0) adam_ema_elem(sc, r.p[q], r.m[q], r.v[q], r.e[q], g[q] * coef, sc.do_adam != 0);
+  }
+  (void)has_e;
+}
+
+// forward read of tokens X[0, n): a wave per token; lane 0 claims the att row's tick with a CAS (a token
+// read many times in the batch is caught up once) and the rep row's tick follows it
+__global__ __launch_bounds__(256) void lazy_touch_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
+                                                              const int32_t* __restrict__ X, long n, float* P,
+                                                              float* M, float* V, float* E,
+                                                              const OptScalars* __restrict__ hist, int tick) {
+  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
+  const long wave = (blockIdx.x * 256L + threadIdx.x) >> 6, nwaves = (long)gridDim.x * 4;
+  const int lane = threadIdx.x & 63;
+  for (long t = wave; t < n; t += nwaves) {
+    const long row = X[t];
+    if (row < 0 || row >= ta.rows) continue;
+    int s = tick, win = 0;
+    if (lane == 0) {
+      int* lp = ta.last + row;
+      s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (s < tick) win = atomicCAS(lp, s, tick) == s;
+    }
+    win = __builtin_amdgcn_readfirstlane(win);
+    if (!win) continue;
+    s = __builtin_amdgcn_readfirstlane(s);
+    PairRow r;
+    pair_load(r, ta, tb, row, P, M, V, E);
+    pair_replay(r, E != nullptr, hist, s, tick, nullptr, 0.f);
+    pair_store(r, P, M, V, E);
+    if (lane == 0) tb.last[row] = tick;
+  }
+}
+
+// one optimizer tick for the unique keys [0, *n_uniq) shared by the att grads Ga and the rep grads Gb
+__global__ __launch_bounds__(256) void lazy_update_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
+                                                               const uint32_t* __restrict__ keys,
+                                                               const float* __restrict__ Ga,
+                                                               const float* __restrict__ Gb, int g_ld,
+                                                               const uint32_t* __restrict__ n_uniq, long cap,
+                                                               const float* __restrict__ coef_ptr, float* P,
+                                                               float* M, float* V, float* E,
+                                                               const OptScalars* __restrict__ hist, int tick) {
+  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
+  const long wave = (blockIdx.x * 256L + threadIdx.x) >> 6, nwaves = (long)gridDim.x * 4;
+  const int lane = threadIdx.x & 63, W = ta.width;
+  const long nu = min(cap, (long)*n_uniq);
+  const float coef = coef_ptr ? *coef_ptr : 1.0f;
+  for (long it = wave; it < nu; it += nwaves) {
+    const uint32_t key = keys[it];
+    if (key == LAZY_INVALID || (long)(key - ta.key_base) >= ta.rows) continue;
+    const long row = (long)(key - ta.key_base);
+    const int s = __builtin_amdgcn_readfirstlane(ta.last[row]);
+    PairRow r;
+    pair_load(r, ta, tb, row, P, M, V, E);
+    float g[PAIR_EPL];
+#pragma unroll
+    for (int q = 0; q < PAIR_EPL; ++q) {
+      const int el = lane + 64 * q;
+      g[q] = el < W ? Ga[it * (long)g_ld + el] : el < 2 * W ? Gb[it * (long)g_ld + (el - W)] : 0.f;
+    }
+    pair_replay(r, E != nullptr, hist, s, tick - 1, g, coef);
+    pair_store(r, P, M, V, E);
+    if (lane == 0) {
+      ta.last[row] = tick;
+      tb.last[row] = tick;
+    }
+  }
+}
+
+// every row pair not yet at tick (flush of the DARE tables)
+__global__ __launch_bounds__(256) void lazy_flush_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs, float* P,
+                                                              float* M, float* V, float* E,
+                                                              const OptScalars* __restrict__ hist, int tick) {
+  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
+  const long wave = (blockIdx.x * 256L + threadIdx.x) >> 6, nwaves = (long)gridDim.x * 4;
+  const int lane = threadIdx.x & 63;
+  for (long row = wave; row < ta.rows; row += nwaves) {
+    const int s = __builtin_amdgcn_readfirstlane(ta.last[row]);
+    if (s >= tick) continue;
+    PairRow r;
+    pair_load(r, ta, tb, row, P, M, V, E);
+    pair_replay(r, E != nullptr, hist, s, tick, nullptr, 0.f);
+    pair_store(r, P, M, V, E);
+    if (lane == 0) {
+      ta.last[row] = tick;
+      tb.last[row] = tick;
+    }
+  }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
@@ -358,4 +530,37 @@ extern "C" int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_ro
   if (ntabs <= 0 || tick <= 0 || max_rows <= 0) return 0;
   lazy_flush_kernel<<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist, tick);
   return check_launch("lazy_flush");
+}
+
+static int pair_grid(long n) { return (int)std::max<long>(1, std::min<long>((n + 3) / 4, 256L * 16)); }
+
+static bool pair_ok(const ctr_lazy_tab_t* tabs_host_view) { return tabs_host_view != nullptr; }
+
+extern "C" int ctr_lazy_touch_pair(const ctr_lazy_tab_t* tabs, int width, const int32_t* X, long n, float* P,
+                                   float* M, float* V, float* E, const void* hist, int tick, void* stream) {
+  CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_touch_pair: two tables of width <= 64");
+  if (tick <= 0 || n <= 0) return 0;
+  lazy_touch_pair_kernel<<<pair_grid(n), 256, 0, (hipStream_t)stream>>>(tabs, X, n, P, M, V, E,
+                                                                        (const OptScalars*)hist, tick);
+  return check_launch("lazy_touch_pair");
+}
+
+extern "C" int ctr_lazy_update_pair(const ctr_lazy_tab_t* tabs, int width, const uint32_t* keys, const float* Ga,
+                                    const float* Gb, int g_ld, const uint32_t* n_uniq, long cap, const float* coef,
+                                    float* P, float* M, float* V, float* E, const void* hist, int tick, void* stream) {
+  CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64 && tick > 0, "ctr_lazy_update_pair: bad tables / tick");
+  if (cap <= 0) return 0;
+  lazy_update_pair_kernel<<<pair_grid(cap), 256, 0, (hipStream_t)stream>>>(tabs, keys, Ga, Gb, g_ld, n_uniq, cap,
+                                                                           coef, P, M, V, E,
+                                                                           (const OptScalars*)hist, tick);
+  return check_launch("lazy_update_pair");
+}
+
+extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long rows, float* P, float* M, float* V,
+                                   float* E, const void* hist, int tick, void* stream) {
+  CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_flush_pair: two tables of width <= 64");
+  if (tick <= 0 || rows <= 0) return 0;
+  lazy_flush_pair_kernel<<<pair_grid(rows), 256, 0, (hipStream_t)stream>>>(tabs, P, M, V, E,
+                                                                            (const OptScalars*)hist, tick);
+  return check_launch("lazy_flush_pair");
 }

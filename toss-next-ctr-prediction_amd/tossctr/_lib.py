@@ -99,6 +99,9 @@ SIGS = {
     "ctr_lazy_touch": (i, [p, i, p, l, i, i, p, p, p, p, p, i, p]),
     "ctr_lazy_update": (i, [p, i, p, p, i, p, l, p, p, p, p, p, p, i, p]),
     "ctr_lazy_flush": (i, [p, i, l, p, p, p, p, p, i, p]),
+    "ctr_lazy_touch_pair": (i, [p, i, p, l, p, p, p, p, p, i, p]),
+    "ctr_lazy_update_pair": (i, [p, i, p, p, p, i, p, l, p, p, p, p, p, p, i, p]),
+    "ctr_lazy_flush_pair": (i, [p, i, l, p, p, p, p, p, i, p]),
     "ctr_shard_plan_ws_size": (z, [l]),
     "ctr_shard_plan": (i, [p, l, i, i, i, p, i, i, i, p, p, p, p, p, z, p]),
     "ctr_shard_strip": (i, [p, l, u, p, p]),

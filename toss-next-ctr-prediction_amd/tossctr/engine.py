@@ -605,11 +605,11 @@ class Engine:
              rws.numel(), self.s())
         return dict(keys=uk, G=ug, n_uniq=nu, width=width, n=n)
 
-    def _rowgrad2(self, W, keys, contrib_a, contrib_b, n, width, key_bits):
-        uk = W.get("seq_uk", (n,), torch.int32)
-        ua = W.get("att_ug", (n, width))
-        ub = W.get("rep_ug", (n, width))
-        nu = W.get("seq_nu", (1,), torch.int32)
+    def _rowgrad2(self, W, keys, contrib_a, contrib_b, n, width, key_bits, name="seq"):
+        uk = W.get(f"{name}_uk", (n,), torch.int32)
+        ua = W.get(f"{name}_ug_a", (n, width))
+        ub = W.get(f"{name}_ug_b", (n, width))
+        nu = W.get(f"{name}_nu", (1,), torch.int32)
         wsz = _lib.query("ctr_rowgrad_ws_size", n)
         rws = W.get("rowgrad_ws", (max(wsz, W.t["rowgrad_ws"].numel() if "rowgrad_ws" in W.t else 0),),
                     torch.uint8)

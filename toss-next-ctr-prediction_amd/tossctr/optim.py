@@ -255,6 +255,8 @@ class FusedAdamW:
         cat = [f"cat_embs.{c}.weight" for c in a.cat_names]     # key_base ascending = X_cat column order
         self._lazy_tabs = {"att": dev_tabs(keys[:1]), "rep": dev_tabs(keys[1:2]), "seq": dev_tabs(keys[:2]),
                            "cat": dev_tabs(cat), "all": dev_tabs(keys)}
+        self._seq_width = ar.shapes[keys[0]][1]
+        self._seq_rows = ar.shapes[keys[0]][0]
         self._hist_entry = _lib.query("ctr_opt_hist_entry_bytes")
         self.hist = torch.zeros(1024 * self._hist_entry, dtype=torch.uint8, device=dev)
 
@@ -274,8 +276,13 @@ class FusedAdamW:
         row of both DARE tables."""
         if self.tick == self._flushed_tick:
             return
+        if group == "seq":      # both DARE tables of each token: one wave per token (lazy.hip, pair kernels)
+            call("ctr_lazy_touch_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, ptr(X), X.numel(),
+                 ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
+                 self.engine.s())
+            return
         tabs, n = self._lazy_tabs[group]
-        call("ctr_lazy_touch", ptr(tabs), n, ptr(X), X.shape[0], X.shape[1], 1 if group == "cat" else 0,
+        call("ctr_lazy_touch", ptr(tabs), n, ptr(X), X.shape[0], X.shape[1], 1,
              ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
              self.engine.s())
 
@@ -285,12 +292,14 @@ class FusedAdamW:
         if self.tick == self._flushed_tick:
             return
         st = self.engine.s()
-        for X, group, mode in ((loc_seq, "seq", 0), (loc_cat, "cat", 2)):
-            if X.numel() == 0:
-                continue
-            tabs, n = self._lazy_tabs[group]
-            call("ctr_lazy_touch", ptr(tabs), n, ptr(X), X.numel(), 1, mode, ptr(self.arena.buf), ptr(self.m),
-                 ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
+        if loc_seq.numel():
+            call("ctr_lazy_touch_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, ptr(loc_seq),
+                 loc_seq.numel(), ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist),
+                 self.tick, st)
+        if loc_cat.numel():
+            tabs, n = self._lazy_tabs["cat"]
+            call("ctr_lazy_touch", ptr(tabs), n, ptr(loc_cat), loc_cat.numel(), 1, 2, ptr(self.arena.buf),
+                 ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
 
     @torch.no_grad()
     def flush(self):
@@ -298,9 +307,12 @@ class FusedAdamW:
         exactly what the dense stream would (call before reading them as a whole)."""
         if not self.lazy or self.tick == self._flushed_tick:
             return
-        tabs, n = self._lazy_tabs["all"]
+        st = self.engine.s()
+        call("ctr_lazy_flush_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, self._seq_rows,
+             ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
+        tabs, n = self._lazy_tabs["cat"]
         call("ctr_lazy_flush", ptr(tabs), n, self._lazy_max_rows, ptr(self.arena.buf), ptr(self.m), ptr(self.v),
-             self._ema_ptr(), ptr(self.hist), self.tick, self.engine.s())
+             self._ema_ptr(), ptr(self.hist), self.tick, st)
         self._flushed_tick = self.tick
 
     def _segs_device(self, tg):
@@ -346,7 +358,7 @@ class FusedAdamW:
         out = {}
         st = eng.s()
         W = eng.ws(-1, -1)
-        for name in ("att", "rep", "cat"):
+        for name in ("att", "cat"):
             t = tg[name]
             n, w = t["n"], t["width"]
             keys = W.get(f"dp_{name}_keys", (self.world * n,), torch.int32)
@@ -354,8 +366,15 @@ class FusedAdamW:
             cnt = W.get(f"dp_{name}_cnt", (self.world,), torch.int32)
             D.gather_compact(t["keys"][:n], t["G"][:n], t["n_uniq"], keys, rows, cnt, self.pg)
             call("ctr_mask_tail_keys", ptr(keys), n, self.world, ptr(cnt), st)
-            bits = eng.seq_key_bits if name != "cat" else eng.cat_key_bits
-            out[name] = eng._rowgrad(W, f"dp_{name}", keys, rows, self.world * n, w, w, bits)
+            if name == "cat":
+                out[name] = eng._rowgrad(W, "dp_cat", keys, rows, self.world * n, w, w, eng.cat_key_bits)
+                continue
+            # rep grads share att's keys (ctr_rowgrad2 in the backward): gather their rows in the same
+            # slot order and merge both with one sort
+            rrows = W.get("dp_rep_rows", (self.world * n, w))
+            D.all_gather_into(rrows, tg["rep"]["G"][:n], self.pg)
+            out["att"], out["rep"] = eng._rowgrad2(W, keys, rows, rrows, self.world * n, w, eng.seq_key_bits,
+                                                   name="dp_seq")
         return out
 
     def time_kernels(self, on):
@@ -406,7 +425,16 @@ class FusedAdamW:
              ptr(self.norm_out, 1), float(g["lr"]), float(g["weight_decay"]),
              float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1, do_ema, st)
         if self.lazy:
-            for name in ("att", "rep", "cat"):
+            ta, tr, tc = tg["att"], tg["rep"], tg["cat"]
+            if ta["keys"] is tr["keys"] and ta["G"].shape[1] == tr["G"].shape[1]:
+                # att and rep grads share their keys: one wave per key updates both rows
+                call("ctr_lazy_update_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, ptr(ta["keys"]),
+                     ptr(ta["G"]), ptr(tr["G"]), ta["G"].shape[1], ptr(ta["n_uniq"]), ta["n"], ptr(self.norm_out, 1),
+                     ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
+                names = ("cat",)
+            else:
+                names = ("att", "rep", "cat")
+            for name in names:
                 t = tg[name]
                 tabs, nt = self._lazy_tabs[name]
                 call("ctr_lazy_update", ptr(tabs), nt, ptr(t["keys"]), ptr(t["G"]), t["G"].shape[1], ptr(t["n_uniq"]),

@@ -197,6 +197,18 @@ class TableShards:
              self._stream())
         return dict(keys=uk, G=ug, n_uniq=nu, width=width, n=n)
 
+    def _rowgrad2(self, name, keys, rows_a, rows_b, n, width, bits):
+        """Owner-side merge of the att and rep grads, which share their keys: one sort for both."""
+        uk = self.buf.get(f"{name}_uk", n, dtype=torch.int32)
+        ua = self.buf.get(f"{name}_ua", n, width)
+        ub = self.buf.get(f"{name}_ub", n, width)
+        nu = self.buf.get(f"{name}_nu", 1, dtype=torch.int32)
+        wsz = _lib.query("ctr_rowgrad_ws_size", n)
+        ws = self.buf.get("rowgrad_ws", wsz, dtype=torch.uint8)
+        call("ctr_rowgrad2", _ptr(keys), _ptr(rows_a), _ptr(rows_b), n, width, width, bits, _ptr(uk), _ptr(ua),
+             _ptr(ub), _ptr(nu), _ptr(ws), wsz, self._stream())
+        return (dict(keys=uk, G=ua, n_uniq=nu, width=width, n=n), dict(keys=uk, G=ub, n_uniq=nu, width=width, n=n))
+
     def route(self, tg, fx):
         """Compact grads on fetched-row ids (tg from Engine.backward) -> the owners' merged grads on
         local keys: {"att", "rep", "cat"} in the layout the optimizer consumes."""
@@ -225,9 +237,8 @@ class TableShards:
         D.all_to_all_var(rg_r, tr["G"][:ns], recv_s, send_s, self.group)
         D.all_to_all_var(rk_c, kc[:nc], recv_c, send_c, self.group)
         D.all_to_all_var(rg_c, tc["G"][:nc], recv_c, send_c, self.group)
-        return {"att": self._rowgrad("sh_att", rk_s, rg_a, rs, Dm, self.seq_lbits),
-                "rep": self._rowgrad("sh_rep", rk_s, rg_r, rs, Dm, self.seq_lbits),
-                "cat": self._rowgrad("sh_cat", rk_c, rg_c, rc, tc["width"], self.cat_lbits)}
+        att, rep = self._rowgrad2("sh_seq", rk_s, rg_a, rg_r, rs, Dm, self.seq_lbits)
+        return {"att": att, "rep": rep, "cat": self._rowgrad("sh_cat", rk_c, rg_c, rc, tc["width"], self.cat_lbits)}
 
     # ------------------------------------------------------------------ full-table views (checkpoints)
     def gather_full(self, local: torch.Tensor, rows: int) -> torch.Tensor:
