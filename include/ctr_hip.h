@@ -168,6 +168,16 @@ int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const flo
 int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
                 const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const uint32_t* mask,
                 float* dx, float* slab, long ld_slab, int o_b1, int o_w2, void* stream);
+/* The FFN backward fused with the transformer layer's two RMSNorm backwards (x1 = norm1(h1),
+ * h2 = x1 + FFN(x1), x2 = norm2(h2); src/models/dare.py TransformerEncoderLayer norm_first=False):
+ * dy = grad wrt x2 -> dh1 = grad wrt h1.  Slab rows (ld_slab floats) hold d norm1.w at o_n1, dW1 at o_w1,
+ * db1 at o_b1, dW2 at o_w2, db2 at o_b2, d norm2.w at o_n2 (the arena's parameter order, so one colsum
+ * lands all six in the grad buffer).  Replaces ctr_rmsnorm_bwd x2 + ctr_ffn_bwd + the db2 colsum.     */
+int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h2, const float* r2, const float* nw2,
+                      const float* h1, const float* r1, const float* nw1, int M, int D, int FF, const float* W1,
+                      const float* b1, const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale,
+                      const uint32_t* mask, float* dh1, float* slab, long ld_slab, int o_n1, int o_w1, int o_b1,
+                      int o_w2, int o_b2, int o_n2, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Row / column ops                                                                (rowops.hip)

@@ -297,6 +297,71 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     assert float(red[o_b1 + FF:o_w2].abs().max()) == 0.0 if o_w2 > o_b1 + FF else True
 
 
+@pytest.mark.parametrize("M,D,FF,p", [(300, 32, 384, 0.1), (1000, 16, 48, 0.1), (130, 64, 384, 0.15),
+                                      (4097, 32, 384, 0.0), (64, 32, 16, 0.5)])
+def test_ffn_bwd_norms_vs_torch(M, D, FF, p):
+    """ctr_ffn_bwd_norms: the encoder layer's norm2 backward -> FFN backward (+ residual) -> norm1
+    backward in one kernel (dare.py:53-70, norm_first=False) vs autograd through
+    h1 -> x1 = RMSNorm(h1; n1) -> h2 = x1 + FFN(x1) -> x2 = RMSNorm(h2; n2): dh1 and the six parameter
+    grads from the per-workgroup slab (arena order, padding gaps stay zero)."""
+    from oracle.rng import keep_mask
+    from tossctr.rng import drop_args
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(7 * M + D + FF)
+    h1 = torch.randn(M, D, device="cuda", generator=g) * 1.5
+    W1 = torch.randn(FF, D, device="cuda", generator=g) / math.sqrt(D)
+    b1 = torch.randn(FF, device="cuda", generator=g) * 0.1
+    W2 = torch.randn(D, FF, device="cuda", generator=g) / math.sqrt(FF)
+    b2 = torch.randn(D, device="cuda", generator=g) * 0.1
+    n1 = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    n2 = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    seed, site = (3 << 32) | 11, 6
+    key, thresh, scale = drop_args(seed, site, p, True)
+    r1 = 1.0 / torch.sqrt((h1 * h1).mean(1) + 1e-6)
+    x1 = (n1 * h1 * r1[:, None]).contiguous()
+    x2, h2, r2 = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
+    fmask = torch.zeros(L.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
+    L.call("ctr_ffn_fwd", ptr(x1), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(n2), 1e-6, key, thresh, scale,
+           ptr(fmask), ptr(x2), ptr(h2), ptr(r2), stream())
+    mask = torch.from_numpy(keep_mask(seed, site, p, (M, FF)).astype(np.float32)).cuda() if p > 0 else \
+        torch.ones(M, FF, device="cuda")
+    h1r, W1r, b1r, W2r, b2r, n1r, n2r = (t.detach().double().requires_grad_() for t in (h1, W1, b1, W2, b2, n1, n2))
+    x1r = n1r * h1r / torch.sqrt((h1r * h1r).mean(1, keepdim=True) + 1e-6)
+    fo = torch.nn.functional.gelu(x1r @ W1r.t() + b1r) * mask.double() * float(np.float32(scale if p > 0 else 1.0))
+    h2r = x1r + (fo @ W2r.t() + b2r)
+    x2r = n2r * h2r / torch.sqrt((h2r * h2r).mean(1, keepdim=True) + 1e-6)
+    dy = torch.randn(M, D, device="cuda", generator=g)
+    x2r.backward(dy.double())
+    # slab in an arena-like layout with 64-float alignment gaps
+    al = lambda v: (v + 63) // 64 * 64
+    o_n1 = 0
+    o_w1 = al(o_n1 + D)
+    o_b1 = al(o_w1 + FF * D)
+    o_w2 = al(o_b1 + FF)
+    o_b2 = al(o_w2 + D * FF)
+    o_n2 = al(o_b2 + D)
+    ld = o_n2 + D
+    nb = L.query("ctr_ffn_slab_rows", M, D)
+    slab = torch.zeros(nb, ld, device="cuda")
+    dh1 = torch.empty(M, D, device="cuda")
+    L.call("ctr_ffn_bwd_norms", ptr(x1), ptr(dy), ptr(h2), ptr(r2), ptr(n2), ptr(h1), ptr(r1), ptr(n1), M, D, FF,
+           ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask), ptr(dh1), ptr(slab), ld,
+           o_n1, o_w1, o_b1, o_w2, o_b2, o_n2, stream())
+    red = slab.double().sum(0)
+    assert rel(dh1.double(), h1r.grad) < 1e-5
+    assert rel(red[o_n1:o_n1 + D], n1r.grad) < 1e-5
+    assert rel(red[o_w1:o_w1 + FF * D].view(FF, D), W1r.grad) < 1e-5
+    assert rel(red[o_b1:o_b1 + FF], b1r.grad) < 1e-5
+    assert rel(red[o_w2:o_w2 + D * FF].view(D, FF), W2r.grad) < 1e-5
+    assert rel(red[o_b2:o_b2 + D], b2r.grad) < 1e-5
+    assert rel(red[o_n2:o_n2 + D], n2r.grad) < 1e-5
+    used = torch.zeros(ld, dtype=torch.bool)
+    for o, n in ((o_n1, D), (o_w1, FF * D), (o_b1, FF), (o_w2, D * FF), (o_b2, D), (o_n2, D)):
+        used[o:o + n] = True
+    gaps = slab[:, ~used.cuda()]
+    assert gaps.numel() == 0 or float(gaps.abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("B,F,D,QR", [(37, 23, 16, 8), (64, 200, 32, 96), (9, 27, 64, 96), (5, 3, 32, 20)])
 def test_qnn_gram_vs_torch(B, F, D, QR):
     """qnn.hip Gram form of _pair_interaction_all (src/models/qnn_alpha.py:86-97) vs the A = z @ U

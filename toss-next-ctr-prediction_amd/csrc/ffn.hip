@@ -43,9 +43,19 @@ struct FfnArgs {
   // backward
   const float* dh;     // (M, D) grad wrt the pre-norm sum (from ctr_rmsnorm_bwd)
   float* dx;           // (M, D) grad wrt x1 (ffn path + residual)
-  float* slab;         // (gridDim.x, ld_slab): [dW1 at 0 | db1 at o_b1 | dW2 at o_w2] per workgroup
+  float* slab;         // (gridDim.x, ld_slab): [dW1 at o_w1 | db1 at o_b1 | dW2 at o_w2] per workgroup
   long ld_slab;
   int o_b1, o_w2;
+  // norm-fused backward (ctr_ffn_bwd_norms): the layer's two RMSNorm backwards around the FFN
+  int o_w1, o_b2, o_n1, o_n2;   // slab offsets of dW1, db2, d norm1.w, d norm2.w
+  const float* dy;     // (M, D) grad wrt the layer output x2 = norm2(h2)
+  const float* h2;     // (M, D) pre-norm2 sum, r2 (M) its rsqrt, nw2 norm2.w
+  const float* r2;
+  const float* nw2;
+  const float* h1;     // (M, D) pre-norm1 sum (x + attn(x)), r1 (M), nw1 norm1.w
+  const float* r1;
+  const float* nw1;
+  float* dh1;          // (M, D) output: grad wrt h1
 };
 
 template <int D>
@@ -215,7 +225,59 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
 }
 
 // ---------------------------------------------------------------- backward
+// Norm-fused loader: dh2 = RMSNorm-backward(dy; h2, r2, nw2) for the tile's rows, written as the dh
+// tile (rmsnorm_bwd_small's formula: dh = w dy r - h r^3/D sum_k w_k dy_k h_k); the workgroup's
+// column sums of dh2 (ffn.3.bias grad) and of dy h2 r2 (norm2.w grad) go to the slab.  `red` holds
+// 2 * 256 * 4 floats of scratch.
 template <int D>
+__device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, float* slab) {
+  using T = FfnTile<D>;
+  constexpr int TPR = D / 4;                  // threads per row (one float4 each)
+  float cb[4] = {0.f, 0.f, 0.f, 0.f}, cn[4] = {0.f, 0.f, 0.f, 0.f};
+  const int c4 = (threadIdx.x % TPR) * 4;
+  f32x4 w2 = *(const f32x4*)(a.nw2 + c4);
+  for (int q = threadIdx.x; q < T::RT * TPR; q += 256) {
+    const int i = q / TPR, m = m0 + i;
+    f32x4 gy = {0.f, 0.f, 0.f, 0.f}, hv = {0.f, 0.f, 0.f, 0.f};
+    float rm = 0.f;
+    if (m < a.M) {
+      gy = *(const f32x4*)(a.dy + (long)m * D + c4);
+      hv = *(const f32x4*)(a.h2 + (long)m * D + c4);
+      rm = a.r2[m];
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dot = fmaf(w2[t] * gy[t], hv[t], dot);
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) dot += __shfl_xor(dot, o, 64);
+    const float coef = rm * rm * rm / (float)D * dot;
+    f32x4 g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      g[t] = w2[t] * gy[t] * rm - hv[t] * coef;
+      cb[t] += g[t];
+      cn[t] = fmaf(gy[t] * hv[t], rm, cn[t]);
+    }
+    *(f32x4*)(dst + i * T::S + c4) = g;
+  }
+  // column sums over the tile rows: threads with the same c4 hold disjoint row sets; fixed-order sum
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    red[threadIdx.x * 4 + t] = cb[t];
+    red[1024 + threadIdx.x * 4 + t] = cn[t];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * D) {
+    const int which = threadIdx.x / D, col = threadIdx.x % D;
+    const int sub = col / 4 % TPR, t = col % 4;
+    float sum = 0.f;
+    for (int u = sub; u < 256; u += TPR) sum += red[which * 1024 + u * 4 + t];
+    slab[(which ? a.o_n2 : a.o_b2) + col] = sum;
+  }
+  __syncthreads();
+}
+
+template <int D, bool NORMS>
 __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   using T = FfnTile<D>;
   // [x tile | dh tile | two buffers of 4 per-wave regions]; chunk k uses buffer k & 1 for its dact
@@ -225,12 +287,13 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * T::TILE + 4 * T::NBUF * T::RG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   const int m0 = blockIdx.x * T::RT;
+  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
   load_tile<D>(a.x, a.M, m0, smem);
-  load_tile<D>(a.dh, a.M, m0, smem + T::TILE);
+  if (NORMS) load_dh_norm2<D>(a, m0, smem + T::TILE, smem + 2 * T::TILE, slab);
+  else load_tile<D>(a.dh, a.M, m0, smem + T::TILE);
   __syncthreads();
   const float* xw = smem + w * T::RW * T::S;
   const float* dw = smem + T::TILE + w * T::RW * T::S;
-  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
 
   f32x4 dxacc[T::NI][T::NJ];
 #pragma unroll
@@ -322,7 +385,7 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
     const float* red = smem + 2 * T::TILE + buf * 4 * T::RG;
     for (int q = tid; q < T::PW; q += 256) {
       const float sum = ((red[q] + red[T::RG + q]) + red[2 * T::RG + q]) + red[3 * T::RG + q];
-      if (q < 16 * D) slab[(long)f0 * D + q] = sum;
+      if (q < 16 * D) slab[a.o_w1 + (long)f0 * D + q] = sum;
       else if (q < 32 * D) {
         const int u = q - 16 * D;
         slab[a.o_w2 + (long)(u >> 4) * a.FF + f0 + (u & 15)] = sum;
@@ -348,25 +411,74 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   }
 
   // dx = dact W1 (complete over FF in this wave) + dh (residual path)
+  if (!NORMS) {
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
+        if (m < a.M) {
+#pragma unroll
+          for (int j = 0; j < T::NJ; ++j) {
+            const int d = 16 * j + c;
+            a.dx[(long)m * D + d] = dxacc[i][j][rr] + dw[row * T::S + d];
+          }
+        }
+      }
+    return;
+  }
+  // norm-fused: dh1 = RMSNorm-backward(dx1; h1, r1, nw1) per row (a row's D values sit in the 16 lanes
+  // of one lane group, NJ per lane), and this workgroup's norm1.w grad partial sum_rows dx1 h1 r1
+  float nw[T::NJ], cn1[T::NJ];
+#pragma unroll
+  for (int j = 0; j < T::NJ; ++j) {
+    nw[j] = a.nw1[16 * j + c];
+    cn1[j] = 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < T::NI; ++i)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-      if (m < a.M) {
+      const bool live = m < a.M;
+      float dx1[T::NJ], hv[T::NJ];
+      float dot = 0.f;
+      const float rm = live ? a.r1[m] : 0.f;
 #pragma unroll
-        for (int j = 0; j < T::NJ; ++j) {
-          const int d = 16 * j + c;
-          a.dx[(long)m * D + d] = dxacc[i][j][rr] + dw[row * T::S + d];
-        }
+      for (int j = 0; j < T::NJ; ++j) {
+        const int d = 16 * j + c;
+        dx1[j] = dxacc[i][j][rr] + dw[row * T::S + d];
+        hv[j] = live ? a.h1[(long)m * D + d] : 0.f;
+        dot = fmaf(nw[j] * dx1[j], hv[j], dot);
+      }
+      dot = group_sum<16>(dot);
+      const float coef = rm * rm * rm / (float)D * dot;
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) {
+        if (live) a.dh1[(long)m * D + 16 * j + c] = nw[j] * dx1[j] * rm - hv[j] * coef;
+        cn1[j] = fmaf(dx1[j] * hv[j], rm, cn1[j]);
       }
     }
+  // sum the norm1.w partials over the lane groups, then over the waves (fixed order)
+#pragma unroll
+  for (int j = 0; j < T::NJ; ++j) {
+    cn1[j] += __shfl_xor(cn1[j], 16, 64);
+    cn1[j] += __shfl_xor(cn1[j], 32, 64);
+  }
+  __syncthreads();                         // the last chunk's sum has read the regions
+  float* red = smem + 2 * T::TILE;
+  if (g == 0)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) red[w * D + 16 * j + c] = cn1[j];
+  __syncthreads();
+  if (tid < D) slab[a.o_n1 + tid] = ((red[tid] + red[D + tid]) + red[2 * D + tid]) + red[3 * D + tid];
 }
 
 template <int D>
 static void launch_ffn(const FfnArgs& a, bool bwd, hipStream_t s) {
   const int blocks = cdiv(a.M, FfnTile<D>::RT);
-  if (bwd) ffn_bwd_kernel<D><<<blocks, 256, 0, s>>>(a);
+  if (bwd && a.dy) ffn_bwd_kernel<D, true><<<blocks, 256, 0, s>>>(a);
+  else if (bwd) ffn_bwd_kernel<D, false><<<blocks, 256, 0, s>>>(a);
   else ffn_fwd_kernel<D><<<blocks, 256, 0, s>>>(a);
 }
 
@@ -417,5 +529,28 @@ extern "C" int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF
   a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = (uint16_t*)const_cast<uint32_t*>(mask);
   a.dh = dh; a.dx = dx; a.slab = slab; a.ld_slab = ld_slab; a.o_b1 = o_b1; a.o_w2 = o_w2;
+  return ffn_dispatch(a, D, true, (hipStream_t)stream);
+}
+
+extern "C" int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h2, const float* r2, const float* nw2,
+                                 const float* h1, const float* r1, const float* nw1, int M, int D, int FF,
+                                 const float* W1, const float* b1, const float* W2, uint32_t drop_key,
+                                 uint32_t drop_thresh, float drop_scale, const uint32_t* mask, float* dh1,
+                                 float* slab, long ld_slab, int o_n1, int o_w1, int o_b1, int o_w2, int o_b2, int o_n2,
+                                 void* stream) {
+  CTR_REQUIRE(!drop_thresh || mask, "ctr_ffn_bwd_norms with dropout needs the forward's keep bits");
+  CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd_norms: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(dy && h2 && r2 && nw2 && h1 && r1 && nw1 && dh1, "ctr_ffn_bwd_norms: missing norm operands");
+  CTR_REQUIRE(o_n1 + D <= o_w1 && o_w1 + FF * D <= o_b1 && o_b1 + FF <= o_w2 && o_w2 + D * FF <= o_b2 &&
+                  o_b2 + D <= o_n2 && ld_slab >= (long)o_n2 + D,
+              "ctr_ffn_bwd_norms: slab layout");
+  if (M <= 0) return 0;
+  FfnArgs a = {};
+  a.M = M; a.FF = FF; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2;
+  a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = (uint16_t*)const_cast<uint32_t*>(mask);
+  a.slab = slab; a.ld_slab = ld_slab; a.o_b1 = o_b1; a.o_w2 = o_w2;
+  a.o_w1 = o_w1; a.o_b2 = o_b2; a.o_n1 = o_n1; a.o_n2 = o_n2;
+  a.dy = dy; a.h2 = h2; a.r2 = r2; a.nw2 = nw2; a.h1 = h1; a.r1 = r1; a.nw1 = nw1; a.dh1 = dh1;
   return ffn_dispatch(a, D, true, (hipStream_t)stream);
 }

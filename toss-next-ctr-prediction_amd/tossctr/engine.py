@@ -169,13 +169,14 @@ class Engine:
         return torch.from_numpy(raw).to(self.device), len(keys)
 
     def _ffn_contiguous(self):
-        """The fused FFN backward colsums its [dW1 | db1 | dW2] slab straight into the grad arena."""
+        """The fused FFN backward colsums its [d norm1.w | dW1 | db1 | dW2 | db2 | d norm2.w] slab straight
+        into the grad arena: the six must be dense and in that order."""
         off = self.arena.offsets
+        keys = ("norm1.w", "ffn.0.weight", "ffn.0.bias", "ffn.3.weight", "ffn.3.bias", "norm2.w")
         for li in range(self.a.n_layers):
             p = f"dare.layers.{li}."
-            if not (off[p + "ffn.0.weight"] < off[p + "ffn.0.bias"] < off[p + "ffn.3.weight"]):
-                return False
-            if self.arena.kind[p + "ffn.0.weight"] != "dense" or self.arena.kind[p + "ffn.3.weight"] != "dense":
+            o = [off[p + k] for k in keys]
+            if o != sorted(o) or any(self.arena.kind[p + k] != "dense" for k in keys):
                 return False
         return True
 
@@ -626,31 +627,34 @@ class Engine:
         Ls = sv["layers"][li]
         pre = f"dare.layers.{li}."
         seed, training = sv["seed"], sv["training"]
-        # x2 = norm2(x1 + ffn(x1))
-        dh2 = W.get("dh2", (M, D))
-        npart = _lib.query("ctr_rmsnorm_bwd_nparts", M, D)
-        dwp = W.get("dw_part", (npart, D))
-        call("ctr_rmsnorm_bwd", ptr(dx2), D, ptr(Ls["h2"]), D, ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]), M, D,
-             ptr(dh2), D, None, 0, ptr(dwp), st)
-        self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm2.w"]))
         dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
-        dx1 = W.get("dx1", (M, D))
         if self.ffn_fused:
-            # one kernel: recompute pre/GELU/dropout from x1, dx1 = dh2 + dact W1, per-workgroup slabs
-            # [dW1 | db1 | dW2] laid out like the grad arena from ffn.0.weight on -> one colsum lands them
-            o0 = self.arena.offsets[pre + "ffn.0.weight"]
-            o_b1 = self.arena.offsets[pre + "ffn.0.bias"] - o0
-            o_w2 = self.arena.offsets[pre + "ffn.3.weight"] - o0
-            n_sl = o_w2 + D * FF
+            # one kernel for norm2 backward -> FFN backward (+ residual) -> norm1 backward: recompute
+            # pre/GELU/dropout from x1, per-workgroup slabs [d norm1.w | dW1 | db1 | dW2 | db2 | d norm2.w]
+            # laid out like the grad arena from norm1.w on -> one colsum lands all six
+            off = self.arena.offsets
+            o0 = off[pre + "norm1.w"]
+            o = [off[pre + k] - o0 for k in ("norm1.w", "ffn.0.weight", "ffn.0.bias", "ffn.3.weight", "ffn.3.bias",
+                                             "norm2.w")]
+            n_sl = o[5] + D
             ld_sl = (n_sl + 3) // 4 * 4
             nb = _lib.query("ctr_ffn_slab_rows", M, D)
             slab = W.get_zeroed("ffn_slab", (nb, ld_sl))
-            call("ctr_ffn_bwd", ptr(Ls["x1"]), ptr(dh2), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
-                 ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dx1),
-                 ptr(slab), ld_sl, o_b1, o_w2, st)
+            dh1 = W.get("dh1", (M, D))
+            call("ctr_ffn_bwd_norms", ptr(Ls["x1"]), ptr(dx2), ptr(Ls["h2"]), ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]),
+                 ptr(Ls["h1"]), ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
+                 ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dh1),
+                 ptr(slab), ld_sl, *o, st)
             self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
-            self.colsum(ptr(dh2), D, M, D, ptr(G[pre + "ffn.3.bias"]))
         else:
+            # x2 = norm2(x1 + ffn(x1))
+            dh2 = W.get("dh2", (M, D))
+            npart = _lib.query("ctr_rmsnorm_bwd_nparts", M, D)
+            dwp = W.get("dw_part", (npart, D))
+            call("ctr_rmsnorm_bwd", ptr(dx2), D, ptr(Ls["h2"]), D, ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]), M, D,
+                 ptr(dh2), D, None, 0, ptr(dwp), st)
+            self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm2.w"]))
+            dx1 = W.get("dx1", (M, D))
             # ffn.3: f @ W2^T + b2
             self.wgrad(ptr(dh2), D, ptr(Ls["fo"]), FF, M, D, FF, ptr(G[pre + "ffn.3.weight"]),
                        bias_grad=ptr(G[pre + "ffn.3.bias"]))
@@ -662,11 +666,11 @@ class Engine:
                        bias_grad=ptr(G[pre + "ffn.0.bias"]))
             self.gemm(M, D, FF, ptr(dact), FF, 0, ptr(P[pre + "ffn.0.weight"]), D, 0, ptr(dx1), D,
                       GemmEpi(add=ptr(dh2), ld_add=D))
-        # x1 = norm1(x + attn(x))
-        dh1 = W.get("dh1", (M, D))
-        call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,
-             ptr(dh1), D, None, 0, ptr(dwp), st)
-        self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
+            # x1 = norm1(x + attn(x))
+            dh1 = W.get("dh1", (M, D))
+            call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,
+                 ptr(dh1), D, None, 0, ptr(dwp), st)
+            self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
         # out_proj
         do = W.get("do", (M, D))
         if self.rowgemm:
