@@ -71,7 +71,7 @@ def kernel_work(name, a, B, ffn_M):
     """(bound, algorithmic units per launch, unit) of the timed entry points -- SURVEY §8(d) per-unit
     figures x the units one launch processes ("Roofline accounting")."""
     D, FF = a.D, a.ffn_hidden
-    if name == "ctr_ffn_bwd":     # dfo = dh W2, dW2 = dh^T fo, dW1 = dact^T x, dx = dact W1 (pre recompute excluded)
+    if name in ("ctr_ffn_bwd", "ctr_ffn_bwd_norms"):     # dfo = dh W2, dW2 = dh^T fo, dW1 = dact^T x, dx = dact W1 (pre recompute excluded)
         return "mfma", 8.0 * ffn_M * FF * D, "flop"
     if name == "ctr_ffn_fwd":     # pre = x W1^T, y = fo W2^T
         return "mfma", 4.0 * ffn_M * FF * D, "flop"
@@ -115,7 +115,8 @@ def pmc_traffic(name):
     corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE counts half of wide streaming reads:
     x2).  None when the summaries are absent."""
     import csv
-    kern = {"ctr_ffn_bwd": "ffn_bwd_kernel", "ctr_ffn_fwd": "ffn_fwd_kernel"}.get(name)
+    kern = {"ctr_ffn_bwd": "ffn_bwd_kernel", "ctr_ffn_bwd_norms": "ffn_bwd_kernel",
+            "ctr_ffn_fwd": "ffn_fwd_kernel"}.get(name)
     base = os.path.join(REPO, "profiles", "r01")
     if kern is None:
         return None
@@ -243,7 +244,7 @@ def main():
     torch.cuda.synchronize()
     opt.time_kernels(True)
     from tossctr import _lib
-    timed = ("ctr_ffn_bwd", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
+    timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
              "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_update", "ctr_lazy_update_pair", "ctr_adamw_ema")
     _lib.time_calls(timed)
     t0 = time.perf_counter()

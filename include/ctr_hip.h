@@ -158,7 +158,7 @@ int ctr_ffn_supported(int D, int FF);          /* D in {16, 32, 64}, FF % 16 == 
 int ctr_ffn_slab_rows(int M, int D);           /* workgroups of ctr_ffn_bwd = rows of its grad slab */
 int ctr_ffn_mask_words(int M, int FF);         /* uint32 words of the dropout keep-bit mask (16 bits per 16 cols) */
 /* y = norm_w * h * r, h = x + (gelu(x W1^T + b1) [dropout] W2^T + b2), r = 1/rms(h).  mask (nullable
- * without dropout) receives the keep bits, row-major (M, FF/16) uint16.                            */
+ * without dropout) receives the keep bits, chunk-major (FF/16, M) uint16.                           */
 int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
                 const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
                 float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* stream);

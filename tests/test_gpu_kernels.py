@@ -275,7 +275,7 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     assert rel(r.double(), rr) < 1e-5
     assert rel(y.double(), nw.double() * hr * rr[:, None]) < 1e-5
     if p > 0:   # stored keep bits == the oracle mask
-        words = fmask.cpu().numpy().view(np.uint16)[:M * (FF // 16)].reshape(M, FF // 16)
+        words = fmask.cpu().numpy().view(np.uint16)[:M * (FF // 16)].reshape(FF // 16, M).T   # chunk-major
         bits = (words[:, np.arange(FF) // 16] >> (np.arange(FF) % 16).astype(np.uint16)) & 1
         assert np.array_equal(bits.astype(bool), mask.cpu().numpy().astype(bool))
     # backward from a random grad wrt h

@@ -47,7 +47,7 @@ def test_kfold_loop_end_to_end(tmp_path, variant):
     assert list(res) == [0] and np.isfinite(res[0])
     ckpt = os.path.join(cfg["logging"]["log_dir"], "tiny", "ckpt_folds_0.pt")
     assert os.path.exists(ckpt)
-    st = torch.load(ckpt, weights_only=False)
+    st = torch.load(ckpt, weights_only=True)
     assert set(st) == {"state", "score"} and set(st["state"]) >= {"model", "cfg", "best_score", "epoch", "ema"}
     cards = {c: 203 for c in ["c0", "c1", "c2", "c3"]}
     m = CTRModel(cfg, 3000, 6, 6, cards, ["c0", "c1", "c2", "c3"], device="cuda:0")
@@ -86,7 +86,7 @@ def test_kfold_loop_world2_sharded_tables(tmp_path):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     with open(out) as f:
         score = json.load(f)["0"]
-    st = torch.load(os.path.join(cfg["logging"]["log_dir"], "tiny", "ckpt_folds_0.pt"), weights_only=False)
+    st = torch.load(os.path.join(cfg["logging"]["log_dir"], "tiny", "ckpt_folds_0.pt"), weights_only=True)
     assert st["state"]["model"]["dare.emb_att.weight"].shape == (3000, 16)
     m = CTRModel(cfg, 3000, 6, 6, {c: 203 for c in cols}, cols, device="cuda:0")
     m.load_state_dict(st["state"]["model"], strict=True)

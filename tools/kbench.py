@@ -123,6 +123,10 @@ def main():
                                   None, sp, ptr(ws), st)
                 t = timeit(fn, args.iters)
                 res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
+            torch.backends.cuda.matmul.allow_tf32 = False      # the library's fp32 path, for reference
+            a_op, b_op = (Ag.t() if ta else Ag), (Bg.t() if tb else Bg)
+            t = timeit(lambda: torch.matmul(a_op, b_op, out=Cg), args.iters)
+            res.append(f"torch:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
             print(f"gemm M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
     if "attn" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")

@@ -24,6 +24,11 @@
 namespace ctr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
 
 struct FfnArgs {
   int M, FF;
@@ -35,7 +40,7 @@ struct FfnArgs {
   const float* nw;     // (D) norm2 weight
   float eps;
   Drop drop;
-  uint16_t* mask;      // (M, FF/16) dropout keep bits: written by the forward, read by the backward
+  uint16_t* mask;      // (FF/16, M) dropout keep bits, chunk-major: written by the forward, read by the backward
   // forward outputs
   float* y;            // (M, D) = norm2(x + ffn(x))
   float* h;            // (M, D) pre-norm sum (saved for the norm backward)
@@ -145,56 +150,68 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // W slices of chunk f0 are prefetched one chunk ahead (global latency overlaps the chunk's MFMAs)
-  float bv[T::KQ], bw[T::NJ][4], bias;
-  auto load_w = [&](int f0, float (&v1)[T::KQ], float (&v2)[T::NJ][4], float& b) {
-    const int ff = f0 + c;
+  // W slices of chunk f0 are prefetched one chunk ahead into the other of two register sets (the chunk
+  // loop is unrolled by two, so no copies and no wait on the prefetch until its chunk); buffer loads keep
+  // the per-lane offsets fixed and move the chunk offset to an SGPR
+  const auto rW1 = buf_rsrc(a.W1, (uint32_t)a.FF * D * 4);
+  const auto rW2 = buf_rsrc(a.W2, (uint32_t)a.FF * D * 4);
+  const auto rb1 = buf_rsrc(a.b1, (uint32_t)a.FF * 4);
+  const auto rmask = buf_rsrc(a.mask, a.mask ? (uint32_t)(a.FF / 16) * a.M * 2 : 0u);
+  struct Wc {
+    float v1[T::KQ], v2[T::NJ][4], b;
+  };
+  auto load_w = [&](int f0, Wc& W) {
+    // the chunk offsets are wave-uniform: readfirstlane puts them in SGPRs (a VGPR soffset would make
+    // the compiler emit a waterfall loop per load)
+    const uint32_t s1 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * D * 4);
+    const uint32_t s2 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * 4);
 #pragma unroll
-    for (int kq = 0; kq < T::KQ; kq += 4) *(f32x4*)&v1[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
+    for (int kq = 0; kq < T::KQ; kq += 4)
+      *(f32x4*)&W.v1[kq] = buf_ld4(rW1, (uint32_t)(c * D + g * T::KQ + kq) * 4, s1);
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) {
-      const f32x4 v = *(const f32x4*)(a.W2 + (long)(16 * j + c) * a.FF + f0 + 4 * g);
+      const f32x4 v = buf_ld4(rW2, ((uint32_t)(16 * j + c) * a.FF + 4 * g) * 4, s2);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) v2[j][t] = v[t];
+      for (int t = 0; t < 4; ++t) W.v2[j][t] = v[t];
     }
-    b = a.b1[ff];
+    W.b = buf_ld(rb1, (uint32_t)c * 4, s2);
   };
-  load_w(0, bv, bw, bias);
-  const int FW = a.FF / 16;
-  for (int f0 = 0; f0 < a.FF; f0 += 16) {
+  auto chunk = [&](int f0, const Wc& W) {
     const int ff = f0 + c;
-    float bvn[T::KQ], bwn[T::NJ][4], biasn;
-    if (f0 + 16 < a.FF) load_w(f0 + 16, bvn, bwn, biasn);
     f32x4 pre[T::NI];
-    dcontract<D>(xw, bv, pre, g, c);
-    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]; keep bits -> mask (16 per row and chunk)
+    dcontract<D>(xw, W.v1, pre, g, c);
+    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]; keep bits -> mask, chunk-major (FF/16, M)
 #pragma unroll
     for (int i = 0; i < T::NI; ++i)
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-        float v = gelu_f(pre[i][rr] + bias);
+        float v = gelu_f(pre[i][rr] + W.b);
         if (a.drop.thresh) {
           const bool keep = drop_keep(a.drop, (uint32_t)((long)m * a.FF + ff));
           v = keep ? v * a.drop.scale : 0.f;
           const unsigned long long bal = __ballot(keep);
-          if (c == 0 && a.mask && m < a.M) a.mask[(long)m * FW + (f0 >> 4)] = (uint16_t)(bal >> (16 * g));
+          buf_st_u16((uint32_t)(bal >> (16 * g)), rmask,
+                     (c == 0 && m < a.M) ? ((uint32_t)(f0 >> 4) * a.M + m) * 2 : BUF_OOB);
         }
         st[row * T::SS + c] = v;
       }
     __builtin_amdgcn_wave_barrier();
-    fcontract<D>(st, bw, yacc, g, c);
+    fcontract<D>(st, W.v2, yacc, g, c);
     __builtin_amdgcn_wave_barrier();
-    if (f0 + 16 < a.FF) {
-#pragma unroll
-      for (int kq = 0; kq < T::KQ; ++kq) bv[kq] = bvn[kq];
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bw[j][t] = bwn[j][t];
-      bias = biasn;
-    }
+  };
+  Wc wa, wb;
+  load_w(0, wa);
+  int f0 = 0;
+  for (; f0 + 32 <= a.FF; f0 += 32) {      // sched_barrier: see the backward
+    load_w(f0 + 16, wb);
+    chunk(f0, wa);
+    __builtin_amdgcn_sched_barrier(0);
+    load_w(min(f0 + 32, a.FF - 16), wa);     // past the end: a harmless reload of the last chunk
+    chunk(f0 + 16, wb);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  if (f0 < a.FF) chunk(f0, wa);               // odd chunk count: wa holds chunk FF-16
 
   // h = x + (y + b2); RMSNorm over the row (the row's D values sit in the 16 lanes of one lane group)
 #pragma unroll
@@ -301,40 +318,46 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // W slices and dropout keep words of chunk f0 are prefetched one chunk ahead
+  // W slices and dropout keep words of chunk f0 are prefetched one chunk ahead into the other of two
+  // register sets (chunk loop unrolled by two: no copies, no early wait); buffer loads, the chunk offset
+  // in an SGPR, the keep words' row bound checked by the buffer (no branches)
   constexpr int NR = 4 * T::NI;         // rows of this lane: 16 i + 4 g + rr
-  const int FW = a.FF / 16;
   const bool drop = a.drop.thresh != 0;
-  float bv1[T::KQ], bv2[T::KQ], bw[T::NJ][4], bias;
-  uint32_t mw[NR];
-  auto load_w = [&](int f0, float (&v1)[T::KQ], float (&v2)[T::KQ], float (&v3)[T::NJ][4], float& b,
-                    uint32_t (&mk)[NR]) {
-    const int ff = f0 + c;
+  const auto rW1 = buf_rsrc(a.W1, (uint32_t)a.FF * D * 4);
+  const auto rW2 = buf_rsrc(a.W2, (uint32_t)a.FF * D * 4);
+  const auto rb1 = buf_rsrc(a.b1, (uint32_t)a.FF * 4);
+  const auto rmask = buf_rsrc(a.mask, drop ? (uint32_t)(a.FF / 16) * a.M * 2 : 0u);
+  const uint32_t mrow = (uint32_t)(m0 + w * T::RW + 4 * g);
+  struct Wc {
+    float v1[T::KQ], v2[T::KQ], v3[T::NJ][4], b;
+    uint32_t mk[NR];
+  };
+  auto load_w = [&](int f0, Wc& W) {
+    // the chunk offsets are wave-uniform: readfirstlane puts them in SGPRs (a VGPR soffset would make
+    // the compiler emit a waterfall loop per load)
+    const uint32_t s1 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * D * 4);
+    const uint32_t s2 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * 4);
 #pragma unroll
-    for (int kq = 0; kq < T::KQ; kq += 4) *(f32x4*)&v1[kq] = *(const f32x4*)(a.W1 + (long)ff * D + g * T::KQ + kq);
+    for (int kq = 0; kq < T::KQ; kq += 4)
+      *(f32x4*)&W.v1[kq] = buf_ld4(rW1, (uint32_t)(c * D + g * T::KQ + kq) * 4, s1);
 #pragma unroll
-    for (int kk = 0; kk < T::KQ; ++kk) v2[kk] = a.W2[(long)(g * T::KQ + kk) * a.FF + ff];
+    for (int kk = 0; kk < T::KQ; ++kk) W.v2[kk] = buf_ld(rW2, ((uint32_t)(g * T::KQ + kk) * a.FF + c) * 4, s2);
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < T::NJ; ++j) v3[j][t] = a.W1[(long)(f0 + 4 * g + t) * D + 16 * j + c];
-    b = a.b1[ff];
+      for (int j = 0; j < T::NJ; ++j) W.v3[j][t] = buf_ld(rW1, (uint32_t)((4 * g + t) * D + 16 * j + c) * 4, s1);
+    W.b = buf_ld(rb1, (uint32_t)c * 4, s2);
+    // rows past M read the next chunk's words (their dact and fo are 0 anyway) or, in the last chunk,
+    // fall off the buffer (0)
+    const uint32_t mb = ((uint32_t)(f0 >> 4) * a.M + mrow) * 2;
 #pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const int m = m0 + w * T::RW + 16 * (q >> 2) + 4 * g + (q & 3);
-      mk[q] = (drop && m < a.M) ? (uint32_t)a.mask[(long)m * FW + (f0 >> 4)] : 0u;
-    }
+    for (int q = 0; q < NR; ++q) W.mk[q] = buf_ld_u16(rmask, mb + (16 * (q >> 2) + (q & 3)) * 2);
   };
-  load_w(0, bv1, bv2, bw, bias, mw);
-  for (int f0 = 0; f0 < a.FF; f0 += 16) {
-    const int buf = T::NBUF == 2 ? ((f0 >> 4) & 1) : 0;
+  auto chunk = [&](int f0, int buf, const Wc& W) {
     float* rg = smem + 2 * T::TILE + (buf * 4 + w) * T::RG;
-    float bv1n[T::KQ], bv2n[T::KQ], bwn[T::NJ][4], biasn;
-    uint32_t mwn[NR];
-    if (f0 + 16 < a.FF) load_w(f0 + 16, bv1n, bv2n, bwn, biasn, mwn);
     f32x4 pre[T::NI], dact[T::NI];
-    dcontract<D>(xw, bv1, pre, g, c);
-    dcontract<D>(dw, bv2, dact, g, c);
+    dcontract<D>(xw, W.v1, pre, g, c);
+    dcontract<D>(dw, W.v2, dact, g, c);
     f32x4 dw2[T::NJ], dw1[T::NJ];
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) dw2[j] = dw1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -344,12 +367,12 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-        const float z = pre[i][rr] + bias;
-        // gelu and gelu' share erf; exp on the hardware exp2 (a few ulp on gelu' only)
-        const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+        const float z = pre[i][rr] + W.b;
+        // gelu and gelu' share Phi (branch-free norm_cdf); exp on the hardware exp2
+        const float cdf = norm_cdf(z);
         const float gz = z * cdf;
         const float gg = cdf + z * (__builtin_amdgcn_exp2f(-0.72134752044448170f * z * z) * 0.39894228040143268f);
-        const bool keep = !drop || ((mw[4 * i + rr] >> c) & 1u);
+        const bool keep = !drop || ((W.mk[4 * i + rr] >> c) & 1u);
         const float sc = drop ? (keep ? a.drop.scale : 0.f) : 1.f;
         const float fo = (m < a.M) ? gz * sc : 0.f;
         const float da = dact[i][rr] * sc * gg;
@@ -370,7 +393,7 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) rg[(16 * i + 4 * g + rr) * T::SS + c] = dact[i][rr];
     __builtin_amdgcn_wave_barrier();
-    fcontract<D>(rg, bw, dxacc, g, c);
+    fcontract<D>(rg, W.v3, dxacc, g, c);
     __builtin_amdgcn_wave_barrier();
     // this wave's weight-grad partial over its rows -> the same region; fixed-order 4-wave sum -> slab
 #pragma unroll
@@ -383,32 +406,35 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
     if (g == 0) rg[32 * D + c] = db;
     __syncthreads();
     const float* red = smem + 2 * T::TILE + buf * 4 * T::RG;
-    for (int q = tid; q < T::PW; q += 256) {
-      const float sum = ((red[q] + red[T::RG + q]) + red[2 * T::RG + q]) + red[3 * T::RG + q];
-      if (q < 16 * D) slab[a.o_w1 + (long)f0 * D + q] = sum;
-      else if (q < 32 * D) {
-        const int u = q - 16 * D;
-        slab[a.o_w2 + (long)(u >> 4) * a.FF + f0 + (u & 15)] = sum;
-      } else {
-        slab[a.o_b1 + f0 + (q - 32 * D)] = sum;
-      }
+    auto sum4 = [&](int q) { return ((red[q] + red[T::RG + q]) + red[2 * T::RG + q]) + red[3 * T::RG + q]; };
+    static_assert((16 * D) % 256 == 0, "dW1 / dW2 partial rows split evenly over the workgroup");
+#pragma unroll
+    for (int it = 0; it < 16 * D / 256; ++it) {
+      const int q = it * 256 + tid;
+      slab[a.o_w1 + (long)f0 * D + q] = sum4(q);
     }
+#pragma unroll
+    for (int it = 0; it < 16 * D / 256; ++it) {
+      const int u = it * 256 + tid;
+      slab[a.o_w2 + (long)(u >> 4) * a.FF + f0 + (u & 15)] = sum4(16 * D + u);
+    }
+    if (tid < 16) slab[a.o_b1 + f0 + tid] = sum4(32 * D + tid);
     if (T::NBUF == 1) __syncthreads();     // single buffer: the sum must finish before the next staging
-    if (f0 + 16 < a.FF) {
-#pragma unroll
-      for (int kq = 0; kq < T::KQ; ++kq) {
-        bv1[kq] = bv1n[kq];
-        bv2[kq] = bv2n[kq];
-      }
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) bw[j][t] = bwn[j][t];
-      bias = biasn;
-#pragma unroll
-      for (int q = 0; q < NR; ++q) mw[q] = mwn[q];
-    }
+  };
+  Wc wa, wb;
+  load_w(0, wa);
+  int f0 = 0;
+  // sched_barrier: a set's reload stays after its chunk's last use, so the two sets keep their registers
+  // across the back edge (no copies, which would wait for the in-flight prefetch)
+  for (; f0 + 32 <= a.FF; f0 += 32) {
+    load_w(f0 + 16, wb);
+    chunk(f0, 0, wa);
+    __builtin_amdgcn_sched_barrier(0);
+    load_w(min(f0 + 32, a.FF - 16), wa);     // past the end: a harmless reload of the last chunk
+    chunk(f0 + 16, T::NBUF == 2 ? 1 : 0, wb);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  if (f0 < a.FF) chunk(f0, 0, wa);            // odd chunk count: wa holds chunk FF-16
 
   // dx = dact W1 (complete over FF in this wave) + dh (residual path)
   if (!NORMS) {
@@ -417,46 +443,57 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-        if (m < a.M) {
+        const auto rdx = buf_rsrc(a.dx, (uint32_t)a.M * D * 4);     // rows past M: dropped
 #pragma unroll
-          for (int j = 0; j < T::NJ; ++j) {
-            const int d = 16 * j + c;
-            a.dx[(long)m * D + d] = dxacc[i][j][rr] + dw[row * T::S + d];
-          }
+        for (int j = 0; j < T::NJ; ++j) {
+          const int d = 16 * j + c;
+          buf_st(dxacc[i][j][rr] + dw[row * T::S + d], rdx, (uint32_t)(m * D + d) * 4);
         }
       }
     return;
   }
   // norm-fused: dh1 = RMSNorm-backward(dx1; h1, r1, nw1) per row (a row's D values sit in the 16 lanes
   // of one lane group, NJ per lane), and this workgroup's norm1.w grad partial sum_rows dx1 h1 r1
+  // h1 / r1 rows past M read 0 and their dh1 stores are dropped (buffer bounds): no branches, so all
+  // the row loads are in flight together
+  const auto rh1 = buf_rsrc(a.h1, (uint32_t)a.M * D * 4), rr1 = buf_rsrc(a.r1, (uint32_t)a.M * 4);
+  const auto rdh1 = buf_rsrc(a.dh1, (uint32_t)a.M * D * 4);
   float nw[T::NJ], cn1[T::NJ];
 #pragma unroll
   for (int j = 0; j < T::NJ; ++j) {
     nw[j] = a.nw1[16 * j + c];
     cn1[j] = 0.f;
   }
+  float hv[T::NI][4][T::NJ], rmv[T::NI][4];
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = m0 + w * T::RW + 16 * i + 4 * g + rr;
+      rmv[i][rr] = buf_ld(rr1, (uint32_t)m * 4);
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) hv[i][rr][j] = buf_ld(rh1, (uint32_t)(m * D + 16 * j + c) * 4);
+    }
 #pragma unroll
   for (int i = 0; i < T::NI; ++i)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-      const bool live = m < a.M;
-      float dx1[T::NJ], hv[T::NJ];
+      float dx1[T::NJ];
       float dot = 0.f;
-      const float rm = live ? a.r1[m] : 0.f;
+      const float rm = rmv[i][rr];
 #pragma unroll
       for (int j = 0; j < T::NJ; ++j) {
         const int d = 16 * j + c;
         dx1[j] = dxacc[i][j][rr] + dw[row * T::S + d];
-        hv[j] = live ? a.h1[(long)m * D + d] : 0.f;
-        dot = fmaf(nw[j] * dx1[j], hv[j], dot);
+        dot = fmaf(nw[j] * dx1[j], hv[i][rr][j], dot);
       }
       dot = group_sum<16>(dot);
       const float coef = rm * rm * rm / (float)D * dot;
 #pragma unroll
       for (int j = 0; j < T::NJ; ++j) {
-        if (live) a.dh1[(long)m * D + 16 * j + c] = nw[j] * dx1[j] * rm - hv[j] * coef;
-        cn1[j] = fmaf(dx1[j] * hv[j], rm, cn1[j]);
+        buf_st(nw[j] * dx1[j] * rm - hv[i][rr][j] * coef, rdh1, (uint32_t)(m * D + 16 * j + c) * 4);
+        cn1[j] = fmaf(dx1[j] * hv[i][rr][j], rm, cn1[j]);
       }
     }
   // sum the norm1.w partials over the lane groups, then over the waves (fixed order)
@@ -484,6 +521,12 @@ static void launch_ffn(const FfnArgs& a, bool bwd, hipStream_t s) {
 
 static bool ffn_shape_ok(int D, int FF) { return (D == 16 || D == 32 || D == 64) && FF > 0 && FF % 16 == 0; }
 
+// buffer resources carry 32-bit byte extents: (M, D) activations, (FF, D) weights, the keep-bit words
+static bool ffn_extent_ok(long M, int D, int FF) {
+  const long lim = 1L << 31;
+  return M * D * 4 < lim && (long)FF * D * 4 < lim && M * (FF / 16) * 2 < lim;
+}
+
 static int ffn_dispatch(const FfnArgs& a, int D, bool bwd, hipStream_t s) {
   switch (D) {
     case 16: launch_ffn<16>(a, bwd, s); break;
@@ -507,6 +550,7 @@ extern "C" int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1
                            const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
                            float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* stream) {
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_fwd: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(ffn_extent_ok(M, D, FF), "ctr_ffn_fwd: M x D too large for 32-bit buffer offsets");
   if (M <= 0) return 0;
   FfnArgs a = {};
   a.M = M; a.FF = FF; a.x = x; a.W1 = W1; a.b1 = b1; a.W2 = W2; a.b2 = b2; a.nw = norm_w; a.eps = eps;
@@ -522,6 +566,7 @@ extern "C" int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF
                            void* stream) {
   CTR_REQUIRE(!drop_thresh || mask, "ctr_ffn_bwd with dropout needs the forward's keep bits");
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(ffn_extent_ok(M, D, FF), "ctr_ffn_bwd: M x D too large for 32-bit buffer offsets");
   CTR_REQUIRE(o_b1 >= FF * D && o_w2 >= o_b1 + FF && ld_slab >= (long)o_w2 + (long)D * FF, "ctr_ffn_bwd: slab layout");
   if (M <= 0) return 0;
   FfnArgs a = {};
@@ -540,6 +585,7 @@ extern "C" int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h
                                  void* stream) {
   CTR_REQUIRE(!drop_thresh || mask, "ctr_ffn_bwd_norms with dropout needs the forward's keep bits");
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd_norms: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(ffn_extent_ok(M, D, FF), "ctr_ffn_bwd_norms: M x D too large for 32-bit buffer offsets");
   CTR_REQUIRE(dy && h2 && r2 && nw2 && h1 && r1 && nw1 && dh1, "ctr_ffn_bwd_norms: missing norm operands");
   CTR_REQUIRE(o_n1 + D <= o_w1 && o_w1 + FF * D <= o_b1 && o_b1 + FF <= o_w2 && o_w2 + D * FF <= o_b2 &&
                   o_b2 + D <= o_n2 && ld_slab >= (long)o_n2 + D,

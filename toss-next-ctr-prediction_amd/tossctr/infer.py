@@ -29,12 +29,26 @@ from .engine import ptr
 ENSEMBLE_METHODS = {"mean": 0, "geom_mean": 1, "logit_mean": 2, "median": 3, "trim_mean": 4, "weighted": 5}
 
 
+def _load(path):
+    """torch.load with the safe (weights-only) unpickler: this package's checkpoints hold tensors, dicts,
+    lists and floats only.  A checkpoint written by the reference's own trainer pickles its sklearn
+    calibrator object, which only the full unpickler reads -- that executes code from the file, so it is
+    opt-in (CTR_TRUST_CHECKPOINTS=1) for files the user produced themselves."""
+    try:
+        return torch.load(path, map_location="cpu", weights_only=True)
+    except Exception as e:
+        if os.environ.get("CTR_TRUST_CHECKPOINTS") != "1":
+            raise RuntimeError(f"{path}: not loadable with weights_only=True ({e}); set CTR_TRUST_CHECKPOINTS=1 "
+                               "to unpickle a checkpoint you wrote yourself") from e
+        return torch.load(path, map_location="cpu", weights_only=False)
+
+
 def load_checkpoints(paths):
     """[(state, score)] from checkpoint files in the reference's three formats (src/infer.py:31-67):
     a (state, score) tuple, a dict ({"state", "score"} or the state itself), or {"folds": [...]}."""
     entries = []
     for path in paths:
-        obj = torch.load(path, map_location="cpu", weights_only=False)
+        obj = _load(path)
         if isinstance(obj, tuple) and len(obj) == 2:
             state, score = obj
             entries.append((state, float(score) if score is not None else -1.0))

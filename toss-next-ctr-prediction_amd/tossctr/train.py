@@ -71,7 +71,7 @@ def _feature_dims(manifest_path):
 def _cal_state(cal):
     """The fitted calibrator as plain data (temperature, isotonic thresholds) for the checkpoint;
     tossctr.infer applies it on device."""
-    out = {"method": cal.method, "temperature": cal.temperature}
+    out = {"method": cal.method, "temperature": None if cal.temperature is None else float(cal.temperature)}
     if cal.iso is not None:
         out["iso_x"] = [float(v) for v in cal.iso.X_thresholds_]
         out["iso_y"] = [float(v) for v in cal.iso.y_thresholds_]
@@ -191,7 +191,7 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
         if cur > best_score:
             best_score = cur
             best_state = {"model": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()},
-                          "cfg": cfg, "best_score": best_score, "epoch": epoch,
+                          "cfg": cfg, "best_score": float(best_score), "epoch": int(epoch),
                           "calibrator": (_cal_state(cal) if cal else None),
                           "ema": (ema.state_dict() if ema is not None else None), "global_step": global_step}
             wait = 0
@@ -238,7 +238,7 @@ def main(cfg_path_or_dict):
         state, score = train_one_fold(cfg, fold, tr, va, manifest_path, logger, store=store, device=device)
         if rank == 0:
             os.makedirs(out_dir, exist_ok=True)
-            torch.save({"state": state, "score": score}, ckpt)
+            torch.save({"state": state, "score": float(score)}, ckpt)
         results[fold] = score
     return results
 
