@@ -243,8 +243,22 @@ def test_fused_adamw_matches_torch():
     assert torch.allclose(E.cpu(), shadow_ref, rtol=1e-6, atol=1e-6)
 
 
+def ffn_keep_bits(fmask, M, FF, D):
+    """(M, FF) keep bits from ctr_ffn_fwd's mask buffer (ffn.hip FfnTile::LW): D <= 32 lane words
+    ((chunk, 128-row tile, g, c) dwords, bit 4i + rr of row 128t + 16i + 4g + rr), else chunk-major
+    (FF/16, M) uint16 row words."""
+    rows, cols = np.arange(M), np.arange(FF)
+    if D <= 32:
+        T = (M + 127) // 128
+        words = fmask.cpu().numpy().view(np.uint32)[:FF // 16 * T * 64].reshape(FF // 16, T, 4, 16)
+        w = words[(cols // 16)[None, :], (rows // 128)[:, None], ((rows % 16) // 4)[:, None], (cols % 16)[None, :]]
+        return ((w >> (4 * ((rows % 128) // 16) + rows % 4).astype(np.uint32)[:, None]) & 1).astype(bool)
+    words = fmask.cpu().numpy().view(np.uint16)[:M * (FF // 16)].reshape(FF // 16, M).T
+    return ((words[:, cols // 16] >> (cols % 16).astype(np.uint16)) & 1).astype(bool)
+
+
 @pytest.mark.parametrize("M,D,FF,p", [(300, 32, 384, 0.1), (1000, 16, 48, 0.1), (130, 64, 384, 0.15),
-                                      (4097, 32, 384, 0.0), (64, 32, 16, 0.5)])
+                                      (4097, 32, 384, 0.0), (64, 32, 16, 0.5), (517, 32, 64, 0.2)])
 def test_fused_ffn_vs_torch(M, D, FF, p):
     """ffn.hip: Linear -> GELU -> Dropout -> Linear -> +x -> RMSNorm forward, and its backward
     (dx incl. the residual, per-workgroup [dW1 | db1 | dW2] slabs reduced by ctr_colsum) vs autograd."""
@@ -275,9 +289,7 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     assert rel(r.double(), rr) < 1e-5
     assert rel(y.double(), nw.double() * hr * rr[:, None]) < 1e-5
     if p > 0:   # stored keep bits == the oracle mask
-        words = fmask.cpu().numpy().view(np.uint16)[:M * (FF // 16)].reshape(FF // 16, M).T   # chunk-major
-        bits = (words[:, np.arange(FF) // 16] >> (np.arange(FF) % 16).astype(np.uint16)) & 1
-        assert np.array_equal(bits.astype(bool), mask.cpu().numpy().astype(bool))
+        assert np.array_equal(ffn_keep_bits(fmask, M, FF, D), mask.cpu().numpy().astype(bool))
     # backward from a random grad wrt h
     dh = torch.randn(M, D, device="cuda", generator=g)
     hr.backward(dh.double())

@@ -92,6 +92,9 @@ __device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, uint32
 __device__ __forceinline__ void buf_st_u16(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
   __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, r, voff, 0, 0);
 }
+__device__ __forceinline__ void buf_st_u8(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  __builtin_amdgcn_raw_buffer_store_b8((unsigned char)v, r, voff, 0, 0);
+}
 constexpr uint32_t BUF_OOB = 0x80000000u;   // a VGPR offset past any resource: load 0 / drop the store
 
 // sum over groups of G consecutive lanes (G power of two <= 64)

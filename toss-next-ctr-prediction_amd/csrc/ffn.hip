@@ -40,7 +40,7 @@ struct FfnArgs {
   const float* nw;     // (D) norm2 weight
   float eps;
   Drop drop;
-  uint16_t* mask;      // (FF/16, M) dropout keep bits, chunk-major: written by the forward, read by the backward
+  uint16_t* mask;      // dropout keep bits (layout: FfnTile::LW), written by the forward, read by the backward
   // forward outputs
   float* y;            // (M, D) = norm2(x + ffn(x))
   float* h;            // (M, D) pre-norm sum (saved for the norm backward)
@@ -78,21 +78,49 @@ struct FfnTile {
   static constexpr int RG = PW > STG ? PW : STG;  // backward: per-wave region (staging, then partial)
   // backward: double-buffered regions (one barrier per chunk) when two workgroups still fit a CU
   static constexpr int NBUF = (2 * TILE + 8 * RG) * 4 <= 80 * 1024 ? 2 : 1;
+  // keep-bit layout.  LW ("lane words", D <= 32, RT = 128): for 16-column chunk ci and 128-row tile t,
+  // dword ((ci * T128 + t) * 4 + g) * 16 + c holds the bits of column 16 ci + c for the rows
+  // 128 t + 16 i + 4 g + rr at bit 4 i + rr -- exactly what lane (g, c) of a kernel whose 16-row blocks
+  // start on a tile boundary needs (one dword per chunk).  Otherwise (D = 64): chunk-major (FF/16, M)
+  // uint16 row words.
+  static constexpr bool LW = D <= 32;
 };
+
+// dword index of lane (g, c)'s keep bits for chunk ci, 128-row tile t (LW layout)
+__device__ __forceinline__ uint32_t lw_word(int ci, int t, int T128, int g, int c) {
+  return ((uint32_t)(ci * T128 + t) * 4 + g) * 16 + c;
+}
+__host__ __device__ __forceinline__ long lw_words(long M, int FF) { return (long)(FF / 16) * ((M + 127) / 128) * 64; }
 
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// rows [m0, m0+RT) of a (M, D) matrix -> LDS tile with stride S (zero rows past M)
+// Column position of d in a PERM tile (column-owner backward): the NJ values 16j + c of lane column c
+// sit next to each other, so a lane reads them with one ds_read_b64 at a per-row immediate offset.
 template <int D>
+__device__ __forceinline__ constexpr int pcol(int d) { return (d % 16) * (D / 16) + d / 16; }
+
+// store a row segment (columns c4..c4+3) into an LDS tile row, permuted (pcol) or not
+template <int D, bool PERM>
+__device__ __forceinline__ void put4(float* row, int c4, f32x4 v) {
+  if (PERM) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) row[pcol<D>(c4 + t)] = v[t];
+  } else {
+    *(f32x4*)(row + c4) = v;
+  }
+}
+
+// rows [m0, m0+RT) of a (M, D) matrix -> LDS tile with stride S (zero rows past M)
+template <int D, bool PERM = false>
 __device__ __forceinline__ void load_tile(const float* __restrict__ src, int M, int m0, float* dst) {
   using T = FfnTile<D>;
   for (int q = threadIdx.x; q < T::RT * D / 4; q += 256) {
     const int i = q / (D / 4), c4 = (q % (D / 4)) * 4;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (m0 + i < M) v = *(const f32x4*)(src + (long)(m0 + i) * D + c4);
-    *(f32x4*)(dst + i * T::S + c4) = v;
+    put4<D, PERM>(dst + i * T::S, c4, v);
   }
 }
 
@@ -156,7 +184,9 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
   const auto rW1 = buf_rsrc(a.W1, (uint32_t)a.FF * D * 4);
   const auto rW2 = buf_rsrc(a.W2, (uint32_t)a.FF * D * 4);
   const auto rb1 = buf_rsrc(a.b1, (uint32_t)a.FF * 4);
-  const auto rmask = buf_rsrc(a.mask, a.mask ? (uint32_t)(a.FF / 16) * a.M * 2 : 0u);
+  const uint32_t mask_bytes = !a.mask ? 0u : T::LW ? (uint32_t)lw_words(a.M, a.FF) * 4 : (uint32_t)(a.FF / 16) * a.M * 2;
+  const auto rmask = buf_rsrc(a.mask, mask_bytes);
+  const int T128 = (a.M + 127) / 128;
   struct Wc {
     float v1[T::KQ], v2[T::NJ][4], b;
   };
@@ -180,7 +210,8 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
     const int ff = f0 + c;
     f32x4 pre[T::NI];
     dcontract<D>(xw, W.v1, pre, g, c);
-    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]; keep bits -> mask, chunk-major (FF/16, M)
+    // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]; keep bits -> mask (layout FfnTile::LW)
+    uint32_t kbyte = 0;
 #pragma unroll
     for (int i = 0; i < T::NI; ++i)
 #pragma unroll
@@ -190,12 +221,18 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
         if (a.drop.thresh) {
           const bool keep = drop_keep(a.drop, (uint32_t)((long)m * a.FF + ff));
           v = keep ? v * a.drop.scale : 0.f;
-          const unsigned long long bal = __ballot(keep);
-          buf_st_u16((uint32_t)(bal >> (16 * g)), rmask,
-                     (c == 0 && m < a.M) ? ((uint32_t)(f0 >> 4) * a.M + m) * 2 : BUF_OOB);
+          if (T::LW) {
+            kbyte |= (keep ? 1u : 0u) << (4 * i + rr);
+          } else {
+            const unsigned long long bal = __ballot(keep);
+            buf_st_u16((uint32_t)(bal >> (16 * g)), rmask,
+                       (c == 0 && m < a.M) ? ((uint32_t)(f0 >> 4) * a.M + m) * 2 : BUF_OOB);
+          }
         }
         st[row * T::SS + c] = v;
       }
+    // this wave's rows are bits 8w .. 8w+7 of the lane word: one byte store
+    if (T::LW && a.drop.thresh) buf_st_u8(kbyte, rmask, lw_word(f0 >> 4, blockIdx.x, T128, g, c) * 4 + w);
     __builtin_amdgcn_wave_barrier();
     fcontract<D>(st, W.v2, yacc, g, c);
     __builtin_amdgcn_wave_barrier();
@@ -246,7 +283,7 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
 // tile (rmsnorm_bwd_small's formula: dh = w dy r - h r^3/D sum_k w_k dy_k h_k); the workgroup's
 // column sums of dh2 (ffn.3.bias grad) and of dy h2 r2 (norm2.w grad) go to the slab.  `red` holds
 // 2 * 256 * 4 floats of scratch.
-template <int D>
+template <int D, bool PERM = false>
 __device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, float* slab) {
   using T = FfnTile<D>;
   constexpr int TPR = D / 4;                  // threads per row (one float4 each)
@@ -275,7 +312,7 @@ __device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, 
       cb[t] += g[t];
       cn[t] = fmaf(gy[t] * hv[t], rm, cn[t]);
     }
-    *(f32x4*)(dst + i * T::S + c4) = g;
+    put4<D, PERM>(dst + i * T::S, c4, g);
   }
   // column sums over the tile rows: threads with the same c4 hold disjoint row sets; fixed-order sum
 #pragma unroll
@@ -292,6 +329,88 @@ __device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, 
     slab[(which ? a.o_n2 : a.o_b2) + col] = sum;
   }
   __syncthreads();
+}
+
+// dx = dact W1 (complete over FF) + dh (residual path) for this wave's RW rows (dx[i][j][rr]: row
+// 16i+4g+rr, col 16j+c; dw = the wave's rows of the dh tile); NORMS: the norm1 backward.  `scratch`:
+// 4*D floats of LDS no wave still reads.
+template <int D, bool NORMS, bool PERM = false>
+__device__ __forceinline__ void ffn_bwd_epilogue(const FfnArgs& a, const f32x4 (&dxacc)[FfnTile<D>::NI][FfnTile<D>::NJ],
+                                                 const float* dw, int m0, float* slab, float* scratch) {
+  using T = FfnTile<D>;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  if (!NORMS) {
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
+        const auto rdx = buf_rsrc(a.dx, (uint32_t)a.M * D * 4);     // rows past M: dropped
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) {
+          const int d = 16 * j + c;
+          buf_st(dxacc[i][j][rr] + dw[row * T::S + (PERM ? pcol<D>(d) : d)], rdx, (uint32_t)(m * D + d) * 4);
+        }
+      }
+    return;
+  }
+  // norm-fused: dh1 = RMSNorm-backward(dx1; h1, r1, nw1) per row (a row's D values sit in the 16 lanes
+  // of one lane group, NJ per lane), and this workgroup's norm1.w grad partial sum_rows dx1 h1 r1
+  // h1 / r1 rows past M read 0 and their dh1 stores are dropped (buffer bounds): no branches, so all
+  // the row loads are in flight together
+  const auto rh1 = buf_rsrc(a.h1, (uint32_t)a.M * D * 4), rr1 = buf_rsrc(a.r1, (uint32_t)a.M * 4);
+  const auto rdh1 = buf_rsrc(a.dh1, (uint32_t)a.M * D * 4);
+  float nw[T::NJ], cn1[T::NJ];
+#pragma unroll
+  for (int j = 0; j < T::NJ; ++j) {
+    nw[j] = a.nw1[16 * j + c];
+    cn1[j] = 0.f;
+  }
+  float hv[T::NI][4][T::NJ], rmv[T::NI][4];
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = m0 + w * T::RW + 16 * i + 4 * g + rr;
+      rmv[i][rr] = buf_ld(rr1, (uint32_t)m * 4);
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) hv[i][rr][j] = buf_ld(rh1, (uint32_t)(m * D + 16 * j + c) * 4);
+    }
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
+      float dx1[T::NJ];
+      float dot = 0.f;
+      const float rm = rmv[i][rr];
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) {
+        const int d = 16 * j + c;
+        dx1[j] = dxacc[i][j][rr] + dw[row * T::S + (PERM ? pcol<D>(d) : d)];
+        dot = fmaf(nw[j] * dx1[j], hv[i][rr][j], dot);
+      }
+      dot = group_sum<16>(dot);
+      const float coef = rm * rm * rm / (float)D * dot;
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) {
+        buf_st(nw[j] * dx1[j] * rm - hv[i][rr][j] * coef, rdh1, (uint32_t)(m * D + 16 * j + c) * 4);
+        cn1[j] = fmaf(dx1[j] * hv[i][rr][j], rm, cn1[j]);
+      }
+    }
+  // sum the norm1.w partials over the lane groups, then over the waves (fixed order)
+#pragma unroll
+  for (int j = 0; j < T::NJ; ++j) {
+    cn1[j] += __shfl_xor(cn1[j], 16, 64);
+    cn1[j] += __shfl_xor(cn1[j], 32, 64);
+  }
+  __syncthreads();                         // the last chunk's sum has read the regions
+  float* red = scratch;
+  if (g == 0)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) red[w * D + 16 * j + c] = cn1[j];
+  __syncthreads();
+  if (tid < D) slab[a.o_n1 + tid] = ((red[tid] + red[D + tid]) + red[2 * D + tid]) + red[3 * D + tid];
 }
 
 template <int D, bool NORMS>
@@ -326,11 +445,13 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   const auto rW1 = buf_rsrc(a.W1, (uint32_t)a.FF * D * 4);
   const auto rW2 = buf_rsrc(a.W2, (uint32_t)a.FF * D * 4);
   const auto rb1 = buf_rsrc(a.b1, (uint32_t)a.FF * 4);
-  const auto rmask = buf_rsrc(a.mask, drop ? (uint32_t)(a.FF / 16) * a.M * 2 : 0u);
+  const uint32_t mask_bytes = !drop ? 0u : T::LW ? (uint32_t)lw_words(a.M, a.FF) * 4 : (uint32_t)(a.FF / 16) * a.M * 2;
+  const auto rmask = buf_rsrc(a.mask, mask_bytes);
   const uint32_t mrow = (uint32_t)(m0 + w * T::RW + 4 * g);
+  const int T128 = (a.M + 127) / 128;
   struct Wc {
     float v1[T::KQ], v2[T::KQ], v3[T::NJ][4], b;
-    uint32_t mk[NR];
+    uint32_t mk[T::LW ? 1 : NR];
   };
   auto load_w = [&](int f0, Wc& W) {
     // the chunk offsets are wave-uniform: readfirstlane puts them in SGPRs (a VGPR soffset would make
@@ -349,9 +470,14 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
     W.b = buf_ld(rb1, (uint32_t)c * 4, s2);
     // rows past M read the next chunk's words (their dact and fo are 0 anyway) or, in the last chunk,
     // fall off the buffer (0)
-    const uint32_t mb = ((uint32_t)(f0 >> 4) * a.M + mrow) * 2;
+    if (T::LW) {             // one lane word: this wave's rows at bits 8w + 4i + rr
+      const uint32_t word = __builtin_bit_cast(uint32_t, buf_ld(rmask, lw_word(f0 >> 4, blockIdx.x, T128, g, c) * 4));
+      W.mk[0] = word >> (8 * w);
+    } else {
+      const uint32_t mb = ((uint32_t)(f0 >> 4) * a.M + mrow) * 2;
 #pragma unroll
-    for (int q = 0; q < NR; ++q) W.mk[q] = buf_ld_u16(rmask, mb + (16 * (q >> 2) + (q & 3)) * 2);
+      for (int q = 0; q < NR; ++q) W.mk[q] = buf_ld_u16(rmask, mb + (16 * (q >> 2) + (q & 3)) * 2);
+    }
   };
   auto chunk = [&](int f0, int buf, const Wc& W) {
     float* rg = smem + 2 * T::TILE + (buf * 4 + w) * T::RG;
@@ -372,7 +498,7 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
         const float cdf = norm_cdf(z);
         const float gz = z * cdf;
         const float gg = cdf + z * (__builtin_amdgcn_exp2f(-0.72134752044448170f * z * z) * 0.39894228040143268f);
-        const bool keep = !drop || ((W.mk[4 * i + rr] >> c) & 1u);
+        const bool keep = !drop || (T::LW ? (W.mk[0] >> (4 * i + rr)) & 1u : (W.mk[4 * i + rr] >> c) & 1u);
         const float sc = drop ? (keep ? a.drop.scale : 0.f) : 1.f;
         const float fo = (m < a.M) ? gz * sc : 0.f;
         const float da = dact[i][rr] * sc * gg;
@@ -436,87 +562,228 @@ __global__ __launch_bounds__(256) void ffn_bwd_kernel(FfnArgs a) {
   }
   if (f0 < a.FF) chunk(f0, 0, wa);            // odd chunk count: wa holds chunk FF-16
 
-  // dx = dact W1 (complete over FF in this wave) + dh (residual path)
-  if (!NORMS) {
+  ffn_bwd_epilogue<D, NORMS>(a, dxacc, dw, m0, slab, smem + 2 * T::TILE);
+}
+
+// ---------------------------------------------------------------- backward, column-owner form
+// D <= 32 with FF/16 a multiple of 4: wave w walks chunks w, w+4, w+8, ... over ALL 128 rows of the
+// tile, so each chunk's dW1 / dW2 / db1 slices are complete over the tile in one wave's registers (no
+// per-chunk cross-wave sum, no workgroup barrier in the chunk loop) and go straight to the slab.  The
+// price is a per-wave dx accumulator over all 128 rows (its FF quarter), exchanged once at the end:
+// each wave writes the three row groups it does not own, then sums its own 32 rows in the fixed order
+// of the source waves -- deterministic like the rows-per-wave kernel (different summation order).
+template <int D>
+struct FfnCols {
+  using T = FfnTile<D>;
+  static_assert(T::RT == 128 && T::LW, "column-owner backward: 128-row tiles with lane-word keep bits");
+  static constexpr int NB = 8;                      // 16-row blocks of the tile
+  static constexpr int STG = 16 * T::SS;            // one wave's dact staging block
+  static constexpr int XCH = 12 * 32 * D;           // dx exchange: (source wave, other group) slots
+  static constexpr int LOAD = T::TILE + 2048;       // x tile + the norm loader's scratch
+  static constexpr int MAIN = T::TILE + 4 * STG;    // x tile + staging
+  static constexpr int UNION = XCH > LOAD ? (XCH > MAIN ? XCH : MAIN) : (LOAD > MAIN ? LOAD : MAIN);
+};
+
+template <int D, bool NORMS>
+__global__ __launch_bounds__(256) void ffn_bwd_cols_kernel(FfnArgs a) {
+  using T = FfnTile<D>;
+  using C = FfnCols<D>;
+  // [dh tile | union { x tile, 4 staging blocks } / { norm loader scratch } / { dx exchange }]
+  __shared__ __attribute__((aligned(16))) float smem[T::TILE + C::UNION];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int m0 = blockIdx.x * T::RT;
+  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
+  float* dht = smem;
+  float* xt = smem + T::TILE;
+  load_tile<D, true>(a.x, a.M, m0, xt);
+  if (NORMS) load_dh_norm2<D, true>(a, m0, dht, xt + T::TILE, slab);
+  else load_tile<D, true>(a.dh, a.M, m0, dht);
+  __syncthreads();
+  float* st = xt + T::TILE + w * C::STG;
+
+  f32x4 dxacc[C::NB][T::NJ];
 #pragma unroll
-    for (int i = 0; i < T::NI; ++i)
+  for (int i = 0; i < C::NB; ++i)
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-        const auto rdx = buf_rsrc(a.dx, (uint32_t)a.M * D * 4);     // rows past M: dropped
+    for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool drop = a.drop.thresh != 0;
+  const auto rW1 = buf_rsrc(a.W1, (uint32_t)a.FF * D * 4);
+  const auto rW2 = buf_rsrc(a.W2, (uint32_t)a.FF * D * 4);
+  const auto rb1 = buf_rsrc(a.b1, (uint32_t)a.FF * 4);
+  const auto rmask = buf_rsrc(a.mask, drop ? (uint32_t)lw_words(a.M, a.FF) * 4 : 0u);
+  const int T128 = (a.M + 127) / 128;
+  struct Wc {
+    float v1[T::KQ], v2[T::KQ], v3[T::NJ][4], b;
+    uint32_t mk;
+  };
+  // per-lane buffer offsets: one VGPR base per operand, everything chunk- or k-dependent is uniform
+  // (SGPR soffset).  The D-contraction's k order follows the permuted tile: tile position g*KQ + q holds
+  // d = 16 (q % NJ) + 4g + q / NJ.
+  const uint32_t vo1 = (uint32_t)(c * D + 4 * g) * 4, vo2 = (uint32_t)(4 * g * a.FF + c) * 4;
+  const uint32_t vo3 = (uint32_t)(4 * g * D + c) * 4, vob = (uint32_t)c * 4;
+  auto load_w = [&](int ci, Wc& W) {
+    const int f0 = 16 * ci;
+    const uint32_t s1 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * D * 4);
+    const uint32_t s2 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * 4);
 #pragma unroll
-        for (int j = 0; j < T::NJ; ++j) {
-          const int d = 16 * j + c;
-          buf_st(dxacc[i][j][rr] + dw[row * T::S + d], rdx, (uint32_t)(m * D + d) * 4);
+    for (int j = 0; j < T::NJ; ++j) {
+      const f32x4 v = buf_ld4(rW1, vo1, s1 + 64 * j);                // W1[ff][16j + 4g .. +3]
+#pragma unroll
+      for (int t = 0; t < 4; ++t) W.v1[t * T::NJ + j] = v[t];
+    }
+#pragma unroll
+    for (int q = 0; q < T::KQ; ++q)
+      W.v2[q] = buf_ld(rW2, vo2, s2 + (uint32_t)((16 * (q % T::NJ) + q / T::NJ) * a.FF) * 4);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) W.v3[j][t] = buf_ld(rW1, vo3, s1 + (uint32_t)(t * D + 16 * j) * 4);
+    W.b = buf_ld(rb1, vob, s2);
+    W.mk = __builtin_bit_cast(uint32_t, buf_ld(rmask, lw_word(ci, blockIdx.x, T128, g, c) * 4));
+  };
+  auto chunk = [&](int ci, const Wc& W) {
+    const int f0 = 16 * ci;
+    // the x / dh tiles are loop-invariant: without this the compiler hoists all 8 blocks' tile reads out
+    // of the chunk loop and keeps them in ~200 VGPRs (one wave per SIMD)
+    asm volatile("" ::: "memory");
+    f32x4 dw2[T::NJ], dw1[T::NJ];
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) dw2[j] = dw1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float db = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::NB; ++i) {
+      // pre = x W1^T and dfo = dh W2 for rows 16i.. (two interleaved chains over the D-contraction)
+      f32x4 pre = {0.f, 0.f, 0.f, 0.f}, dact = {0.f, 0.f, 0.f, 0.f};
+      const float* xr = xt + (16 * i + c) * T::S + g * T::KQ;
+      const float* hr = dht + (16 * i + c) * T::S + g * T::KQ;
+#pragma unroll
+      for (int kq = 0; kq < T::KQ; kq += 4) {
+        const f32x4 ax = *(const f32x4*)(xr + kq), ah = *(const f32x4*)(hr + kq);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          pre = mfma4(ax[t], W.v1[kq + t], pre);
+          dact = mfma4(ah[t], W.v2[kq + t], dact);
         }
       }
-    return;
-  }
-  // norm-fused: dh1 = RMSNorm-backward(dx1; h1, r1, nw1) per row (a row's D values sit in the 16 lanes
-  // of one lane group, NJ per lane), and this workgroup's norm1.w grad partial sum_rows dx1 h1 r1
-  // h1 / r1 rows past M read 0 and their dh1 stores are dropped (buffer bounds): no branches, so all
-  // the row loads are in flight together
-  const auto rh1 = buf_rsrc(a.h1, (uint32_t)a.M * D * 4), rr1 = buf_rsrc(a.r1, (uint32_t)a.M * 4);
-  const auto rdh1 = buf_rsrc(a.dh1, (uint32_t)a.M * D * 4);
-  float nw[T::NJ], cn1[T::NJ];
 #pragma unroll
-  for (int j = 0; j < T::NJ; ++j) {
-    nw[j] = a.nw1[16 * j + c];
-    cn1[j] = 0.f;
-  }
-  float hv[T::NI][4][T::NJ], rmv[T::NI][4];
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * i + 4 * g + rr, m = m0 + row;
+        const float z = pre[rr] + W.b;
+        const float cdf = norm_cdf(z);
+        const float gz = z * cdf;
+        const float gg = cdf + z * (__builtin_amdgcn_exp2f(-0.72134752044448170f * z * z) * 0.39894228040143268f);
+        const bool keep = !drop || ((W.mk >> (4 * i + rr)) & 1u);
+        const float sc = drop ? (keep ? a.drop.scale : 0.f) : 1.f;
+        const float fo = (m < a.M) ? gz * sc : 0.f;
+        const float da = dact[rr] * sc * gg;
+        dact[rr] = da;
+        db += da;
+        float hd[T::NJ], xd[T::NJ];                  // columns 16j + c: adjacent in the permuted tiles
 #pragma unroll
-  for (int i = 0; i < T::NI; ++i)
+        for (int j = 0; j < T::NJ; ++j) {
+          hd[j] = dht[row * T::S + c * T::NJ + j];
+          xd[j] = xt[row * T::S + c * T::NJ + j];
+        }
 #pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int m = m0 + w * T::RW + 16 * i + 4 * g + rr;
-      rmv[i][rr] = buf_ld(rr1, (uint32_t)m * 4);
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j) hv[i][rr][j] = buf_ld(rh1, (uint32_t)(m * D + 16 * j + c) * 4);
-    }
-#pragma unroll
-  for (int i = 0; i < T::NI; ++i)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-      float dx1[T::NJ];
-      float dot = 0.f;
-      const float rm = rmv[i][rr];
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j) {
-        const int d = 16 * j + c;
-        dx1[j] = dxacc[i][j][rr] + dw[row * T::S + d];
-        dot = fmaf(nw[j] * dx1[j], hv[i][rr][j], dot);
+        for (int j = 0; j < T::NJ; ++j) {
+          dw2[j] = mfma4(hd[j], fo, dw2[j]);
+          dw1[j] = mfma4(da, xd[j], dw1[j]);
+        }
       }
-      dot = group_sum<16>(dot);
-      const float coef = rm * rm * rm / (float)D * dot;
+      // dx[rows 16i..] += dact W1 over this chunk: the dact block through this wave's staging tile
 #pragma unroll
-      for (int j = 0; j < T::NJ; ++j) {
-        buf_st(nw[j] * dx1[j] * rm - hv[i][rr][j] * coef, rdh1, (uint32_t)(m * D + 16 * j + c) * 4);
-        cn1[j] = fmaf(dx1[j] * hv[i][rr][j], rm, cn1[j]);
-      }
+      for (int rr = 0; rr < 4; ++rr) st[(4 * g + rr) * T::SS + c] = dact[rr];
+      __builtin_amdgcn_wave_barrier();
+      const f32x4 av = *(const f32x4*)(st + c * T::SS + 4 * g);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = mfma4(av[t], W.v3[j][t], dxacc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);      // keep the next block's tile reads from piling up registers
     }
-  // sum the norm1.w partials over the lane groups, then over the waves (fixed order)
+    db += __shfl_xor(db, 16);
+    db += __shfl_xor(db, 32);
+    // the chunk's weight-grad slices, complete over the tile: C[ff = 4g+rr][d = 16j+c], C[d = 16j+4g+rr][ff = c]
 #pragma unroll
-  for (int j = 0; j < T::NJ; ++j) {
-    cn1[j] += __shfl_xor(cn1[j], 16, 64);
-    cn1[j] += __shfl_xor(cn1[j], 32, 64);
+    for (int j = 0; j < T::NJ; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        slab[a.o_w1 + (long)(f0 + 4 * g + rr) * D + 16 * j + c] = dw1[j][rr];
+        slab[a.o_w2 + (long)(16 * j + 4 * g + rr) * a.FF + f0 + c] = dw2[j][rr];
+      }
+    if (g == 0) slab[a.o_b1 + f0 + c] = db;
+  };
+  // chunks w, w+4, ...: ping-pong prefetch as in the rows-per-wave kernel
+  const int nk = a.FF / 64;
+  for (int k = 0; k < nk; ++k) {
+    Wc wa;
+    load_w(w + 4 * k, wa);
+    chunk(w + 4 * k, wa);
   }
-  __syncthreads();                         // the last chunk's sum has read the regions
-  float* red = smem + 2 * T::TILE;
-  if (g == 0)
+
+  // dx exchange: slot (src, grp) for grp != src holds src's partial of group grp's 32 rows, lane-major
+  __syncthreads();                                  // x tile / staging no longer read
+  float* xch = xt;
+  auto slot = [&](int src, int grp) { return xch + (src * 3 + (grp < src ? grp : grp - 1)) * 32 * D; };
 #pragma unroll
-    for (int j = 0; j < T::NJ; ++j) red[w * D + 16 * j + c] = cn1[j];
+  for (int grp = 0; grp < 4; ++grp) {
+    if (grp == w) continue;
+    float* dst = slot(w, grp);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) dst[((ii * T::NJ + j) * 4 + rr) * 64 + lane] = dxacc[2 * grp + ii][j][rr];
+  }
   __syncthreads();
-  if (tid < D) slab[a.o_n1 + tid] = ((red[tid] + red[D + tid]) + red[2 * D + tid]) + red[3 * D + tid];
+  f32x4 own[2][T::NJ], dxs[2][T::NJ];
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) {
+      own[ii][j] = dxacc[ii][j];
+#pragma unroll
+      for (int grp = 1; grp < 4; ++grp)
+        if (grp == w) own[ii][j] = dxacc[2 * grp + ii][j];
+    }
+#pragma unroll
+  for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        float sum = 0.f;
+#pragma unroll
+        for (int src = 0; src < 4; ++src) {
+          const float v = src == w ? own[ii][j][rr]
+                                   : slot(src, w == src ? 0 : w)[((ii * T::NJ + j) * 4 + rr) * 64 + lane];
+          sum += v;
+        }
+        dxs[ii][j][rr] = sum;
+      }
+  static_assert(T::NI == 2 && T::RW == 32, "the epilogue takes 32 rows per wave");
+  ffn_bwd_epilogue<D, NORMS, true>(a, dxs, dht + w * T::RW * T::S, m0, slab, xt);
 }
 
 template <int D>
 static void launch_ffn(const FfnArgs& a, bool bwd, hipStream_t s) {
   const int blocks = cdiv(a.M, FfnTile<D>::RT);
-  if (bwd && a.dy) ffn_bwd_kernel<D, true><<<blocks, 256, 0, s>>>(a);
-  else if (bwd) ffn_bwd_kernel<D, false><<<blocks, 256, 0, s>>>(a);
-  else ffn_fwd_kernel<D><<<blocks, 256, 0, s>>>(a);
+  if (!bwd) {
+    ffn_fwd_kernel<D><<<blocks, 256, 0, s>>>(a);
+    return;
+  }
+  if constexpr (D <= 32) {
+    if ((a.FF / 16) % 4 == 0) {       // column-owner backward: chunks split evenly over the four waves
+      if (a.dy) ffn_bwd_cols_kernel<D, true><<<blocks, 256, 0, s>>>(a);
+      else ffn_bwd_cols_kernel<D, false><<<blocks, 256, 0, s>>>(a);
+      return;
+    }
+  }
+  if (a.dy) ffn_bwd_kernel<D, true><<<blocks, 256, 0, s>>>(a);
+  else ffn_bwd_kernel<D, false><<<blocks, 256, 0, s>>>(a);
 }
 
 static bool ffn_shape_ok(int D, int FF) { return (D == 16 || D == 32 || D == 64) && FF > 0 && FF % 16 == 0; }
@@ -544,7 +811,11 @@ extern "C" int ctr_ffn_supported(int D, int FF) { return ffn_shape_ok(D, FF) ? 1
 
 extern "C" int ctr_ffn_slab_rows(int M, int D) { return cdiv(M, D >= 64 ? 64 : 128); }
 
-extern "C" int ctr_ffn_mask_words(int M, int FF) { return (int)(((long)M * (FF / 16) + 1) / 2); }
+// enough for either keep-bit layout (FfnTile::LW)
+extern "C" int ctr_ffn_mask_words(int M, int FF) {
+  const long rowwords = ((long)M * (FF / 16) + 1) / 2;
+  return (int)(lw_words(M, FF) > rowwords ? lw_words(M, FF) : rowwords);
+}
 
 extern "C" int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
                            const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
