@@ -115,24 +115,29 @@ def pmc_traffic(name):
     corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE counts half of wide streaming reads:
     x2).  None when the summaries are absent."""
     import csv
-    kern = {"ctr_ffn_bwd": "ffn_bwd_kernel", "ctr_ffn_bwd_norms": "ffn_bwd_kernel",
-            "ctr_ffn_fwd": "ffn_fwd_kernel"}.get(name)
+    bwd = ("ffn_bwd_cols_kernel", "ffn_bwd_kernel")       # the entry point's kernels, preferred first
+    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_kernel",)}.get(name)
     base = os.path.join(REPO, "profiles", "r01")
-    if kern is None:
+    if kerns is None:
         return None
     vals = {}
     for ctr, fn in (("FETCH_SIZE", "pmc_fetch.csv"), ("WRITE_SIZE", "pmc_write.csv")):
         path = os.path.join(base, fn)
         if not os.path.exists(path):
             return None
-        xs = []
+        xs = {k: [] for k in kerns}
         with open(path) as fh:
             for r in csv.DictReader(fh):
-                if kern in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
-                    xs.append(float(r["Counter_Value"]))
-        if not xs:
+                if r.get("Counter_Name") != ctr:
+                    continue
+                for k in kerns:
+                    if k + "<" in r.get("Kernel_Name", ""):
+                        xs[k].append(float(r["Counter_Value"]))
+                        break
+        hit = next((xs[k] for k in kerns if xs[k]), None)
+        if not hit:
             return None
-        vals[ctr] = sum(xs) / len(xs) * 1024.0      # rocprofv3 reports KB
+        vals[ctr] = sum(hit) / len(hit) * 1024.0    # rocprofv3 reports KB
     return round(2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"])
 
 
