@@ -51,7 +51,7 @@ __device__ __forceinline__ float epi_elem(const ctr_gemm_epi_t& e, float v, int 
 }
 
 template <int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_kernel(GemmArgs g) {
   constexpr int BK = 16;
   constexpr int SA = BM + 16, SB = BN + 16;
   constexpr int WM = BM / 2, WN = BN / 2;

@@ -214,20 +214,27 @@ class Engine:
     def gemm(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, splits=1):
         """C = op(A) op(B) (+ epilogue); A/B/C are raw pointers.  A grid too small to fill the 256 CUs
         with a deep K (e.g. the QNN MLP's first layer, 32x4 tiles over K = 6400) is split along K."""
-        if splits == 1 and K >= 512 and not (epi is not None and epi.norm_w):
-            tiles = self._tiles(M, N)
-            if tiles < 512:     # ~1200 workgroups (tools/kbench.py --which gemm sweeps)
-                splits = int(max(1, min(round(1200 / tiles), K // 256)))
+        if splits == 1 and K >= 512 and not (epi is not None and epi.norm_w) and self._tiles(M, N) < 256:
+            splits = self._split_factor(M, N, K, 256)
         wsp = None
         if splits > 1:
             wsp = ptr(self.splitk_ws(splits * M * N))
         call("ctr_gemm", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, self.s())
 
     @staticmethod
+    def _split_factor(M, N, K, min_depth):
+        """Split-K factor: ~1024 workgroups (4 resident per CU), at most 8 splits once the grid has >= 32
+        tiles and 32 below 64k-deep K, each split >= min_depth deep (tools/kbench.py --which gemm sweeps,
+        profiles/r01/microbench_gemm.log)."""
+        tiles = Engine._tiles(M, N)
+        s = math.ceil(1024 / tiles)
+        s = min(s, 8 if tiles >= 32 else 32 if K < 65536 else s)
+        return int(max(1, min(s, K // min_depth)))
+
+    @staticmethod
     def wgrad_splits(M, N, K):
-        """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows): ~1024 workgroups,
-        each split >= 64 rows deep (tile shapes as in ctr_gemm's dispatch)."""
-        return int(max(1, min(K // 64, math.ceil(1024 / Engine._tiles(M, N)))))
+        """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows), splits >= 64 rows deep."""
+        return Engine._split_factor(M, N, K, 64)
 
     def rowgemm_call(self, M, K, N, A, W, tb, C, bias=None, add=None, resid=None, norm_w=None, norm_h=None,
                      norm_r=None):
