@@ -11,8 +11,8 @@
  *     sized by the matching *_ws_size query.
  *   - `stream` is a hipStream_t (torch.cuda.current_stream().cuda_stream); no host sync inside.
  *   - return 0 on success, negative on error; ctr_last_error() returns a thread-local message.
- *   - dropout everywhere uses the counter-based mask {key, thresh24, scale} of csrc/common.h
- *     (spec shared with oracle/rng.py); thresh24 == 0 disables it.
+ *   - dropout everywhere uses the counter-based mask {key, thresh16, scale} of csrc/common.h
+ *     (spec shared with oracle/rng.py); thresh16 == 0 disables it.
  */
 #ifndef CTR_HIP_H
 #define CTR_HIP_H

@@ -13,8 +13,9 @@ follows the reference: ``y = x * (mask / (1 - p))`` (``_dropout_impl``).
 Spec (all u32 arithmetic, wrapping):
     mix32(x)      = lowbias32 finaliser
     site_key      = mix32(lo(seed) ^ mix32(hi(seed) + site * 0x9E3779B9))
-    bits(key, i)  = mix32(i ^ key)
-    keep(i)       = (bits >> 8) >= round(p * 2^24)
+    bits(key, i)  = mix32((i >> 1) ^ key)           # one hash per element pair (2k, 2k+1)
+    u(i)          = i odd ? bits >> 16 : bits & 0xFFFF
+    keep(i)       = u(i) >= thresh16(p),  thresh16 = max(1, round(p * 2^16)) for p > 0
 """
 from __future__ import annotations
 
@@ -48,8 +49,10 @@ def site_key(seed: int, site: int) -> int:
     return mix32_int(lo ^ mix32_int((hi + site * 0x9E3779B9) & M32))
 
 
-def thresh24(p: float) -> int:
-    return min(1 << 24, int(round(float(p) * (1 << 24))))
+def thresh16(p: float) -> int:
+    if p <= 0.0:
+        return 0
+    return min(1 << 16, max(1, int(round(float(p) * (1 << 16)))))
 
 
 def keep_mask(seed: int, site: int, p: float, shape) -> np.ndarray:
@@ -57,8 +60,9 @@ def keep_mask(seed: int, site: int, p: float, shape) -> np.ndarray:
     n = int(np.prod(shape))
     key = np.uint32(site_key(seed, site))
     idx = np.arange(n, dtype=np.uint32)
-    b = mix32_np(idx ^ key)
-    return ((b >> np.uint32(8)) >= np.uint32(thresh24(p))).reshape(shape)
+    b = mix32_np((idx >> np.uint32(1)) ^ key)
+    u = np.where((idx & np.uint32(1)) != 0, b >> np.uint32(16), b & np.uint32(0xFFFF))
+    return (u >= np.uint32(thresh16(p))).reshape(shape)
 
 
 def dropout_scale(p: float) -> np.float32:

@@ -54,7 +54,7 @@ def test_dropout_keys_match_oracle_spec():
         for site in (0, 1, 2, 100, 101, 102, 110):
             assert rng.site_key(seed, site) == orng.site_key(seed, site)
     key, th, sc = rng.drop_args(5, 3, 0.1, True)
-    assert th == orng.thresh24(0.1) and np.float32(sc) == orng.dropout_scale(0.1)
+    assert th == orng.thresh16(0.1) and np.float32(sc) == orng.dropout_scale(0.1)
     assert rng.drop_args(5, 3, 0.1, False) == (0, 0, 1.0)
 
 

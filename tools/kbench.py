@@ -58,7 +58,7 @@ def main():
         W2 = torch.randn(D, FF, device="cuda") / math.sqrt(FF)
         b2 = torch.randn(D, device="cuda") * 0.1
         nw = torch.ones(D, device="cuda")
-        thr = int(round(args.p * (1 << 24)))
+        thr = int(round(args.p * (1 << 16)))
         mask = torch.zeros(_lib.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
         y, h, r = torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda")
         dh, dx = torch.randn(M, D, device="cuda"), torch.empty(M, D, device="cuda")
@@ -131,7 +131,7 @@ def main():
     if "attn" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1
-        thr = int(round(args.p * (1 << 24)))
+        thr = int(round(args.p * (1 << 16)))
         scale = 1.0 / math.sqrt(D // H)
         amask = torch.zeros(_lib.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
         o = torch.empty(M, D, device="cuda")

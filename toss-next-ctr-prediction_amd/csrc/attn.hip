@@ -87,19 +87,29 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   for (int j0 = 0; j0 < K; j0 += 32) {          // one keep-bit word per 32 keys
     const int j1 = min(K, j0 + 32);
     uint32_t word = 0;
-#pragma unroll 4
-    for (int j = j0; j < j1; ++j) {
+    auto elem = [&](int j, bool keep) {
       const float s = (BIAS ? rb[j] : 0.f) + dotv<DH>(qs, kg + j * DH);
       const float e = fexp(s - m);
       l += e;
       float w = e;
       if (DROP) {
-        const bool keep = drop_keep(a.drop, rowbase + j);
         word |= (uint32_t)keep << (j - j0);
         w = keep ? e * a.drop.scale : 0.f;
       }
 #pragma unroll
       for (int c = 0; c < DH; ++c) acc[c] = fmaf(w, vg[j * DH + c], acc[c]);
+    };
+    if (DROP && (K & 1) == 0) {
+      // even K: every row starts on an even element index, so keys (j, j+1) share one pair hash
+#pragma unroll 2
+      for (int j = j0; j < j1; j += 2) {
+        const uint32_t bits = drop_pair_bits(a.drop, (rowbase + j) >> 1);
+        elem(j, drop_pair_keep(a.drop, bits, 0));
+        elem(j + 1, drop_pair_keep(a.drop, bits, 1));
+      }
+    } else {
+#pragma unroll 4
+      for (int j = j0; j < j1; ++j) elem(j, DROP ? drop_keep(a.drop, rowbase + j) : true);
     }
     if (DROP) mrow_bits[j0 >> 5] = word;
   }

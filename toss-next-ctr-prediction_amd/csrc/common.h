@@ -28,12 +28,14 @@ constexpr int WAVE = 64;
 // ----------------------------------------------------------------------------------------------
 // dropout RNG: counter-based, identical to oracle/rng.py (lowbias32 finaliser)
 //   key  = per (step seed, site), computed on the host (tossctr/rng.py)
-//   bits = mix32(idx ^ key);  keep = (bits >> 8) >= thresh24   (one lowbias32 round per element: the
-//   key is already a mixed per-(step, site) value; 2 quarter-rate integer multiplies per element)
+//   bits = mix32((idx >> 1) ^ key);  u = idx odd ? bits >> 16 : bits & 0xFFFF;  keep = u >= thresh16
+// One lowbias32 round (2 quarter-rate integer multiplies) serves the element pair (2k, 2k+1): the
+// kernels that hold both elements of a pair (attention rows, the FFN forward via a lane swap) hash
+// once per pair.  p resolves to 2^-16 (thresh16 = round(p * 65536), at least 1 for p > 0).
 // ----------------------------------------------------------------------------------------------
 struct Drop {
   uint32_t key;
-  uint32_t thresh;   // round(p * 2^24); 0 => no dropout
+  uint32_t thresh;   // round(p * 2^16); 0 => no dropout
   float scale;       // 1 / (1 - p) in fp32 (reference: bernoulli_(1-p).div_(1-p))
 };
 
@@ -47,8 +49,14 @@ __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 }
 
 __device__ __forceinline__ bool drop_keep(const Drop& d, uint32_t idx) {
-  uint32_t b = mix32(idx ^ d.key);
-  return (b >> 8) >= d.thresh;
+  const uint32_t b = mix32((idx >> 1) ^ d.key);
+  return ((idx & 1u) ? b >> 16 : b & 0xFFFFu) >= d.thresh;
+}
+
+// the pair hash of elements 2k, 2k+1 (bits: drop_pair_keep)
+__device__ __forceinline__ uint32_t drop_pair_bits(const Drop& d, uint32_t pair) { return mix32(pair ^ d.key); }
+__device__ __forceinline__ bool drop_pair_keep(const Drop& d, uint32_t bits, uint32_t odd) {
+  return (odd ? bits >> 16 : bits & 0xFFFFu) >= d.thresh;
 }
 
 // x * (mask / (1-p)): the value the reference's dropout produces

@@ -3,10 +3,11 @@
 //
 // Unfused, each layer writes and re-reads two M x FF fp32 activations (pre-GELU and post-dropout:
 // 2 x 377 MB at M = 245,760, FF = 384) and the backward writes/reads a third (dact) -- ~2.3 GB of HBM
-// traffic per layer.  Here a workgroup owns RT rows, each wave RW = RT/4 of them, and all four waves
-// walk FF in lock-step 16-column chunks; the FF-wide values live only in registers (plus a 16-column
-// wave-private LDS tile).  The backward recomputes pre = x1 W1^T + b1 and the dropout mask
-// (counter-based hash, common.h) instead of reading them.
+// traffic per layer.  Here a workgroup owns RT rows; the FF-wide values live only in registers (plus a
+// 16-column wave-private LDS tile).  Forward: each wave RW = RT/4 rows, all waves walk FF in 16-column
+// chunks and store the dropout keep bits.  Backward (recomputes pre = x1 W1^T + b1, reads the keep
+// bits): for D <= 32 the column-owner form (ffn_bwd_cols_kernel: wave w takes chunks w, w+4, ... over
+// all the tile's rows), otherwise the rows-per-wave form (ffn_bwd_kernel).
 //
 // All products are v_mfma_f32_16x16x4_f32 (exact fp32).  Operand layouts (lane l, g = l>>4, c = l&15):
 //   A[i][k] -> lane holds A[c][g],  B[k][j] -> lane holds B[g][c],  C[i][j] -> reg r holds C[4g+r][c].
@@ -16,8 +17,9 @@
 //   * row-contractions (dW1, dW2) use the C-layout register r of a 16-row block directly as the A / B
 //     operand whose k-set is the rows {4g + r}.
 // Only the FF-contractions (fo W2^T forward, dact W1 backward) stage the chunk through LDS.
-// Weight / bias grads: per chunk the four waves' partials are summed in a fixed order and written to
-// the workgroup's slab; ctr_colsum (rowops.hip) reduces the slabs in a fixed order -- deterministic.
+// Weight / bias grads go to a per-workgroup slab row (rows-per-wave form: the four waves' partials summed
+// in a fixed order per chunk; column-owner form: complete per wave); ctr_colsum (rowops.hip) reduces the
+// slabs in a fixed order -- deterministic.
 #include "common.h"
 #include "ctr_hip.h"
 
@@ -207,19 +209,33 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
     W.b = buf_ld(rb1, (uint32_t)c * 4, s2);
   };
   auto chunk = [&](int f0, const Wc& W) {
-    const int ff = f0 + c;
     f32x4 pre[T::NI];
     dcontract<D>(xw, W.v1, pre, g, c);
     // fo = dropout(gelu(pre + b1)) -> staging tile [row][16]; keep bits -> mask (layout FfnTile::LW)
     uint32_t kbyte = 0;
 #pragma unroll
-    for (int i = 0; i < T::NI; ++i)
+    for (int i = 0; i < T::NI; ++i) {
+      // columns (ff even, ff + 1) of a row are one RNG pair held by lanes c, c^1: each lane hashes two
+      // of the block's four rows and swaps the results with its neighbour (DPP quad_perm [1,0,3,2])
+      uint32_t pb[4] = {0u, 0u, 0u, 0u};
+      const uint32_t odd = c & 1;
+      if (a.drop.thresh) {
+        const uint32_t mb = (uint32_t)(m0 + w * T::RW + 16 * i + 4 * g + 2 * odd), ffe = (uint32_t)(f0 + (c & ~1));
+        const uint32_t h0 = drop_pair_bits(a.drop, (mb * (uint32_t)a.FF + ffe) >> 1);
+        const uint32_t h1 = drop_pair_bits(a.drop, ((mb + 1) * (uint32_t)a.FF + ffe) >> 1);
+        const uint32_t o0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)h0, 0xB1, 0xF, 0xF, true);
+        const uint32_t o1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)h1, 0xB1, 0xF, 0xF, true);
+        pb[0] = odd ? o0 : h0;
+        pb[1] = odd ? o1 : h1;
+        pb[2] = odd ? h0 : o0;
+        pb[3] = odd ? h1 : o1;
+      }
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
         float v = gelu_f(pre[i][rr] + W.b);
         if (a.drop.thresh) {
-          const bool keep = drop_keep(a.drop, (uint32_t)((long)m * a.FF + ff));
+          const bool keep = drop_pair_keep(a.drop, pb[rr], odd);
           v = keep ? v * a.drop.scale : 0.f;
           if (T::LW) {
             kbyte |= (keep ? 1u : 0u) << (4 * i + rr);
@@ -231,6 +247,7 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
         }
         st[row * T::SS + c] = v;
       }
+    }
     // this wave's rows are bits 8w .. 8w+7 of the lane word: one byte store
     if (T::LW && a.drop.thresh) buf_st_u8(kbyte, rmask, lw_word(f0 >> 4, blockIdx.x, T128, g, c) * 4 + w);
     __builtin_amdgcn_wave_barrier();

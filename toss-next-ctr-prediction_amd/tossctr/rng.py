@@ -32,11 +32,12 @@ def site_key(seed: int, site: int) -> int:
 
 
 def drop_args(seed: int, site: int, p: float, training: bool):
-    """(key, thresh24, scale) for the kernels; thresh 0 disables dropout (eval or p == 0)."""
+    """(key, thresh16, scale) for the kernels (csrc/common.h); thresh 0 disables dropout (eval or p == 0),
+    so any p > 0 gets at least 1."""
     import numpy as np
     if not training or p <= 0.0:
         return (0, 0, 1.0)
-    thresh = min(1 << 24, int(round(float(p) * (1 << 24))))
+    thresh = min(1 << 16, max(1, int(round(float(p) * (1 << 16)))))
     scale = float(np.float32(1.0) / np.float32(1.0 - p))
     return (site_key(seed, site), thresh, scale)
 
