@@ -115,7 +115,8 @@ def test_rowgrad_dedup_matches_numpy():
     assert torch.equal(ug[:u], ug2[:u])
 
 
-@pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (148, 8, 64, 0.1), (37, 2, 16, 0.3)])
+@pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (148, 8, 64, 0.1), (37, 2, 16, 0.3),
+                                     (64, 4, 16, 0.2), (61, 8, 32, 0.1)])
 def test_attention_fwd_bwd_vs_torch(K, H, D, p):
     L = _lib()
     from tossctr.rng import drop_args
