@@ -369,6 +369,17 @@ int ctr_gather_rows(const void* src, long row_words, const long* idx, int n, voi
 int ctr_scatter_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int max_uniq, int width, int ld,
                      uint32_t key_base, long n_rows, float* out, void* stream);
 
+/* ---- host-side hot loops of the Parquet -> NPY cache builder (src/data/build_cache_v1.py)  (hostio.cpp)
+ * Arrow string columns: offsets (n + 1, int32) into UTF-8 data.  No GPU involved.
+ * XXH64(string, seed) per row: the build's stable replacement for polars Series.hash (:104-111,128-129)
+ */
+int ctr_hash_utf8(const int32_t* offsets, const uint8_t* data, long n, uint64_t seed, uint64_t* out);
+/* seq strings -> (n, L) int32 (:149-156): ',' split, empty tokens dropped, int() each, last L tokens
+ * right-aligned over pad_id; valid (nullable, 1 byte per row) marks null rows (all pad).  Returns 0, or
+ * -(2 + row) for the first row whose token int() would reject / that overflows int32              */
+long ctr_parse_seq(const int32_t* offsets, const uint8_t* data, const uint8_t* valid, long n, int L, int pad_id,
+                   int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

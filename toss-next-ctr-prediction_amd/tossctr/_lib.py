@@ -115,6 +115,8 @@ SIGS = {
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
     "ctr_gather_rows": (i, [p, l, p, i, p, p]),
     "ctr_scatter_rows": (i, [p, p, p, i, i, i, u, l, p, p]),
+    "ctr_hash_utf8": (i, [p, p, l, C.c_uint64, p]),
+    "ctr_parse_seq": (l, [p, p, p, l, i, i, p]),
 }
 
 _lib = None
