@@ -369,6 +369,19 @@ int ctr_gather_rows(const void* src, long row_words, const long* idx, int n, voi
 int ctr_scatter_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int max_uniq, int width, int ld,
                      uint32_t key_base, long n_rows, float* out, void* stream);
 
+/* ---- validation metrics + temperature objective of the K-fold loop (src/utils/metrics.py:5-29,
+ * src/utils/calibration.py:23-52)                                                         (metrics.hip)
+ * p = sigmoid(z) (f64), or calibrated = 1: clip(sigmoid(clip(f32(z/T), +-50)), 1e-7, 1-1e-7)         */
+int ctr_val_prob(const float* z, int n, float T, int calibrated, double* p, void* stream);
+size_t ctr_metrics_ws_size(int n);
+/* out[0] = sklearn average_precision_score, out[1] = 50:50 weighted logloss, out[2] = #positives (all f64,
+ * device); the reference's nan_to_num / clip(1e-12) and one-class rules; deterministic               */
+int ctr_ap_wll(const double* p, const float* y, int n, double* out, void* ws, size_t ws_bytes, void* stream);
+/* fit_temperature's closure at T: out = {sum y log p, sum (1-y) log(1-p), and their d/dT} over n rows,
+ * p = clamp(sigmoid(z/T), 1e-7, 1-1e-7) in f32 (clamped rows: zero grad); ws: ctr_metrics_ws_size */
+int ctr_temp_nll(const float* z, const float* y, int n, float T, double* out, void* ws, size_t ws_bytes,
+                 void* stream);
+
 /* ---- host-side hot loops of the Parquet -> NPY cache builder (src/data/build_cache_v1.py)  (hostio.cpp)
  * Arrow string columns: offsets (n + 1, int32) into UTF-8 data.  No GPU involved.
  * XXH64(string, seed) per row: the build's stable replacement for polars Series.hash (:104-111,128-129)

@@ -115,6 +115,10 @@ SIGS = {
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
     "ctr_gather_rows": (i, [p, l, p, i, p, p]),
     "ctr_scatter_rows": (i, [p, p, p, i, i, i, u, l, p, p]),
+    "ctr_val_prob": (i, [p, i, f, i, p, p]),
+    "ctr_metrics_ws_size": (z, [i]),
+    "ctr_ap_wll": (i, [p, p, i, p, p, z, p]),
+    "ctr_temp_nll": (i, [p, p, i, f, p, p, z, p]),
     "ctr_hash_utf8": (i, [p, p, l, C.c_uint64, p]),
     "ctr_parse_seq": (l, [p, p, p, l, i, i, p]),
 }

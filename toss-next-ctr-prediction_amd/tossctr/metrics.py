@@ -1,4 +1,4 @@
-"""Validation metrics, calibration and logging for the K-fold loop (host harness, not accelerated).
+"""Validation metrics, calibration and logging for the K-fold loop (host reference versions + DeviceMetrics).
 
 Restates src/utils/metrics.py:5-29 (AP, 50:50 weighted logloss, Score), src/utils/calibration.py
 (temperature scaling by LBFGS on the 50:50 WLL, optional isotonic) and src/utils/log.py (console + CSV;
@@ -46,6 +46,73 @@ def _sigmoid_np(z):
     return 1.0 / (1.0 + np.exp(-z))
 
 
+class DeviceMetrics:
+    """The same metrics and the temperature fit on device (csrc/metrics.hip) for logits / labels that are
+    already in HBM: AP + 50:50 WLL + Score of sigmoid(z) (or of the temperature-calibrated probabilities)
+    and fit_temperature's LBFGS (torch.optim.LBFGS on the scalar log-temperature, as the reference runs it)
+    whose closure evaluates the loss and its gradient over all rows in one kernel."""
+
+    def __init__(self, device):
+        import torch
+        self.device = torch.device(device)
+        self._ws = None
+        self._out = torch.empty(8, dtype=torch.float64, device=self.device)
+
+    def _stream(self):
+        import torch
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _workspace(self, n):
+        import torch
+        from . import _lib
+        need = int(_lib.query("ctr_metrics_ws_size", n))
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def final_score(self, z, y, T=None):
+        """(AP, WLL, Score) of sigmoid(z) (f64, as the loop's p_raw) or, with T, of the calibrator's
+        clip(sigmoid(z/T)) -- src/utils/metrics.py:26-29 on device.  z, y: float32 device tensors."""
+        import torch
+        from ._lib import call
+        n = z.numel()
+        p = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
+        st = self._stream()
+        call("ctr_val_prob", z.data_ptr(), n, float(T or 1.0), int(T is not None), p.data_ptr(), st)
+        ws = self._workspace(n)
+        call("ctr_ap_wll", p.data_ptr(), y.data_ptr(), n, self._out.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        ap, wll = (float(v) for v in self._out[:2].cpu())
+        return ap, wll, 0.5 * ap + 0.5 * wll
+
+    def fit_temperature(self, z, y, lr=0.05, iters=200, clamp_T=(0.2, 5.0), l2_reg=1e-3):
+        """src/utils/calibration.py:23-52: LBFGS(strong_wolfe) on log T of the 50:50 WLL + l2 (T - 1)^2.
+        Returns the fitted log-temperature (CPU scalar tensor)."""
+        import torch
+        from ._lib import call
+        n = z.numel()
+        w_pos = max(float((y == 1).float().mean()), 1e-6)
+        w_neg = 1.0 - w_pos
+        ws = self._workspace(n)
+        st = self._stream()
+        log_temp = torch.nn.Parameter(torch.tensor(np.log(1.0), dtype=torch.float32))
+        opt = torch.optim.LBFGS([log_temp], lr=lr, max_iter=iters, line_search_fn="strong_wolfe")
+
+        def closure():
+            opt.zero_grad()
+            t_raw = float(torch.exp(log_temp.detach()))
+            clamped = clamp_T is not None and not (clamp_T[0] <= t_raw <= clamp_T[1])
+            T = float(np.float32(min(max(t_raw, clamp_T[0]), clamp_T[1]) if clamp_T is not None else t_raw))
+            call("ctr_temp_nll", z.data_ptr(), y.data_ptr(), n, T, self._out.data_ptr(), ws.data_ptr(), ws.numel(), st)
+            s_pos, s_neg, g_pos, g_neg = (float(v) for v in self._out[:4].cpu())
+            loss = 0.5 * (-(s_pos / n) / w_pos - (s_neg / n) / w_neg) + l2_reg * (T - 1.0) ** 2
+            dT = 0.5 * (-(g_pos / n) / w_pos - (g_neg / n) / w_neg) + 2.0 * l2_reg * (T - 1.0)
+            log_temp.grad = torch.tensor(0.0 if clamped else dT * T, dtype=torch.float32)
+            return torch.tensor(loss, dtype=torch.float32)
+
+        opt.step(closure)
+        return log_temp.detach()
+
+
 class Calibrator:
     """src/utils/calibration.py:54-110: 'temperature' | 'isotonic' | 'temperature+isotonic'."""
 
@@ -85,11 +152,17 @@ class Calibrator:
     def temperature(self):
         return None if self.log_temp is None else float(self._T(self.log_temp))
 
-    def fit(self, logits, y):
+    def fit(self, logits, y, device_metrics=None, z_dev=None, y_dev=None):
+        """``device_metrics`` (+ the same logits / labels as float32 device tensors): the temperature's
+        LBFGS closure runs on device (DeviceMetrics.fit_temperature); isotonic stays on the host."""
         z = np.asarray(logits, dtype=np.float64)
         y = np.asarray(y, dtype=np.int32)
         if self.method in ("temperature", "temperature+isotonic"):
-            self._fit_temperature(z, y)
+            if device_metrics is not None:
+                self.log_temp = device_metrics.fit_temperature(z_dev, y_dev, lr=self.lr, iters=self.iters,
+                                                               clamp_T=self.clamp_T, l2_reg=self.l2_reg)
+            else:
+                self._fit_temperature(z, y)
         if self.method in ("isotonic", "temperature+isotonic"):
             from sklearn.isotonic import IsotonicRegression
             p = _sigmoid_np(z / self.temperature if self.log_temp is not None else z)

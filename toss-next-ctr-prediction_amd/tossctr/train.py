@@ -79,8 +79,9 @@ def _cal_state(cal):
 
 
 @torch.no_grad()
-def predict_logits(model, store, idx_np, bs):
-    """Eval-mode forward over rows idx (src/train.py:211-225); returns logits (numpy).
+def predict_logits(model, store, idx_np, bs, as_tensor=False):
+    """Eval-mode forward over rows idx (src/train.py:211-225); returns logits (numpy, or the float32 device
+    tensor with ``as_tensor``).
 
     The batches are the reference's (consecutive bs-row slices of idx, which matters: the SE gate uses
     the batch mean).  Data parallel: rank r runs batches r, r + world, ... and the logits are
@@ -95,7 +96,7 @@ def predict_logits(model, store, idx_np, bs):
     n = idx_all.numel()
     nb = (n + bs - 1) // bs
     if nb == 0:
-        return np.zeros(0, np.float32)
+        return torch.zeros(0, dtype=torch.float32, device=dev) if as_tensor else np.zeros(0, np.float32)
     per_rank = (nb + world - 1) // world
     mine = torch.zeros(per_rank * bs, dtype=torch.float32, device=dev)
     for i in range(per_rank):
@@ -105,19 +106,19 @@ def predict_logits(model, store, idx_np, bs):
         logits, _, _, _ = model.engine.forward(*inputs, training=False, seed=0, save=False)
         mine[i * bs:i * bs + sl.numel()] = logits
     if world == 1:
-        return mine[:n].cpu().numpy()
+        return mine[:n] if as_tensor else mine[:n].cpu().numpy()
     from . import dist as D
     allr = torch.empty(world * per_rank * bs, dtype=torch.float32, device=dev)
     D.all_gather_into(allr, mine, dist.group.WORLD)
     out = allr.view(world, per_rank, bs).transpose(0, 1).reshape(-1)     # batch j = (i, r), j = i*world + r
-    return out[:n].cpu().numpy()
+    return out[:n].contiguous() if as_tensor else out[:n].cpu().numpy()
 
 
 def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None, device=None):
     """src/train.py:92-317 (same signature + optional pre-staged ``store``). Returns (best_state, best_score)."""
     from .configs import cat_cardinals  # noqa: F401
     from .data import DeviceShards
-    from .metrics import Calibrator, final_score
+    from .metrics import Calibrator, DeviceMetrics, final_score
     from .optim import FusedAdamW, build_ema
     from .wrapper import CTRModel
     dist = _dist()
@@ -145,6 +146,7 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
     gen = torch.Generator(device=device).manual_seed(int(cfg.get("seed", 777)) * 1000 + fold)
     idx_tr_dev = torch.from_numpy(idx_tr).to(device)
     global_step, best_score, best_state, wait = 0, -1e9, None, 0
+    dmet = DeviceMetrics(device)
     for epoch in range(1, epochs + 1):
         model.train()
         perm = idx_tr_dev[torch.randperm(len(idx_tr), generator=gen, device=device)]
@@ -164,16 +166,22 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
         if use_ema_eval:
             ema.store(model)
             ema.copy_to(model)
-        z_raw = predict_logits(model, store, idx_va, bs)
+        # validation metrics and the temperature fit on device (csrc/metrics.hip): the logits stay in HBM
+        z_dev = predict_logits(model, store, idx_va, bs, as_tensor=True)
         y_true = y_host[np.asarray(idx_va, dtype=np.int64)].astype(np.int64)
-        p_raw = 1.0 / (1.0 + np.exp(-z_raw.astype(np.float64)))
-        ap, wll, score = final_score(y_true, p_raw)
+        y_dev = torch.from_numpy(y_true.astype(np.float32)).to(device)
+        ap, wll, score = dmet.final_score(z_dev, y_dev)
         cal, score_cal = None, None
         if cfg.get("calibration", {}).get("enabled", False):
             cc = cfg["calibration"]
+            z_raw = z_dev.cpu().numpy()
             cal = Calibrator(method=cc.get("method", "temperature"), lr=float(cc.get("lr", 0.05)),
-                             iters=int(cc.get("iters", 200))).fit(z_raw, y_true)
-            ap_cal, wll_cal, score_cal = final_score(y_true, cal.predict_proba(z_raw))
+                             iters=int(cc.get("iters", 200))).fit(z_raw, y_true, device_metrics=dmet,
+                                                                  z_dev=z_dev, y_dev=y_dev)
+            if cal.iso is None:
+                ap_cal, wll_cal, score_cal = dmet.final_score(z_dev, y_dev, T=cal.temperature)
+            else:                       # isotonic map: host (sklearn), as the reference
+                ap_cal, wll_cal, score_cal = final_score(y_true, cal.predict_proba(z_raw))
         if rank == 0:
             K, tau = cfg["sequence"]["top_k"], cfg["sequence"]["recency_tau"]
             lr = opt.param_groups[0]["lr"]
