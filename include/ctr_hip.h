@@ -393,6 +393,38 @@ int ctr_hash_utf8(const int32_t* offsets, const uint8_t* data, long n, uint64_t 
 long ctr_parse_seq(const int32_t* offsets, const uint8_t* data, const uint8_t* valid, long n, int L, int pad_id,
                    int32_t* out);
 
+/* seq strings exploded for the co-visitation features (src/features/covis.py:60-80, :174-183): pieces of
+ * str.split(",") (empty pieces kept, null seq = no pieces), each a non-strict Int32 cast (null unless
+ * [+-]digits within int32), the last top_k kept; an empty list explodes to one null.  _count fills row_ptr
+ * (n + 1, int64) and returns the exploded length (or -1); ctr_covis_explode fills tok / pos / ok per
+ * element: ok = 1 for a non-null token, pos = (# non-null tokens so far in the row) - 1 (cum_count - 1) */
+long ctr_covis_explode_count(const int32_t* offsets, const uint8_t* data, const uint8_t* valid, long n, int top_k,
+                             int64_t* row_ptr);
+int ctr_covis_explode(const int32_t* offsets, const uint8_t* data, const uint8_t* valid, long n, int top_k,
+                      const int64_t* row_ptr, int32_t* tok, int32_t* pos, uint8_t* ok);
+
+/* ---- co-visitation pair statistics and row features (src/features/covis.py:155-292)        (covis.hip)
+ * Exploded elements: tok / pos / ok and erow (source row of each element); per source row: tgt (target
+ * code, -1 null), tb (time-bin code < 2^tb_bits, -1 null), click (0/1), keep (nullable: all rows).
+ * Pair table (device outputs, capacity n): sorted unique keys ((tok ^ 2^31) << 32 | tgt << tb_bits | tb),
+ * impr, clicks, w_rec_sum = sum exp(-pos/tau), max_pos, ctr = clip(clip((clicks + p0 S) / (impr + p0 S +
+ * (1 - p0) S), 1e-9, 1 - 1e-9), clip_lo, clip_hi), is_lowcount = impr < min_impr; n_pairs and
+ * p0 = mean(click) over the kept exploded elements (device scalars).  Deterministic.                  */
+size_t ctr_covis_ws_size(long n);
+int ctr_covis_pair_stats(const int32_t* tok, const int32_t* pos, const uint8_t* ok, const int32_t* erow, long n,
+                         const int32_t* tgt, const int32_t* tb, const uint8_t* click, const uint8_t* keep,
+                         int tb_bits, double tau, double prior_strength, double clip_lo, double clip_hi, int min_impr,
+                         uint64_t* out_keys, int32_t* out_impr, int64_t* out_clicks, double* out_wsum,
+                         int32_t* out_maxpos, double* out_ctr, uint8_t* out_low, int64_t* n_pairs, double* p0,
+                         void* ws, size_t ws_bytes, void* stream);
+/* per source row in rows[0, nq): its exploded elements (row_ptr) left-joined on the pair table ->
+ * out[i*8 + c] = sum_ctr, mean_ctr, max_ctr, top-n mean (polars nulls-first sort, topn <= 16), wmean_ctr
+ * = sum(ctr w) / sum(w), sum_impr, max_impr, pnorm_ctr = sqrt(mean ctr^2); nulls -> 0                  */
+int ctr_covis_row_features(const int64_t* rows, long nq, const int64_t* row_ptr, const int32_t* tok, const int32_t* pos,
+                           const uint8_t* ok, const int32_t* tgt, const int32_t* tb, int tb_bits, double tau,
+                           const uint64_t* keys, const double* ctr, const int32_t* impr, const int64_t* n_pairs,
+                           int topn, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -151,3 +151,106 @@ extern "C" long ctr_parse_seq(const int32_t* offsets, const uint8_t* data, const
   }
   return 0;
 }
+
+// ---------------------------------------------------------------------------------------------------------
+// Co-visitation features (tossctr/covis.py, the drop-in for src/features/covis.py): the seq column exploded
+// the way _parse_seq_topk + explode + cum_count do it (covis.py:60-80, :174-183):
+//   pieces = str.split(",") (empty pieces kept; a null seq is the empty list), each cast to Int32 non-strictly
+//   (null unless [+-]digits within int32), the LAST top_k pieces kept; an empty list explodes to one null;
+//   pos = (# non-null tokens so far in the row) - 1.
+// ctr_covis_explode_count fills row_ptr (n + 1) and returns the exploded length; ctr_covis_explode fills
+// tok / pos / ok (ok = 1 for a non-null token).  Rows are split over threads (disjoint output ranges).
+// ---------------------------------------------------------------------------------------------------------
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace {
+
+bool parse_i32_strict(const uint8_t* a, const uint8_t* b, int32_t* v) {
+  bool neg = false;
+  if (a < b && (*a == '+' || *a == '-')) neg = *a++ == '-';
+  if (a == b) return false;
+  int64_t x = 0;
+  for (; a < b; ++a) {
+    if (*a < '0' || *a > '9') return false;
+    x = x * 10 + (*a - '0');
+    if (x > ((int64_t)1 << 31)) return false;
+  }
+  x = neg ? -x : x;
+  if (x > INT32_MAX || x < INT32_MIN) return false;
+  *v = (int32_t)x;
+  return true;
+}
+
+inline long covis_pieces(const int32_t* off, const uint8_t* data, const uint8_t* valid, long i) {
+  if (valid && !valid[i]) return 0;
+  return 1 + (long)std::count(data + off[i], data + off[i + 1], (uint8_t)',');
+}
+
+template <class F>
+void parallel_rows(long n, F&& f) {
+  unsigned nt = std::thread::hardware_concurrency();
+  nt = std::max(1u, std::min(nt, 16u));
+  if (n < 65536) nt = 1;
+  std::vector<std::thread> th;
+  const long chunk = (n + nt - 1) / nt;
+  for (unsigned t = 0; t < nt; ++t) {
+    const long a = t * chunk, b = std::min(n, a + chunk);
+    if (a >= b) break;
+    th.emplace_back([&f, a, b] { f(a, b); });
+  }
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" long ctr_covis_explode_count(const int32_t* offsets, const uint8_t* data, const uint8_t* valid, long n,
+                                        int top_k, int64_t* row_ptr) {
+  if (n < 0 || !row_ptr || (n > 0 && !offsets)) return -1;
+  row_ptr[0] = 0;
+  for (long i = 0; i < n; ++i) {
+    const long m = std::min<long>(covis_pieces(offsets, data, valid, i), top_k > 0 ? top_k : 0);
+    row_ptr[i + 1] = row_ptr[i] + std::max<long>(m, 1);
+  }
+  return (long)row_ptr[n];
+}
+
+extern "C" int ctr_covis_explode(const int32_t* offsets, const uint8_t* data, const uint8_t* valid, long n, int top_k,
+                                 const int64_t* row_ptr, int32_t* tok, int32_t* pos, uint8_t* ok) {
+  if (n < 0 || (n > 0 && (!offsets || !row_ptr || !tok || !pos || !ok))) return -1;
+  parallel_rows(n, [&](long a, long b) {
+    for (long i = a; i < b; ++i) {
+      const int64_t o = row_ptr[i];
+      const long pieces = covis_pieces(offsets, data, valid, i);
+      const long m = std::min<long>(pieces, top_k > 0 ? top_k : 0);
+      if (m == 0) {                                   // [] explodes to one null
+        tok[o] = 0;
+        pos[o] = -1;
+        ok[o] = 0;
+        continue;
+      }
+      const uint8_t* s = data + offsets[i];
+      const uint8_t* e = data + offsets[i + 1];
+      long skip = pieces - m, k = 0;
+      int32_t cnt = 0;
+      for (const uint8_t* q = s; q <= e;) {
+        const uint8_t* t = q;
+        while (t < e && *t != ',') ++t;
+        if (skip > 0) {
+          --skip;
+        } else {
+          int32_t v = 0;
+          const bool good = parse_i32_strict(q, t, &v);
+          cnt += good;
+          tok[o + k] = good ? v : 0;
+          ok[o + k] = good;
+          pos[o + k] = cnt - 1;
+          ++k;
+        }
+        q = t + 1;
+      }
+    }
+  });
+  return 0;
+}

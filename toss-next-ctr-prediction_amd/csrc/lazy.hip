@@ -110,8 +110,9 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
       for (int q = 0; q < LQ; ++q) m[q] = v[q] = 0.0f;    // a dense idle tick leaves +0 moments
     }
   } else {
+    OptScalars sc = hv[s + 1 <= t_idle ? s + 1 : t_idle];
     for (int k = s + 1; k <= t_idle; ++k) {
-      const OptScalars sc = hv[k];
+      const OptScalars nx = hv[k + 1 <= t_idle ? k + 1 : t_idle];      // next tick's scalars in flight
 #pragma unroll
       for (int q = 0; q < LQ; ++q) {
         if (q < nq) {
@@ -119,6 +120,7 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
           if (sc.do_ema) ema_elem(sc, p[q], e[q]);
         }
       }
+      sc = nx;
     }
   }
   if (grow) {
@@ -322,18 +324,20 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
 // token: lanes [0, W) hold the att row's elements, [W, 2W) the rep row's (2 per lane when W = 64),
 // so every lane replays the same tick range -- no divergence between row groups -- and each tick's
 // scalars are a wave-uniform (scalar) load.
-constexpr int PAIR_EPL = 2;     // elements per lane (W <= 64)
 
+// EPL = elements per lane: 1 for W <= 32 (no dead lane slot replayed), 2 for W <= 64
+template <int EPL>
 struct PairRow {
-  float p[PAIR_EPL], m[PAIR_EPL], v[PAIR_EPL], e[PAIR_EPL];
-  long o[PAIR_EPL];             // arena offsets; -1 = lane slot unused
+  float p[EPL], m[EPL], v[EPL], e[EPL];
+  long o[EPL];             // arena offsets; -1 = lane slot unused
 };
 
-__device__ __forceinline__ void pair_load(PairRow& r, const ctr_lazy_tab_t& ta, const ctr_lazy_tab_t& tb, long row,
+template <int EPL>
+__device__ __forceinline__ void pair_load(PairRow<EPL>& r, const ctr_lazy_tab_t& ta, const ctr_lazy_tab_t& tb, long row,
                                           const float* P, const float* M, const float* V, const float* E) {
   const int W = ta.width, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int q = 0; q < PAIR_EPL; ++q) {
+  for (int q = 0; q < EPL; ++q) {
     const int el = lane + 64 * q;
     r.o[q] = el < W ? ta.p_off + row * W + el : el < 2 * W ? tb.p_off + row * W + (el - W) : -1;
     r.p[q] = r.m[q] = r.v[q] = r.e[q] = 0.f;
@@ -346,9 +350,10 @@ __device__ __forceinline__ void pair_load(PairRow& r, const ctr_lazy_tab_t& ta, 
   }
 }
 
-__device__ __forceinline__ void pair_store(const PairRow& r, float* P, float* M, float* V, float* E) {
+template <int EPL>
+__device__ __forceinline__ void pair_store(const PairRow<EPL>& r, float* P, float* M, float* V, float* E) {
 #pragma unroll
-  for (int q = 0; q < PAIR_EPL; ++q)
+  for (int q = 0; q < EPL; ++q)
     if (r.o[q] >= 0) {
       P[r.o[q]] = r.p[q];
       M[r.o[q]] = r.m[q];
@@ -359,11 +364,12 @@ __device__ __forceinline__ void pair_store(const PairRow& r, float* P, float* M,
 
 // ticks (s, t_idle] with grad 0, then (g != null) tick t_idle + 1 with grad g[q] * coef; same
 // arithmetic as replay_row (adam.h), decided per wave (s and the zero test are wave-uniform)
-__device__ __forceinline__ void pair_replay(PairRow& r, bool has_e, const OptScalars* __restrict__ hist, int s,
+template <int EPL>
+__device__ __forceinline__ void pair_replay(PairRow<EPL>& r, bool has_e, const OptScalars* __restrict__ hist, int s,
                                             int t_idle, const float* g, float coef) {
   bool nz = false;
 #pragma unroll
-  for (int q = 0; q < PAIR_EPL; ++q) nz = nz || r.m[q] != 0.0f || r.v[q] != 0.0f;
+  for (int q = 0; q < EPL; ++q) nz = nz || r.m[q] != 0.0f || r.v[q] != 0.0f;
   const bool zero = __ballot(nz) == 0;      // every element of both rows never stepped with a grad
   if (zero) {
     bool stepped = false;
@@ -372,31 +378,33 @@ __device__ __forceinline__ void pair_replay(PairRow& r, bool has_e, const OptSca
       if (sc.do_adam) {
         stepped = true;
 #pragma unroll
-        for (int q = 0; q < PAIR_EPL; ++q) r.p[q] = r.p[q] * sc.decay_mul;
+        for (int q = 0; q < EPL; ++q) r.p[q] = r.p[q] * sc.decay_mul;
       }
       if (sc.do_ema) {
 #pragma unroll
-        for (int q = 0; q < PAIR_EPL; ++q) ema_elem(sc, r.p[q], r.e[q]);
+        for (int q = 0; q < EPL; ++q) ema_elem(sc, r.p[q], r.e[q]);
       }
     }
     if (stepped) {
 #pragma unroll
-      for (int q = 0; q < PAIR_EPL; ++q) r.m[q] = r.v[q] = 0.0f;
+      for (int q = 0; q < EPL; ++q) r.m[q] = r.v[q] = 0.0f;
     }
   } else {
+    OptScalars sc = hist[s + 1 <= t_idle ? s + 1 : t_idle];
     for (int k = s + 1; k <= t_idle; ++k) {
-      const OptScalars sc = hist[k];
+      const OptScalars nx = hist[k + 1 <= t_idle ? k + 1 : t_idle];    // next tick's scalars in flight
 #pragma unroll
-      for (int q = 0; q < PAIR_EPL; ++q) {
+      for (int q = 0; q < EPL; ++q) {
         if (sc.do_adam) idle_adam_elem(sc, r.p[q], r.m[q], r.v[q]);
         if (sc.do_ema) ema_elem(sc, r.p[q], r.e[q]);
       }
+      sc = nx;
     }
   }
   if (g) {
     const OptScalars sc = hist[t_idle + 1];
 #pragma unroll
-    for (int q = 0; q < PAIR_EPL; ++q)
+    for (int q = 0; q < EPL; ++q)
       if (r.o[q] >= 0) adam_ema_elem(sc, r.p[q], r.m[q], r.v[q], r.e[q], g[q] * coef, sc.do_adam != 0);
   }
   (void)has_e;
@@ -404,6 +412,7 @@ __device__ __forceinline__ void pair_replay(PairRow& r, bool has_e, const OptSca
 
 // forward read of tokens X[0, n): a wave per token; lane 0 claims the att row's tick with a CAS (a token
 // read many times in the batch is caught up once) and the rep row's tick follows it
+template <int EPL>
 __global__ __launch_bounds__(256) void lazy_touch_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
                                                               const int32_t* __restrict__ X, long n, float* P,
                                                               float* M, float* V, float* E,
@@ -423,7 +432,7 @@ __global__ __launch_bounds__(256) void lazy_touch_pair_kernel(const ctr_lazy_tab
     win = __builtin_amdgcn_readfirstlane(win);
     if (!win) continue;
     s = __builtin_amdgcn_readfirstlane(s);
-    PairRow r;
+    PairRow<EPL> r;
     pair_load(r, ta, tb, row, P, M, V, E);
     pair_replay(r, E != nullptr, hist, s, tick, nullptr, 0.f);
     pair_store(r, P, M, V, E);
@@ -432,6 +441,7 @@ __global__ __launch_bounds__(256) void lazy_touch_pair_kernel(const ctr_lazy_tab
 }
 
 // one optimizer tick for the unique keys [0, *n_uniq) shared by the att grads Ga and the rep grads Gb
+template <int EPL>
 __global__ __launch_bounds__(256) void lazy_update_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
                                                                const uint32_t* __restrict__ keys,
                                                                const float* __restrict__ Ga,
@@ -450,11 +460,11 @@ __global__ __launch_bounds__(256) void lazy_update_pair_kernel(const ctr_lazy_ta
     if (key == LAZY_INVALID || (long)(key - ta.key_base) >= ta.rows) continue;
     const long row = (long)(key - ta.key_base);
     const int s = __builtin_amdgcn_readfirstlane(ta.last[row]);
-    PairRow r;
+    PairRow<EPL> r;
     pair_load(r, ta, tb, row, P, M, V, E);
-    float g[PAIR_EPL];
+    float g[EPL];
 #pragma unroll
-    for (int q = 0; q < PAIR_EPL; ++q) {
+    for (int q = 0; q < EPL; ++q) {
       const int el = lane + 64 * q;
       g[q] = el < W ? Ga[it * (long)g_ld + el] : el < 2 * W ? Gb[it * (long)g_ld + (el - W)] : 0.f;
     }
@@ -468,6 +478,7 @@ __global__ __launch_bounds__(256) void lazy_update_pair_kernel(const ctr_lazy_ta
 }
 
 // every row pair not yet at tick (flush of the DARE tables)
+template <int EPL>
 __global__ __launch_bounds__(256) void lazy_flush_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs, float* P,
                                                               float* M, float* V, float* E,
                                                               const OptScalars* __restrict__ hist, int tick) {
@@ -477,7 +488,7 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_kernel(const ctr_lazy_tab
   for (long row = wave; row < ta.rows; row += nwaves) {
     const int s = __builtin_amdgcn_readfirstlane(ta.last[row]);
     if (s >= tick) continue;
-    PairRow r;
+    PairRow<EPL> r;
     pair_load(r, ta, tb, row, P, M, V, E);
     pair_replay(r, E != nullptr, hist, s, tick, nullptr, 0.f);
     pair_store(r, P, M, V, E);
@@ -540,8 +551,12 @@ extern "C" int ctr_lazy_touch_pair(const ctr_lazy_tab_t* tabs, int width, const 
                                    float* M, float* V, float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_touch_pair: two tables of width <= 64");
   if (tick <= 0 || n <= 0) return 0;
-  lazy_touch_pair_kernel<<<pair_grid(n), 256, 0, (hipStream_t)stream>>>(tabs, X, n, P, M, V, E,
-                                                                        (const OptScalars*)hist, tick);
+  if (width <= 32)
+    lazy_touch_pair_kernel<1><<<pair_grid(n), 256, 0, (hipStream_t)stream>>>(tabs, X, n, P, M, V, E,
+                                                                             (const OptScalars*)hist, tick);
+  else
+    lazy_touch_pair_kernel<2><<<pair_grid(n), 256, 0, (hipStream_t)stream>>>(tabs, X, n, P, M, V, E,
+                                                                             (const OptScalars*)hist, tick);
   return check_launch("lazy_touch_pair");
 }
 
@@ -550,9 +565,12 @@ extern "C" int ctr_lazy_update_pair(const ctr_lazy_tab_t* tabs, int width, const
                                     float* P, float* M, float* V, float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64 && tick > 0, "ctr_lazy_update_pair: bad tables / tick");
   if (cap <= 0) return 0;
-  lazy_update_pair_kernel<<<pair_grid(cap), 256, 0, (hipStream_t)stream>>>(tabs, keys, Ga, Gb, g_ld, n_uniq, cap,
-                                                                           coef, P, M, V, E,
-                                                                           (const OptScalars*)hist, tick);
+  if (width <= 32)
+    lazy_update_pair_kernel<1><<<pair_grid(cap), 256, 0, (hipStream_t)stream>>>(
+        tabs, keys, Ga, Gb, g_ld, n_uniq, cap, coef, P, M, V, E, (const OptScalars*)hist, tick);
+  else
+    lazy_update_pair_kernel<2><<<pair_grid(cap), 256, 0, (hipStream_t)stream>>>(
+        tabs, keys, Ga, Gb, g_ld, n_uniq, cap, coef, P, M, V, E, (const OptScalars*)hist, tick);
   return check_launch("lazy_update_pair");
 }
 
@@ -560,7 +578,11 @@ extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long r
                                    float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_flush_pair: two tables of width <= 64");
   if (tick <= 0 || rows <= 0) return 0;
-  lazy_flush_pair_kernel<<<pair_grid(rows), 256, 0, (hipStream_t)stream>>>(tabs, P, M, V, E,
-                                                                            (const OptScalars*)hist, tick);
+  if (width <= 32)
+    lazy_flush_pair_kernel<1><<<pair_grid(rows), 256, 0, (hipStream_t)stream>>>(tabs, P, M, V, E,
+                                                                                 (const OptScalars*)hist, tick);
+  else
+    lazy_flush_pair_kernel<2><<<pair_grid(rows), 256, 0, (hipStream_t)stream>>>(tabs, P, M, V, E,
+                                                                                 (const OptScalars*)hist, tick);
   return check_launch("lazy_flush_pair");
 }

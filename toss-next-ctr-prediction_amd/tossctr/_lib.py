@@ -121,6 +121,12 @@ SIGS = {
     "ctr_temp_nll": (i, [p, p, i, f, p, p, z, p]),
     "ctr_hash_utf8": (i, [p, p, l, C.c_uint64, p]),
     "ctr_parse_seq": (l, [p, p, p, l, i, i, p]),
+    "ctr_covis_explode_count": (l, [p, p, p, l, i, p]),
+    "ctr_covis_explode": (i, [p, p, p, l, i, p, p, p, p]),
+    "ctr_covis_ws_size": (z, [l]),
+    "ctr_covis_pair_stats": (i, [p, p, p, p, l, p, p, p, p, i, C.c_double, C.c_double, C.c_double, C.c_double, i,
+                                 p, p, p, p, p, p, p, p, p, p, z, p]),
+    "ctr_covis_row_features": (i, [p, l, p, p, p, p, p, p, i, C.c_double, p, p, p, p, i, p, p]),
 }
 
 _lib = None

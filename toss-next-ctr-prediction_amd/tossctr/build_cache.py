@@ -194,19 +194,59 @@ def _save_shard(shard_dir: str, arrays: Dict[str, np.ndarray]) -> Dict:
     return meta
 
 
+def _join_covis(rb, covis, row_cursor):
+    """build_cache_v2.py:270-287: left join of the covis row features (global rid / ID), nulls -> 0.0."""
+    pa, pc, _ = _pa()
+    key, kcol, vals = covis
+    if key == "rid":
+        probe = pa.array(np.arange(row_cursor, row_cursor + rb.num_rows, dtype=np.int64))
+        kcol = pc.cast(kcol, pa.int64())
+    else:
+        if "ID" not in rb.schema.names:
+            return rb
+        probe = pc.cast(rb.column("ID"), pa.string())
+        kcol = pc.cast(kcol, pa.string())
+    pos = pc.index_in(probe, value_set=kcol)
+    valid = np.asarray(pc.is_valid(pos).to_numpy(zero_copy_only=False), bool)
+    idx = np.asarray(pc.fill_null(pos, 0).to_numpy(zero_copy_only=False), np.int64)
+    tbl = pa.Table.from_batches([rb])
+    for c, v in vals.items():
+        col = np.where(valid, v[idx] if len(v) else 0.0, 0.0)
+        col = np.nan_to_num(col, nan=0.0)
+        if c in tbl.schema.names:
+            tbl = tbl.drop_columns([c])
+        tbl = tbl.append_column(c, pa.array(col))
+    return tbl
+
+
 def build_sharded_cache(parquet_path: str, out_dir: str, *, is_train: bool, target_col: Optional[str],
                         seq_col: str, cat_cols: List[str], hash_buckets: Dict[str, int], hash_buckets_margin: int,
                         num_patterns: List[str], max_len: int, pad_id: int, group_key: str,
                         time_key: Optional[str] = None, composite_group: bool = False,
                         shard_rows: int = 2_000_000, impute_strategy: str = "median",
                         num_cols_explicit: List[str] | None = None, remove_cols: List[str] | None = None,
-                        batch_size: int = 200_000) -> str:
-    """build_cache_v1.py:169-307.  Returns the manifest path."""
-    _, _, ds = _pa()
+                        batch_size: int = 200_000, covis_enabled: bool = False,
+                        covis_dir: str = "./cache/covis") -> str:
+    """build_cache_v1.py:169-307 (build_cache_v2.py:177-347 with ``covis_enabled``: the co-visitation row
+    features of tossctr.covis left-joined on the global row id (train) or ``ID`` (test), nulls -> 0.0,
+    appended to the numeric columns with median 0.0).  Returns the manifest path."""
+    pa, pc, ds = _pa()
     os.makedirs(out_dir, exist_ok=True)
     schema = analyze_schema_and_stats(parquet_path, target_col, seq_col, cat_cols, num_patterns, group_key,
                                       impute_strategy, num_cols_explicit, remove_cols)
     num_cols, med_map = schema["num_cols"], schema["med_map"]
+    covis = None
+    if covis_enabled:
+        import pyarrow.parquet as pq
+        cv = pq.read_table(os.path.join(covis_dir, "rowfeat_oof_all.parquet" if is_train else "rowfeat_test.parquet"))
+        key = "rid" if is_train else "ID"
+        covis_cols = [c for c in cv.schema.names if c not in ("rid", "ID") and
+                      (pa.types.is_floating(cv.schema.field(c).type) or pa.types.is_integer(cv.schema.field(c).type))]
+        for c in covis_cols:
+            if c not in num_cols:
+                num_cols.append(c)
+                med_map[c] = 0.0
+        covis = (key, cv.column(key), {c: _column_f64(cv.column(c)) for c in covis_cols})
     manifest = {"parquet": parquet_path, "is_train": is_train, "rows": 0, "shards": [],
                 "num_cols": num_cols, "cat_cols": cat_cols, "group_key": group_key, "seq_col": seq_col}
     acc = {k: [] for k in ARRAYS}
@@ -221,12 +261,16 @@ def build_sharded_cache(parquet_path: str, out_dir: str, *, is_train: bool, targ
         manifest["shards"].append(meta)
         manifest["rows"] += meta["rows"]
 
+    row_cursor = 0
     keep = None
     if remove_cols:
         keep = [c for c in ds.dataset(parquet_path, format="parquet").schema.names if c not in remove_cols]
     for rb in ds.dataset(parquet_path, format="parquet").scanner(columns=keep, batch_size=batch_size).to_batches():
         if rb.num_rows == 0:
             continue
+        if covis is not None:
+            rb = _join_covis(rb, covis, row_cursor)
+        row_cursor += rb.num_rows
         batch = process_batch(rb, is_train=is_train, target_col=target_col, seq_col=seq_col, cat_cols=cat_cols,
                               hash_buckets=hash_buckets, hash_buckets_margin=hash_buckets_margin,
                               num_cols=num_cols, med_map=med_map, max_len=max_len, pad_id=pad_id,
@@ -247,8 +291,10 @@ def build_sharded_cache(parquet_path: str, out_dir: str, *, is_train: bool, targ
     return man_path
 
 
-def build_train_and_test(cfg: dict) -> Tuple[str, str]:
-    """build_cache_v1.py:310-351."""
+def build_train_and_test(cfg: dict, covis_enabled: bool = False) -> Tuple[str, str]:
+    """build_cache_v1.py:310-351 / build_cache_v2.py:350-389.  The reference's v2 helper never passes
+    ``covis_enabled`` (so its caches carry no covis columns); ``covis_enabled=True`` joins the features built
+    by tossctr.covis from ``cfg["features"]["covis"]["work_dir"]``."""
     common = dict(seq_col=cfg["sequence"]["col"], cat_cols=cfg["data"]["cat_cols"],
                   hash_buckets=cfg["data"]["hash_buckets"],
                   hash_buckets_margin=cfg["data"].get("hash_buckets_margin", 0),
@@ -258,6 +304,9 @@ def build_train_and_test(cfg: dict) -> Tuple[str, str]:
                   composite_group=bool(cfg["cv"].get("composite_group", False)),
                   shard_rows=cfg["data"].get("shard_rows", 2_000_000),
                   impute_strategy=cfg["data"]["impute_strategy"], remove_cols=cfg["data"].get("remove_cols"))
+    if covis_enabled:
+        common.update(covis_enabled=True,
+                      covis_dir=cfg.get("features", {}).get("covis", {}).get("work_dir", "./cache/covis"))
     mp_train = build_sharded_cache(cfg["data"]["train_path"], os.path.join(cfg["data"]["cache_dir"], "train"),
                                    is_train=True, target_col="clicked", **common)
     mp_test = build_sharded_cache(cfg["data"]["test_path"], os.path.join(cfg["data"]["cache_dir"], "test"),
