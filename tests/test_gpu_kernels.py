@@ -116,7 +116,8 @@ def test_rowgrad_dedup_matches_numpy():
 
 
 @pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (148, 8, 64, 0.1), (37, 2, 16, 0.3),
-                                     (64, 4, 16, 0.2), (61, 8, 32, 0.1)])
+                                     (64, 4, 16, 0.2), (61, 8, 32, 0.1), (50, 8, 16, 0.1), (64, 8, 64, 0.1),
+                                     (40, 6, 24, 0.1), (1, 8, 32, 0.1)])
 def test_attention_fwd_bwd_vs_torch(K, H, D, p):
     L = _lib()
     from tossctr.rng import drop_args
@@ -167,7 +168,10 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p):
     drel = torch.empty(2 * tk + 1, H, device="cuda")
     L.call("ctr_pos_bias_grad", ptr(drp), nparts, H, 2 * tk + 1, ptr(drel), stream())
     assert rel(dqkv, qkv.grad) < 1e-5
-    assert rel(drel, rel_w.grad) < 1e-5
+    if K == 1:      # softmax over one key: the exact grad is 0, ours is the rounding residue of dp - do.o
+        assert drel.abs().max() < 1e-6 and rel_w.grad.abs().max() == 0
+    else:
+        assert rel(drel, rel_w.grad) < 1e-5
 
 
 @pytest.mark.parametrize("L_,K,D", [(100, 60, 32), (40, 40, 16), (400, 148, 64), (7, 3, 8)])

@@ -294,6 +294,180 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   }
 }
 
+// K <= 64: one head per WAVE (lane = key column j in the column pass, query row i in the row pass), G heads
+// per workgroup, and no K x K dS tile in LDS: the row pass recomputes p_ij / dS_ij (the same arithmetic as
+// the column pass, so dS and dq are bit-identical to a stored tile) instead of reading it back.  That cuts
+// the LDS per head from ~20 KB to ~6 KB, so six workgroups (24 waves) share a CU instead of two -- the
+// kernel is latency-bound on its LDS broadcasts and exp, and occupancy is what hides that.
+// Positional-bias grad without a dS tile: at row step ii lane j adds dS_ij to diagonal j - ii, so a
+// diagonal's running sum moves one lane right per step -- a DPP wave_shr:1 of one accumulator register.
+// Lane K-1 holds a finished diagonal after every step (stored to LDS); the negative diagonals finish in
+// lanes 0..K-2 after the last step.  Each head sums its diagonals in row order, heads add in fixed order.
+template <int DH, bool BIAS, bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void attn_bwd_wave_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int K = a.K, D = a.D, G = a.G, KW = a.KW;
+  const int b = blockIdx.x, hg = blockIdx.y;
+  const int nrel = 2 * a.tk + 1, ND = 2 * K - 1;
+  float* sq = sm;                          // [G][K][DH] scaled q
+  float* sk = sq + G * K * DH;
+  float* sv = sk + G * K * DH;
+  float* sdo = sv + G * K * DH;
+  f32x4* sst = (f32x4*)(sdo + G * K * DH); // [G][K] {row max, 1 / row sum, do_i . o_i, 0}
+  float* srel = (float*)(sst + G * K);     // [nrel]
+  uint32_t* smask = (uint32_t*)(srel + nrel);   // [G][K][KW]
+  float* sdiag = (float*)(smask + G * K * KW);  // [G][2K-1] diagonal sums of dS, o + K - 1
+  const float* base = a.qkv + (long)b * K * 3 * D;
+  for (int e = threadIdx.x; e < G * K * DH; e += blockDim.x) {
+    const int g = e / (K * DH), r = e % (K * DH), j = r / DH, c = r % DH;
+    const int col = (hg * G + g) * DH + c;
+    sq[e] = base[(long)j * 3 * D + col] * a.scale;
+    sk[e] = base[(long)j * 3 * D + D + col];
+    sv[e] = base[(long)j * 3 * D + 2 * D + col];
+    sdo[e] = a.dO[((long)b * K + j) * D + col];
+  }
+  const long r0 = ((long)b * a.H + hg * G) * K;     // first (head, row) of the group
+  if (DROP)
+    for (int e = threadIdx.x; e < G * K * KW; e += blockDim.x) smask[e] = a.mask[r0 * KW + e];
+  if (BIAS)
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) srel[e] = a.relmean[e];
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63, h = hg * G + g;
+  const bool act = lane < K;
+  const int li = act ? lane : K - 1;                // inactive lanes mirror the last column / row
+  if (act) {
+    float di = 0.f;
+#pragma unroll
+    for (int c = 0; c < DH; ++c)
+      di = fmaf(a.dO[((long)b * K + lane) * D + h * DH + c], a.o[((long)b * K + lane) * D + h * DH + c], di);
+    sst[g * K + lane] = f32x4{a.mrow[r0 + g * K + lane], 1.0f / a.lrow[r0 + g * K + lane], di, 0.f};
+  }
+  __syncthreads();
+  const float* qg = sq + g * K * DH;
+  const float* kg = sk + g * K * DH;
+  const float* vg = sv + g * K * DH;
+  const float* dog = sdo + g * K * DH;
+  const f32x4* stg = sst + g * K;
+  const uint32_t* mk = smask + g * K * KW;
+  float* dg = sdiag + g * ND;
+  const float dscale = a.drop.scale;
+  const float live = act ? 1.0f : 0.0f;
+  // ---- column pass (lane = key column j): dk_j = sum_i dS_ij qs_i, dv_j = sum_i p~_ij do_i
+  {
+    constexpr int NB = DH <= 4 ? 2 : 1;   // row batch (all LDS operands loaded first); fits 80 VGPRs
+    const int j = li;
+    float kj[DH], vj[DH], dk[DH], dv[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) {
+      kj[c] = kg[j * DH + c];
+      vj[c] = vg[j * DH + c];
+      dk[c] = 0.f;
+      dv[c] = 0.f;
+    }
+    const float* rb = srel + a.tk + j;
+    const int jw = j >> 5, jb = j & 31;
+    float diag = 0.f;
+    for (int ii = 0; ii < K; ii += NB) {
+      float q[NB][DH], dov[NB][DH], rel[NB];
+      f32x4 st[NB];
+      uint32_t mw[NB];
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int r = ii + u < K ? ii + u : K - 1;
+#pragma unroll
+        for (int c = 0; c < DH; ++c) {
+          q[u][c] = qg[r * DH + c];
+          dov[u][c] = dog[r * DH + c];
+        }
+        st[u] = stg[r];
+        rel[u] = BIAS ? rb[-r] : 0.f;
+        mw[u] = DROP ? mk[r * KW + jw] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        if (ii + u < K) {                               // wave-uniform
+          const float sc = rel[u] + dotv<DH>(kj, q[u]);
+          const float p = fexp(sc - st[u][0]) * st[u][1];
+          float dp = dotv<DH>(vj, dov[u]);
+          float pt = p;
+          if (DROP) {
+            const float ks = ((mw[u] >> jb) & 1u) ? dscale : 0.f;
+            dp *= ks;
+            pt = p * ks;
+          }
+          const float ds = p * (dp - st[u][2]) * live;
+          pt *= live;
+#pragma unroll
+          for (int c = 0; c < DH; ++c) {
+            dk[c] = fmaf(ds, q[u][c], dk[c]);
+            dv[c] = fmaf(pt, dov[u][c], dv[c]);
+          }
+          if (BIAS) {
+            if (ii + u > 0) diag = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                0, __builtin_bit_cast(int, diag), 0x138 /* wave_shr:1 */, 0xF, 0xF, false));
+            diag += ds;
+            if (lane == K - 1) dg[2 * K - 2 - (ii + u)] = diag;   // diagonal K-1-(ii+u) is complete
+          }
+        }
+      }
+    }
+    if (BIAS && lane < K - 1) dg[lane] = diag;         // diagonals lane - (K-1) < 0
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < DH; ++c) {
+        a.dqkv[((long)b * K + j) * 3 * D + D + h * DH + c] = dk[c];
+        a.dqkv[((long)b * K + j) * 3 * D + 2 * D + h * DH + c] = dv[c];
+      }
+    }
+  }
+  // ---- row pass (lane = query row i): dq_i = scale * sum_j dS_ij k_j, dS recomputed as above
+  {
+    const int i = li;
+    float qi[DH], doi[DH], dq[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) {
+      qi[c] = qg[i * DH + c];
+      doi[c] = dog[i * DH + c];
+      dq[c] = 0.f;
+    }
+    const f32x4 st = stg[i];
+    const float* rb = srel + a.tk - i;                  // rb[j] = relmean[j - i + tk]
+    for (int j0 = 0; j0 < K; j0 += 32) {
+      const uint32_t mw = DROP ? mk[i * KW + (j0 >> 5)] : 0u;
+      const int j1 = j0 + 32 < K ? j0 + 32 : K;
+#pragma unroll 4
+      for (int j = j0; j < j1; ++j) {
+        float kj[DH], vj[DH];
+#pragma unroll
+        for (int c = 0; c < DH; ++c) {
+          kj[c] = kg[j * DH + c];
+          vj[c] = vg[j * DH + c];
+        }
+        const float sc = (BIAS ? rb[j] : 0.f) + dotv<DH>(kj, qi);
+        const float p = fexp(sc - st[0]) * st[1];
+        float dp = dotv<DH>(vj, doi);
+        if (DROP) dp *= ((mw >> (j - j0)) & 1u) ? dscale : 0.f;
+        const float ds = p * (dp - st[2]);
+#pragma unroll
+        for (int c = 0; c < DH; ++c) dq[c] = fmaf(ds, kj[c], dq[c]);
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < DH; ++c) a.dqkv[((long)b * K + i) * 3 * D + h * DH + c] = dq[c] * a.scale;
+    }
+  }
+  if (BIAS) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
+      const int o = e - a.tk;
+      float s = 0.f;
+      if (o > -K && o < K)
+        for (int gg = 0; gg < G; ++gg) s += sdiag[gg * ND + o + K - 1];
+      a.drel_part[((long)b * gridDim.y + hg) * nrel + e] = s;
+    }
+  }
+}
+
 static int pick_group(int H, int K, size_t per_head_lds, size_t lds_cap) {
   int best = 1;
   for (int g = 1; g <= H; ++g)
@@ -316,6 +490,35 @@ static size_t bwd_lds(int G, int K, int dh, int tk) {
 
 static int bwd_group(int H, int K, int dh) {
   return pick_group(H, K, (size_t)(K * bwd_kp(K) + 4 * K * dh + 4 * K + K * bwd_mkw(K)) * 4, 80 * 1024);
+}
+
+// the wave-per-head backward (K <= 64, dh <= 8): G = the largest divisor of H up to 4 (one wave per head)
+static bool bwd_use_wave(int K, int dh) { return K <= 64 && dh <= 8; }
+
+static int bwd_wave_group(int H) {
+  int g = 1;
+  for (int c = 1; c <= 4; ++c)
+    if (H % c == 0) g = c;
+  return g;
+}
+
+static size_t bwd_wave_lds(int G, int K, int dh, int tk) {
+  return ((size_t)4 * G * K * dh + 4 * G * K + (2 * tk + 1) + (size_t)G * K * ((K + 31) / 32) +
+          (size_t)G * (2 * K - 1)) * sizeof(float);
+}
+
+template <int DH, bool BIAS, bool DROP>
+static void launch_bwd_wave3(const AttnArgs& a, size_t sm, hipStream_t s) {
+  attn_bwd_wave_kernel<DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), a.G * 64, sm, s>>>(a);
+}
+
+template <int DH>
+static void launch_bwd_wave(const AttnArgs& a, size_t sm, hipStream_t s) {
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  if (bias && drop) launch_bwd_wave3<DH, true, true>(a, sm, s);
+  else if (bias) launch_bwd_wave3<DH, true, false>(a, sm, s);
+  else if (drop) launch_bwd_wave3<DH, false, true>(a, sm, s);
+  else launch_bwd_wave3<DH, false, false>(a, sm, s);
 }
 
 template <int DH, bool BIAS, bool DROP>
@@ -391,7 +594,9 @@ extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const 
   return check_launch("attn_fwd");
 }
 
-extern "C" int ctr_attn_bwd_nparts(int H, int K, int D) { return H / bwd_group(H, K, D / H); }
+extern "C" int ctr_attn_bwd_nparts(int H, int K, int D) {
+  return H / (bwd_use_wave(K, D / H) ? bwd_wave_group(H) : bwd_group(H, K, D / H));
+}
 
 extern "C" int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D,
                             const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
@@ -402,16 +607,26 @@ extern "C" int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, i
   CTR_REQUIRE(D % H == 0 && (dh == 2 || dh == 4 || dh == 8 || dh == 16), "head dim must be 2, 4, 8 or 16");
   CTR_REQUIRE(K <= 256, "K > 256");
   CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
-  const int G = bwd_group(H, K, dh);
+  const bool wave = bwd_use_wave(K, dh);
+  const int G = wave ? bwd_wave_group(H) : bwd_group(H, K, dh);
   AttnArgs a{};
   a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = G;
   a.relmean = relmean; a.tk = tk; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = const_cast<uint32_t*>(mask); a.KW = (K + 31) / 32;
   a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow); a.lrow = const_cast<float*>(lrow);
   a.dO = dO; a.dqkv = dqkv; a.drel_part = drel_part;
-  const size_t sm = bwd_lds(G, K, dh, tk);
+  const size_t sm = wave ? bwd_wave_lds(G, K, dh, tk) : bwd_lds(G, K, dh, tk);
   CTR_REQUIRE(sm <= 160 * 1024, "attention backward tile exceeds LDS");
   hipStream_t s = (hipStream_t)stream;
+  if (wave) {
+    CTR_REQUIRE(sm <= 64 * 1024, "attention backward (wave form) tile exceeds 64 KB");
+    switch (dh) {
+      case 2: launch_bwd_wave<2>(a, sm, s); break;
+      case 4: launch_bwd_wave<4>(a, sm, s); break;
+      default: launch_bwd_wave<8>(a, sm, s); break;
+    }
+    return check_launch("attn_bwd");
+  }
   switch (dh) {
     case 2: launch_bwd<2>(a, sm, s); break;
     case 4: launch_bwd<4>(a, sm, s); break;
