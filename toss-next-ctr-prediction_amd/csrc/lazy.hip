@@ -410,8 +410,13 @@ __device__ __forceinline__ void pair_replay(PairRow<EPL>& r, bool has_e, const O
   (void)has_e;
 }
 
-// forward read of tokens X[0, n): a wave per token; lane 0 claims the att row's tick with a CAS (a token
-// read many times in the batch is caught up once) and the rep row's tick follows it
+// The pair kernels take NT tokens per wave iteration: the NT claims / tick reads go out together (lane u
+// handles token u), then all NT rows' loads, then the NT replays, then the stores -- one memory latency per
+// NT rows instead of one per row (a wave per token was latency-bound on the CAS -> load -> store chain).
+constexpr int PAIR_NT = 4;
+
+// forward read of tokens X[0, n): lane u of a wave claims token u's att-row tick with a CAS (a token read
+// many times in the batch is caught up once) and the rep row's tick follows it
 template <int EPL>
 __global__ __launch_bounds__(256) void lazy_touch_pair_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
                                                               const int32_t* __restrict__ X, long n, float* P,
@@ -420,23 +425,39 @@ __global__ __launch_bounds__(256) void lazy_touch_pair_kernel(const ctr_lazy_tab
   const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
   const long wave = (blockIdx.x * 256L + threadIdx.x) >> 6, nwaves = (long)gridDim.x * 4;
   const int lane = threadIdx.x & 63;
-  for (long t = wave; t < n; t += nwaves) {
-    const long row = X[t];
-    if (row < 0 || row >= ta.rows) continue;
-    int s = tick, win = 0;
-    if (lane == 0) {
-      int* lp = ta.last + row;
-      s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (s < tick) win = atomicCAS(lp, s, tick) == s;
+  for (long t0 = wave * PAIR_NT; t0 < n; t0 += nwaves * PAIR_NT) {
+    int my_row = -1, my_s = tick;
+    if (lane < PAIR_NT && t0 + lane < n) {
+      const long row = X[t0 + lane];
+      // a token equal to its predecessor's is that position's job: runs of one token (the left padding of
+      // every sequence: ~half the batch is the pad row) claim once instead of hammering one tick word
+      const bool dup = t0 + lane > 0 && X[t0 + lane - 1] == row;
+      if (!dup && row >= 0 && row < ta.rows) {
+        int* lp = ta.last + row;
+        const int s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s < tick && atomicCAS(lp, s, tick) == s) {
+          my_row = (int)row;
+          my_s = s;
+        }
+      }
     }
-    win = __builtin_amdgcn_readfirstlane(win);
-    if (!win) continue;
-    s = __builtin_amdgcn_readfirstlane(s);
-    PairRow<EPL> r;
-    pair_load(r, ta, tb, row, P, M, V, E);
-    pair_replay(r, E != nullptr, hist, s, tick, nullptr, 0.f);
-    pair_store(r, P, M, V, E);
-    if (lane == 0) tb.last[row] = tick;
+    int rows[PAIR_NT], ss[PAIR_NT];
+    PairRow<EPL> r[PAIR_NT];
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u) {
+      rows[u] = __builtin_amdgcn_readlane(my_row, u);
+      ss[u] = __builtin_amdgcn_readlane(my_s, u);
+      if (rows[u] >= 0) pair_load(r[u], ta, tb, rows[u], P, M, V, E);
+    }
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u)
+      if (rows[u] >= 0) pair_replay(r[u], E != nullptr, hist, ss[u], tick, nullptr, 0.f);
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u)
+      if (rows[u] >= 0) {
+        pair_store(r[u], P, M, V, E);
+        if (lane == 0) tb.last[rows[u]] = tick;
+      }
   }
 }
 
@@ -455,25 +476,44 @@ __global__ __launch_bounds__(256) void lazy_update_pair_kernel(const ctr_lazy_ta
   const int lane = threadIdx.x & 63, W = ta.width;
   const long nu = min(cap, (long)*n_uniq);
   const float coef = coef_ptr ? *coef_ptr : 1.0f;
-  for (long it = wave; it < nu; it += nwaves) {
-    const uint32_t key = keys[it];
-    if (key == LAZY_INVALID || (long)(key - ta.key_base) >= ta.rows) continue;
-    const long row = (long)(key - ta.key_base);
-    const int s = __builtin_amdgcn_readfirstlane(ta.last[row]);
-    PairRow<EPL> r;
-    pair_load(r, ta, tb, row, P, M, V, E);
-    float g[EPL];
+  for (long it0 = wave * PAIR_NT; it0 < nu; it0 += nwaves * PAIR_NT) {
+    int my_row = -1, my_s = 0;
+    if (lane < PAIR_NT && it0 + lane < nu) {
+      const uint32_t key = keys[it0 + lane];
+      if (key != LAZY_INVALID && (long)(key - ta.key_base) < ta.rows) {
+        my_row = (int)(key - ta.key_base);
+        my_s = ta.last[my_row];
+      }
+    }
+    int rows[PAIR_NT], ss[PAIR_NT];
+    PairRow<EPL> r[PAIR_NT];
+    float g[PAIR_NT][EPL];
 #pragma unroll
-    for (int q = 0; q < EPL; ++q) {
-      const int el = lane + 64 * q;
-      g[q] = el < W ? Ga[it * (long)g_ld + el] : el < 2 * W ? Gb[it * (long)g_ld + (el - W)] : 0.f;
+    for (int u = 0; u < PAIR_NT; ++u) {
+      rows[u] = __builtin_amdgcn_readlane(my_row, u);
+      ss[u] = __builtin_amdgcn_readlane(my_s, u);
+      if (rows[u] >= 0) {
+        pair_load(r[u], ta, tb, rows[u], P, M, V, E);
+        const long it = it0 + u;
+#pragma unroll
+        for (int q = 0; q < EPL; ++q) {
+          const int el = lane + 64 * q;
+          g[u][q] = el < W ? Ga[it * (long)g_ld + el] : el < 2 * W ? Gb[it * (long)g_ld + (el - W)] : 0.f;
+        }
+      }
     }
-    pair_replay(r, E != nullptr, hist, s, tick - 1, g, coef);
-    pair_store(r, P, M, V, E);
-    if (lane == 0) {
-      ta.last[row] = tick;
-      tb.last[row] = tick;
-    }
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u)
+      if (rows[u] >= 0) pair_replay(r[u], E != nullptr, hist, ss[u], tick - 1, g[u], coef);
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u)
+      if (rows[u] >= 0) {
+        pair_store(r[u], P, M, V, E);
+        if (lane == 0) {
+          ta.last[rows[u]] = tick;
+          tb.last[rows[u]] = tick;
+        }
+      }
   }
 }
 
@@ -485,17 +525,28 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_kernel(const ctr_lazy_tab
   const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
   const long wave = (blockIdx.x * 256L + threadIdx.x) >> 6, nwaves = (long)gridDim.x * 4;
   const int lane = threadIdx.x & 63;
-  for (long row = wave; row < ta.rows; row += nwaves) {
-    const int s = __builtin_amdgcn_readfirstlane(ta.last[row]);
-    if (s >= tick) continue;
-    PairRow<EPL> r;
-    pair_load(r, ta, tb, row, P, M, V, E);
-    pair_replay(r, E != nullptr, hist, s, tick, nullptr, 0.f);
-    pair_store(r, P, M, V, E);
-    if (lane == 0) {
-      ta.last[row] = tick;
-      tb.last[row] = tick;
+  for (long r0 = wave * PAIR_NT; r0 < ta.rows; r0 += nwaves * PAIR_NT) {
+    int my_s = tick;
+    if (lane < PAIR_NT && r0 + lane < ta.rows) my_s = ta.last[r0 + lane];
+    int ss[PAIR_NT];
+    PairRow<EPL> r[PAIR_NT];
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u) {
+      ss[u] = __builtin_amdgcn_readlane(my_s, u);
+      if (ss[u] < tick) pair_load(r[u], ta, tb, r0 + u, P, M, V, E);
     }
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u)
+      if (ss[u] < tick) pair_replay(r[u], E != nullptr, hist, ss[u], tick, nullptr, 0.f);
+#pragma unroll
+    for (int u = 0; u < PAIR_NT; ++u)
+      if (ss[u] < tick) {
+        pair_store(r[u], P, M, V, E);
+        if (lane == 0) {
+          ta.last[r0 + u] = tick;
+          tb.last[r0 + u] = tick;
+        }
+      }
   }
 }
 
@@ -543,7 +594,9 @@ extern "C" int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_ro
   return check_launch("lazy_flush");
 }
 
-static int pair_grid(long n) { return (int)std::max<long>(1, std::min<long>((n + 3) / 4, 256L * 16)); }
+static int pair_grid(long n) {   // 4 waves per block, PAIR_NT rows per wave iteration
+  return (int)std::max<long>(1, std::min<long>((n + 4 * PAIR_NT - 1) / (4 * PAIR_NT), 256L * 16));
+}
 
 static bool pair_ok(const ctr_lazy_tab_t* tabs_host_view) { return tabs_host_view != nullptr; }
 
