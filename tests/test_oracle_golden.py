@@ -31,8 +31,11 @@ def test_oracle_matches_reference(case):
         assert np.array_equal(rec["topk_idx"].numpy(), fx.z[f"out{t}/topk_idx"])
         fx.check(f"out{t}/topk_vals", rec["topk_vals"], 1e-6, 1e-5)
         if t == 0:
+            # north-star tolerance (1e-4 rtol): the fixtures come from one host's CPU kernels, and the
+            # reduction order of torch's CPU GEMMs differs between CPU models (1.4e-5 seen on the
+            # cfg2-width DARE rep-table grad on a host other than the one that wrote the fixtures)
             for k, g in grads.items():
-                fx.check(f"grad0/{k}", g, 1e-5, 1e-8)
+                fx.check(f"grad0/{k}", g, 1e-4, 1e-8)
     # AdamW turns gradients that are pure rounding noise (e.g. the MHA key bias: softmax is shift-invariant,
     # so its exact gradient is 0) into +-lr-sized steps; elementwise tolerance is therefore one Adam step.
     adam_step = 2.0 * max(m["lrs"])
