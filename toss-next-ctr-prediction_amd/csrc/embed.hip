@@ -192,51 +192,86 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_rows(const int* __restrict_
 
 // dP_c[d,k] = sum_b dcat[b,c,d] * T_c[row_b, k]   -- block (c, chunk) partials over a row chunk.
 // The chunk's gathered table rows and dcat rows are staged in LDS 64 samples at a time (the gather is
-// the latency-bound part), then each thread reduces its (d, k) outputs from LDS.
+// the latency-bound part).  Each thread owns a 4x4 (d, k) register tile and reads its operands as two
+// 16-byte LDS loads per row; when D x dc has fewer than 256/4x4 tiles the block's threads split the rows
+// into groups (row i -> group i % ngrp), whose tiles are summed in fixed group order at the end.
 constexpr int CP_SUB = 64;
+constexpr int CP_LD = 68;        // LDS row stride (floats): 16-byte aligned, rows offset by 4 banks
 
 __global__ __launch_bounds__(256) void cat_embed_bwd_proj_partial(const int* __restrict__ xcat, int B, int Fc,
                                                                   const float* __restrict__ arena, CatMeta cm,
                                                                   int D, const float* __restrict__ dcat,
                                                                   int rows_per_chunk, float* __restrict__ part) {
-  __shared__ float sT[CP_SUB][65];
-  __shared__ float sG[CP_SUB][65];
+  __shared__ __attribute__((aligned(16))) float sT[CP_SUB * CP_LD];
+  __shared__ __attribute__((aligned(16))) float sG[CP_SUB * CP_LD];
   const int c = blockIdx.x, chunk = blockIdx.y;
   const int dc = cm.dims[c];
   const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
   const float* T = cm.tabs + cm.tab_off[c];
   const long tld = cm.row_ld ? cm.row_ld : dc;
   float* out = part + ((long)chunk * Fc + c) * (64 * 64);
-  const int nq = D * dc;                 // <= 4096 outputs: up to 16 per thread
-  float acc[16];
+  const int nd4 = (D + 3) >> 2, nk4 = (dc + 3) >> 2;
+  const int ntile = nd4 * nk4;                       // <= 256
+  const int ngrp = 256 / ntile;
+  const int tile = threadIdx.x % ntile, grp = threadIdx.x / ntile;
+  const bool active = grp < ngrp;
+  const int d0 = (tile / nk4) * 4, k0 = (tile % nk4) * 4;
+  float acc[4][4];
 #pragma unroll
-  for (int u = 0; u < 16; ++u) acc[u] = 0.f;
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   for (int s0 = b0; s0 < b1; s0 += CP_SUB) {
     const int ns = min(CP_SUB, b1 - s0);
     __syncthreads();
-    for (int e = threadIdx.x; e < ns * 64; e += 256) {
+    for (int e = threadIdx.x; e < CP_SUB * 64; e += 256) {
       const int i = e >> 6, k = e & 63;
-      const long b = s0 + i;
-      const long row = xcat[b * Fc + c];
-      sT[i][k] = k < dc ? T[row * tld + k] : 0.f;
-      sG[i][k] = k < D ? dcat[(b * Fc + c) * D + k] : 0.f;
+      float tv = 0.f, gv = 0.f;
+      if (i < ns) {
+        const long b = s0 + i;
+        if (k < dc) tv = T[(long)xcat[b * Fc + c] * tld + k];
+        if (k < D) gv = dcat[(b * Fc + c) * D + k];
+      }
+      sT[i * CP_LD + k] = tv;
+      sG[i * CP_LD + k] = gv;
     }
     __syncthreads();
+    if (active) {
+      for (int i = grp; i < ns; i += ngrp) {
+        const float4 g = *reinterpret_cast<const float4*>(&sG[i * CP_LD + d0]);
+        const float4 tv = *reinterpret_cast<const float4*>(&sT[i * CP_LD + k0]);
+        const float gg[4] = {g.x, g.y, g.z, g.w};
+        const float tt[4] = {tv.x, tv.y, tv.z, tv.w};
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int q = threadIdx.x + 256 * u;
-      if (q < nq) {
-        const int d = q / dc, k = q - d * dc;
-        float a = acc[u];
-        for (int i = 0; i < ns; ++i) a = fmaf(sG[i][d], sT[i][k], a);
-        acc[u] = a;
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) acc[u][v] = fmaf(gg[u], tt[v], acc[u][v]);
       }
     }
   }
+  // fixed-order sum over the row groups (through LDS), then the (d, k) tile store
+  __syncthreads();
+  float* red = sT;                                   // ngrp * ntile * 16 <= 4096 floats
+  if (active && grp > 0) {
 #pragma unroll
-  for (int u = 0; u < 16; ++u) {
-    const int q = threadIdx.x + 256 * u;
-    if (q < nq) out[q] = acc[u];
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[((grp * ntile) + tile) * 16 + u * 4 + v] = acc[u][v];
+  }
+  __syncthreads();
+  if (active && grp == 0) {
+    for (int g2 = 1; g2 < ngrp; ++g2)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] += red[((g2 * ntile) + tile) * 16 + u * 4 + v];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int d = d0 + u, k = k0 + v;
+        if (d < D && k < dc) out[d * dc + k] = acc[u][v];
+      }
   }
 }
 
@@ -267,38 +302,64 @@ struct CtxArgs {
   float* query;                               // (B, D)
 };
 
-__global__ __launch_bounds__(64) void context_fwd_kernel(CtxArgs a) {
-  __shared__ float sctx[3 * 64];
-  const int b = blockIdx.x, d = threadIdx.x;
+// One wave per sample (4 per workgroup): lane = (part pp = lane / D, dim d = lane % D), P = 64 / D parts;
+// part pp sums features pp, pp + P, ... and the parts combine in fixed order through the wave's LDS row.
+// Then the ctx_mlp row and the query (lane = d).
+__device__ __forceinline__ float ctx_wave_mean(const float* __restrict__ x, int F, int D, float* sp) {
+  const int lane = threadIdx.x & 63, P = 64 / D;
+  const int d = lane % D, pp = lane / D;
+  float s0 = 0.f, s1 = 0.f;
+  if (pp < P) {
+    int f = pp;
+    for (; f + P < F; f += 2 * P) {
+      s0 += x[(long)f * D + d];
+      s1 += x[(long)(f + P) * D + d];
+    }
+    if (f < F) s0 += x[(long)f * D + d];
+  }
+  sp[lane] = s0 + s1;
+  __builtin_amdgcn_wave_barrier();
+  float m = 0.f;
+  if (lane < D) {
+    for (int q = 0; q < P; ++q) m += sp[q * D + lane];
+    m = m / (float)F;
+  }
+  __builtin_amdgcn_wave_barrier();
+  return m;
+}
+
+__global__ __launch_bounds__(256) void context_fwd_kernel(CtxArgs a) {
+  __shared__ float sctx_all[4][3 * 64];
+  __shared__ float sp_all[4][64];
+  const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + w;
+  if (b >= a.B) return;
+  float* sctx = sctx_all[w];
+  float* sp = sp_all[w];
   const int D = a.D;
   int nctx = 0;
-  if (d < D) {
-    if (a.Fn > 0) {
-      float s = 0.f;
-#pragma unroll 8
-      for (int f = 0; f < a.Fn; ++f) s += a.num_e[(long)b * a.num_ld + (long)f * D + d];
-      sctx[nctx * D + d] = s / (float)a.Fn;
-    }
+  if (a.Fn > 0) {
+    const float m = ctx_wave_mean(a.num_e + (long)b * a.num_ld, a.Fn, D, sp);
+    if (t < D) sctx[nctx * D + t] = m;
+    ++nctx;
   }
-  if (a.Fn > 0) ++nctx;
-  if (d < D && a.Fm > 0) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int f = 0; f < a.Fm; ++f) s += a.mask_e[(long)b * a.mask_ld + (long)f * D + d];
-    sctx[nctx * D + d] = s / (float)a.Fm;
+  if (a.Fm > 0) {
+    const float m = ctx_wave_mean(a.mask_e + (long)b * a.mask_ld, a.Fm, D, sp);
+    if (t < D) sctx[nctx * D + t] = m;
+    ++nctx;
   }
-  if (a.Fm > 0) ++nctx;
-  if (d < D) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int c = 0; c < a.Fc; ++c) s += a.cat_e[((long)b * a.Fc + c) * D + d];
-    sctx[nctx * D + d] = a.Fc > 0 ? s / (float)a.Fc : 0.f;
+  if (a.Fc > 0) {
+    const float m = ctx_wave_mean(a.cat_e + (long)b * a.Fc * D, a.Fc, D, sp);
+    if (t < D) sctx[nctx * D + t] = m;
+  } else if (t < D) {
+    sctx[nctx * D + t] = 0.f;
   }
   ++nctx;
-  __syncthreads();
+  __builtin_amdgcn_wave_barrier();
   const int W = nctx * D;
-  if (d < D) {
-    for (int j = d; j < W; j += D) a.ctx[(long)b * W + j] = sctx[j];
+  for (int j = t; j < W; j += 64) a.ctx[(long)b * W + j] = sctx[j];
+  if (t < D) {
+    const int d = t;
     float q;
     float h = 0.f;
     if (a.mode != 0) {
@@ -331,64 +392,84 @@ struct CtxBwdArgs {
   float* dpre;              // (B, D) grad of ctx_mlp pre-activation (for dWc, dbc); nullable in S1
 };
 
-__global__ __launch_bounds__(64) void context_bwd_kernel(CtxBwdArgs a) {
+// One 256-thread block per sample: the small dpre / dctx products first, then the three per-feature
+// broadcasts (dnum += g_num[d], dmask += g_mask[d], dcat = ...) as flat element loops over the sample's
+// contiguous F*D slices, so every wave instruction moves 256 contiguous bytes (the earlier one-wave form
+// left half of its lanes idle at D = 32 and walked F serially).
+constexpr int CTXB_T = 256;
+
+__global__ __launch_bounds__(CTXB_T) void context_bwd_kernel(CtxBwdArgs a) {
   __shared__ float sdp[64];
   __shared__ float sdctx[3 * 64];
+  __shared__ float sg[3][64];        // per-slot broadcast grads: num / Fn, mask / Fm, cat / Fc
+  __shared__ float sq[64];           // the query's grad on the query cat slot
   const CtxArgs& f = a.f;
-  const int b = blockIdx.x, d = threadIdx.x, D = f.D;
+  const int b = blockIdx.x, t = threadIdx.x, D = f.D;
   const int nctx = (f.Fn > 0) + (f.Fm > 0) + 1;
   const int W = nctx * D;
-  float dqv = d < D ? a.dquery[(long)b * D + d] : 0.f;
-  float dh = 0.f;
-  if (d < D && f.mode != 0) {
-    dh = f.mode == 2 ? 0.5f * dqv : dqv;
-    dh = f.hq[(long)b * D + d] > 0.f ? dh : 0.f;
-    if (a.dpre) a.dpre[(long)b * D + d] = dh;
+  if (t < 64) {
+    float dqv = t < D ? a.dquery[(long)b * D + t] : 0.f;
+    float dh = 0.f;
+    if (t < D && f.mode != 0) {
+      dh = f.mode == 2 ? 0.5f * dqv : dqv;
+      dh = f.hq[(long)b * D + t] > 0.f ? dh : 0.f;
+      if (a.dpre) a.dpre[(long)b * D + t] = dh;
+    }
+    sdp[t] = dh;
+    sq[t] = f.mode == 1 ? 0.f : (f.mode == 2 ? 0.5f * dqv : dqv);
   }
-  if (d < 64) sdp[d] = dh;
   __syncthreads();
-  // dctx[j] = sum_d dpre[d] * Wc[d, j]
-  for (int j = d; j < W; j += 64) {
+  // dctx[j] = sum_d dpre[d] * Wc[d, j]   (W <= 192 < 256)
+  if (t < W) {
     float acc = 0.f;
     if (f.mode != 0)
 #pragma unroll 8
-      for (int i = 0; i < D; ++i) acc = fmaf(sdp[i], f.Wc[(long)i * W + j], acc);
-    sdctx[j] = acc;
+      for (int i = 0; i < D; ++i) acc = fmaf(sdp[i], f.Wc[(long)i * W + t], acc);
+    sdctx[t] = acc;
   }
   __syncthreads();
-  if (d >= D) return;
-  int slot = 0;
-  const int fcbase = 1;  // fc layout: [u, num_mean?, mask_mean?, cat_0.. cat_{Fc-1}]
-  int fcslot = fcbase;
+  // fc layout: [u, num_mean?, mask_mean?, cat_0 .. cat_{Fc-1}]
+  if (t < D) {
+    int slot = 0, fcslot = 1;
+    if (f.Fn > 0) {
+      float g = sdctx[slot * D + t];
+      if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fcslot * D + t];
+      sg[0][t] = g / (float)f.Fn;
+      ++slot;
+      ++fcslot;
+    }
+    if (f.Fm > 0) {
+      float g = sdctx[slot * D + t];
+      if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fcslot * D + t];
+      sg[1][t] = g / (float)f.Fm;
+      ++slot;
+    }
+    sg[2][t] = f.Fc > 0 ? sdctx[slot * D + t] / (float)f.Fc : 0.f;
+  }
+  __syncthreads();
   if (f.Fn > 0) {
-    float g = sdctx[slot * D + d];
-    if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fcslot * D + d];
-    g = g / (float)f.Fn;
-#pragma unroll 8
-    for (int k = 0; k < f.Fn; ++k) a.dnum[(long)b * f.num_ld + (long)k * D + d] += g;
-    ++slot;
-    ++fcslot;
+    float* dn = a.dnum + (long)b * f.num_ld;
+    const int n = f.Fn * D;
+    for (int e = t; e < n; e += CTXB_T) dn[e] += sg[0][e % D];
   }
   if (f.Fm > 0) {
-    float g = sdctx[slot * D + d];
-    if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fcslot * D + d];
-    g = g / (float)f.Fm;
-#pragma unroll 8
-    for (int k = 0; k < f.Fm; ++k) a.dmask[(long)b * f.mask_ld + (long)k * D + d] += g;
-    ++slot;
-    ++fcslot;
+    float* dm = a.dmask + (long)b * f.mask_ld;
+    const int n = f.Fm * D;
+    for (int e = t; e < n; e += CTXB_T) dm[e] += sg[1][e % D];
   }
-  const float gc = f.Fc > 0 ? sdctx[slot * D + d] / (float)f.Fc : 0.f;
-  for (int c = 0; c < f.Fc; ++c) {
-    const long q = ((long)b * f.Fc + c) * D + d;
+  const int fc0 = 1 + (f.Fn > 0) + (f.Fm > 0);
+  const int n = f.Fc * D;
+  for (int e = t; e < n; e += CTXB_T) {
+    const int c = e / D, d = e - c * D;
+    const long q = (long)b * n + e;
     float g = 0.f;
     if (a.dxf_cat) {
-      const float gx = a.dxf_cat[(long)b * a.dxf_ld + (long)c * D + d];
+      const float gx = a.dxf_cat[(long)b * a.dxf_ld + e];
       g = a.emb_drop.thresh ? (drop_keep(a.emb_drop, (uint32_t)q) ? gx * a.emb_drop.scale : 0.f) : gx;
     }
-    if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)(fcslot + c) * D + d];
-    if (c == f.qi && f.mode != 1) g += f.mode == 2 ? 0.5f * dqv : dqv;
-    g += gc;
+    if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fc0 * D + e];
+    if (c == f.qi) g += sq[d];
+    g += sg[2][d];
     a.dcat[q] = g;
   }
 }
@@ -482,7 +563,7 @@ extern "C" int ctr_context_fwd(const float* num_e, long num_ld, int Fn, const fl
   if (B == 0) return 0;
   CTR_REQUIRE(D <= 64, "D > 64");
   CtxArgs a{num_e, num_ld, Fn, mask_e, mask_ld, Fm, cat_e, Fc, D, B, mode, qi, Wc, bc, ctx, hq, query};
-  context_fwd_kernel<<<B, 64, 0, (hipStream_t)stream>>>(a);
+  context_fwd_kernel<<<cdiv(B, 4), 256, 0, (hipStream_t)stream>>>(a);
   return check_launch("context_fwd");
 }
 
@@ -505,6 +586,7 @@ extern "C" int ctr_context_bwd(const float* num_e, long num_ld, int Fn, const fl
   a.dmask = dmask;
   a.dcat = dcat;
   a.dpre = dpre;
-  context_bwd_kernel<<<B, 64, 0, (hipStream_t)stream>>>(a);
+  CTR_REQUIRE(D <= 64, "D > 64");
+  context_bwd_kernel<<<B, CTXB_T, 0, (hipStream_t)stream>>>(a);
   return check_launch("context_bwd");
 }

@@ -12,8 +12,8 @@
 // stepping the row densely every tick (tests/test_gpu_lazy.py checks that bitwise).
 //
 // Work mapping: a group of lg lanes per row; lane l holds elements l, l+lg, ... (<= 8 per lane, rows
-// are <= 64 wide) in registers across the whole replay, so the history entry of a tick is loaded once
-// per lane and the row's p, m, v, ema are read and written once.
+// are <= 64 wide) in registers across the whole replay, the tick loop wave-uniform (one scalar load of
+// a tick's history entry per wave), and the row's p, m, v, ema read and written once.
 #include "adam.h"
 #include "common.h"
 #include "ctr_hip.h"
@@ -22,41 +22,37 @@ namespace ctr {
 
 constexpr int LQ = 8;           // row elements held per lane (rows are <= 64 wide)
 constexpr int LG = 8;           // lanes per row in touch / update (any table width)
-constexpr int HWIN = 256;       // flush: the last HWIN history entries are staged in LDS
 constexpr int FLUSH_MAXTABS = 64;
 constexpr uint32_t LAZY_INVALID = 0xFFFFFFFFu;
 
 __global__ void opt_hist_record_kernel(OptScalars* hist, int tick, OptScalars s) { hist[tick] = s; }
 
-// History lookup: entries [lo, ..] from LDS when staged, older ones from global memory.
-struct HistView {
-  const OptScalars* g;
-  const OptScalars* lds;
-  int lo;
-  __device__ __forceinline__ OptScalars operator[](int k) const { return (lds && k >= lo) ? lds[k - lo] : g[k]; }
-};
-
-// Brings one row from tick s to tick t_idle with grad 0, then (grow != null) applies tick t_idle+1 with
-// grad grow*coef.  The row is spread over lg lanes.  Element of register slot q in lane l:
-//   strided (any width):          j = l + lg*q, q < nq
-//   contiguous (width % 8 == 0):  j = 8l + q   -- two 16-byte loads / stores per array per lane
-// A row whose moments are all zero (never stepped with a non-zero grad) stays zero under idle ticks:
-// only the decay multiply and the EMA remain.  With m == v == 0, adam_elem(g = 0) gives m = v = +0,
-// denom = eps and p = fmaf(-step, +0, p * decay) == p * decay: bit for bit the same.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Brings rows from their last tick s to tick t_idle with grad 0, then (grow != null) applies tick
+// t_idle+1 with grad grow*coef.  A row is spread over lg lanes.  Element of register slot q in lane l:
+//   strided (any width):          j = l + lg*q, q < nq
+//   contiguous (width % 8 == 0):  j = 8l + q   -- two 16-byte loads / stores per array per lane
+// Every lane of the wave takes part (dead lanes: live = false) and the tick loop runs over the
+// wave-uniform range (min over the wave's rows of s, t_idle], each tick's scalars one scalar load; a lane
+// applies tick k only when k > its own s (exec-masked).  (A per-lane form that walked each row's own
+// range with a per-lane history load every tick was bound on that load, and a wave holding both
+// zero-moment and stepped rows ran both loops.)
+// A row whose moments are all zero (never stepped with a non-zero grad) stays zero under idle ticks:
+// only the decay multiply and the EMA remain.  With m == v == 0, adam_elem(g = 0) gives m = v = +0,
+// denom = eps and p = fmaf(-step, +0, p * decay) == p * decay: bit for bit the same -- so a wave with
+// any stepped row runs the full idle-tick arithmetic on all its rows, and an all-zero wave the short form.
 template <bool VEC>
-__device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __restrict__ m_row,
-                                           float* __restrict__ v_row, float* __restrict__ e_row, int width, int l,
-                                           int lg, int nq, const HistView& hv, int s, int t_idle,
-                                           const float* __restrict__ grow, float coef) {
+__device__ __forceinline__ void replay_rows_wave(float* __restrict__ p_row, float* __restrict__ m_row,
+                                                 float* __restrict__ v_row, float* __restrict__ e_row, int width,
+                                                 int l, int lg, int nq, bool live, int s,
+                                                 const OptScalars* __restrict__ hist, int t_idle,
+                                                 const float* __restrict__ grow = nullptr, float coef = 1.0f) {
   float p[LQ], m[LQ], v[LQ], e[LQ];
-  const bool vlane = VEC && 8 * l < width;
-  auto elem = [&](int q) { return VEC ? 8 * l + q : l + lg * q; };
-  auto live = [&](int q) { return VEC ? vlane : (q < nq && l + lg * q < width); };
-  if (VEC) {
+  const bool vlane = live && (!VEC || 8 * l < width);
 #pragma unroll
-    for (int q = 0; q < LQ; ++q) p[q] = m[q] = v[q] = e[q] = 0.0f;
+  for (int q = 0; q < LQ; ++q) p[q] = m[q] = v[q] = e[q] = 0.0f;
+  if (VEC) {
     if (vlane) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -73,11 +69,10 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
       }
     }
     nq = LQ;
-  } else {
+  } else if (live) {
 #pragma unroll
     for (int q = 0; q < LQ; ++q) {
       const int j = l + lg * q;
-      p[q] = m[q] = v[q] = e[q] = 0.0f;
       if (q < nq && j < width) {
         p[q] = p_row[j];
         m[q] = m_row[j];
@@ -89,20 +84,31 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
   bool zero = true;
 #pragma unroll
   for (int q = 0; q < LQ; ++q) zero = zero && m[q] == 0.0f && v[q] == 0.0f;
-  if (zero) {
+  const bool any_stepped = __ballot(!zero) != 0ull;
+  if (!live) s = t_idle;
+  int smin = s;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
+  smin = __builtin_amdgcn_readfirstlane(smin);
+  if (smin >= t_idle && grow == nullptr) return;
+  if (smin >= t_idle) {
+    // nothing to replay (the gradient tick below only)
+  } else if (!any_stepped) {
     bool stepped = false;
-    for (int k = s + 1; k <= t_idle; ++k) {
-      const OptScalars sc = hv[k];
-      if (sc.do_adam) {
-        stepped = true;
+    for (int k = smin + 1; k <= t_idle; ++k) {
+      const OptScalars sc = hist[k];
+      if (k > s) {
+        if (sc.do_adam) {
+          stepped = true;
 #pragma unroll
-        for (int q = 0; q < LQ; ++q)
-          if (q < nq) p[q] = p[q] * sc.decay_mul;
-      }
-      if (sc.do_ema) {
+          for (int q = 0; q < LQ; ++q)
+            if (q < nq) p[q] = p[q] * sc.decay_mul;
+        }
+        if (sc.do_ema) {
 #pragma unroll
-        for (int q = 0; q < LQ; ++q)
-          if (q < nq) ema_elem(sc, p[q], e[q]);
+          for (int q = 0; q < LQ; ++q)
+            if (q < nq) ema_elem(sc, p[q], e[q]);
+        }
       }
     }
     if (stepped) {
@@ -110,24 +116,29 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
       for (int q = 0; q < LQ; ++q) m[q] = v[q] = 0.0f;    // a dense idle tick leaves +0 moments
     }
   } else {
-    OptScalars sc = hv[s + 1 <= t_idle ? s + 1 : t_idle];
-    for (int k = s + 1; k <= t_idle; ++k) {
-      const OptScalars nx = hv[k + 1 <= t_idle ? k + 1 : t_idle];      // next tick's scalars in flight
+    for (int k = smin + 1; k <= t_idle; ++k) {
+      const OptScalars sc = hist[k];
+      if (k > s) {
 #pragma unroll
-      for (int q = 0; q < LQ; ++q) {
-        if (q < nq) {
-          if (sc.do_adam) idle_adam_elem(sc, p[q], m[q], v[q]);
-          if (sc.do_ema) ema_elem(sc, p[q], e[q]);
+        for (int q = 0; q < LQ; ++q) {
+          if (q < nq) {
+            if (sc.do_adam) idle_adam_elem(sc, p[q], m[q], v[q]);
+            if (sc.do_ema) ema_elem(sc, p[q], e[q]);
+          }
         }
       }
-      sc = nx;
     }
   }
   if (grow) {
-    const OptScalars sc = hv[t_idle + 1];
+    const OptScalars sc = hist[t_idle + 1];
 #pragma unroll
-    for (int q = 0; q < LQ; ++q)
-      if (live(q)) adam_ema_elem(sc, p[q], m[q], v[q], e[q], grow[elem(q)] * coef, sc.do_adam != 0);
+    for (int q = 0; q < LQ; ++q) {
+      const int j = VEC ? 8 * l + q : l + lg * q;
+      const bool lv = VEC ? vlane : (live && q < nq && j < width);
+      if (lv) adam_ema_elem(sc, p[q], m[q], v[q], e[q], grow[j] * coef, sc.do_adam != 0);
+    }
+  } else if (s >= t_idle) {
+    return;
   }
   if (VEC) {
     if (vlane) {
@@ -139,7 +150,7 @@ __device__ __forceinline__ void replay_row(float* __restrict__ p_row, float* __r
         if (e_row) *(f32x4*)(e_row + 8 * l + 4 * h) = f32x4{e[4 * h], e[4 * h + 1], e[4 * h + 2], e[4 * h + 3]};
       }
     }
-  } else {
+  } else if (live) {
 #pragma unroll
     for (int q = 0; q < LQ; ++q) {
       const int j = l + lg * q;
@@ -163,26 +174,12 @@ __device__ __forceinline__ RowPtrs row_ptrs(const ctr_lazy_tab_t& tb, long row, 
   return {P + o, M + o, V + o, E ? E + o : nullptr};
 }
 
-// The history entries a workgroup's rows replay, [lo, tick], are staged in LDS once per workgroup
-// (lo = 1 + the smallest last-applied tick among its rows, at most HWIN back): the replay loop then
-// reads each tick's scalars from LDS instead of a dependent global load per tick.
-__device__ __forceinline__ int stage_hist(OptScalars* hs, int* smin, const OptScalars* __restrict__ hist, int tick) {
-  __syncthreads();                       // every row's start tick is in *smin
-  const int lo = max(max(1, *smin + 1), tick - HWIN + 1);
-  for (int k = lo + (int)threadIdx.x; k <= tick; k += 256) hs[k - lo] = hist[k];
-  __syncthreads();
-  return lo;
-}
-
 // One 8-lane group per (id, table) item.  The group leader claims the row with a CAS on last[row]
 // (s -> tick); only the winner replays, so a row read many times in a batch is caught up once.
 __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
                                                          const int32_t* __restrict__ X, long nitems, int ncols,
                                                          int per_column, float* P, float* M, float* V, float* E,
                                                          const OptScalars* __restrict__ hist, int tick) {
-  __shared__ OptScalars hs[HWIN];
-  __shared__ int smin;
-  if (threadIdx.x == 0) smin = tick;
   const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
   const int l8 = threadIdx.x & (LG - 1);
   int s = tick, win = 0, ti = 0;
@@ -209,22 +206,17 @@ __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* _
       row -= (long)tabs[a].key_base;
     }
   }
-  __syncthreads();                       // smin initialised
   if (item < nitems && l8 == 0 && row >= 0 && row < tabs[ti].rows) {
     int* lp = tabs[ti].last + row;
     s = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (s < tick) win = atomicCAS(lp, s, tick) == s;
-    if (win) atomicMin(&smin, s);
   }
   const int leader = (threadIdx.x & 63) & ~(LG - 1);
   win = __shfl(win, leader);
   s = __shfl(s, leader);
-  const int lo = stage_hist(hs, &smin, hist, tick);
-  if (!win) return;
-  const ctr_lazy_tab_t tb = tabs[ti];
-  const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
-  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, hs, lo}, s, tick,
-                    nullptr, 0.0f);
+  const ctr_lazy_tab_t tb = tabs[win ? ti : 0];
+  const RowPtrs r = row_ptrs(tb, win ? row : 0, P, M, V, E);
+  replay_rows_wave<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), win != 0, s, hist, tick);
 }
 
 // One 8-lane group per compact grad slot: keys are unique, so no claim is needed.
@@ -235,9 +227,6 @@ __global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* 
                                                           const float* __restrict__ coef_ptr, float* P, float* M,
                                                           float* V, float* E, const OptScalars* __restrict__ hist,
                                                           int tick) {
-  __shared__ OptScalars hs[HWIN];
-  __shared__ int smin;
-  if (threadIdx.x == 0) smin = tick - 1;
   const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
   const int l8 = threadIdx.x & (LG - 1);
   const long nu = min(cap, (long)*n_uniq);
@@ -257,16 +246,12 @@ __global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* 
     live = row < tabs[a].rows;
     if (live) s = tabs[a].last[row];
   }
-  __syncthreads();                       // smin initialised
-  if (live && l8 == 0) atomicMin(&smin, s);
-  const int lo = stage_hist(hs, &smin, hist, tick);
-  if (!live) return;
-  const ctr_lazy_tab_t tb = tabs[a];
-  const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
+  const ctr_lazy_tab_t tb = tabs[live ? a : 0];
+  const RowPtrs r = row_ptrs(tb, live ? row : 0, P, M, V, E);
   const float coef = coef_ptr ? *coef_ptr : 1.0f;
-  replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), HistView{hist, hs, lo}, s, tick - 1,
-                    G + item * (long)g_ld, coef);
-  if (l8 == 0) tb.last[row] = tick;
+  replay_rows_wave<false>(r.p, r.m, r.v, r.e, tb.width, l8, LG, cdiv(tb.width, LG), live, s, hist, tick - 1,
+                          G + (live ? item : 0) * (long)g_ld, coef);
+  if (live && l8 == 0) tb.last[row] = tick;
 }
 
 // lanes per row for a table in the flush: enough that a lane holds <= LQ elements, as few as possible
@@ -275,16 +260,14 @@ __device__ __forceinline__ int flush_lg(int width) {
   return need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
 }
 
-// Persistent grid over (table, chunk of 256/lg rows) work items; the recent history is staged in LDS
-// once per workgroup.  Per chunk everything (table, lg, nq) is workgroup-uniform.
+// Persistent grid over (table, chunk of 256/lg rows) work items.  Per chunk everything (table, lg, nq)
+// is workgroup-uniform; every lane enters the wave replay (rows past the table or already current are
+// dead lanes), whose tick loop is wave-uniform.
 __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
                                                          float* P, float* M, float* V, float* E,
                                                          const OptScalars* __restrict__ hist, int tick) {
-  __shared__ OptScalars hs[HWIN];
   __shared__ long chunk0[FLUSH_MAXTABS + 1];
   const int tid = threadIdx.x;
-  const int lo = max(1, tick - HWIN + 1);
-  for (int k = lo + tid; k <= tick; k += 256) hs[k - lo] = hist[k];
   if (tid == 0) {
     long c = 0;
     for (int t = 0; t < ntabs; ++t) {
@@ -294,7 +277,6 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
     chunk0[ntabs] = c;
   }
   __syncthreads();
-  const HistView hv{hist, hs, lo};
   const long nchunks = chunk0[ntabs];
   for (long c = blockIdx.x; c < nchunks; c += gridDim.x) {
     int a = 0, b = ntabs;
@@ -305,16 +287,16 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
     const ctr_lazy_tab_t tb = tabs[a];
     const int lg = flush_lg(tb.width);
     const long row = (c - chunk0[a]) * (256 / lg) + tid / lg;
-    if (row >= tb.rows) continue;
-    const int s = tb.last[row];
-    if (s >= tick) continue;
+    const bool in = row < tb.rows;
+    const int s = in ? tb.last[row] : tick;
+    const bool live = in && s < tick;
     const int l = tid & (lg - 1);
-    const RowPtrs r = row_ptrs(tb, row, P, M, V, E);
+    const RowPtrs r = row_ptrs(tb, in ? row : 0, P, M, V, E);
     if ((tb.width & 7) == 0 && (tb.p_off & 3) == 0)     // block-uniform
-      replay_row<true>(r.p, r.m, r.v, r.e, tb.width, l, lg, LQ, hv, s, tick, nullptr, 0.0f);
+      replay_rows_wave<true>(r.p, r.m, r.v, r.e, tb.width, l, lg, LQ, live, s, hist, tick);
     else
-      replay_row<false>(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), hv, s, tick, nullptr, 0.0f);
-    if (l == 0) tb.last[row] = tick;
+      replay_rows_wave<false>(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), live, s, hist, tick);
+    if (live && l == 0) tb.last[row] = tick;
   }
 }
 
@@ -363,7 +345,7 @@ __device__ __forceinline__ void pair_store(const PairRow<EPL>& r, float* P, floa
 }
 
 // ticks (s, t_idle] with grad 0, then (g != null) tick t_idle + 1 with grad g[q] * coef; same
-// arithmetic as replay_row (adam.h), decided per wave (s and the zero test are wave-uniform)
+// arithmetic as replay_rows_wave (adam.h), decided per wave (s and the zero test are wave-uniform)
 template <int EPL>
 __device__ __forceinline__ void pair_replay(PairRow<EPL>& r, bool has_e, const OptScalars* __restrict__ hist, int s,
                                             int t_idle, const float* g, float coef) {

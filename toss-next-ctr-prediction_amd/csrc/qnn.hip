@@ -148,8 +148,11 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
   }
 }
 
-// One wave per sample: M = U diag(dquad) U^T (MFMA over the QR columns), w = U (dquad o S);
-// dz_f = 2 w - 2 M z_f (+ dz_add) with M's C-layout registers as the B operand (k-set {16i+4g+r}).
+// One sample per 4-wave workgroup: M = U diag(dquad) U^T (MFMA over the QR columns; the waves share its
+// 16x16 tiles via LDS) and w = U (dquad o S) (QR quarters summed in fixed wave order); then the waves take
+// every fourth 16-row F block: dz_f = 2 w - 2 M z_f (+ dz_add) with M's C-layout registers as the B
+// operand (k-set {16i+4g+r}).  (One wave per sample left only 4 waves per SIMD at B = 4096, each a long
+// serial load -> MFMA chain.)
 template <int D>
 __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restrict__ z, int B, int F,
                                                            const float* __restrict__ ucat, int QR,
@@ -160,54 +163,65 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
   constexpr int NT = D / 16;
   extern __shared__ float sU[];
   const int QRp = (QR + 15) / 16 * 16, US = QRp + 1;
-  float* sdq = sU + D * US;                      // [4 waves][QRp] dquad, then [QRp] dquad*S
+  float* dq = sU + D * US;                       // [QRp] dquad
+  float* dqs = dq + QRp;                         // [QRp] dquad * S
+  float* sM = dqs + QRp;                         // [NT*NT tiles][4][64] M (C layout)
+  float* sW = sM + NT * NT * 4 * 64;             // [4 waves][D] w partials
+  const int b = blockIdx.x;
   stage_ucat<D>(ucat, QR, QRp, sU);
-  __syncthreads();
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int b = blockIdx.x * 4 + w;
-  if (b >= B) return;
-  float* dq = sdq + w * 2 * QRp;
-  float* dqs = dq + QRp;
-  for (int q = lane; q < QRp; q += 64) {
+  for (int q = threadIdx.x; q < QRp; q += 256) {
     const float d = q < QR ? dquad[(long)b * QR + q] : 0.f;
     const float sv = q < QR ? S[(long)b * QR + q] : 0.f;
     dq[q] = d;
     dqs[q] = d * sv;
     if (q < QR) DS[(long)b * QR + q] = d * sv;
   }
-  __builtin_amdgcn_wave_barrier();
-  // M[d][e] = sum_c U[d][c] dq[c] U[e][c]
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  // M tiles (i, j) = t, t + 4, ... of this wave over the whole QR range
+  for (int t = w; t < NT * NT; t += 4) {
+    const int i = t / NT, j = t - i * NT;
+    f32x4 Mt = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < QRp; k0 += 4) {
+      const int k = k0 + g;
+      const float bi = sU[(16 * i + c) * US + k];
+      const float bj = sU[(16 * j + c) * US + k];
+      Mt = mfma4q(bi * dq[k], bj, Mt);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sM[(t * 4 + r) * 64 + lane] = Mt[r];
+  }
+  {
+    // w partial: this wave's QR quarter; lane (g, c) sums q = k0w + g, k0w + g + 4, ... for e = 16j + c
+    const int kq = QRp / 4;
+    const int k0w = w * kq, k1w = k0w + kq;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      float a = 0.f;
+      for (int q = k0w + g; q < k1w; q += 4) a = fmaf(sU[(16 * j + c) * US + q], dqs[q], a);
+      a += __shfl_xor(a, 16);
+      a += __shfl_xor(a, 32);
+      if (g == 0) sW[w * D + 16 * j + c] = a;
+    }
+  }
+  __syncthreads();
   f32x4 M[NT][NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) M[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < QRp; k0 += 4) {
-    const int k = k0 + g;
-    float av[NT], bv[NT];
+    for (int j = 0; j < NT; ++j)
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      bv[i] = sU[(16 * i + c) * US + k];
-      av[i] = bv[i] * dq[k];
-    }
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) M[i][j] = mfma4q(av[i], bv[j], M[i][j]);
-  }
-  // w[e] for e = 16j + c
+      for (int r = 0; r < 4; ++r) M[i][j][r] = sM[((i * NT + j) * 4 + r) * 64 + lane];
   float wv[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
-    float a = 0.f;
-#pragma unroll 8
-    for (int q = 0; q < QRp; ++q) a = fmaf(sU[(16 * j + c) * US + q], dqs[q], a);
-    wv[j] = 2.f * a;
+    const int e = 16 * j + c;
+    wv[j] = 2.f * (((sW[e] + sW[D + e]) + sW[2 * D + e]) + sW[3 * D + e]);
   }
   const float* zb = z + (long)b * F * D;
   const float* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
   float* ob = dz + (long)b * F * D;
-  for (int f0 = 0; f0 < F; f0 += 16) {
+  for (int f0 = 16 * w; f0 < F; f0 += 64) {
     const int fa = f0 + c;                       // A-operand row of this lane
     f32x4 acc[NT];
 #pragma unroll
@@ -400,10 +414,22 @@ extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float
                                 const float* dquad, const float* dz_add, float* dz, float* DS, void* stream) {
   CTR_REQUIRE(D == 16 || D == 32 || D == 64, "qnn gram: D must be 16, 32 or 64");
   if (B == 0) return 0;
-  const size_t sm = gram_lds(D, QR);
-  CTR_REQUIRE(sm <= 64 * 1024, "qnn gram: U exceeds LDS");
+  const int QRp = (QR + 15) / 16 * 16, NT = D / 16;
+  const size_t sm = ((size_t)D * (QRp + 1) + 2 * (size_t)QRp + (size_t)NT * NT * 4 * 64 + 4 * (size_t)D) *
+                    sizeof(float);
+  CTR_REQUIRE(sm <= 160 * 1024, "qnn gram bwd: U + M partials exceed LDS");
   hipStream_t s = (hipStream_t)stream;
-  const int blocks = cdiv(B, 4);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  const int blocks = B;
   if (D == 16) qnn_gram_bwd_kernel<16><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
   else if (D == 32) qnn_gram_bwd_kernel<32><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
   else qnn_gram_bwd_kernel<64><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
