@@ -81,4 +81,25 @@ __device__ __forceinline__ void idle_adam_elem(const OptScalars& s, float& p, fl
   p = fmaf(-s.step_size, m * __builtin_amdgcn_rcpf(denom), p);
 }
 
+// Two elements of idle_adam_elem / ema_elem at once on packed f32 pairs (v_pk_mul_f32 / v_pk_fma_f32:
+// each half is the same IEEE multiply / fused multiply-add as the scalar form, so the bits are equal);
+// the square root and reciprocal stay per element.  For the VALU-bound replay of stepped rows.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 splat2(float a) { return f32x2{a, a}; }
+
+__device__ __forceinline__ void idle_adam_pk(const OptScalars& s, f32x2& p, f32x2& m, f32x2& v) {
+  p = p * splat2(s.decay_mul);
+  m = __builtin_elementwise_fma(splat2(s.b1w), -m, m);
+  v = v * splat2(s.b2);
+  const f32x2 sq = {__builtin_amdgcn_sqrtf(v.x), __builtin_amdgcn_sqrtf(v.y)};
+  const f32x2 denom = __builtin_elementwise_fma(sq, splat2(s.rbc2), splat2(s.eps));
+  const f32x2 r = {__builtin_amdgcn_rcpf(denom.x), __builtin_amdgcn_rcpf(denom.y)};
+  p = __builtin_elementwise_fma(splat2(-s.step_size), m * r, p);
+}
+
+__device__ __forceinline__ void ema_pk(const OptScalars& s, f32x2 p, f32x2& e) {
+  e = __builtin_elementwise_fma(e, splat2(s.ema_d), splat2(s.ema_omd) * p);
+}
+
 }  // namespace ctr

@@ -29,6 +29,22 @@ __global__ void opt_hist_record_kernel(OptScalars* hist, int tick, OptScalars s)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Ticks k0..k1 of the history, four per step: the four entries' scalar loads go out together (one wait)
+// and the loop overhead is paid once per four ticks; f(sc, k) applies one tick.
+template <class F>
+__device__ __forceinline__ void for_ticks(const OptScalars* __restrict__ hist, int k0, int k1, F&& f) {
+  int k = k0;
+  for (; k + 3 <= k1; k += 4) {
+    const OptScalars* h = hist + k;
+    const OptScalars a = h[0], b = h[1], c = h[2], d = h[3];
+    f(a, k);
+    f(b, k + 1);
+    f(c, k + 2);
+    f(d, k + 3);
+  }
+  for (; k <= k1; ++k) f(hist[k], k);
+}
+
 // Brings rows from their last tick s to tick t_idle with grad 0, then (grow != null) applies tick
 // t_idle+1 with grad grow*coef.  A row is spread over lg lanes.  Element of register slot q in lane l:
 //   strided (any width):          j = l + lg*q, q < nq
@@ -95,8 +111,7 @@ __device__ __forceinline__ void replay_rows_wave(float* __restrict__ p_row, floa
     // nothing to replay (the gradient tick below only)
   } else if (!any_stepped) {
     bool stepped = false;
-    for (int k = smin + 1; k <= t_idle; ++k) {
-      const OptScalars sc = hist[k];
+    for_ticks(hist, smin + 1, t_idle, [&](const OptScalars& sc, int k) {
       if (k > s) {
         if (sc.do_adam) {
           stepped = true;
@@ -110,23 +125,42 @@ __device__ __forceinline__ void replay_rows_wave(float* __restrict__ p_row, floa
             if (q < nq) ema_elem(sc, p[q], e[q]);
         }
       }
-    }
+    });
     if (stepped) {
 #pragma unroll
       for (int q = 0; q < LQ; ++q) m[q] = v[q] = 0.0f;    // a dense idle tick leaves +0 moments
     }
   } else {
-    for (int k = smin + 1; k <= t_idle; ++k) {
-      const OptScalars sc = hist[k];
+    // element pairs (q, q+1) in packed f32 (slots past nq hold zeros and are never stored)
+    f32x2 pp[LQ / 2], mm[LQ / 2], vv[LQ / 2], ee[LQ / 2];
+#pragma unroll
+    for (int h = 0; h < LQ / 2; ++h) {
+      pp[h] = f32x2{p[2 * h], p[2 * h + 1]};
+      mm[h] = f32x2{m[2 * h], m[2 * h + 1]};
+      vv[h] = f32x2{v[2 * h], v[2 * h + 1]};
+      ee[h] = f32x2{e[2 * h], e[2 * h + 1]};
+    }
+    for_ticks(hist, smin + 1, t_idle, [&](const OptScalars& sc, int k) {
       if (k > s) {
 #pragma unroll
-        for (int q = 0; q < LQ; ++q) {
-          if (q < nq) {
-            if (sc.do_adam) idle_adam_elem(sc, p[q], m[q], v[q]);
-            if (sc.do_ema) ema_elem(sc, p[q], e[q]);
+        for (int h = 0; h < LQ / 2; ++h) {
+          if (2 * h < nq) {
+            if (sc.do_adam) idle_adam_pk(sc, pp[h], mm[h], vv[h]);
+            if (sc.do_ema) ema_pk(sc, pp[h], ee[h]);
           }
         }
       }
+    });
+#pragma unroll
+    for (int h = 0; h < LQ / 2; ++h) {
+      p[2 * h] = pp[h].x;
+      p[2 * h + 1] = pp[h].y;
+      m[2 * h] = mm[h].x;
+      m[2 * h + 1] = mm[h].y;
+      v[2 * h] = vv[h].x;
+      v[2 * h + 1] = vv[h].y;
+      e[2 * h] = ee[h].x;
+      e[2 * h + 1] = ee[h].y;
     }
   }
   if (grow) {
@@ -355,8 +389,7 @@ __device__ __forceinline__ void pair_replay(PairRow<EPL>& r, bool has_e, const O
   const bool zero = __ballot(nz) == 0;      // every element of both rows never stepped with a grad
   if (zero) {
     bool stepped = false;
-    for (int k = s + 1; k <= t_idle; ++k) {
-      const OptScalars sc = hist[k];
+    for_ticks(hist, s + 1, t_idle, [&](const OptScalars& sc, int) {
       if (sc.do_adam) {
         stepped = true;
 #pragma unroll
@@ -366,22 +399,19 @@ __device__ __forceinline__ void pair_replay(PairRow<EPL>& r, bool has_e, const O
 #pragma unroll
         for (int q = 0; q < EPL; ++q) ema_elem(sc, r.p[q], r.e[q]);
       }
-    }
+    });
     if (stepped) {
 #pragma unroll
       for (int q = 0; q < EPL; ++q) r.m[q] = r.v[q] = 0.0f;
     }
   } else {
-    OptScalars sc = hist[s + 1 <= t_idle ? s + 1 : t_idle];
-    for (int k = s + 1; k <= t_idle; ++k) {
-      const OptScalars nx = hist[k + 1 <= t_idle ? k + 1 : t_idle];    // next tick's scalars in flight
+    for_ticks(hist, s + 1, t_idle, [&](const OptScalars& sc, int) {
 #pragma unroll
       for (int q = 0; q < EPL; ++q) {
         if (sc.do_adam) idle_adam_elem(sc, r.p[q], r.m[q], r.v[q]);
         if (sc.do_ema) ema_elem(sc, r.p[q], r.e[q]);
       }
-      sc = nx;
-    }
+    });
   }
   if (g) {
     const OptScalars sc = hist[t_idle + 1];

@@ -59,6 +59,43 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ c
   }
 }
 
+// Two contribution arrays sharing the keys (the DARE att / rep rows, width <= 32): one wave per unique
+// key, lanes [0, 32) sum array a and lanes [32, 64) array b -- one set of index loads for both and no
+// idle half-wave (two segsum_kernel launches at width 32 left half of every wave idle).
+__global__ __launch_bounds__(256) void segsum2_kernel(const float* __restrict__ ca, const float* __restrict__ cb,
+                                                      int ld, int width, const uint32_t* __restrict__ uniq_keys,
+                                                      const uint32_t* __restrict__ sorted_idx,
+                                                      const uint32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ offsets,
+                                                      const uint32_t* __restrict__ n_uniq, float* __restrict__ oa,
+                                                      float* __restrict__ ob) {
+  const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  if (u >= *n_uniq) return;
+  const float* __restrict__ src = lane < 32 ? ca : cb;
+  float* __restrict__ dst = lane < 32 ? oa : ob;
+  if (c >= width) return;
+  if (uniq_keys[u] == 0xFFFFFFFFu) {
+    dst[(long)u * width + c] = 0.f;
+    return;
+  }
+  const uint32_t off = offsets[u], cnt = counts[u];
+  float acc = 0.f;
+  uint32_t i = 0;
+  for (; i + 4 <= cnt; i += 4) {   // issue 4 independent row loads, add in order
+    const float a0 = src[(long)sorted_idx[off + i] * ld + c];
+    const float a1 = src[(long)sorted_idx[off + i + 1] * ld + c];
+    const float a2 = src[(long)sorted_idx[off + i + 2] * ld + c];
+    const float a3 = src[(long)sorted_idx[off + i + 3] * ld + c];
+    acc += a0;
+    acc += a1;
+    acc += a2;
+    acc += a3;
+  }
+  for (; i < cnt; ++i) acc += src[(long)sorted_idx[off + i] * ld + c];
+  dst[(long)u * width + c] = acc;
+}
+
 struct RowgradWs {
   size_t temp_bytes;
   size_t total;
@@ -122,9 +159,13 @@ static int rowgrad_core(const uint32_t* keys, const float* const* contrib, float
   tb = w.temp_bytes;
   e = rocprim::exclusive_scan(base, tb, (const uint32_t*)counts, offsets, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
   CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
-  for (int q = 0; q < ncontrib; ++q)
-    segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
-                                             uniq_grad[q]);
+  if (ncontrib == 2 && width <= 32)
+    segsum2_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, counts, offsets,
+                                              n_uniq, uniq_grad[0], uniq_grad[1]);
+  else
+    for (int q = 0; q < ncontrib; ++q)
+      segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
+                                               uniq_grad[q]);
   return check_launch("rowgrad");
 }
 
