@@ -53,9 +53,26 @@ typedef struct {
   float norm_eps;
 } ctr_gemm_epi_t;
 
+/* Operand / result segments of one GEMM over concatenated buffers (ctr_gemm_seg): A columns k >= ka are
+ * read from A2 (row stride lda2; A not transposed), B columns n >= nb from B2 (row stride ldb2; B not
+ * transposed), C columns n >= nc are written to C2 (row stride ldc2; no row-indexed epilogue operand).
+ * Null pointers disable a segment.  Used for the QNN MLP's first layer, whose input is [z | inter]
+ * (src/models/qnn_alpha.py:120-124) -- one launch instead of two per product. */
+typedef struct {
+  const float* A2;
+  int lda2, ka;
+  const float* B2;
+  int ldb2, nb;
+  float* C2;
+  int ldc2, nc;
+} ctr_gemm_seg_t;
+
 size_t ctr_gemm_ws_size(int M, int N, int splits);
 int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
              float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, void* stream);
+int ctr_gemm_seg(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                 float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
+                 void* stream);
 
 
 /* Row-streaming GEMMs of the DARE encoder layer (MHA in_proj / out_proj, src/models/dare.py:53-62, and

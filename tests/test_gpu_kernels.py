@@ -476,3 +476,42 @@ def test_rowgemm_wgrad_vs_torch(NO, NIN, M):
     assert rel(out[:NO * NIN].double().view(NO, NIN), dY.double().t() @ X.double()) < 1e-6
     assert rel(out[o_db:].double(), dY.double().sum(0)) < 1e-6
     assert float(out[NO * NIN:o_db].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("M,N,K,cut,splits", [(4096, 512, 7552, 6400, 8), (300, 200, 130, 70, 1),
+                                              (257, 130, 99, 33, 3), (64, 7552, 512, 6400, 1)])
+def test_gemm_segments_vs_torch(M, N, K, cut, splits):
+    """ctr_gemm_seg: A = [A1 | A2] split at column `cut` (the QNN MLP input [z | inter]), B = [B1 | B2]
+    split at column `cut`, C written as [C1 | C2] -- each against torch on the concatenated operands."""
+    from tossctr._lib import GemmEpi, GemmSeg
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + cut)
+    ws = torch.empty(splits * M * max(N, K) + 16, device="cuda")
+    # A segments (ta = 0), B as a (N, K) weight (tb = 1), bias + ReLU epilogue
+    kc = min(cut, K)
+    A1, A2 = torch.randn(M, kc, device="cuda", generator=g), torch.randn(M, K - kc, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    C = torch.empty(M, N, device="cuda")
+    L.call("ctr_gemm_seg", M, N, K, ptr(A1), kc, 0, ptr(W), K, 1, ptr(C), N, GemmEpi(bias=ptr(bias), act=1), splits,
+           ptr(ws), GemmSeg(A2=ptr(A2), lda2=K - kc, ka=kc), stream())
+    ref = torch.relu(torch.cat([A1, A2], 1).double() @ W.double().t() + bias.double())
+    assert rel(C.double(), ref) < 1e-5
+    # B segments (tb = 0): C = X^T [B1 | B2]
+    nc = min(cut, N)
+    X = torch.randn(K, M, device="cuda", generator=g)
+    B1, B2 = torch.randn(K, nc, device="cuda", generator=g), torch.randn(K, N - nc, device="cuda", generator=g)
+    C = torch.empty(M, N, device="cuda")
+    L.call("ctr_gemm_seg", M, N, K, ptr(X), M, 1, ptr(B1), nc, 0, ptr(C), N, None, splits, ptr(ws),
+           GemmSeg(B2=ptr(B2), ldb2=N - nc, nb=nc), stream())
+    assert rel(C.double(), X.double().t() @ torch.cat([B1, B2], 1).double()) < 1e-5
+    # C segments: [C1 | C2] = A W
+    if N > 96:
+        A = torch.randn(M, K, device="cuda", generator=g)
+        Wt = torch.randn(K, N, device="cuda", generator=g)
+        C1 = torch.full((M, nc), float("nan"), device="cuda")
+        C2 = torch.full((M, N - nc), float("nan"), device="cuda")
+        L.call("ctr_gemm_seg", M, N, K, ptr(A), K, 0, ptr(Wt), N, 0, ptr(C1), nc, None, splits, ptr(ws),
+               GemmSeg(C2=ptr(C2), ldc2=N - nc, nc=nc), stream())
+        ref = A.double() @ Wt.double()
+        assert rel(torch.cat([C1, C2], 1).double(), ref) < 1e-5

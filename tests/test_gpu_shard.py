@@ -43,8 +43,12 @@ def _compare(a, b, rtol, atol=1e-6, what=""):
     assert a["sd"].keys() == b["sd"].keys()
     for k in a["sd"]:
         assert a["sd"][k].shape == b["sd"][k].shape, k
-        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), rtol, atol, what + k)
-        close_enough(a["ema"][k].double().numpy().ravel(), b["ema"][k].double().numpy().ravel(), rtol, atol,
+        # the MHA key bias's exact gradient is 0 (softmax shift invariance): what it receives is rounding
+        # noise that AdamW normalises into lr-sized steps, so any change of summation order anywhere (e.g.
+        # the clip norm's cross-rank sum) moves it -- compared at the north-star 1e-4 instead
+        rt = max(rtol, 1e-4) if k.endswith("mha.in_proj_bias") else rtol
+        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), rt, atol, what + k)
+        close_enough(a["ema"][k].double().numpy().ravel(), b["ema"][k].double().numpy().ravel(), rt, atol,
                      what + "ema:" + k)
 
 

@@ -27,7 +27,19 @@ struct GemmArgs {
   int klen;        // K elements per split
   float* ws;       // split-K slabs [splits][M][N]
   int vecA, vecB;  // 16-byte loads legal
+  // operand / result segments (ctr_gemm_seg): A columns k >= ka from A2, B columns n >= nb from B2 (both
+  // non-transposed), C columns n >= nc to C2 -- one launch for a GEMM over concatenated buffers
+  const float* A2;
+  int lda2, ka;
+  const float* B2;
+  int ldb2, nb;
+  float* C2;
+  int ldc2, nc;
 };
+
+__device__ __forceinline__ float* cptr(const GemmArgs& g, int m, int n) {
+  return (g.C2 && n >= g.nc) ? g.C2 + (long)m * g.ldc2 + (n - g.nc) : g.C + (long)m * g.ldc + n;
+}
 
 __device__ __forceinline__ float epi_elem(const ctr_gemm_epi_t& e, float v, int m, int n, int N, int ldc) {
   if (e.dact) {
@@ -88,11 +100,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
           const int i = e / (BK / 4), kq = (e % (BK / 4)) * 4;
           const int m = m0 + i, k = k0 + kq;
           if (m < g.M) {
-            const float* p = g.A + (long)m * g.lda + k;
-            if (g.vecA && k + 3 < kz1) v = *(const f32x4*)p;
-            else {
+            if (g.A2 == nullptr || k + 3 < g.ka) {
+              const float* p = g.A + (long)m * g.lda + k;
+              if (g.vecA && k + 3 < kz1) v = *(const f32x4*)p;
+              else {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] = (k + j < kz1) ? p[j] : 0.f;
+                for (int j = 0; j < 4; ++j) v[j] = (k + j < kz1) ? p[j] : 0.f;
+              }
+            } else if (k >= g.ka) {
+              const float* p = g.A2 + (long)m * g.lda2 + (k - g.ka);
+              if (g.vecA && k + 3 < kz1) v = *(const f32x4*)p;
+              else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (k + j < kz1) ? p[j] : 0.f;
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int kk = k + j;
+                v[j] = kk >= kz1 ? 0.f : kk < g.ka ? g.A[(long)m * g.lda + kk] : g.A2[(long)m * g.lda2 + (kk - g.ka)];
+              }
             }
           }
         } else {    // A stored [k][m], m contiguous
@@ -121,11 +148,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
           const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
           const int kk = k0 + k, n = n0 + nq;
           if (kk < kz1) {
-            const float* p = g.B + (long)kk * g.ldb + n;
-            if (g.vecB && n + 3 < g.N) v = *(const f32x4*)p;
-            else {
+            if (g.B2 == nullptr || n + 3 < g.nb) {
+              const float* p = g.B + (long)kk * g.ldb + n;
+              if (g.vecB && n + 3 < g.N) v = *(const f32x4*)p;
+              else {
 #pragma unroll
-              for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? p[j] : 0.f;
+                for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? p[j] : 0.f;
+              }
+            } else if (n >= g.nb) {
+              const float* p = g.B2 + (long)kk * g.ldb2 + (n - g.nb);
+              if (g.vecB && n + 3 < g.N) v = *(const f32x4*)p;
+              else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? p[j] : 0.f;
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int nn = n + j;
+                v[j] = nn >= g.N ? 0.f : nn < g.nb ? g.B[(long)kk * g.ldb + nn] : g.B2[(long)kk * g.ldb2 + (nn - g.nb)];
+              }
             }
           }
         } else {    // B stored [n][k], k contiguous
@@ -241,7 +283,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + lrow + i * 16 + r;
-          if (m < g.M && n < g.N) g.C[(long)m * g.ldc + n] = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
+          if (m < g.M && n < g.N) *cptr(g, m, n) = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
         }
       }
     return;
@@ -302,7 +344,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? epi_elem(e, Cs[i * SC + jq + j], m, n + j, g.N, g.ldc) : 0.f;
     float* p = g.C + (long)m * g.ldc + n;
-    if (vecC && n + 3 < g.N) *(f32x4*)p = v;
+    if (g.C2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (n + j < g.N) *cptr(g, m, n + j) = v[j];
+    } else if (vecC && n + 3 < g.N) *(f32x4*)p = v;
     else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -326,7 +372,7 @@ __global__ void splitk_reduce_kernel(GemmArgs g, int splits) {
     }
     for (; z < splits; ++z) s += g.ws[z * MN + q];
     const int m = (int)(q / g.N), n = (int)(q % g.N);
-    g.C[(long)m * g.ldc + n] = epi_elem(g.epi, s, m, n, g.N, g.ldc);
+    *cptr(g, m, n) = epi_elem(g.epi, s, m, n, g.N, g.ldc);
   }
 }
 
@@ -362,8 +408,9 @@ extern "C" size_t ctr_gemm_ws_size(int M, int N, int splits) {
   return splits > 1 ? (size_t)splits * M * N * sizeof(float) : 0;
 }
 
-extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
-                        float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, void* stream) {
+static int gemm_core(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                     float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
+                     void* stream) {
   CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative dims");
   if (M == 0 || N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -377,6 +424,26 @@ extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, co
   CTR_REQUIRE(!(splits > 1 && (g.epi.norm_w || !ws)), "split-K needs ws and no fused norm");
   g.vecA = ((lda & 3) == 0) && ((((uintptr_t)A) & 15) == 0);
   g.vecB = ((ldb & 3) == 0) && ((((uintptr_t)B) & 15) == 0);
+  g.A2 = nullptr; g.lda2 = 0; g.ka = K;
+  g.B2 = nullptr; g.ldb2 = 0; g.nb = N;
+  g.C2 = nullptr; g.ldc2 = 0; g.nc = N;
+  if (seg) {
+    CTR_REQUIRE(!(seg->A2 && ta) && !(seg->B2 && tb), "gemm segments: A2 needs ta = 0, B2 needs tb = 0");
+    CTR_REQUIRE(!seg->A2 || (seg->ka >= 0 && seg->ka <= K), "gemm segments: ka out of range");
+    CTR_REQUIRE(!seg->B2 || (seg->nb >= 0 && seg->nb <= N), "gemm segments: nb out of range");
+    CTR_REQUIRE(!seg->C2 || (seg->nc >= 0 && seg->nc <= N && N > 96 && !g.epi.norm_w && !g.epi.aux && !g.epi.pre &&
+                             !g.epi.add),
+                "gemm segments: C2 needs N > 96 and no row-indexed epilogue operand");
+    if (seg->A2) {
+      g.A2 = seg->A2; g.lda2 = seg->lda2; g.ka = seg->ka;
+      g.vecA = g.vecA && ((seg->lda2 & 3) == 0) && ((((uintptr_t)seg->A2) & 15) == 0) && ((seg->ka & 3) == 0);
+    }
+    if (seg->B2) {
+      g.B2 = seg->B2; g.ldb2 = seg->ldb2; g.nb = seg->nb;
+      g.vecB = g.vecB && ((seg->ldb2 & 3) == 0) && ((((uintptr_t)seg->B2) & 15) == 0) && ((seg->nb & 3) == 0);
+    }
+    if (seg->C2) { g.C2 = seg->C2; g.ldc2 = seg->ldc2; g.nc = seg->nc; }
+  }
   const int BK = 16;
   int klen = K;
   if (splits > 1) {
@@ -385,7 +452,7 @@ extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, co
   }
   g.klen = klen > 0 ? klen : 1;
   g.ws = ws;
-  if (K <= 4 && !g.epi.norm_w && splits == 1) {
+  if (K <= 4 && !g.epi.norm_w && splits == 1 && !seg) {
     const long MN = (long)M * N;
     gemm_smallk_kernel<<<(int)std::min<long>((MN + 255) / 256, 8192), 256, 0, s>>>(g, ta, tb);
     return check_launch("ctr_gemm");
@@ -412,4 +479,15 @@ extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, co
     splitk_reduce_kernel<<<blocks, 256, 0, s>>>(g, splits);
   }
   return check_launch("ctr_gemm");
+}
+
+extern "C" int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                        float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, void* stream) {
+  return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, nullptr, stream);
+}
+
+extern "C" int ctr_gemm_seg(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                            float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws,
+                            const ctr_gemm_seg_t* seg, void* stream) {
+  return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, stream);
 }

@@ -21,6 +21,11 @@ class GemmEpi(C.Structure):
                 ("norm_w", p), ("norm_h", p), ("norm_r", p), ("norm_eps", f)]
 
 
+class GemmSeg(C.Structure):
+    _fields_ = [("A2", p), ("lda2", i), ("ka", i), ("B2", p), ("ldb2", i), ("nb", i), ("C2", p), ("ldc2", i),
+                ("nc", i)]
+
+
 class OptSeg(C.Structure):
     _fields_ = [("p_off", C.c_int64), ("n", C.c_int64), ("width", C.c_int32), ("kind", C.c_int32),
                 ("g_off", C.c_int64), ("keys", p), ("G", p), ("n_uniq", p), ("g_ld", C.c_int32),
@@ -42,6 +47,7 @@ SIGS = {
     "ctr_abi_version": (i, []),
     "ctr_gemm_ws_size": (z, [i, i, i]),
     "ctr_gemm": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, p]),
+    "ctr_gemm_seg": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), p]),
     "ctr_rowgemm_supported": (i, [i, i]),
     "ctr_rowgemm": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
     "ctr_rowgemm_wgrad_rows": (i, [i]),

@@ -211,7 +211,7 @@ class Engine:
         bm = 64 if (M <= 64 and bn == 128) else 128
         return math.ceil(M / bm) * math.ceil(N / bn)
 
-    def gemm(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, splits=1):
+    def gemm(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, splits=1, seg=None):
         """C = op(A) op(B) (+ epilogue); A/B/C are raw pointers.  A grid too small to fill the 256 CUs
         with a deep K (e.g. the QNN MLP's first layer, 32x4 tiles over K = 6400) is split along K."""
         if splits == 1 and K >= 512 and not (epi is not None and epi.norm_w) and self._tiles(M, N) < 256:
@@ -219,7 +219,10 @@ class Engine:
         wsp = None
         if splits > 1:
             wsp = ptr(self.splitk_ws(splits * M * N))
-        call("ctr_gemm", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, self.s())
+        if seg is not None:
+            call("ctr_gemm_seg", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg, self.s())
+        else:
+            call("ctr_gemm", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, self.s())
 
     @staticmethod
     def _split_factor(M, N, K, min_depth):
@@ -456,8 +459,6 @@ class Engine:
         din = FD + C
         W0 = P["qnn.mlp.0.weight"]
         H0 = a.mlp_hidden[0] if a.mlp_hidden else 1
-        tmp = W.get("mlp_tmp", (B, H0))
-        self.gemm(B, H0, FD, ptr(z), FD, 0, ptr(W0), din, 1, ptr(tmp), H0)
         nh = len(a.mlp_hidden)
         for j in range(nh + 1):
             last = j == nh
@@ -469,8 +470,9 @@ class Engine:
             epi = GemmEpi(bias=ptr(P[bkey]), act=0 if last else 1, pre=ptr(pre), drop_key=dm[0], drop_thresh=dm[1],
                           drop_scale=dm[2])
             if j == 0:
-                epi.add, epi.ld_add = ptr(tmp), H0
-                self.gemm(B, n_out, C, ptr(inter), C, 0, ptr(P[wkey], FD), din, 1, ptr(out), n_out, epi)
+                # input [z | inter] (qnn_alpha.py:120-124): one GEMM over both K segments
+                self.gemm(B, n_out, FD + C, ptr(z), FD, 0, ptr(W0), din, 1, ptr(out), n_out, epi,
+                          seg=_lib.GemmSeg(A2=ptr(inter), lda2=C, ka=FD))
             else:
                 kin = a.mlp_hidden[j - 1]
                 self.gemm(B, n_out, kin, ptr(hs[-1]), kin, 0, ptr(P[wkey]), kin, 1, ptr(out), n_out, epi)
@@ -736,17 +738,17 @@ class Engine:
                 dcur, ncur = dprev, kin
             else:
                 # first layer: W0 = [W0a (over z) | W0b (over inter)]
-                self.gemm(ncur, FD, B, ptr(dcur), ncur, 1, ptr(q["z"]), FD, 0, ptr(G[wkey]), din, None,
-                          self.wgrad_splits(ncur, FD, B))
-                self.gemm(ncur, C, B, ptr(dcur), ncur, 1, ptr(q["inter"]), C, 0, ptr(G[wkey], FD), din, None,
-                          self.wgrad_splits(ncur, C, B))
+                self.gemm(ncur, FD + C, B, ptr(dcur), ncur, 1, ptr(q["z"]), FD, 0, ptr(G[wkey]), din, None,
+                          self.wgrad_splits(ncur, FD + C, B), seg=_lib.GemmSeg(B2=ptr(q["inter"]), ldb2=C, nb=FD))
                 self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
         W0 = P["qnn.mlp.0.weight"]
         dinter = W.get("dinter", (B, C))
-        self.gemm(B, C, ncur, ptr(dcur), ncur, 0, ptr(W0, FD), din, 0, ptr(dinter), C)
         dz_mlp = W.get("dz_mlp", (B, FD))
-        if a.use_residual:
-            self.gemm(B, FD, ncur, ptr(dcur), ncur, 0, ptr(W0), din, 0, ptr(dz_mlp), FD)
+        if a.use_residual:     # [dz | dinter] = dcur W0: one GEMM, output split at column FD
+            self.gemm(B, FD + C, ncur, ptr(dcur), ncur, 0, ptr(W0), din, 0, ptr(dz_mlp), FD,
+                      seg=_lib.GemmSeg(C2=ptr(dinter), ldc2=C, nc=FD))
+        else:
+            self.gemm(B, C, ncur, ptr(dcur), ncur, 0, ptr(W0, FD), din, 0, ptr(dinter), C)
         # SE + dropout
         dinter_pre = W.get("dinter_pre", (B, C))
         dq_ = drop_args(seed, SITE_QNN, a.qnn_p, training)
