@@ -142,51 +142,81 @@ struct CatMeta {
   int row_ld;             // row stride of every table in tabs (0: d_c)
 };
 
+// Workgroup = (categorical c, 64 samples): the projection P_c (D x d_c) and the block's gathered table
+// rows are staged in LDS once, then thread (sample i, dim d) forms sum_k T[i][k] P_c[d][k] from LDS
+// (row values broadcast across the D lanes of a sample, P_c rows at a 65-float stride: no bank conflicts).
+// The per-output arithmetic (fmaf over k in order) is unchanged from a thread-per-output form, whose
+// strided P_c reads (32 cache lines per load instruction) bounded it.
+constexpr int CE_SPB = 64;     // samples per workgroup
+constexpr int CE_LD = 65;      // LDS row stride (floats)
+
 __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restrict__ xcat, int B, int Fc,
                                                             const float* __restrict__ arena, CatMeta cm, int D,
                                                             float* __restrict__ cat_e, float* __restrict__ xf,
                                                             long xf_ld, Drop drop) {
-  const uint32_t total = (uint32_t)B * Fc * D;   // host checks < 2^32; 32-bit index math
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
-    const uint32_t bc = q / (uint32_t)D;
-    const int d = (int)(q - bc * D);
-    const uint32_t b = bc / (uint32_t)Fc;
-    const int c = (int)(bc - b * Fc);
-    const int dc = cm.dims[c];
-    const long row = xcat[(long)b * Fc + c];
-    const float* t = cm.tabs + cm.tab_off[c] + row * (cm.row_ld ? cm.row_ld : dc);
-    const float* p = arena + cm.proj_off[c] + (long)d * dc;
+  __shared__ float sP[64 * CE_LD];
+  __shared__ float sT[CE_SPB * CE_LD];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int dc = cm.dims[c];
+  const int b0 = blockIdx.y * CE_SPB, nb = min(CE_SPB, B - b0);
+  const float* P = arena + cm.proj_off[c];
+  for (int e = tid; e < D * dc; e += 256) {
+    const int d = e / dc, k = e - d * dc;
+    sP[d * CE_LD + k] = P[e];
+  }
+  const float* T = cm.tabs + cm.tab_off[c];
+  const long tld = cm.row_ld ? cm.row_ld : dc;
+  for (int e = tid; e < nb * 64; e += 256) {
+    const int i = e >> 6, k = e & 63;
+    if (k < dc) sT[i * CE_LD + k] = T[(long)xcat[(long)(b0 + i) * Fc + c] * tld + k];
+  }
+  __syncthreads();
+  for (int e = tid; e < nb * D; e += 256) {
+    const int i = e / D, d = e - i * D;
+    const float* t = sT + i * CE_LD;
+    const float* pp = sP + d * CE_LD;
     float acc = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < dc; ++k) acc = fmaf(t[k], p[k], acc);
+    for (int k = 0; k < dc; ++k) acc = fmaf(t[k], pp[k], acc);
+    const uint32_t q = ((uint32_t)(b0 + i) * Fc + c) * D + d;
     cat_e[q] = acc;
-    if (xf) xf[(long)b * xf_ld + (long)c * D + d] = drop_apply(drop, q, acc);
+    if (xf) xf[(long)(b0 + i) * xf_ld + (long)c * D + d] = drop_apply(drop, q, acc);
   }
 }
 
 // row-grad contributions: contrib[(b*Fc+c)*64 + k] = sum_d dcat[b,c,d] P_c[d,k]  (zero-padded to 64)
-// keys[b*Fc+c] = row_base[c] + X_cat[b,c]
+// keys[b*Fc+c] = row_base[c] + X_cat[b,c].  Same (c, 64 samples) workgroups and LDS staging as the forward.
 __global__ __launch_bounds__(256) void cat_embed_bwd_rows(const int* __restrict__ xcat, int B, int Fc,
                                                           const float* __restrict__ arena, CatMeta cm, int D,
                                                           const float* __restrict__ dcat,
                                                           const uint32_t* __restrict__ row_base,
                                                           float* __restrict__ contrib, uint32_t* __restrict__ keys) {
-  const uint32_t total = (uint32_t)B * Fc * 64;
-  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < total; q += gridDim.x * blockDim.x) {
-    const int k = (int)(q & 63);
-    const uint32_t bc = q >> 6;
-    const uint32_t b = bc / (uint32_t)Fc;
-    const int c = (int)(bc - b * Fc);
-    const int dc = cm.dims[c];
+  __shared__ float sP[64 * CE_LD];
+  __shared__ float sG[CE_SPB * CE_LD];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int dc = cm.dims[c];
+  const int b0 = blockIdx.y * CE_SPB, nb = min(CE_SPB, B - b0);
+  const float* P = arena + cm.proj_off[c];
+  for (int e = tid; e < D * dc; e += 256) {
+    const int d = e / dc, k = e - d * dc;
+    sP[d * CE_LD + k] = P[e];
+  }
+  for (int e = tid; e < nb * D; e += 256) {
+    const int i = e / D, d = e - i * D;
+    sG[i * CE_LD + d] = dcat[((long)(b0 + i) * Fc + c) * D + d];
+  }
+  __syncthreads();
+  for (int e = tid; e < nb * 64; e += 256) {
+    const int i = e >> 6, k = e & 63;
+    const long bc = (long)(b0 + i) * Fc + c;
     float acc = 0.f;
     if (k < dc) {
-      const float* p = arena + cm.proj_off[c] + k;
-      const float* g = dcat + (long)bc * D;
+      const float* g = sG + i * CE_LD;
 #pragma unroll 8
-      for (int d = 0; d < D; ++d) acc = fmaf(g[d], p[(long)d * dc], acc);
+      for (int d = 0; d < D; ++d) acc = fmaf(g[d], sP[d * CE_LD + k], acc);
     }
-    contrib[q] = acc;
-    if (k == 0) keys[bc] = row_base[c] + (uint32_t)xcat[(long)b * Fc + c];
+    contrib[bc * 64 + k] = acc;
+    if (k == 0) keys[bc] = row_base[c] + (uint32_t)xcat[bc];
   }
 }
 
@@ -524,10 +554,9 @@ extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* ar
   CTR_REQUIRE((long)B * Fc * 64 < (1L << 32), "cat_embed: B*Fc*64 must fit 32-bit indexing");
   CTR_REQUIRE(row_ld >= 0 && row_ld <= 64, "cat_embed: row_ld must be in [0, 64]");
   CatMeta cm{tab_base ? tab_base : arena, tab_off, proj_off, dims, row_ld};
-  long total = (long)B * Fc * D;
-  int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  cat_embed_fwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(xcat, B, Fc, arena, cm, D, cat_e, xf, xf_ld,
-                                                                 Drop{drop_key, drop_thresh, drop_scale});
+  CTR_REQUIRE(D <= 64, "cat_embed: D > 64");
+  cat_embed_fwd_kernel<<<dim3(Fc, cdiv(B, CE_SPB)), 256, 0, (hipStream_t)stream>>>(
+      xcat, B, Fc, arena, cm, D, cat_e, xf, xf_ld, Drop{drop_key, drop_thresh, drop_scale});
   return check_launch("cat_embed_fwd");
 }
 
@@ -547,9 +576,8 @@ extern "C" int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* ar
   CTR_REQUIRE(row_ld >= 0 && row_ld <= 64, "cat_embed: row_ld must be in [0, 64]");
   hipStream_t s = (hipStream_t)stream;
   CatMeta cm{tab_base ? tab_base : arena, tab_off, proj_off, dims, row_ld};
-  long total = (long)B * Fc * 64;
-  int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  cat_embed_bwd_rows<<<blocks, 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, row_base, contrib, keys);
+  cat_embed_bwd_rows<<<dim3(Fc, cdiv(B, CE_SPB)), 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, row_base, contrib,
+                                                                keys);
   const int rpc = 256;
   const int nchunk = (B + rpc - 1) / rpc;
   cat_embed_bwd_proj_partial<<<dim3(Fc, nchunk), 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, rpc, ws);
