@@ -305,17 +305,28 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_proj_partial(const int* __r
   }
 }
 
+// one thread per (c, output q): the nchunk partials summed in chunk order, eight loads in flight
 __global__ __launch_bounds__(256) void cat_embed_bwd_proj_final(int nchunk, int Fc, int D, CatMeta cm,
                                                                 const long* __restrict__ proj_goff,
                                                                 const float* __restrict__ part,
                                                                 float* __restrict__ grad) {
   const int c = blockIdx.x;
   const int dc = cm.dims[c];
-  for (int q = threadIdx.x; q < D * dc; q += blockDim.x) {
-    float s = 0.f;
-    for (int ch = 0; ch < nchunk; ++ch) s += part[((long)ch * Fc + c) * (64 * 64) + q];
-    grad[proj_goff[c] + q] = s;
+  const int q = blockIdx.y * 256 + threadIdx.x;
+  if (q >= D * dc) return;
+  const float* pc = part + (long)c * (64 * 64) + q;
+  const long cs = (long)Fc * (64 * 64);
+  float s = 0.f;
+  int ch = 0;
+  for (; ch + 8 <= nchunk; ch += 8) {
+    float a[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = pc[(ch + j) * cs];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += a[j];
   }
+  for (; ch < nchunk; ++ch) s += pc[ch * cs];
+  grad[proj_goff[c] + q] = s;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -560,8 +571,10 @@ extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* ar
   return check_launch("cat_embed_fwd");
 }
 
+constexpr int CP_RPC = 64;     // rows per projection-grad partial (one LDS sub-chunk per workgroup)
+
 extern "C" size_t ctr_cat_embed_bwd_ws(int B, int Fc) {
-  int nchunk = (B + 255) / 256;
+  int nchunk = (B + CP_RPC - 1) / CP_RPC;
   return (size_t)nchunk * Fc * 64 * 64 * sizeof(float);
 }
 
@@ -578,10 +591,11 @@ extern "C" int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* ar
   CatMeta cm{tab_base ? tab_base : arena, tab_off, proj_off, dims, row_ld};
   cat_embed_bwd_rows<<<dim3(Fc, cdiv(B, CE_SPB)), 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, row_base, contrib,
                                                                 keys);
-  const int rpc = 256;
+  const int rpc = CP_RPC;
   const int nchunk = (B + rpc - 1) / rpc;
   cat_embed_bwd_proj_partial<<<dim3(Fc, nchunk), 256, 0, s>>>(xcat, B, Fc, arena, cm, D, dcat, rpc, ws);
-  cat_embed_bwd_proj_final<<<Fc, 256, 0, s>>>(nchunk, Fc, D, cm, proj_goff, ws, grad_arena);
+  cat_embed_bwd_proj_final<<<dim3(Fc, cdiv(D * 64, 256)), 256, 0, s>>>(nchunk, Fc, D, cm, proj_goff, ws,
+                                                                        grad_arena);
   return check_launch("cat_embed_bwd");
 }
 
