@@ -101,8 +101,21 @@ __global__ __launch_bounds__(256) void topk_bwd_kernel(const int* __restrict__ t
   if (b >= B) return;
   const int* tb = tok + (long)b * K;
   const float* dv = dvals + (long)b * K;
-  if (lane < D) {
+  if (D <= 32) {    // two half-waves take the even / odd k, combined in a fixed order
+    const int d = lane & 31, h = lane >> 5;
     float acc = 0.f;
+    if (d < D) {
+#pragma unroll 4
+      for (int k = h; k < K; k += 2) {
+        const int t = tb[k];
+        if (t != pad_id) acc = fmaf(dv[k], E_att[(long)t * D + d], acc);
+      }
+    }
+    const float other = __shfl_down(acc, 32);
+    if (h == 0 && d < D) dq[(long)b * D + d] = acc + other;
+  } else if (lane < D) {
+    float acc = 0.f;
+#pragma unroll 4
     for (int k = 0; k < K; ++k) {
       const int t = tb[k];
       if (t != pad_id) acc = fmaf(dv[k], E_att[(long)t * D + lane], acc);

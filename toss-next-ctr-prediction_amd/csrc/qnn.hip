@@ -324,6 +324,7 @@ __global__ __launch_bounds__(256) void se_bwd_partial(const float* __restrict__ 
   const int b0 = blockIdx.y * rows_per_block, b1 = min(B, b0 + rows_per_block);
   for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
     float acc = 0.f;
+#pragma unroll 4
     for (int b = b0; b < b1; ++b) {
       const long q = (long)b * C + c;
       float g = dout[(long)b * dout_ld + c];
@@ -340,13 +341,20 @@ __global__ __launch_bounds__(256) void se_bwd_partial(const float* __restrict__ 
 }
 
 // dgate[c] = sum of the row-block partials (fixed order); dz2 = dgate * sigmoid'(.)  -> db2, dz2
+// (64 columns per workgroup; its four waves sum interleaved quarters of the partials, combined in order)
 __global__ __launch_bounds__(256) void se_dgate_kernel(const float* __restrict__ part, int nparts, int C,
                                                        const float* __restrict__ gate, float* __restrict__ db2,
                                                        float* __restrict__ dz2) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float dg = 0.f;
-  for (int p = 0; p < nparts; ++p) dg += part[(long)p * C + c];
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float t = 0.f;
+  if (c < C)
+    for (int p = ty; p < nparts; p += 4) t += part[(long)p * C + c];
+  red[ty][tx] = t;
+  __syncthreads();
+  if (ty != 0 || c >= C) return;
+  const float dg = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
   const float s = gate[c];
   const float v = dg * (s * (1.f - s));
   db2[c] = v;
@@ -460,7 +468,11 @@ extern "C" int ctr_scale_drop(const float* x, int B, int C, const float* gate, u
   return check_launch("scale_drop");
 }
 
-extern "C" size_t ctr_se_bwd_ws(int B, int C) { return ((size_t)cdiv(B, 64) * C + 3 * (size_t)C) * sizeof(float); }
+constexpr int SE_RPB = 32;     // rows per se_bwd_partial workgroup (B = 4096: 5 x 128 workgroups)
+
+extern "C" size_t ctr_se_bwd_ws(int B, int C) {
+  return ((size_t)cdiv(B, SE_RPB) * C + 3 * (size_t)C) * sizeof(float);
+}
 
 extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, int Cr, const float* gate,
                           const float* g1, const float* mean, const float* W1, const float* W2, uint32_t drop_key,
@@ -468,7 +480,7 @@ extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B
                           float* db2, float* ws, void* stream) {
   if (B == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int rpb = 64;
+  const int rpb = SE_RPB;
   const int np = cdiv(B, rpb);
   float* part = ws;                      // [np][C]
   float* dmean = ws + (size_t)np * C;    // [C]
@@ -478,7 +490,7 @@ extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B
   if (gate) {
     float* dz2 = dmean + C;                // [C]
     float* dz1 = dz2 + C;                  // [Cr <= C]
-    se_dgate_kernel<<<cdiv(C, 256), 256, 0, s>>>(part, np, C, gate, db2, dz2);
+    se_dgate_kernel<<<cdiv(C, 64), 256, 0, s>>>(part, np, C, gate, db2, dz2);
     matvec_cols_kernel<<<cdiv(Cr, 4), 256, 0, s>>>(W2, C, Cr, dz2, g1, db1, dz1);     // dz1 = relu'(W2^T dz2)
     matvec_cols_kernel<<<cdiv(C, 4), 256, 0, s>>>(W1, Cr, C, dz1, nullptr, dmean, nullptr);   // W1^T dz1
     se_mlp_bwd_outer<<<cdiv(2L * C * Cr, 256), 256, 0, s>>>(C, Cr, mean, g1, dz2, dz1, dW1, dW2);
