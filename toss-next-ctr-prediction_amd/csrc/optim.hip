@@ -129,7 +129,22 @@ __global__ __launch_bounds__(256) void sqnorm_dense_kernel(const float* __restri
                                                            float* __restrict__ part) {
   __shared__ float red[4];
   float s = 0.f;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+  if ((((uintptr_t)x) & 15) == 0) {   // 16-byte loads, four independent chains; scalar tail
+    const long n4 = n >> 2;
+    const float4* x4 = (const float4*)x;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+      const float4 v = x4[i];
+      s0 = fmaf(v.x, v.x, s0);
+      s1 = fmaf(v.y, v.y, s1);
+      s2 = fmaf(v.z, v.z, s2);
+      s3 = fmaf(v.w, v.w, s3);
+    }
+    s = (s0 + s1) + (s2 + s3);
+    for (long i = 4 * n4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+  } else {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+  }
   s = block_sum(s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
