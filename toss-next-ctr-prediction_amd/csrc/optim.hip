@@ -133,6 +133,7 @@ __global__ __launch_bounds__(256) void sqnorm_dense_kernel(const float* __restri
     const long n4 = n >> 2;
     const float4* x4 = (const float4*)x;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 4
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
       const float4 v = x4[i];
       s0 = fmaf(v.x, v.x, s0);
@@ -162,13 +163,16 @@ __global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __rest
   if ((ld & 3) == 0) {
     const long total4 = (long)nv * ld / 4;
     const float4* G4 = (const float4*)G;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // four chains, four loads in flight
+#pragma unroll 4
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
       const float4 g = G4[i];
-      s = fmaf(g.x, g.x, s);
-      s = fmaf(g.y, g.y, s);
-      s = fmaf(g.z, g.z, s);
-      s = fmaf(g.w, g.w, s);
+      s0 = fmaf(g.x, g.x, s0);
+      s1 = fmaf(g.y, g.y, s1);
+      s2 = fmaf(g.z, g.z, s2);
+      s3 = fmaf(g.w, g.w, s3);
     }
+    s = (s0 + s1) + (s2 + s3);
   } else {
     const long total = (long)nv * width;
     for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
