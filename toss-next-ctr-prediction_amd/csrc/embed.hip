@@ -347,7 +347,35 @@ struct CtxArgs {
 // part pp sums features pp, pp + P, ... and the parts combine in fixed order through the wave's LDS row.
 // Then the ctx_mlp row and the query (lane = d).
 __device__ __forceinline__ float ctx_wave_mean(const float* __restrict__ x, int F, int D, float* sp) {
-  const int lane = threadIdx.x & 63, P = 64 / D;
+  const int lane = threadIdx.x & 63;
+  if ((D & 3) == 0 && (((uintptr_t)x) & 15) == 0) {
+    // 16-byte loads: lane = (part pp, column quad dq), P = 64 / (D/4) parts; sp holds 4 floats per lane, so
+    // element d of part pp sits at sp[pp * D + d]
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const int Dq = D >> 2, P = 64 / Dq;
+    const int dq = lane % Dq, pp = lane / Dq;
+    f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    if (pp < P) {
+      const f4* x4 = (const f4*)x;
+      int f = pp;
+      for (; f + P < F; f += 2 * P) {
+        a0 += x4[(long)f * Dq + dq];
+        a1 += x4[(long)(f + P) * Dq + dq];
+      }
+      if (f < F) a0 += x4[(long)f * Dq + dq];
+    }
+    const f4 v = a0 + a1;
+    if (pp < P) *(f4*)&sp[(pp * Dq + dq) * 4] = v;
+    __builtin_amdgcn_wave_barrier();
+    float m = 0.f;
+    if (lane < D) {
+      for (int q = 0; q < P; ++q) m += sp[q * D + lane];
+      m = m / (float)F;
+    }
+    __builtin_amdgcn_wave_barrier();
+    return m;
+  }
+  const int P = 64 / D;
   const int d = lane % D, pp = lane / D;
   float s0 = 0.f, s1 = 0.f;
   if (pp < P) {
@@ -371,7 +399,7 @@ __device__ __forceinline__ float ctx_wave_mean(const float* __restrict__ x, int 
 
 __global__ __launch_bounds__(256) void context_fwd_kernel(CtxArgs a) {
   __shared__ float sctx_all[4][3 * 64];
-  __shared__ float sp_all[4][64];
+  __shared__ __attribute__((aligned(16))) float sp_all[4][256];
   const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + w;
   if (b >= a.B) return;
