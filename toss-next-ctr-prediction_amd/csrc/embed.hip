@@ -516,16 +516,22 @@ __global__ __launch_bounds__(CTXB_T) void context_bwd_kernel(CtxBwdArgs a) {
     sg[2][t] = f.Fc > 0 ? sdctx[slot * D + t] / (float)f.Fc : 0.f;
   }
   __syncthreads();
-  if (f.Fn > 0) {
-    float* dn = a.dnum + (long)b * f.num_ld;
-    const int n = f.Fn * D;
-    for (int e = t; e < n; e += CTXB_T) dn[e] += sg[0][e % D];
-  }
-  if (f.Fm > 0) {
-    float* dm = a.dmask + (long)b * f.mask_ld;
-    const int n = f.Fm * D;
-    for (int e = t; e < n; e += CTXB_T) dm[e] += sg[1][e % D];
-  }
+  // dnum += g_num[d], dmask += g_mask[d]: 16-byte read-modify-writes when the rows allow it
+  auto bcast_add = [&](float* dst, int F, const float* g) {
+    const int n = F * D;
+    if ((D & 3) == 0 && (((uintptr_t)dst) & 15) == 0) {
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      f4* d4 = (f4*)dst;
+      for (int e4 = t; e4 < (n >> 2); e4 += CTXB_T) {
+        const int d = (e4 << 2) % D;
+        d4[e4] += f4{g[d], g[d + 1], g[d + 2], g[d + 3]};
+      }
+    } else {
+      for (int e = t; e < n; e += CTXB_T) dst[e] += g[e % D];
+    }
+  };
+  if (f.Fn > 0) bcast_add(a.dnum + (long)b * f.num_ld, f.Fn, sg[0]);
+  if (f.Fm > 0) bcast_add(a.dmask + (long)b * f.mask_ld, f.Fm, sg[1]);
   const int fc0 = 1 + (f.Fn > 0) + (f.Fm > 0);
   const int n = f.Fc * D;
   for (int e = t; e < n; e += CTXB_T) {
