@@ -72,18 +72,36 @@ def make_batch(B, Fn, Fm, cards, L, vocab, seed, pad_id=0, edge_rows=True, logno
     return dict(X_num=X_num, X_mask=X_mask, X_cat=X_cat, seq=seq, y=y, groups=groups)
 
 
+NPROJ = 8      # Gaussian projections per fingerprint: a statistical estimate of ||got - ref||
+
+
 def fingerprint(a: np.ndarray, seed: int = 7, n: int = 2048):
-    """Size-independent summary: sampled elements + float64 sum / sumsq / random projection."""
+    """Size-independent summary: sampled elements + float64 sum / sumsq / random projection, plus
+    NPROJ Gaussian projections ``projs``: for d = got - ref, (R got - projs)_i ~ N(0, ||d||^2), so
+    the projections estimate the norm of the difference without storing ref."""
     a = np.asarray(a, dtype=np.float32).ravel()
     r = np.random.default_rng(seed + a.size)
     idx = np.sort(r.choice(a.size, size=min(n, a.size), replace=False)).astype(np.int64)
     proj = r.standard_normal(a.size).astype(np.float32)
     a64 = a.astype(np.float64)
     return dict(idx=idx, vals=a[idx], sum=a64.sum(), sumsq=(a64 * a64).sum(),
-                proj=float(a64 @ proj.astype(np.float64)))
+                proj=float(a64 @ proj.astype(np.float64)), projs=project(a64))
 
 
 def fingerprint_proj_vec(size: int, seed: int = 7):
     r = np.random.default_rng(seed + size)
     r.choice(size, size=min(2048, size), replace=False)
     return r.standard_normal(size).astype(np.float32)
+
+
+def project(a: np.ndarray, seed: int = 11, chunk: int = 1 << 20) -> np.ndarray:
+    """R @ a (float64) for the (NPROJ, a.size) standard-normal matrix R of ``seed`` and a.size,
+    generated in column chunks so large tensors never materialise R."""
+    a = np.asarray(a, dtype=np.float64).ravel()
+    r = np.random.default_rng(seed * 7919 + a.size)
+    out = np.zeros(NPROJ, np.float64)
+    for c0 in range(0, a.size, chunk):
+        c1 = min(a.size, c0 + chunk)
+        R = r.standard_normal((NPROJ, c1 - c0), dtype=np.float32)
+        out += R.astype(np.float64) @ a[c0:c1]
+    return out

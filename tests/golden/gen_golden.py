@@ -43,6 +43,8 @@ from oracle.model import (SITE_DARE, SITE_EMB, SITE_FC, SITE_MLP0, SITE_QNN,  # 
                           make_arch, site_attn, site_ffn)
 
 FULL_LIMIT = 40_000     # tensors up to this many elements are stored in full
+ALLOW_EPS = 1e-5        # relative gradient perturbation of the update-sensitivity replays (update_allowance)
+ALLOW_REPLAYS = 2
 
 
 def load_ref():
@@ -99,7 +101,9 @@ class DropPatch:
         F.dropout = self.orig
 
 
-def put(store, name, a, full=None):
+def put(store, name, a, full=None, rows=None):
+    """Store ``a`` in full when small, else its fingerprint (oracle/synth.py); for an embedding table
+    also the rows the fixture's batches touch (``rows``), in full: ``name@rows`` / ``name@rowvals``."""
     a = np.asarray(a)
     if full is None:
         full = a.size <= FULL_LIMIT
@@ -108,6 +112,74 @@ def put(store, name, a, full=None):
     else:
         for k, v in synth.fingerprint(a).items():
             store[f"{name}@{k}"] = np.asarray(v)
+        if rows is not None:
+            store[f"{name}@rows"] = np.asarray(rows, np.int64)
+            store[f"{name}@rowvals"] = a.reshape(a.shape[0], -1)[rows]
+
+
+def adamw_replay(P0, gsteps, lrs, wd, ema_cfg, eps_rel, seed):
+    """torch.optim.AdamW's single-tensor step (decoupled wd; torch/optim/adam.py) + ModelEMA.update
+    (src/utils/ema.py:92-131) replayed from P0 over recorded clipped gradients, each nonzero gradient
+    element perturbed by N(0, (eps_rel * rms(g))^2) -- a stand-in for another implementation whose
+    gradients differ from the reference's by reduction-order rounding of relative size eps_rel."""
+    from oracle.model import ema_decay
+    gen = torch.Generator().manual_seed(seed)
+    P = {k: torch.from_numpy(v.copy()) for k, v in P0.items()}
+    m, v = {}, {}
+    sh = {k: t.clone() for k, t in P.items()} if ema_cfg else None
+    for t, (gs, lr) in enumerate(zip(gsteps, lrs)):
+        bc1, bc2 = 1 - 0.9 ** (t + 1), 1 - 0.999 ** (t + 1)
+        for k, g in gs.items():
+            if eps_rel > 0:
+                nz = g != 0
+                rms = float(g[nz].pow(2).mean().sqrt()) if bool(nz.any()) else 0.0
+                g = g + torch.randn(g.shape, generator=gen) * (eps_rel * rms) * nz
+            p = P[k]
+            mk, vk = m.setdefault(k, torch.zeros_like(p)), v.setdefault(k, torch.zeros_like(p))
+            p.mul_(1 - lr * wd)
+            mk.lerp_(g, 1 - 0.9)
+            vk.mul_(0.999).addcmul_(g, g, value=1 - 0.999)
+            p.addcdiv_(mk, (vk.sqrt() / bc2 ** 0.5).add_(1e-8), value=-(lr / bc1))
+        if sh is not None:
+            d = ema_decay(float(ema_cfg.get("decay", 0.999)), int(ema_cfg.get("warmup_steps", 0)),
+                          str(ema_cfg.get("warmup_type", "linear")), t)
+            for k in sh:
+                sh[k].mul_(d).add_(P[k], alpha=1.0 - d)
+    return P, sh
+
+
+def update_allowance(P0, gsteps, lrs, wd, ema_cfg, pT, shT):
+    """Per-element allowance for comparing the update pT - p0 (and the EMA shadow's): 3x the largest
+    deviation over ALLOW_REPLAYS replays with ALLOW_EPS-perturbed gradients.  AdamW's
+    m_hat / (sqrt(v_hat) + eps) is ill-conditioned where the (clipped) gradient is within a few eps of 0
+    or is a cancellation residue far below its tensor's scale; the replays measure that conditioning
+    element by element instead of guessing it.  The unperturbed replay must reproduce the reference."""
+    P, sh = adamw_replay(P0, gsteps, lrs, wd, ema_cfg, 0.0, 0)
+    for k in P:
+        assert np.array_equal(P[k].numpy(), pT[k]), f"AdamW replay differs from the reference on {k}"
+    al_p = {k: np.zeros(v.size) for k, v in P0.items()}
+    al_e = {k: np.zeros(v.size) for k, v in P0.items()} if sh is not None else {}
+    for r in range(ALLOW_REPLAYS):
+        Pr, shr = adamw_replay(P0, gsteps, lrs, wd, ema_cfg, ALLOW_EPS, 1000 + r)
+        for k in P:
+            al_p[k] = np.maximum(al_p[k], 3 * np.abs(Pr[k].numpy().astype(np.float64) - pT[k]).ravel())
+            if sh is not None:
+                al_e[k] = np.maximum(al_e[k], 3 * np.abs(shr[k].numpy().astype(np.float64) - shT[k]).ravel())
+    return al_p, al_e
+
+
+def put_allow(store, name, allow, rows, shape):
+    """An allowance vector in full (small tensors) or where the checks read it: at the fingerprint's
+    sampled elements (``@idx``), at the touched rows (``@rows``), and its L2 norm (``@norm``)."""
+    allow = np.asarray(allow, np.float64).ravel()
+    if allow.size <= FULL_LIMIT:
+        store[name] = allow.astype(np.float32)
+        return
+    idx = synth.fingerprint(np.zeros(allow.size, np.float32))["idx"]
+    store[f"{name}@idx"] = allow[idx].astype(np.float32)
+    if rows is not None:
+        store[f"{name}@rows"] = allow.reshape(shape[0], -1)[rows].astype(np.float32)
+    store[f"{name}@norm"] = np.float64(np.linalg.norm(allow))
 
 
 def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, store_params, train_cfg,
@@ -152,12 +224,21 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
     ref_dare.DARE.topk_select = topk_rec_wrap
     patch = DropPatch(A)
     spe = train_cfg["steps_per_epoch"]
+    touched = {}     # table key -> rows any batch of the fixture reads
+    gsteps = []      # the clipped gradients AdamW consumed at each step
+
+    def touch(key, ids):
+        touched[key] = np.union1d(touched.get(key, np.zeros(0, np.int64)), np.asarray(ids, np.int64).ravel())
     try:
         for t in range(steps):
             bt = synth.make_batch(B, Fn, Fm, list(cat_cards.values()), L, vocab, bseed + t,
                                   pad_id=A.pad_id, lognormal=lognormal)
             if y_override is not None and y_override.get(t) is not None:
                 bt["y"] = np.full(B, y_override[t], np.int8)
+            touch("dare.emb_att.weight", bt["seq"])
+            touch("dare.emb_rep.weight", bt["seq"])
+            for i, c in enumerate(cat_cols):
+                touch(f"cat_embs.{c}.weight", bt["X_cat"][:, i])
             for k, v in bt.items():
                 store[f"in{t}/{k}"] = v
             batch = {"X_num": torch.from_numpy(bt["X_num"]).float(),
@@ -186,7 +267,7 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
                     if p.grad is None:
                         continue
                     names.append(k)
-                    put(store, f"grad0/{k}", p.grad.numpy().copy())
+                    put(store, f"grad0/{k}", p.grad.numpy().copy(), rows=touched.get(k))
                 meta["grad_keys"] = names
             gn = nn.utils.clip_grad_norm_(model.parameters(), train_cfg["clip"]) if train_cfg["clip"] > 0 else None
             store[f"out{t}/logits"] = logits.detach().numpy()
@@ -197,17 +278,31 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
             store[f"out{t}/topk_idx"] = topk_rec["idx"].numpy().astype(np.int32)
             store[f"out{t}/topk_vals"] = topk_rec["vals"].numpy()
             store[f"out{t}/query"] = topk_rec["query"].numpy()
+            gsteps.append({k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None})
             opt.step()
             if ema is not None:
                 ema.update(model, t + 1)
+        shadow = dict(ema.shadow_params) if ema is not None else {}
+        # per-element allowances for the update comparisons (see update_allowance)
+        pT = {k: p.detach().numpy() for k, p in model.named_parameters()}
+        allow_p, allow_e = update_allowance(P0, gsteps, meta["lrs"], train_cfg["wd"], cfg.get("ema") if ema else None,
+                                            pT, {k: v.numpy() for k, v in shadow.items()})
         for k, p in model.named_parameters():
+            put_allow(store, f"dTallow/{k}", allow_p[k], touched.get(k), P0[k].shape)
+            if k in allow_e:
+                put_allow(store, f"demaTallow/{k}", allow_e[k], touched.get(k), P0[k].shape)
+            rows = touched.get(k)
             put(store, f"pT/{k}", p.detach().numpy())
+            # the update itself, dT = pT - p0: what the parity tests compare norm-wise
+            put(store, f"dT/{k}", p.detach().numpy().astype(np.float64) - P0[k].astype(np.float64), rows=rows)
             if p in opt.state and len(opt.state[p]):
-                put(store, f"mT/{k}", opt.state[p]["exp_avg"].numpy())
-                put(store, f"vT/{k}", opt.state[p]["exp_avg_sq"].numpy())
+                put(store, f"mT/{k}", opt.state[p]["exp_avg"].numpy(), rows=rows)
+                put(store, f"vT/{k}", opt.state[p]["exp_avg_sq"].numpy(), rows=rows)
         if ema is not None:
             for k, v in ema.shadow_params.items():
                 put(store, f"emaT/{k}", v.numpy())
+                put(store, f"demaT/{k}", v.numpy().astype(np.float64) - P0[k].astype(np.float64),
+                    rows=touched.get(k))
         # eval forward with the final params on the last batch
         model.eval()
         patch.calls = 0
@@ -261,8 +356,103 @@ def k148_cfg():
     return cfg, list(c["data"]["cat_cols"])
 
 
+def cfg3_cfg():
+    """cfgs/dare_qnn_next_k100_s1.yaml (BASELINE config 3: K=100, query S1, EMA on) with the cfg2
+    overrides D=32, L=100."""
+    import yaml
+    c = yaml.safe_load(open(os.path.join(REF, "cfgs/dare_qnn_next_k100_s1.yaml")))
+    cfg = {"model": copy.deepcopy(c["model"]), "sequence": copy.deepcopy(c["sequence"]),
+           "ema": copy.deepcopy(c["ema"])}
+    cfg["model"]["emb_dim"] = 32
+    cfg["sequence"]["max_len"] = 100
+    return cfg, list(c["data"]["cat_cols"])
+
+
+def k120_cfg():
+    """cfgs/v3_k120_s1.yaml as-is (D=64, K=120, S1) with 2 of its 4 encoder layers and a narrower MLP."""
+    import yaml
+    c = yaml.safe_load(open(os.path.join(REF, "cfgs/v3_k120_s1.yaml")))
+    cfg = {"model": copy.deepcopy(c["model"]), "sequence": copy.deepcopy(c["sequence"])}
+    cfg["sequence"]["tfm"]["n_layers"] = 2
+    cfg["model"]["qnn_alpha"]["mlp_hidden"] = [64, 32]
+    return cfg, list(c["data"]["cat_cols"])
+
+
+def gen_infer():
+    """Fold-ensemble + calibration fixtures: the reference's own
+    ``src.utils.metrics.ensemble_probs`` (src/utils/metrics.py:48-86) and ``src.utils.calibration.Calibrator``
+    (src/utils/calibration.py:54-110) run on fixed inputs; writes tests/golden/infer_ref.npz."""
+    from src.utils.calibration import Calibrator
+    from src.utils.metrics import ensemble_probs
+    r = np.random.default_rng(4242)
+    store = {}
+    B = 257
+    methods = ["mean", "geom_mean", "logit_mean", "median", "trim_mean", "weighted", "val_weighted", "rank_avg"]
+    meta = {"B": B, "Ms": [2, 3, 4, 5], "methods": methods, "trim_ratio": 0.34, "val_weight_temperature": 5.0}
+    for M in meta["Ms"]:
+        z = (2.0 * r.standard_normal((M, B))).astype(np.float32)
+        z[:, 5] = 30.0                      # saturated: every model clips to 1 - 1e-7
+        z[:, 6] = -30.0
+        z[1:, 7] = z[0, 7]                  # equal across models (median / trim ties)
+        # the reference's inference loop clamps each model's probabilities (src/infer.py:122);
+        # no exact ties inside one model, so rank_avg's argsort order is unambiguous
+        p = torch.clamp(torch.sigmoid(torch.from_numpy(z)), 1e-7, 1.0 - 1e-7)
+        assert all(torch.unique(p[i]).numel() == B for i in range(M))
+        p_list = [p[i].clone() for i in range(M)]
+        scores = r.uniform(0.30, 0.36, M).astype(np.float32)
+        weights = r.uniform(0.1, 1.0, M).astype(np.float32)
+        store[f"ens{M}/p"] = p.numpy()
+        store[f"ens{M}/scores"] = scores
+        store[f"ens{M}/weights"] = weights
+        for method in methods:
+            w, use = None, method
+            if method == "val_weighted":     # src/infer.py:135-149
+                w = torch.softmax(torch.from_numpy(scores) / max(1e-6, meta["val_weight_temperature"]), dim=0)
+                use = "weighted"
+            elif method == "weighted":       # src/infer.py:150-154
+                w = torch.from_numpy(weights)
+            try:
+                out = ensemble_probs(use, p_list, weights=w, trim_ratio=meta["trim_ratio"])
+            except RuntimeError as e:
+                # rank_avg: _rank_avg_stack scatters an int64 arange into a float tensor
+                # (src/utils/metrics.py:43), which torch rejects -- the reference cannot run it
+                meta.setdefault("raises", {})[method] = str(e).splitlines()[0]
+                continue
+            store[f"ens{M}/{method}"] = out.numpy()
+    # calibration: logits from a miscalibrated model, labels drawn from a sharper one
+    n = 6000
+    z = (1.5 * r.standard_normal(n) - 1.0).astype(np.float32)
+    y = (r.random(n) < 1.0 / (1.0 + np.exp(-(0.6 * z - 1.5)))).astype(np.int64)
+    zq = np.concatenate([np.linspace(-60, 60, 241), z[:500]]).astype(np.float32)
+    store["cal/z"], store["cal/y"], store["cal/zq"] = z, y, zq
+    zf = np.round(z).clip(-2, 2).astype(np.float32)        # 5 distinct values: isotonic falls back
+    store["cal/z_few"] = zf
+    cases = [("temperature", z), ("isotonic", z), ("temperature+isotonic", z), ("isotonic", zf),
+             ("temperature+isotonic", zf)]
+    meta["cal_cases"] = []
+    for i, (method, zz) in enumerate(cases):
+        cal = Calibrator(method=method, lr=0.05, iters=200)
+        cal.fit(zz, y)
+        tag = f"cal{i}"
+        meta["cal_cases"].append({"tag": tag, "method": method, "few": zz is zf})
+        if cal.temp_scaler is not None:
+            T = torch.clamp(torch.exp(cal.temp_scaler.log_temp.detach()), cal.clamp_T[0], cal.clamp_T[1])
+            store[f"{tag}/T"] = np.float64(float(T))
+        if cal.iso is not None:
+            store[f"{tag}/iso_x"] = np.asarray(cal.iso.X_thresholds_, np.float64)
+            store[f"{tag}/iso_y"] = np.asarray(cal.iso.y_thresholds_, np.float64)
+        store[f"{tag}/pq"] = cal.predict_proba(zq)
+    store["meta"] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, "infer_ref.npz")
+    np.savez_compressed(path, **store)
+    print(f"wrote {path}: {os.path.getsize(path) / 1e6:.2f} MB, {len(store)} arrays")
+
+
 def main():
     torch.set_num_threads(8)
+    if "--infer-only" in sys.argv:
+        gen_infer()
+        return
     tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
     cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
     run_case("tiny_concat", tiny_cfg(), B=64, L=32, vocab=5000, Fn=6, Fm=6, cat_cards=cards, steps=3,
@@ -275,14 +465,22 @@ def main():
     run_case("base_fc", tiny_cfg(query_mode="S1", qnn=False, tb=False, K=20, ema=False), B=40, L=40,
              vocab=4000, Fn=4, Fm=4, cat_cards=cards, steps=2, pseed=14, bseed=400, store_params=True,
              train_cfg=dict(tr, clip=1.0))
+    # lr 3e-3 without warmup: the update (~3e-3 per step) spans ~1e4 fp32 ulps of the |p| ~ 1 table
+    # entries it moves, so pT - p0 can be compared at 1e-4 (at warmup lrs ~1e-5 it would be ~100 ulps)
+    big_tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=0, epochs=8)
     cfg2, cols = cfg2_cfg()
     run_case("cfg2_dims", cfg2, B=8, L=100, vocab=3000, Fn=82, Fm=82, cat_cards={c: 200 for c in cols},
-             steps=1, pseed=21, bseed=500, store_params=False,
-             train_cfg=dict(lr=3e-4, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=2, epochs=8))
+             steps=2, pseed=21, bseed=500, store_params=False, train_cfg=big_tr)
+    cfg3, cols3 = cfg3_cfg()
+    run_case("cfg3_dims", cfg3, B=8, L=100, vocab=3000, Fn=82, Fm=82, cat_cards={c: 200 for c in cols3},
+             steps=2, pseed=41, bseed=700, store_params=False, train_cfg=big_tr)
     cfg4, cols4 = k148_cfg()
     run_case("k148", cfg4, B=4, L=160, vocab=2000, Fn=10, Fm=10, cat_cards={c: 100 for c in cols4[:6]},
-             steps=1, pseed=31, bseed=600, store_params=False,
-             train_cfg=dict(lr=3e-4, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=2, epochs=8))
+             steps=2, pseed=31, bseed=600, store_params=False, train_cfg=big_tr)
+    cfg5, cols5 = k120_cfg()
+    run_case("k120", cfg5, B=6, L=150, vocab=2000, Fn=10, Fm=10, cat_cards={c: 100 for c in cols5[:6]},
+             steps=2, pseed=51, bseed=800, store_params=False, train_cfg=big_tr)
+    gen_infer()
 
 
 if __name__ == "__main__":

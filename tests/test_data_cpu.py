@@ -2,6 +2,7 @@
 import json
 
 import numpy as np
+import pytest
 import torch
 
 from tossctr.data import (ShardedDataset, collate_sharded, load_labels_groups_for_split, synth_rows,
@@ -41,3 +42,39 @@ def test_synth_rows_layout():
             assert nz[-1] == 29 and np.all(row[nz[0]:] != 0)
     assert (a["X_num"][a["X_mask"].astype(bool)] == 0).all()
     assert a["X_cat"][:, 0].max() < 10 and a["X_cat"][:, 1].max() < 20
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("n", [1, 7, 96, 100, 257])
+def test_rank_slices_cover_epoch_once(n, world):
+    """Data-parallel epoch split (tossctr.train.rank_slice): every row of the permutation is trained
+    exactly once per epoch, full steps give each rank bs rows, the last step's remainder is spread over
+    the ranks; at world 1 the batches are the reference's (ceil(n / bs) of bs rows, the last short)."""
+    import math
+    from tossctr.train import rank_slice
+    bs = 16
+    steps = math.ceil(n / (bs * world))
+    seen = []
+    for step in range(steps):
+        sizes = []
+        for r in range(world):
+            lo, k = rank_slice(n, bs, world, r, step)
+            seen.extend(range(lo, lo + k))
+            sizes.append(k)
+        assert max(sizes) - min(sizes) <= (0 if step < steps - 1 else 1) or step == steps - 1
+        if step < steps - 1:
+            assert sizes == [bs] * world
+    assert sorted(seen) == list(range(n))
+    if world == 1:
+        assert [rank_slice(n, bs, 1, 0, s) for s in range(steps)] == \
+            [(s * bs, min(bs, n - s * bs)) for s in range(steps)]
+
+
+def test_unsupported_options_raise():
+    from tossctr.train import check_supported
+    check_supported({"amp": "none"})
+    check_supported({"amp": "bf16", "sampler": {"type": "None"}})
+    with pytest.raises(NotImplementedError):
+        check_supported({"amp": "fp16"})
+    with pytest.raises(NotImplementedError):
+        check_supported({"amp": "none", "sampler": {"type": "balanced"}})

@@ -41,3 +41,33 @@ def test_calibrator_params():
 
     T, ix, iy = calibrator_params(RefCal())
     assert T == pytest.approx(5.0) and list(ix) == pytest.approx([0.2, 0.4, 0.9]) and len(iy) == 3
+
+
+def _infer_fixture():
+    import json
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "infer_ref.npz"))
+    return z, json.loads(str(z["meta"]))
+
+
+@pytest.mark.parametrize("i", range(5))
+def test_host_calibrator_matches_reference(i):
+    """tossctr.metrics.Calibrator (host path) vs the reference's own Calibrator run on the same logits
+    (tests/golden/infer_ref.npz, gen_golden.gen_infer; src/utils/calibration.py:54-110): fitted
+    temperature, isotonic thresholds (incl. the min_iso_nodes fallback) and predict_proba."""
+    from tossctr.metrics import Calibrator
+    z, meta = _infer_fixture()
+    case = meta["cal_cases"][i]
+    tag = case["tag"]
+    logits = z["cal/z_few"] if case["few"] else z["cal/z"]
+    cal = Calibrator(method=case["method"], lr=0.05, iters=200).fit(logits, z["cal/y"])
+    if f"{tag}/T" in z.files:
+        assert cal.temperature == pytest.approx(float(z[f"{tag}/T"]), rel=1e-6)
+    else:
+        assert cal.temperature is None
+    if f"{tag}/iso_x" in z.files:
+        np.testing.assert_allclose(cal.iso.X_thresholds_, z[f"{tag}/iso_x"], rtol=1e-7)
+        np.testing.assert_allclose(cal.iso.y_thresholds_, z[f"{tag}/iso_y"], rtol=1e-7)
+    else:
+        assert cal.iso is None
+    np.testing.assert_allclose(cal.predict_proba(z["cal/zq"]), z[f"{tag}/pq"], rtol=1e-6, atol=1e-9)

@@ -150,6 +150,7 @@ class Engine:
         self._splitk = None
         self._gen = 0
         self.stream = None
+        self.last = None
         self.lazy = None     # a lazy FusedAdamW: table rows are brought current before they are read
         # fused FFN kernels (ffn.hip) when the shape allows; the GEMM path otherwise
         # row-streaming in/out-projection kernels (rowgemm.hip) for the D they are built for
@@ -402,6 +403,7 @@ class Engine:
             self._gen += 1
             sv.update(gen=self._gen, xF=xF, cat_e=cat_e, ctx=ctx, hq=hq, query=query, idx=idx, tok=tok, vals=vals,
                       xs=xs, layers=layers, w=w, u=u, aux=aux, logits=logits, prob=prob, fcin=fcin, qnn=q, W=W)
+            self.last = sv      # the most recent training forward's saved tensors (top-K indices etc.)
         return logits, prob, aux, (sv if save else None)
 
     def _table_views(self, X_cat, seq):

@@ -147,6 +147,23 @@ def ensemble(method, P, weights=None, trim_ratio=0.0):
     return out
 
 
+def resolve_weights(method, scores, ens_cfg, n_models, device):
+    """(method used, weights) as src/infer.py:130-156 resolves them: ``val_weighted`` -> softmax of the
+    fold scores / val_weight_temperature with method "weighted"; ``weighted`` -> the configured weights
+    (one per model); anything else unweighted.  A single model ignores the ensemble settings."""
+    if n_models <= 1:
+        return method, None
+    if method == "val_weighted":
+        temp = float(ens_cfg.get("val_weight_temperature", 10.0))
+        s = torch.tensor(scores, dtype=torch.float32, device=device)
+        return "weighted", torch.softmax(s / max(1e-6, temp), dim=0)
+    if method == "weighted":
+        w_cfg = ens_cfg.get("weights", [])
+        assert len(w_cfg) == n_models, "weights length must match #folds/models"
+        return "weighted", torch.tensor(w_cfg, dtype=torch.float32, device=device)
+    return method, None
+
+
 def _read_ids(manifest):
     ids = []
     for m in manifest["shards"]:
@@ -199,16 +216,7 @@ def main(cfg_path_or_dict, device=None):
         calibs.append(_Calib(state.get("calibrator"), device))
     ens = cfg.get("ensemble", {}) or {}
     method, trim = ens.get("method", "logit_mean"), float(ens.get("trim_ratio", 0.0))
-    weights = None
-    if len(models) > 1:
-        if method == "val_weighted":                                            # src/infer.py:135-149
-            temp = float(ens.get("val_weight_temperature", 10.0))
-            s = torch.tensor([sc for _, sc in entries], dtype=torch.float32, device=device)
-            weights, method = torch.softmax(s / max(1e-6, temp), dim=0), "weighted"
-        elif method == "weighted":
-            w_cfg = ens.get("weights", [])
-            assert len(w_cfg) == len(models), "weights length must match #folds/models"
-            weights = torch.tensor(w_cfg, dtype=torch.float32, device=device)
+    method, weights = resolve_weights(method, [sc for _, sc in entries], ens, len(models), device)
     cal_on = bool(cfg.get("calibration", {}).get("enabled", False))
     store = DeviceShards(man_path, device)
     n, bs = store.rows, int(cfg["train"]["batch_size"])

@@ -138,11 +138,15 @@ class Calibrator:
             w_neg = 1.0 - w_pos
 
         def closure():
+            # the reference's autograd graph exactly (src/utils/calibration.py:36-49): T is formed twice,
+            # once for the scaled logits and once for the regulariser, so the two gradient paths through
+            # exp(log_temp) are summed in the same order and LBFGS follows the same iterates bitwise
             opt.zero_grad()
+            p = torch.sigmoid(z / self._T(log_temp)).clamp(1e-7, 1 - 1e-7)
+            loss_pos = -(t * torch.log(p)).mean() / w_pos
+            loss_neg = -((1 - t) * torch.log(1 - p)).mean() / w_neg
             T = self._T(log_temp)
-            p = torch.sigmoid(z / T).clamp(1e-7, 1 - 1e-7)
-            loss = 0.5 * (-(t * torch.log(p)).mean() / w_pos + -((1 - t) * torch.log(1 - p)).mean() / w_neg)
-            loss = loss + self.l2_reg * (T - 1.0) ** 2
+            loss = 0.5 * (loss_pos + loss_neg) + self.l2_reg * (T - 1.0) ** 2
             loss.backward()
             return loss
         opt.step(closure)
@@ -165,7 +169,7 @@ class Calibrator:
                 self._fit_temperature(z, y)
         if self.method in ("isotonic", "temperature+isotonic"):
             from sklearn.isotonic import IsotonicRegression
-            p = _sigmoid_np(z / self.temperature if self.log_temp is not None else z)
+            p = _sigmoid_np(self._scaled(z))
             n_pos, n_neg = max(1, int(y.sum())), max(1, int((y == 0).sum()))
             sw = np.where(y == 1, 0.5 / n_pos, 0.5 / n_neg)
             if np.unique(p).size < self.min_iso_nodes:
@@ -175,11 +179,17 @@ class Calibrator:
                 self.iso.fit(p, y, sample_weight=sw)
         return self
 
+    def _scaled(self, z):
+        """The temperature-scaled logits as the reference forms them: TemperatureScaler on a float32
+        tensor (src/utils/calibration.py:81-83,104-106), so the sigmoid after it runs in float32; the raw
+        float64 logits when no temperature was fitted."""
+        if self.log_temp is None:
+            return z
+        return z.astype(np.float32) / np.float32(self.temperature)
+
     def predict_proba(self, logits):
         z = np.asarray(logits, dtype=np.float64)
-        if self.log_temp is not None:
-            z = (z.astype(np.float32) / np.float32(self.temperature)).astype(np.float64)
-        p = _sigmoid_np(z)
+        p = _sigmoid_np(self._scaled(z))
         if self.iso is not None:
             p = self.iso.predict(np.clip(p, 1e-7, 1 - 1e-7))
         return np.clip(p, 1e-7, 1 - 1e-7)

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import copy
+import gc
 import json
 import math
 import os
@@ -48,6 +49,17 @@ def set_seed(seed: int, deterministic: bool = True):
     torch.manual_seed(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
+
+
+def check_supported(cfg):
+    """Refuse configuration the fused path does not implement instead of silently training something
+    else: ``sampler.type: balanced`` (src/train.py:95-106; no reference yaml enables it) and an ``amp``
+    mode other than none/bf16 (fp16 + GradScaler, src/train.py:133-139,185-190)."""
+    amp = str(cfg.get("amp", "none")).lower()
+    if amp not in ("none", "bf16"):
+        raise NotImplementedError(f"amp: {cfg.get('amp')!r} -- the fused MI355X step runs fp32 or bf16 (amp: bf16)")
+    if str((cfg.get("sampler", {}) or {}).get("type", "") or "").lower() == "balanced":
+        raise NotImplementedError("sampler.type: balanced is not supported (no reference config enables it)")
 
 
 def _dist():
@@ -114,6 +126,35 @@ def predict_logits(model, store, idx_np, bs, as_tensor=False):
     return out[:n].contiguous() if as_tensor else out[:n].cpu().numpy()
 
 
+def release(model, opt, ema):
+    """Break the model <-> optimizer / EMA reference cycle (model._fused_opt, opt.model, engine.lazy,
+    shards.lazy, ema.model) so the fold's arena, moments and EMA shadow are freed when the last
+    reference goes, not at some later gen-2 collection (src/train.py:280-316 _free_fold)."""
+    model.__dict__.pop("_fused_opt", None)
+    model.engine.lazy = None
+    model.engine.last = None
+    if model.shards is not None:
+        model.shards.lazy = None
+    if opt is not None:
+        opt.model = opt.engine = opt.shards = None
+    if ema is not None:
+        ema.model = None
+
+
+def rank_slice(n, bs, world, rank, step):
+    """(start, rows) of rank ``rank``'s batch at ``step`` of an epoch over n permuted rows: every full
+    step gives each rank bs consecutive rows (rank-major); the epoch's last, short step splits its
+    remainder as evenly as possible (the first remainder % world ranks take one row more), so no row
+    is seen twice in an epoch (single GPU: the reference's ceil(n / bs) batches, the last one short)."""
+    g = bs * world
+    lo = step * g
+    rem = min(g, n - lo)
+    if rem >= g:
+        return lo + rank * bs, bs
+    base, extra = divmod(max(0, rem), world)
+    return lo + rank * base + min(rank, extra), base + (1 if rank < extra else 0)
+
+
 def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None, device=None):
     """src/train.py:92-317 (same signature + optional pre-staged ``store``). Returns (best_state, best_score)."""
     from .configs import cat_cardinals  # noqa: F401
@@ -125,6 +166,7 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
     device = device or torch.device("cuda", torch.cuda.current_device())
+    check_supported(cfg)
     bs, epochs, warmup = cfg["train"]["batch_size"], cfg["train"]["epochs"], cfg["train"]["warmup_epochs"]
     cat_cols = cfg["data"]["cat_cols"]
     store = store or DeviceShards(manifest_path, device)
@@ -153,14 +195,14 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
         loss_sum = torch.zeros((), device=device)
         for step in range(steps_per_epoch):
             global_step += 1
-            lo = (step * world + rank) * bs
-            idx = perm[lo:lo + bs]
-            if idx.numel() == 0:
-                idx = perm[:bs]
+            lo, n_rows = rank_slice(len(idx_tr), bs, world, rank, step)
+            # a rank left without rows on the last step still joins the step's collectives with one
+            # row whose loss gradient is zeroed: it adds nothing to the averaged gradient
+            idx = perm[lo:lo + n_rows] if n_rows else perm[:1]
             inputs, y = store.batch(idx)
             opt.param_groups[0]["lr"] = cosine_warmup_lr(epoch - 1, step, steps_per_epoch, cfg["train"]["lr"], warmup,
                                                          epochs)
-            loss_sum += model.train_step(inputs, y, opt, global_step=global_step)[0]
+            loss_sum += model.train_step(inputs, y, opt, global_step=global_step, contribute=n_rows > 0)[0]
         tr_loss = float(loss_sum.item()) / max(1, steps_per_epoch)
         use_ema_eval = ema is not None and cfg["ema"].get("eval_with_ema", True)
         if use_ema_eval:
@@ -179,7 +221,10 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
                              iters=int(cc.get("iters", 200))).fit(z_raw, y_true, device_metrics=dmet,
                                                                   z_dev=z_dev, y_dev=y_dev)
             if cal.iso is None:
-                ap_cal, wll_cal, score_cal = dmet.final_score(z_dev, y_dev, T=cal.temperature)
+                # predict_proba clips even when neither a temperature nor an isotonic map was fitted
+                # (isotonic fallback below min_iso_nodes): score the clipped path with T = 1 then
+                T = cal.temperature if cal.temperature is not None else 1.0
+                ap_cal, wll_cal, score_cal = dmet.final_score(z_dev, y_dev, T=T)
             else:                       # isotonic map: host (sklearn), as the reference
                 ap_cal, wll_cal, score_cal = final_score(y_true, cal.predict_proba(z_raw))
         if rank == 0:
@@ -207,7 +252,9 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
             wait += 1
             if wait >= cfg["train"]["early_stop_patience"]:
                 break
+    release(model, opt, ema)
     del model, opt, ema
+    gc.collect()                    # src/train.py:312
     torch.cuda.empty_cache()
     return best_state, best_score
 

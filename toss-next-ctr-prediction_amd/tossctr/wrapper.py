@@ -218,14 +218,21 @@ class CTRModel(nn.Module):
         return logits.clone(), prob.clone(), aux.clone()
 
     # ------------------------------------------------------------------ fused training step
-    def train_step(self, inputs, y, opt, global_step, seed=None):
+    def train_step(self, inputs, y, opt, global_step, seed=None, contribute=True):
         """One reference step (src/train.py:152-199): forward -> bce_wll_style(+aux) -> backward ->
         clip -> AdamW -> EMA, all on device, no host sync.  ``inputs`` = staged (X_num, X_mask, X_cat,
-        seq) device tensors (see ``stage``), ``y`` float labels on device.  Returns the loss (device)."""
+        seq) device tensors (see ``stage``), ``y`` float labels on device.  Returns the loss (device).
+        ``contribute=False`` (data parallel: a rank without rows on an epoch's last step) runs the step
+        with a zero loss gradient, so the rank joins the collectives but adds nothing to the gradient."""
         seed = self.next_seed() if seed is None else seed
         eng = self.engine
         _, _, _, sv = eng.forward(*inputs, training=True, seed=seed, save=True)
         loss, dz, daux = eng.loss(sv, y)
+        if not contribute:
+            loss.zero_()
+            dz.zero_()
+            if daux is not None:
+                daux.zero_()
         tg = eng.backward(sv, dz, daux)
         opt.step(tg, global_step)
         return loss
