@@ -135,6 +135,18 @@ class Fixture:
                           allow=f"{kind}allow/{key}")
 
 
+    def check_moment(self, kind, key, got, rtol=None):
+        """An Adam moment after the fixture's steps (kind "mT" / "vT"), norm-wise and elementwise at 2e-4
+        for m and 4e-4 for v (quadratic in the gradient: twice its relative error):
+        the gradient of step t > 0 is taken at parameters that already carry the earlier steps' (1e-5 ..
+        1e-4) deviations, and m sums the steps' gradients with cancellation where they oppose -- measured
+        GPU vs reference after two steps: up to 1.5e-4 (a one-element bias), 1.3e-4 (sampled v of the SE
+        fc.2 weight)."""
+        if rtol is None:
+            rtol = 2e-4 if kind == "mT" else 4e-4
+        return self.check(f"{kind}/{key}", got, rtol, 0.0)
+
+
 def close_enough(got, ref, rtol, atol, label, ulp=None, elem_rtol=None):
     """Norm-wise ||got - ref|| <= rtol ||ref|| (+ ||ulp||) AND elementwise
     |d| <= atol (+ ulp) + e*(10|ref| + max|ref|) with e = elem_rtol (default rtol)."""

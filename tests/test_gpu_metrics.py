@@ -46,8 +46,9 @@ def test_device_temperature_fit_matches_host_lbfgs():
     zd, yd = torch.from_numpy(z).cuda(), torch.from_numpy(y.astype(np.float32)).cuda()
     dev = Calibrator("temperature").fit(z, y, device_metrics=dm, z_dev=zd, y_dev=yd)
     assert abs(dev.temperature - host.temperature) <= 1e-4 * host.temperature, (dev.temperature, host.temperature)
-    # calibrated score on device == host predict_proba + final_score
+    # calibrated score on device == host predict_proba + final_score: both form float32 probabilities
+    # (the reference's datapath); the device expf and numpy's float32 exp may differ by an ulp
     got = dm.final_score(zd, yd, T=host.temperature)
     ref = final_score(y, host.predict_proba(z))
     for g, r in zip(got, ref):
-        assert abs(g - r) <= 1e-9 * max(1.0, abs(r)), (got, ref)
+        assert abs(g - r) <= 1e-6 * max(1.0, abs(r)), (got, ref)

@@ -108,7 +108,7 @@ def test_fold_teardown_frees_device_memory(tmp_path):
     from tossctr.train import train_one_fold
 
     class Quiet:
-        def row(self, **kw):
+        def row(self, *a, **kw):
             pass
         csv = scalars = row
 

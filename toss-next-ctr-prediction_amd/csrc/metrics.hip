@@ -3,7 +3,8 @@
 // between epochs over ~N/5 rows).
 //
 //   ctr_val_prob     p = sigmoid(z) in f64 (the loop's raw probabilities), or the calibrator's
-//                    p = clip(sigmoid(clip(z/T, +-50)), 1e-7, 1-1e-7) with z/T in f32 (calibration.py:102-110)
+//                    p = clip(sigmoid(clip(z/T, +-50)), 1e-7, 1-1e-7), all in f32 as the reference's
+//                    predict_proba computes it (calibration.py:102-110)
 //   ctr_ap_wll       sklearn average_precision_score on clip(nan_to_num(p), 1e-12, 1-1e-12) and the 50:50
 //                    weighted logloss: descending radix sort of the f64 probabilities (order-preserving
 //                    u64 keys) with the labels, tp = scan(labels), run-length groups of equal scores
@@ -61,9 +62,11 @@ __device__ __forceinline__ uint64_t order_key(double x) {    // u64 order == dou
 __global__ void val_prob_kernel(const float* __restrict__ z, int n, float T, int calibrated, double* __restrict__ p) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     if (calibrated) {
-      const double zt = fmin(fmax((double)(z[i] / T), -50.0), 50.0);
-      const double v = 1.0 / (1.0 + exp(-zt));
-      p[i] = fmin(fmax(v, 1e-7), 1.0 - 1e-7);
+      // the reference's predict_proba path is float32 end to end: TemperatureScaler on a float32 tensor,
+      // then _sigmoid_stable_numpy and np.clip on the float32 array (src/utils/calibration.py:104-110)
+      const float zt = fminf(fmaxf(z[i] / T, -50.f), 50.f);
+      const float v = 1.0f / (1.0f + expf(-zt));
+      p[i] = (double)fminf(fmaxf(v, 1e-7f), 1.0f - 1e-7f);
     } else {
       p[i] = 1.0 / (1.0 + exp(-(double)z[i]));
     }
