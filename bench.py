@@ -81,13 +81,84 @@ def kernel_work(name, a, B, ffn_M):
 def step_bytes_dense_equiv(a, B, L, with_ema):
     """SURVEY §8(d) algorithmic bytes of one reference-semantics step (dense AdamW/EMA over every
     parameter + the per-sample gather/row-grad traffic):
-        Bopt * (P_emb + P_dense) + B * [inp + 12 * (L*D + K*D + sum d_c)]."""
+        Bopt * (P_emb + P_dense) + B * [inp + 12 * (L*D + K*D + sum d_c)].
+    What a dense implementation must move; NOT this build's roofline (the exact-lazy tables move far
+    less, step_bytes_lazy)."""
     shapes = a.param_shapes()
     p_all = sum(int(np.prod(s)) for _, s, _ in shapes)
     bopt = 56 if with_ema else 44
+    return bopt * p_all + B * per_sample_bytes(a, L)
+
+
+def per_sample_bytes(a, L):
+    """SURVEY §8(d) per-sample term: on-disk inputs + fp32 row gather (4 B) and row-grad read-modify-write
+    (8 B) of the L att rows, K rep rows and sum d_c categorical floats."""
     inp = 4 * a.Fn + a.Fm + 4 * a.Fc + 4 * L + 1
-    per = inp + 12 * (L * a.D + a.K_eff(L) * a.D + sum(a.cat_dims))
-    return bopt * p_all + B * per
+    return inp + 12 * (L * a.D + a.K_eff(L) * a.D + sum(a.cat_dims))
+
+
+def step_bytes_lazy(a, B, L, opt, U, timed_steps, with_ema):
+    """Algorithmic HBM bytes of one step of THIS build (exact-lazy tables, SURVEY §8(d) row-lazy form,
+    with U measured in the run): B x per-sample term; the dense-parameter stream (read p, m, v, (e), grad,
+    write p, m, v, (e)); the forward's touch of the rows the batch reads (a row is brought current once:
+    read + write p, m, v, (e)); the real tick on the rows that get a gradient (same + the compact grad
+    row); and the run's final flush of every table row (same per element) spread over the timed steps.
+    U = {"seq_fwd": unique tokens read, "seq_bwd": unique top-K tokens (both DARE tables),
+    "cat_fwd"/"cat_bwd": unique (table, row) floats} -- rows, or floats for cat (sum of d_c)."""
+    ar = opt.arena
+    st = 32 if with_ema else 24          # p, m, v (, e) read + written, fp32
+    lo, hi = ar.nograd_range
+    dense = ar.n_dense_grad * (st + 4) + ((hi - lo) * 12 if with_ema else 0)
+    D = a.D
+    touch = (2 * U["seq_fwd"] * D + U["cat_fwd"]) * st
+    update = (2 * U["seq_bwd"] * D + U["cat_bwd"]) * (st + 4)
+    t0, t1 = ar.table_range
+    flush = (t1 - t0) * st / max(1, timed_steps)
+    return {"per_sample": B * per_sample_bytes(a, L), "dense_opt": dense, "touch": touch, "update": update,
+            "flush": flush}
+
+
+def fwd_flops_per_sample(a, L):
+    """Multiply-add = 2 FLOPs of the matrix products of one sample's forward (SURVEY §8(a) FLOP census:
+    21.5 MF at cfg2); the backward does twice that (input and weight gradients)."""
+    D, K = a.D, a.K_eff(L)
+    f = 2 * a.Fn * a.f_embed * D + 2 * a.Fm * a.f_embed * D + 2 * sum(a.cat_dims) * D
+    if a.query_mode != "S1":
+        f += 2 * a.nctx * D * D
+    f += 2 * L * D                                    # top-K scores
+    for _ in range(a.n_layers):
+        f += 2 * K * D * 3 * D + 2 * K * D * D        # in / out projections
+        f += 2 * 2 * K * K * D                        # scores + PV over all heads
+        f += 2 * 2 * K * D * a.ffn_hidden             # FFN
+    f += 2 * K * D + 2 * D                            # pool + aux head
+    if a.use_qnn:
+        FD, C = a.F * D, a.C
+        f += a.qh * (2 * a.F * D * a.qr + 2 * a.qr * a.qP)
+        dims = [FD + C] + list(a.mlp_hidden) + [1]
+        f += sum(2 * x * y for x, y in zip(dims[:-1], dims[1:]))
+    else:
+        nin = D * (1 + (a.Fn > 0) + (a.Fm > 0) + a.Fc)
+        f += 2 * nin * 512 + 2 * 512
+    return f
+
+
+def measure_unique(model, batch, tg):
+    """U of one step (step_bytes_lazy): unique tokens / categorical rows of the batch, and the unique
+    keys of its compact table gradients."""
+    a = model.arch
+    X_cat, seq = batch[2], batch[3]
+    seq_fwd = int(torch.unique(seq[seq != a.pad_id]).numel())
+    dims = torch.tensor(a.cat_dims, device=X_cat.device, dtype=torch.int64)
+    base = torch.tensor(np.cumsum([0] + a.cat_cards[:-1]), device=X_cat.device, dtype=torch.int64)
+    keys = torch.unique(X_cat.long() + base[None, :])
+    col = torch.searchsorted(base, keys, right=True) - 1
+    cat_fwd = int(dims[col].sum())
+    seq_bwd = int(tg["att"]["n_uniq"].item())
+    n_cat = int(tg["cat"]["n_uniq"].item())
+    ck = tg["cat"]["keys"][:n_cat].long()
+    col_b = torch.searchsorted(base, ck, right=True) - 1
+    cat_bwd = int(dims[col_b.clamp(0, len(a.cat_dims) - 1)].sum())
+    return {"seq_fwd": seq_fwd, "seq_bwd": seq_bwd, "cat_fwd": cat_fwd, "cat_bwd": cat_bwd}
 
 
 def opt_algorithmic_bytes(opt, with_ema):
@@ -109,16 +180,22 @@ def opt_algorithmic_bytes(opt, with_ema):
     return b
 
 
+PMC_ROUNDS = ("r02", "r01")      # newest committed PMC summaries first
+
+
 def pmc_traffic(name):
     """HBM bytes per launch of the entry point's kernel from the committed rocprofv3 PMC summaries
-    (profiles/r01/pmc_{fetch,write}.csv: separate --pmc FETCH_SIZE / WRITE_SIZE passes of this bench),
+    (profiles/r0N/pmc_{fetch,write}.csv, newest round: separate --pmc FETCH_SIZE / WRITE_SIZE passes of this bench),
     corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE counts half of wide streaming reads:
     x2).  None when the summaries are absent."""
     import csv
     bwd = ("ffn_bwd_cols_kernel", "ffn_bwd_kernel")       # the entry point's kernels, preferred first
     kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_kernel",)}.get(name)
-    base = os.path.join(REPO, "profiles", "r01")
     if kerns is None:
+        return None
+    base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS
+                 if os.path.exists(os.path.join(REPO, "profiles", r, "pmc_fetch.csv"))), None)
+    if base is None:
         return None
     vals = {}
     for ctr, fn in (("FETCH_SIZE", "pmc_fetch.csv"), ("WRITE_SIZE", "pmc_write.csv")):
@@ -141,9 +218,22 @@ def pmc_traffic(name):
     return round(2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"])
 
 
-def cpu_baseline(cfg, B, L, seed=0):
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), as SURVEY §8(d) asks the baseline to state it."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(cfg, B, L, seed=0, timed=3):
     """The CPU oracle (oracle/model.py: torch fp32 restatement of the reference step, pinned against the
-    reference by tests/golden) timed on this host: 1 warm-up + 1 timed step at the benchmark shape."""
+    reference by tests/golden) timed on this host (SURVEY §8(d) protocol): 1 warm-up + ``timed`` steps
+    at the benchmark shape, the median step reported."""
     from oracle.model import TrainState, make_arch
     from tossctr.configs import N_NUM_NEXT, cat_cardinals
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 8)))
@@ -163,7 +253,8 @@ def cpu_baseline(cfg, B, L, seed=0):
         P[k] = t
     st = TrainState(P, A, 3e-4, 1e-4, 0.5, ema_cfg=cfg["ema"])
     del P
-    batches = synth_batches(2, B, L, N_NUM_NEXT, N_NUM_NEXT, list(cards.values()), 10_000_000, "cpu", seed + 1)
+    batches = synth_batches(1 + timed, B, L, N_NUM_NEXT, N_NUM_NEXT, list(cards.values()), 10_000_000, "cpu",
+                            seed + 1)
     times = []
     for (inp, y) in batches:
         X_num, X_mask, X_cat, seq = inp
@@ -171,10 +262,12 @@ def cpu_baseline(cfg, B, L, seed=0):
         t0 = time.perf_counter()
         st.step(b, y, 3e-4, seed)
         times.append(time.perf_counter() - t0)
-    t = times[-1]
+    t = float(np.median(times[1:]))
     return {"value": round(B / t, 2), "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu": cpu_model(),
             "sample": f"oracle fp32 train step (fwd+bwd+clip+AdamW+EMA, 1.24B params) at bs={B}, L={L}: "
-                      f"1 warm-up + 1 timed step ({t:.1f} s)"}
+                      f"1 warm-up + {timed} timed steps, median {t:.1f} s "
+                      f"({', '.join(f'{x:.1f}' for x in times[1:])} s)"}
 
 
 def main():
@@ -187,6 +280,8 @@ def main():
     ap.add_argument("--config", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2",
                     help="BASELINE.json config (the metric is quoted on cfg2; cfg5 needs 8 GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--markers", action="store_true",
+                    help="launch an empty step_marker_kernel around the timed region (tools/prof_summary.py)")
     ap.add_argument("--dense-opt", action="store_true",
                     help="step the tables in the dense AdamW/EMA stream instead of the exact lazy path")
     ap.add_argument("--tables", choices=("sharded", "replicated"), default="sharded",
@@ -252,6 +347,8 @@ def main():
     timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
              "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_update", "ctr_lazy_update_pair", "ctr_adamw_ema")
     _lib.time_calls(timed)
+    if args.markers:
+        _lib.call("ctr_step_marker", 1, torch.cuda.current_stream(dev).cuda_stream)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = run(g, g)
@@ -261,6 +358,8 @@ def main():
     fl[0].record()
     model.sync()
     fl[1].record()
+    if args.markers:
+        _lib.call("ctr_step_marker", 2, torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize()
     if pg is not None:
         torch.distributed.barrier()
@@ -271,6 +370,8 @@ def main():
     opt.time_kernels(False)
     kstats = _lib.timed_ms()
     _lib.time_calls(())
+    # U of the exact-lazy byte count: the unique rows of the last timed step's batch and gradients
+    U = measure_unique(model, data[(g - 1) % nb][0], model.engine.tg) if world == 1 else None
     if pg is not None:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -313,17 +414,27 @@ def main():
                        "parallelism": f"dp{world}" + ("" if world == 1 else
                                                      f", tables {'row-sharded' if shard else 'replicated'}")},
             "roofline": roof,
-            "step_roofline": {"mode": "dense-equivalent bytes of the reference-semantics step (SURVEY §8(d) formula)",
-                              "bytes_per_step": step_bytes_dense_equiv(a, args.batch, args.seq_len, ema is not None),
-                              "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None},
             "kernels": kernels,
             "opt_ms_per_step": round(opt_ms, 3),
             "table_update": "dense stream" if args.dense_opt else "exact lazy (replay on read/grad; final flush timed)",
             "flush_ms": round(flush_ms, 3),
         }
-        sr = rec["step_roofline"]
-        sr["achieved"] = round(sr["bytes_per_step"] / (ms * 1e-3) / 1e9, 1)
-        sr["frac"] = round(sr["achieved"] / HBM_PEAK_GBS, 4)
+        # whole-step figures: FLOPs of the matrix products against the fp32 MFMA peak; HBM bytes of this
+        # build's exact-lazy step (U measured above) against 8 TB/s; the dense-equivalent bytes of the
+        # reference semantics only for comparison with a dense implementation's ceiling
+        flops = 3.0 * fwd_flops_per_sample(a, args.seq_len) * args.batch
+        rec["step_flops"] = {"flop_per_step": flops, "achieved": round(flops / (ms * 1e-3) / 1e12, 2),
+                             "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                             "frac": round(flops / (ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, 4)}
+        if U is not None and not args.dense_opt:
+            parts = step_bytes_lazy(a, args.batch, args.seq_len, opt, U, args.steps, ema is not None)
+            tb = sum(parts.values())
+            rec["step_hbm"] = {"mode": "exact-lazy row bytes (SURVEY 8(d) row-lazy form, U measured)",
+                               "unique": U, "bytes": {k: int(v) for k, v in parts.items()},
+                               "bytes_per_step": int(tb), "achieved": round(tb / (ms * 1e-3) / 1e9, 1),
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": round(tb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        rec["dense_equivalent_bytes"] = step_bytes_dense_equiv(a, args.batch, args.seq_len, ema is not None)
         if world == 1 and not args.no_cpu_baseline and args.config == "cfg2":
             del data
             rec["cpu_baseline"] = cpu_baseline(cfg, args.batch, args.seq_len)

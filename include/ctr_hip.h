@@ -380,6 +380,9 @@ int ctr_ensemble(const float* P, int M, int B, int method, const float* w, int k
 /* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */
 int ctr_sigmoid(const float* x, int n, float* y, void* stream);
 int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream);
+/* profiling aid (no reference counterpart): an empty one-wave kernel, step_marker_kernel, launched on the
+ * stream so a rocprofv3 kernel trace can be cut at the timed region's boundaries (tools/prof_summary.py) */
+int ctr_step_marker(int tag, void* stream);
 /* batch assembly from HBM-resident shard columns (replaces ShardedDataset.__getitem__ + collate_sharded,
  * src/data/dataset.py:77-80,98-124): dst[r, :] = src[idx[r], :], rows of row_words 4-byte words     */
 int ctr_gather_rows(const void* src, long row_words, const long* idx, int n, void* dst, void* stream);

@@ -117,7 +117,11 @@ def test_rowgrad_dedup_matches_numpy():
 
 @pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (148, 8, 64, 0.1), (37, 2, 16, 0.3),
                                      (64, 4, 16, 0.2), (61, 8, 32, 0.1), (50, 8, 16, 0.1), (64, 8, 64, 0.1),
-                                     (40, 6, 24, 0.1), (1, 8, 32, 0.1)])
+                                     (40, 6, 24, 0.1), (1, 8, 32, 0.1),
+                                     # K > 64: the multi-wave recompute backward (dh <= 8; partial last
+                                     # waves, exactly full waves, the K = 100 / 120 configs), dh = 16 tile
+                                     (100, 8, 32, 0.1), (120, 8, 64, 0.15), (65, 2, 16, 0.0), (128, 16, 32, 0.2),
+                                     (200, 4, 8, 0.1), (256, 8, 64, 0.1), (100, 4, 64, 0.1)])
 def test_attention_fwd_bwd_vs_torch(K, H, D, p):
     L = _lib()
     from tossctr.rng import drop_args

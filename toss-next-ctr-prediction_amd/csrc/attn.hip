@@ -468,6 +468,167 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void a
   }
 }
 
+// 64 < K <= 256: one head per workgroup of NW = ceil(K/64) waves, every wave a 64-column segment of the
+// head in the column pass (lane = key column j = 64w + lane) and a 64-row segment in the row pass (lane =
+// query row i), dS recomputed in the row pass as in attn_bwd_wave_kernel -- no K x K tile in LDS.  The
+// stored-tile form (attn_bwd_kernel) needs K (K+1) floats of LDS per head (87 KB at K = 148): one
+// 3-wave workgroup per CU, so nothing hides its LDS and exp latencies; this form takes ~29 KB per head.
+// Positional-bias grad: the DPP diagonal shift of attn_bwd_wave_kernel per wave; a diagonal leaving a
+// wave's last column (lane 63, or the last live lane) is a finished PARTIAL sum over that wave's columns,
+// stored to [wave][diagonal]; the waves' partials are added in wave order at the end (deterministic).
+template <int DH, bool BIAS, bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_multi_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int K = a.K, D = a.D, KW = a.KW;
+  const int b = blockIdx.x, h = blockIdx.y;
+  const int nrel = 2 * a.tk + 1, ND = 2 * K - 1;
+  const int NW = (K + 63) >> 6;
+  float* sq = sm;                          // [K][DH] scaled q
+  float* sk = sq + K * DH;
+  float* sv = sk + K * DH;
+  float* sdo = sv + K * DH;
+  f32x4* sst = (f32x4*)(sdo + K * DH);     // [K] {row max, 1 / row sum, do_i . o_i, 0}
+  float* srel = (float*)(sst + K);         // [nrel]
+  uint32_t* smask = (uint32_t*)(srel + nrel);   // [K][KW]
+  float* sdiag = (float*)(smask + K * KW); // [NW][2K-1] per-wave partial diagonal sums
+  const float* base = a.qkv + (long)b * K * 3 * D;
+  for (int e = threadIdx.x; e < K * DH; e += blockDim.x) {
+    const int j = e / DH, c = e % DH;
+    const int col = h * DH + c;
+    sq[e] = base[(long)j * 3 * D + col] * a.scale;
+    sk[e] = base[(long)j * 3 * D + D + col];
+    sv[e] = base[(long)j * 3 * D + 2 * D + col];
+    sdo[e] = a.dO[((long)b * K + j) * D + col];
+  }
+  const long r0 = ((long)b * a.H + h) * K;     // first row of the head
+  if (DROP)
+    for (int e = threadIdx.x; e < K * KW; e += blockDim.x) smask[e] = a.mask[r0 * KW + e];
+  if (BIAS) {
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) srel[e] = a.relmean[e];
+    for (int e = threadIdx.x; e < NW * ND; e += blockDim.x) sdiag[e] = 0.f;
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = threadIdx.x;                        // column j (column pass) / row i (row pass)
+  const bool act = t < K;
+  const int li = act ? t : K - 1;                   // dead lanes mirror the last column / row
+  if (act) {
+    float di = 0.f;
+#pragma unroll
+    for (int c = 0; c < DH; ++c)
+      di = fmaf(a.dO[((long)b * K + t) * D + h * DH + c], a.o[((long)b * K + t) * D + h * DH + c], di);
+    sst[t] = f32x4{a.mrow[r0 + t], 1.0f / a.lrow[r0 + t], di, 0.f};
+  }
+  __syncthreads();
+  const float dscale = a.drop.scale;
+  const float live = act ? 1.0f : 0.0f;
+  const int last_lane = min(63, K - 1 - 64 * w);    // the wave's last live column
+  // ---- column pass (lane = key column j): dk_j = sum_i dS_ij qs_i, dv_j = sum_i p~_ij do_i
+  {
+    const int j = li;
+    float kj[DH], vj[DH], dk[DH], dv[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) {
+      kj[c] = sk[j * DH + c];
+      vj[c] = sv[j * DH + c];
+      dk[c] = 0.f;
+      dv[c] = 0.f;
+    }
+    const float* rb = srel + a.tk + j;
+    const int jw = j >> 5, jb = j & 31;
+    float diag = 0.f;
+    float* dgw = sdiag + w * ND + (K - 1);          // dgw[o] = partial of diagonal o = j - i over this wave
+    for (int ii = 0; ii < K; ++ii) {
+      float q[DH], dov[DH];
+#pragma unroll
+      for (int c = 0; c < DH; ++c) {
+        q[c] = sq[ii * DH + c];
+        dov[c] = sdo[ii * DH + c];
+      }
+      const f32x4 st = sst[ii];
+      const float rel = BIAS ? rb[-ii] : 0.f;
+      const uint32_t mw = DROP ? smask[ii * KW + jw] : 0u;
+      const float sc = rel + dotv<DH>(kj, q);
+      const float p = fexp(sc - st[0]) * st[1];
+      float dp = dotv<DH>(vj, dov);
+      float pt = p;
+      if (DROP) {
+        const float ks = ((mw >> jb) & 1u) ? dscale : 0.f;
+        dp *= ks;
+        pt = p * ks;
+      }
+      const float ds = p * (dp - st[2]) * live;
+      pt *= live;
+#pragma unroll
+      for (int c = 0; c < DH; ++c) {
+        dk[c] = fmaf(ds, q[c], dk[c]);
+        dv[c] = fmaf(pt, dov[c], dv[c]);
+      }
+      if (BIAS) {
+        if (ii > 0) diag = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+            0, __builtin_bit_cast(int, diag), 0x138 /* wave_shr:1 */, 0xF, 0xF, false));
+        diag += ds;
+        // the diagonal in the wave's last live column leaves the wave's columns at the next step
+        if (lane == last_lane) dgw[64 * w + lane - ii] = diag;
+      }
+    }
+    if (BIAS && lane < last_lane) dgw[64 * w + lane - (K - 1)] = diag;   // diagonals still inside at the end
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < DH; ++c) {
+        a.dqkv[((long)b * K + j) * 3 * D + D + h * DH + c] = dk[c];
+        a.dqkv[((long)b * K + j) * 3 * D + 2 * D + h * DH + c] = dv[c];
+      }
+    }
+  }
+  // ---- row pass (lane = query row i): dq_i = scale * sum_j dS_ij k_j, dS recomputed as above
+  {
+    const int i = li;
+    float qi[DH], doi[DH], dq[DH];
+#pragma unroll
+    for (int c = 0; c < DH; ++c) {
+      qi[c] = sq[i * DH + c];
+      doi[c] = sdo[i * DH + c];
+      dq[c] = 0.f;
+    }
+    const f32x4 st = sst[i];
+    const float* rb = srel + a.tk - i;                  // rb[j] = relmean[j - i + tk]
+    for (int j0 = 0; j0 < K; j0 += 32) {
+      const uint32_t mw = DROP ? smask[i * KW + (j0 >> 5)] : 0u;
+      const int j1 = j0 + 32 < K ? j0 + 32 : K;
+#pragma unroll 4
+      for (int j = j0; j < j1; ++j) {
+        float kj[DH], vj[DH];
+#pragma unroll
+        for (int c = 0; c < DH; ++c) {
+          kj[c] = sk[j * DH + c];
+          vj[c] = sv[j * DH + c];
+        }
+        const float sc = (BIAS ? rb[j] : 0.f) + dotv<DH>(kj, qi);
+        const float p = fexp(sc - st[0]) * st[1];
+        float dp = dotv<DH>(vj, doi);
+        if (DROP) dp *= ((mw >> (j - j0)) & 1u) ? dscale : 0.f;
+        const float ds = p * (dp - st[2]);
+#pragma unroll
+        for (int c = 0; c < DH; ++c) dq[c] = fmaf(ds, kj[c], dq[c]);
+      }
+    }
+    if (act) {
+#pragma unroll
+      for (int c = 0; c < DH; ++c) a.dqkv[((long)b * K + i) * 3 * D + h * DH + c] = dq[c] * a.scale;
+    }
+  }
+  if (BIAS) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
+      const int o = e - a.tk;
+      float s = 0.f;
+      if (o > -K && o < K)
+        for (int ww = 0; ww < NW; ++ww) s += sdiag[ww * ND + o + K - 1];
+      a.drel_part[((long)b * gridDim.y + h) * nrel + e] = s;
+    }
+  }
+}
+
 static int pick_group(int H, int K, size_t per_head_lds, size_t lds_cap) {
   int best = 1;
   for (int g = 1; g <= H; ++g)
@@ -494,6 +655,23 @@ static int bwd_group(int H, int K, int dh) {
 
 // the wave-per-head backward (K <= 64, dh <= 8): G = the largest divisor of H up to 4 (one wave per head)
 static bool bwd_use_wave(int K, int dh) { return K <= 64 && dh <= 8; }
+// the multi-wave recompute backward (64 < K <= 256, dh <= 8): one head per workgroup
+static bool bwd_use_multi(int K, int dh) { return K > 64 && K <= 256 && dh <= 8; }
+
+static size_t bwd_multi_lds(int K, int dh, int tk) {
+  return ((size_t)4 * K * dh + 4 * K + (2 * tk + 1) + (size_t)K * ((K + 31) / 32) +
+          (size_t)((K + 63) / 64) * (2 * K - 1)) * sizeof(float);
+}
+
+template <int DH>
+static void launch_bwd_multi(const AttnArgs& a, size_t sm, hipStream_t s) {
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  const dim3 grid(a.B, a.H), blk((a.K + 63) / 64 * 64);
+  if (bias && drop) attn_bwd_multi_kernel<DH, true, true><<<grid, blk, sm, s>>>(a);
+  else if (bias) attn_bwd_multi_kernel<DH, true, false><<<grid, blk, sm, s>>>(a);
+  else if (drop) attn_bwd_multi_kernel<DH, false, true><<<grid, blk, sm, s>>>(a);
+  else attn_bwd_multi_kernel<DH, false, false><<<grid, blk, sm, s>>>(a);
+}
 
 static int bwd_wave_group(int H) {
   int g = 1;
@@ -595,7 +773,8 @@ extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const 
 }
 
 extern "C" int ctr_attn_bwd_nparts(int H, int K, int D) {
-  return H / (bwd_use_wave(K, D / H) ? bwd_wave_group(H) : bwd_group(H, K, D / H));
+  const int dh = D / H;
+  return H / (bwd_use_wave(K, dh) ? bwd_wave_group(H) : bwd_use_multi(K, dh) ? 1 : bwd_group(H, K, dh));
 }
 
 extern "C" int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D,
@@ -607,17 +786,26 @@ extern "C" int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, i
   CTR_REQUIRE(D % H == 0 && (dh == 2 || dh == 4 || dh == 8 || dh == 16), "head dim must be 2, 4, 8 or 16");
   CTR_REQUIRE(K <= 256, "K > 256");
   CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
-  const bool wave = bwd_use_wave(K, dh);
-  const int G = wave ? bwd_wave_group(H) : bwd_group(H, K, dh);
+  const bool wave = bwd_use_wave(K, dh), multi = !wave && bwd_use_multi(K, dh);
+  const int G = wave ? bwd_wave_group(H) : multi ? 1 : bwd_group(H, K, dh);
   AttnArgs a{};
   a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = G;
   a.relmean = relmean; a.tk = tk; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = const_cast<uint32_t*>(mask); a.KW = (K + 31) / 32;
   a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow); a.lrow = const_cast<float*>(lrow);
   a.dO = dO; a.dqkv = dqkv; a.drel_part = drel_part;
-  const size_t sm = wave ? bwd_wave_lds(G, K, dh, tk) : bwd_lds(G, K, dh, tk);
+  const size_t sm = wave ? bwd_wave_lds(G, K, dh, tk) : multi ? bwd_multi_lds(K, dh, tk) : bwd_lds(G, K, dh, tk);
   CTR_REQUIRE(sm <= 160 * 1024, "attention backward tile exceeds LDS");
   hipStream_t s = (hipStream_t)stream;
+  if (multi) {
+    CTR_REQUIRE(sm <= 64 * 1024, "attention backward (multi-wave form) tile exceeds 64 KB");
+    switch (dh) {
+      case 2: launch_bwd_multi<2>(a, sm, s); break;
+      case 4: launch_bwd_multi<4>(a, sm, s); break;
+      default: launch_bwd_multi<8>(a, sm, s); break;
+    }
+    return check_launch("attn_bwd");
+  }
   if (wave) {
     CTR_REQUIRE(sm <= 64 * 1024, "attention backward (wave form) tile exceeds 64 KB");
     switch (dh) {

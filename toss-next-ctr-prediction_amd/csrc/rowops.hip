@@ -491,6 +491,16 @@ extern "C" int ctr_gather_rows(const void* src, long row_words, const long* idx,
   return check_launch("gather_rows");
 }
 
+namespace ctr {
+__global__ void step_marker_kernel(int tag) { (void)tag; }
+}  // namespace ctr
+
+// an empty dispatch that marks a point of the stream in a rocprofv3 kernel trace (bench.py --markers)
+extern "C" int ctr_step_marker(int tag, void* stream) {
+  step_marker_kernel<<<1, 64, 0, (hipStream_t)stream>>>(tag);
+  return check_launch("step_marker");
+}
+
 // strided 2-D copy (feature concatenation for the fc head, src/models/wrapper.py:168-172)
 extern "C" int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream) {
   if ((long)rows * cols == 0) return 0;
