@@ -364,8 +364,8 @@ class TrainState:
         self.ema_n = 0
         self.shadow = {k: v.detach().clone() for k, v in self.P.items()} if ema_cfg else None
 
-    def step(self, batch, y, lr, seed, record=None):
-        """One step: forward -> loss -> backward -> clip -> AdamW -> EMA. Returns (loss, outputs, grads, gnorm)."""
+    def grads(self, batch, y, seed, record=None):
+        """forward -> loss (+aux) -> backward on one batch (src/train.py:158-192): (loss, outputs, grads)."""
         drop = Dropper(seed, training=True)
         for p in self.P.values():
             p.grad = None
@@ -375,26 +375,50 @@ class TrainState:
             loss = loss + self.A.aux_w * bce_wll_style(aux, y)
         loss.backward()
         grads = {k: self.P[k].grad.detach().clone() for k in self.grad_keys}
-        with torch.no_grad():
-            gnorm = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in grads.values()]))
-            coef = torch.clamp(self.clip / (gnorm + 1e-6), max=1.0) if self.clip > 0 else None
-            self.step_n += 1
-            bc1 = 1 - self.b1 ** self.step_n
-            bc2 = 1 - self.b2 ** self.step_n
-            for k in self.grad_keys:   # torch/optim/adam.py _single_tensor_adam (decoupled wd)
-                p, g, m, v = self.P[k], self.P[k].grad, self.m[k], self.v[k]
-                if coef is not None:
-                    g.mul_(coef)
-                p.mul_(1 - lr * self.wd)
-                m.lerp_(g, 1 - self.b1)
-                v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
-                denom = (v.sqrt() / (bc2 ** 0.5)).add_(self.eps)
-                p.addcdiv_(m, denom, value=-(lr / bc1))
-            if self.shadow is not None:   # src/utils/ema.py:92-131
-                e = self.ema_cfg
-                d = ema_decay(float(e.get("decay", 0.999)), int(e.get("warmup_steps", 0)),
-                              str(e.get("warmup_type", "linear")), self.ema_n)
-                for k, p in self.P.items():
-                    self.shadow[k].mul_(d).add_(p.detach(), alpha=1.0 - d)
-                self.ema_n += 1
-        return loss.detach(), (logits.detach(), prob.detach(), aux.detach()), grads, gnorm
+        return loss.detach(), (logits.detach(), prob.detach(), aux.detach()), grads
+
+    @torch.no_grad()
+    def apply(self, grads, lr):
+        """clip_grad_norm_ -> AdamW -> EMA with the given grads (src/train.py:185-199).  Returns the norm."""
+        gnorm = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(g) for g in grads.values()]))
+        coef = torch.clamp(self.clip / (gnorm + 1e-6), max=1.0) if self.clip > 0 else None
+        self.step_n += 1
+        bc1 = 1 - self.b1 ** self.step_n
+        bc2 = 1 - self.b2 ** self.step_n
+        for k in self.grad_keys:   # torch/optim/adam.py _single_tensor_adam (decoupled wd)
+            p, g, m, v = self.P[k], grads[k], self.m[k], self.v[k]
+            if coef is not None:
+                g.mul_(coef)
+            p.mul_(1 - lr * self.wd)
+            m.lerp_(g, 1 - self.b1)
+            v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            denom = (v.sqrt() / (bc2 ** 0.5)).add_(self.eps)
+            p.addcdiv_(m, denom, value=-(lr / bc1))
+        if self.shadow is not None:   # src/utils/ema.py:92-131
+            e = self.ema_cfg
+            d = ema_decay(float(e.get("decay", 0.999)), int(e.get("warmup_steps", 0)),
+                          str(e.get("warmup_type", "linear")), self.ema_n)
+            for k, p in self.P.items():
+                self.shadow[k].mul_(d).add_(p.detach(), alpha=1.0 - d)
+            self.ema_n += 1
+        return gnorm
+
+    def step(self, batch, y, lr, seed, record=None):
+        """One step: forward -> loss -> backward -> clip -> AdamW -> EMA. Returns (loss, outputs, grads, gnorm)."""
+        loss, outs, grads = self.grads(batch, y, seed, record=record)
+        gnorm = self.apply({k: g.clone() for k, g in grads.items()}, lr)
+        return loss, outs, grads, gnorm
+
+    def step_data_parallel(self, batches, ys, lr, seeds):
+        """One data-parallel step of the reference applied per replica: every replica's
+        grads on its own batch (its own SE batch mean and loss class counts), averaged as DDP does, then
+        one clip -> AdamW -> EMA.  Returns (losses, averaged grads before the clip, gnorm)."""
+        losses, acc = [], None
+        for b, y, sd in zip(batches, ys, seeds):
+            loss, _, g = self.grads(b, y, sd)
+            losses.append(loss)
+            acc = g if acc is None else {k: acc[k] + g[k] for k in acc}
+        avg = {k: v / len(batches) for k, v in acc.items()}
+        mean_grads = {k: v.clone() for k, v in avg.items()}
+        gnorm = self.apply(avg, lr)
+        return losses, mean_grads, gnorm

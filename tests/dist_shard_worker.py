@@ -3,7 +3,13 @@ ranks before anything in it touches the GPU).  World-2 runs put both ranks on cu
 (host-staged): the same collective sequence the RCCL run issues, on one card.
 
     python tests/dist_shard_worker.py --mode {single,replicated,sharded} --same-batch {0,1}
-                                      --lazy {0,1} --out FILE
+                                      --lazy {0,1} [--steps N] [--config tiny|cfg5r] --out FILE
+
+--config cfg5r: BASELINE config 5 at reduced scale (tossctr.configs.hb1e8_d64 with hash_buckets=4e6:
+D = 64, the yaml's d_c, 35 tables of 4M rows = 140M rows -> 28-bit owner-major keys at world 2; one
+encoder layer, B = 32).  Tables are filled by a function of (global row, column) so that the sharded
+and the single-GPU layouts start from the same values; only the rows the batches touch (and the dense
+params) are dumped, per rank (OUT.rank<r>).
 """
 import argparse
 import os
@@ -17,6 +23,30 @@ for _p in (HERE, REPO, os.path.join(REPO, "toss-next-ctr-prediction_amd")):
         sys.path.insert(0, _p)
 
 CASE, STEPS, B = "tiny_concat", 4, 40
+
+
+def _fill_tables_by_index(model, rank, world):
+    """Every embedding table = sin(0.7071 * global_row + 1.3 * column + table index), pad rows 0: the
+    same values whatever the row sharding (global row = local * world + rank)."""
+    import torch
+    ar = model.arena
+    sharded = model.shards is not None
+    for ti, k in enumerate(ar.order):
+        if ar.kind[k] != "table":
+            continue
+        t = ar.views[k]
+        rows, width = t.shape
+        g = torch.arange(rows, device=t.device, dtype=torch.float64)
+        if sharded:
+            g = g * world + rank
+        c = torch.arange(width, device=t.device, dtype=torch.float64)
+        t.copy_(torch.sin(0.7071 * g[:, None] + 1.3 * c[None, :] + ti).float())
+        if ".emb_" in k:
+            pad = model.arch.pad_id
+            if not sharded:
+                t[pad].zero_()
+            elif pad % world == rank:
+                t[pad // world].zero_()
 
 
 def run(rank, world, port, args):
@@ -34,43 +64,95 @@ def run(rank, world, port, args):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist.group.WORLD
     torch.cuda.set_device(0)
-    fx = Fixture(CASE)
-    m, tr = fx.meta, fx.meta["train"]
-    vocab = int(m["vocab"]) * 8                 # sparse tables: most rows skip most ticks
-    cards = {k: v * 4 + 1 for k, v in fx.cat_cards.items()}
+    if args.config == "tiny":
+        fx = Fixture(CASE)
+        m = fx.meta
+        cfg, Fn, Fm, L, Bs = m["cfg"], m["Fn"], m["Fm"], int(m["L"]), B
+        clip = m["train"]["clip"] or 1.0
+        vocab = int(m["vocab"]) * 8                 # sparse tables: most rows skip most ticks
+        cards = {k: v * 4 + 1 for k, v in fx.cat_cards.items()}
+    else:
+        from tossctr.configs import N_NUM_NEXT, cat_cardinals, hb1e8_d64
+        cfg = hb1e8_d64(hash_buckets=4_000_000)
+        cfg["sequence"]["tfm"]["n_layers"] = 1
+        Fn = Fm = N_NUM_NEXT
+        L, Bs, clip = 100, 32, 0.5
+        vocab = 10_000_000
+        cards = cat_cardinals(cfg)
     cols = list(cards)
-    arch = make_arch(m["cfg"], vocab, m["Fn"], m["Fm"], cards, cols)
-    params = {k: torch.from_numpy(v) for k, v in make_params(arch.param_shapes(), 5, arch.pad_id).items()}
-    model = CTRModel(m["cfg"], vocab, m["Fn"], m["Fm"], cards, cols, device="cuda:0", process_group=pg,
+    arch = make_arch(cfg, vocab, Fn, Fm, cards, cols)
+    model = CTRModel(cfg, vocab, Fn, Fm, cards, cols, device="cuda:0", process_group=pg,
                      shard_tables=args.mode == "sharded")
-    model.load_state_dict(params)
+    if args.config == "tiny":
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in make_params(arch.param_shapes(), 5,
+                                                                              arch.pad_id).items()})
+    else:
+        dense = [(k, s) for k, s in arch.param_shapes() if not (k.startswith("cat_embs.") or ".emb_" in k)]
+        with torch.no_grad():
+            for k, v in make_params(dense, 5, arch.pad_id).items():
+                model.arena.views[k].copy_(torch.from_numpy(v))
+            _fill_tables_by_index(model, rank, world)
     ema = ArenaEMA(model, base_decay=0.9)
-    opt = FusedAdamW(model, lr=3e-3, weight_decay=0.05, max_grad_norm=tr["clip"] or 1.0, ema=ema, process_group=pg,
+    opt = FusedAdamW(model, lr=3e-3, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
                      lazy=bool(args.lazy))
-    L = int(m["L"])
-    losses = []
-    for t in range(STEPS):
+    losses, batches = [], []
+    for t in range(args.steps):
         bseed = 1000 + t + (0 if args.same_batch else 100 * rank)
-        b = make_batch(B, m["Fn"], m["Fm"], list(cards.values()), L, vocab, seed=bseed)
+        b = make_batch(Bs, Fn, Fm, list(cards.values()), L, vocab, seed=bseed)
+        batches.append(b)
         opt.param_groups[0]["lr"] = 3e-3 * (1.0 - 0.2 * t)
         inputs = model.stage(to_torch_batch(b))
         y = torch.from_numpy(b["y"]).float().cuda()
         model.train()
         loss = model.train_step(inputs, y, opt, global_step=t + 1, seed=(9 << 32) | t)
         losses.append(float(loss.item()))
-    model.eval()
-    eb = make_batch(B, m["Fn"], m["Fm"], list(cards.values()), L, vocab, seed=4242 + 7 * rank)
-    with torch.no_grad():
-        logits = model(to_torch_batch(eb), seed=1)[0].cpu()
-    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-    shadow = {k: v.detach().cpu() for k, v in ema.state_dict()["shadow_params"].items()}
-    local_rows = int(model.arena.shapes["dare.emb_att.weight"][0])
-    if rank == 0:
-        torch.save({"sd": sd, "ema": shadow, "losses": losses, "logits": logits, "gnorm": float(opt.norm_out[0]),
-                    "local_rows": local_rows, "vocab": vocab}, args.out)
+    if args.config == "cfg5r":
+        _dump_touched(model, opt, ema, batches, arch, rank, world, losses, args)
+    else:
+        model.eval()
+        eb = make_batch(Bs, Fn, Fm, list(cards.values()), L, vocab, seed=4242 + 7 * rank)
+        with torch.no_grad():
+            logits = model(to_torch_batch(eb), seed=1)[0].cpu()
+        sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        shadow = {k: v.detach().cpu() for k, v in ema.state_dict()["shadow_params"].items()}
+        mom = {k: model.full_table(opt.m, k).detach().cpu() for k in model.arena.order}
+        vel = {k: model.full_table(opt.v, k).detach().cpu() for k in model.arena.order}
+        local_rows = int(model.arena.shapes["dare.emb_att.weight"][0])
+        if rank == 0:
+            torch.save({"sd": sd, "ema": shadow, "m": mom, "v": vel, "losses": losses, "logits": logits,
+                        "gnorm": float(opt.norm_out[0]), "local_rows": local_rows, "vocab": vocab, "cards": cards},
+                       args.out)
     if pg is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _dump_touched(model, opt, ema, batches, arch, rank, world, losses, args):
+    """cfg5r: dense params / moments / EMA in full, and of every table the rows any batch touched that
+    this rank owns (global ids with them), to OUT.rank<r>."""
+    import numpy as np
+    import torch
+    model.sync()
+    ar = model.arena
+    sharded = model.shards is not None
+    out = {"losses": losses, "dense": {}, "rows": {}}
+    seq_ids = np.unique(np.concatenate([b["seq"].ravel() for b in batches]))
+    for k in ar.order:
+        if ar.kind[k] != "table":
+            out["dense"][k] = {n: ar._view(buf, k).detach().cpu() for n, buf in
+                               (("p", ar.buf), ("m", opt.m), ("v", opt.v), ("e", ema.shadow))}
+            continue
+        if ".emb_" in k:
+            ids = seq_ids
+        else:
+            c = arch.cat_names.index(k[len("cat_embs."):-len(".weight")])
+            ids = np.unique(np.concatenate([b["X_cat"][:, c] for b in batches]))
+        ids = ids[ids % world == rank] if sharded else ids
+        loc = torch.from_numpy((ids // world if sharded else ids).astype(np.int64)).cuda()
+        out["rows"][k] = {"ids": torch.from_numpy(ids.astype(np.int64))}
+        for n, buf in (("p", ar.buf), ("m", opt.m), ("v", opt.v), ("e", ema.shadow)):
+            out["rows"][k][n] = ar._view(buf, k)[loc].detach().cpu()
+    torch.save(out, f"{args.out}.rank{rank}")
 
 
 def _free_port():
@@ -86,6 +168,8 @@ def main():
     ap.add_argument("--mode", choices=("single", "replicated", "sharded"), required=True)
     ap.add_argument("--same-batch", type=int, default=0)
     ap.add_argument("--lazy", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=STEPS)
+    ap.add_argument("--config", choices=("tiny", "cfg5r"), default="tiny")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     if args.mode == "single":

@@ -25,15 +25,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 _cache = {}
 
 
-def _run(tmp_path_factory, mode, same, lazy=1):
-    key = (mode, same, lazy)
+def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny"):
+    key = (mode, same, lazy, steps, config)
     if key not in _cache:
-        out = str(tmp_path_factory.mktemp("shard") / f"{mode}_{same}_{lazy}.pt")
+        out = str(tmp_path_factory.mktemp("shard") / f"{mode}_{same}_{lazy}_{steps}_{config}.pt")
         r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", mode,
-                            "--same-batch", str(same), "--lazy", str(lazy), "--out", out],
-                           capture_output=True, text=True, timeout=110)
+                            "--same-batch", str(same), "--lazy", str(lazy), "--steps", str(steps), "--config", config,
+                            "--out", out], capture_output=True, text=True, timeout=250)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-        _cache[key] = torch.load(out, weights_only=True)
+        if config == "tiny":
+            _cache[key] = torch.load(out, weights_only=True)
+        else:
+            ranks = 1 if mode == "single" else 2
+            _cache[key] = [torch.load(f"{out}.rank{r}", weights_only=True) for r in range(ranks)]
     return _cache[key]
 
 
@@ -74,3 +78,91 @@ def test_sharded_lazy_equals_dense_stream(tmp_path_factory):
     for k in lazy["sd"]:
         assert torch.equal(lazy["sd"][k], dense["sd"][k]), k
         assert torch.equal(lazy["ema"][k], dense["ema"][k]), k
+
+
+@pytest.mark.parametrize("mode", ["replicated", "sharded"])
+def test_data_parallel_step_matches_oracle(tmp_path_factory, mode):
+    """world 2 with a different batch per rank against the CPU restatement applied per
+    replica (oracle.model.TrainState.step_data_parallel: each rank's grads on its own batch -- its own SE
+    batch mean and loss class counts -- averaged as DDP does, then one clip -> AdamW -> EMA).  After one
+    step from zero moments m = (1 - b1) * clip_coef * mean grad and v = (1 - b2) (clip_coef * mean grad)^2,
+    so both moments pin the averaged gradient of every parameter, tables included (rows routed to and
+    merged on their owners when sharded); checked norm-wise at 2e-4 / 4e-4 (moment tolerances,
+    golden_util.Fixture.check_moment).  The update pT - p0 is checked norm-wise at 1e-4 (+ 2 fp32 ulps)
+    on the elements whose AdamW step is well conditioned (sqrt(v_hat) >= 100 eps), and everywhere
+    elementwise within one lr."""
+    from golden_util import Fixture, to_torch_batch
+    from oracle.model import TrainState, make_arch
+    from oracle.synth import make_batch, make_params
+    res = _run(tmp_path_factory, mode, 0, steps=1)
+    fx = Fixture("tiny_concat")
+    m = fx.meta
+    cards = res["cards"]
+    cols = list(cards)
+    vocab = res["vocab"]
+    A = make_arch(m["cfg"], vocab, m["Fn"], m["Fm"], cards, cols)
+    P0 = {k: torch.from_numpy(v) for k, v in make_params(A.param_shapes(), 5, A.pad_id).items()}
+    lr = 3e-3
+    st = TrainState(P0, A, lr, 0.05, m["train"]["clip"] or 1.0, ema_cfg={"enabled": True, "decay": 0.9})
+    bs = [make_batch(40, m["Fn"], m["Fm"], list(cards.values()), int(m["L"]), vocab, seed=1000 + 100 * r)
+          for r in range(2)]
+    losses, _, gnorm = st.step_data_parallel([to_torch_batch(b) for b in bs],
+                                             [torch.from_numpy(b["y"]).float() for b in bs], lr, [(9 << 32)] * 2)
+    assert abs(res["losses"][0] - float(losses[0])) <= 1e-5 * max(1.0, abs(float(losses[0])))
+    assert abs(res["gnorm"] - float(gnorm)) <= 1e-4 * float(gnorm), (res["gnorm"], float(gnorm))
+    for k in st.grad_keys:
+        close_enough(res["m"][k].double().numpy().ravel(), st.m[k].double().numpy().ravel(), 2e-4, 0.0, f"{mode} m:{k}")
+        close_enough(res["v"][k].double().numpy().ravel(), st.v[k].double().numpy().ravel(), 4e-4, 0.0, f"{mode} v:{k}")
+    for k in P0:
+        p0 = P0[k].double().numpy().ravel()
+        got = res["sd"][k].double().numpy().ravel() - p0
+        ref = st.P[k].detach().double().numpy().ravel() - p0
+        assert np.abs(got - ref).max(initial=0) <= lr, k
+        if k in st.grad_keys:
+            good = np.sqrt(st.v[k].double().numpy().ravel() / (1 - 0.999)) >= 100 * 1e-8
+            ulp = 2.0 * np.spacing(np.abs(p0 + ref).astype(np.float32)).astype(np.float64)
+            close_enough(got[good], ref[good], 1e-4, 0.0, f"{mode} dp:{k}", ulp[good], elem_rtol=1e-2)
+        ge = res["ema"][k].double().numpy().ravel() - p0
+        re = st.shadow[k].double().numpy().ravel() - p0
+        assert np.abs(ge - re).max(initial=0) <= 0.1 * lr + 1e-6, k
+
+
+def test_cfg5_reduced_sharded_matches_single(tmp_path_factory):
+    """BASELINE config 5 at reduced scale (tests/dist_shard_worker.py --config cfg5r: D = 64, the yaml's
+    d_c, 35 hashed tables of 4M rows + the 10M-row DARE tables, 28-bit owner-major keys at world 2):
+    two row-sharded ranks on the same batch = the single-GPU step, over two steps -- every touched row's
+    parameters, both moments and EMA shadow (gathered from their owners) and every dense parameter."""
+    single = _run(tmp_path_factory, "single", 1, steps=2, config="cfg5r")[0]
+    shards = _run(tmp_path_factory, "sharded", 1, steps=2, config="cfg5r")
+    close_enough(np.asarray(shards[0]["losses"]), np.asarray(single["losses"]), 1e-5, 1e-6, "cfg5r loss")
+    lr = 3e-3
+
+    def cmp(got, ref, label):
+        """m, v: norm-wise + elementwise 1e-5 -- they pin each step's routed / merged gradient.  p, EMA:
+        norm-wise 1e-5 (+ 2 ulp) and elementwise within one lr: the global-norm summation order differs
+        (per-owner partials), which moves the clip coefficient by an ulp, and AdamW amplifies that where a
+        step's sqrt(v_hat) is near eps (that can be step 1 of an element whose final v is large)."""
+        g = {n: got[n].double().numpy().ravel() for n in ("p", "m", "v", "e")}
+        r = {n: ref[n].double().numpy().ravel() for n in ("p", "m", "v", "e")}
+        rt = 1e-4 if label.endswith("mha.in_proj_bias") else 1e-5
+        close_enough(g["m"], r["m"], rt, 0.0, f"cfg5r m:{label}")
+        close_enough(g["v"], r["v"], 2 * rt, 0.0, f"cfg5r v:{label}")
+        for n in ("p", "e"):
+            assert np.abs(g[n] - r[n]).max(initial=0) <= lr, (label, n)
+            ulp = 2.0 * np.spacing(np.abs(r[n]).astype(np.float32)).astype(np.float64)
+            err, nrm = np.linalg.norm(g[n] - r[n]), np.linalg.norm(r[n])
+            assert err <= rt * nrm + np.linalg.norm(ulp), (label, n, err / nrm)
+
+    for k, d in single["dense"].items():
+        if float(d["v"].abs().max()) == 0.0:          # no gradient (e.g. ctx_mlp in S1 mode): p, e only
+            for n in ("p", "e"):
+                close_enough(shards[0]["dense"][k][n].double().numpy().ravel(), d[n].double().numpy().ravel(),
+                             1e-6, 0.0, f"cfg5r {n}:{k}")
+            continue
+        cmp(shards[0]["dense"][k], d, k)
+    for k, d in single["rows"].items():
+        ids = np.concatenate([s["rows"][k]["ids"].numpy() for s in shards])
+        order = np.argsort(ids)
+        assert np.array_equal(ids[order], d["ids"].numpy()), k
+        got = {n: torch.cat([s["rows"][k][n] for s in shards])[torch.from_numpy(order)] for n in ("p", "m", "v", "e")}
+        cmp(got, d, k)
