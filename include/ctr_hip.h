@@ -361,11 +361,17 @@ int ctr_shard_strip(const uint32_t* okeys, long n, uint32_t mask, int32_t* local
  * out0 / out1; mode 1: tabs sorted by key_base, row zero-padded to out_ld floats into out0          */
 int ctr_shard_gather(const int32_t* local, long n, int mode, const ctr_lazy_tab_t* tabs, int ntabs, const float* P,
                      float* out0, float* out1, int out_ld, void* stream);
-/* backward: sorted unique fetched-row ids uk[0, *nu) (INVALID last) -> out_local[i] = the owner's local
- * key; counts[w] = entries owned by rank w (runs in rank order; fwd_counts = the plan's send_counts) */
-int ctr_shard_route(const uint32_t* uk, const uint32_t* nu, long cap, const uint32_t* uniq_okeys,
-                    const long long* fwd_counts, int world, uint32_t mask, uint32_t* out_local, long long* counts,
-                    void* stream);
+/* categorical rows / grads on the wire at their table's width d_c: widths of keys[0, n) (n = *n_ptr when
+ * n_ptr is given, INVALID keys width 0; table = last lbase <= key & mask, width dims[table]) ->
+ * offsets[0, cap] (exclusive scan; offsets[i+1] - offsets[i] = width of key i) and, with float_counts,
+ * the per-owner float sums of owner-major sorted unique keys (the exchange's splits)                 */
+size_t ctr_shard_offsets_ws_size(long cap);
+int ctr_shard_offsets(const uint32_t* keys, const uint32_t* n_ptr, long n, long cap, uint32_t mask,
+                      const uint32_t* lbase, const int32_t* dims, int ntabs, uint32_t* offsets, int world, int lbits,
+                      long long* float_counts, void* ws, size_t ws_bytes, void* stream);
+/* rows (n, ld) -> packed[offsets[i], offsets[i+1]) ; packed -> rows (n, out_ld) zero-padded           */
+int ctr_shard_pack(const float* rows, int ld, long n, const uint32_t* offsets, float* packed, void* stream);
+int ctr_shard_unpack(const float* packed, const uint32_t* offsets, long n, float* out, int out_ld, void* stream);
 
 /* ---- fold-ensemble inference tail (src/infer.py:102-158)                                (infer.hip)
  * p = clip(iso(clip(sigmoid(clip(z/T, +-50))))) with the checkpoint's calibrator (has_T: temperature,

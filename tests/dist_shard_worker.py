@@ -58,12 +58,15 @@ def run(rank, world, port, args):
     from tossctr import ArenaEMA, CTRModel, FusedAdamW
 
     pg = None
-    if world > 1:
+    torch.cuda.set_device(0)
+    if world > 1 or args.nccl:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if args.nccl:       # RCCL, one rank: the async bucketed all-reduce path on real device streams
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist.group.WORLD
-    torch.cuda.set_device(0)
     if args.config == "tiny":
         fx = Fixture(CASE)
         m = fx.meta
@@ -170,10 +173,14 @@ def main():
     ap.add_argument("--lazy", type=int, default=1)
     ap.add_argument("--steps", type=int, default=STEPS)
     ap.add_argument("--config", choices=("tiny", "cfg5r"), default="tiny")
+    ap.add_argument("--nccl", type=int, default=0, help="world 1 over RCCL instead of world 2 over gloo")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     if args.mode == "single":
         run(0, 1, 0, args)
+        return
+    if args.nccl:
+        run(0, 1, _free_port(), args)
         return
     import torch.multiprocessing as mp
     mp.spawn(run, args=(2, _free_port(), args), nprocs=2, join=True)

@@ -25,13 +25,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 _cache = {}
 
 
-def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny"):
-    key = (mode, same, lazy, steps, config)
+def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0):
+    key = (mode, same, lazy, steps, config, nccl)
     if key not in _cache:
-        out = str(tmp_path_factory.mktemp("shard") / f"{mode}_{same}_{lazy}_{steps}_{config}.pt")
+        out = str(tmp_path_factory.mktemp("shard") / f"{mode}_{same}_{lazy}_{steps}_{config}_{nccl}.pt")
         r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", mode,
                             "--same-batch", str(same), "--lazy", str(lazy), "--steps", str(steps), "--config", config,
-                            "--out", out], capture_output=True, text=True, timeout=250)
+                            "--nccl", str(nccl), "--out", out], capture_output=True, text=True, timeout=250)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         if config == "tiny":
             _cache[key] = torch.load(out, weights_only=True)
@@ -166,3 +166,20 @@ def test_cfg5_reduced_sharded_matches_single(tmp_path_factory):
         assert np.array_equal(ids[order], d["ids"].numpy()), k
         got = {n: torch.cat([s["rows"][k][n] for s in shards])[torch.from_numpy(order)] for n in ("p", "m", "v", "e")}
         cmp(got, d, k)
+
+
+@pytest.mark.parametrize("mode", ["replicated", "sharded"])
+def test_rccl_world1_equals_single(tmp_path_factory, mode):
+    """The RCCL (nccl backend) code path on one card: world 1 over RCCL -- the head bucket's all-reduce
+    started mid-backward on the process group's stream and waited for before the clip, the sharded
+    exchange's all-to-alls -- gives the single-process step: bitwise with replicated tables (a world-1
+    sum is the identity); sharded sums the clip norm's table partials separately (1e-5, as above)."""
+    single = _run(tmp_path_factory, "single", 1)
+    got = _run(tmp_path_factory, mode, 1, nccl=1)
+    if mode == "sharded":
+        _compare(got, single, 1e-5, what="RCCL world-1 sharded vs single: ")
+        return
+    assert got["losses"] == single["losses"]
+    for k in single["sd"]:
+        assert torch.equal(got["sd"][k], single["sd"][k]), k
+        assert torch.equal(got["ema"][k], single["ema"][k]), k

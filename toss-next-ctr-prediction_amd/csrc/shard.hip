@@ -13,10 +13,14 @@
 //      ctr_shard_strip (okey -> local key), ctr_lazy_touch (rows brought current), ctr_shard_gather
 //      (rows into the reply buffer), and an all-to-all of the rows back: the requester receives them
 //      in exactly its unique-key order, i.e. fetched row u+1 is unique key u.
-//   3. backward: the row-grad dedup (rowgrad.hip) runs on fetched-row ids; ctr_shard_route turns its
-//      sorted unique ids back into the owners' local keys and per-owner counts (the same contiguous
-//      runs), an all-to-all ships (key, row) pairs to their owners, and the owner's second dedup
-//      merges contributions from all ranks in rank order (deterministic) before the optimizer.
+//   3. backward: the row-grad dedup (rowgrad.hip) runs on fetched-row ids; its rows are scattered to the
+//      fetched-row order (ctr_scatter_rows; rows without a gradient stay 0, which AdamW treats exactly as
+//      an untouched row), so the grads travel back along the forward's request splits -- no second count
+//      exchange -- and the owner's second dedup over the keys it was asked for merges the ranks'
+//      contributions in rank order (deterministic) before the optimizer.
+// Categorical rows and grads travel at their table's width d_c (ctr_shard_offsets / _pack / _unpack:
+// per-key widths, exclusive-scan offsets, per-owner float counts for the exchange's splits), not in the
+// 64-float fetched-row layout the forward kernels read.
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -117,28 +121,58 @@ __global__ void shard_gather_kernel(const int32_t* __restrict__ local, long n, i
   }
 }
 
-// backward: sorted unique fetched-row ids uk[0, *nu) (INVALID last) -> owners' local keys
-__global__ void shard_route_keys_kernel(const uint32_t* __restrict__ uk, const uint32_t* __restrict__ nu, long cap,
-                                        const uint32_t* __restrict__ uniq_okeys, uint32_t mask,
-                                        uint32_t* __restrict__ out_local) {
-  const uint32_t n = *nu;
+// ragged categorical rows on the wire (d_c floats each instead of the 64-float fetched-row layout):
+// width of unique key i = dims[table of its local key] (table = last lbase <= local key); keys past
+// *n (or INVALID) have width 0
+__global__ void shard_widths_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ n_ptr, long n_fix,
+                                    long cap, uint32_t mask, const uint32_t* __restrict__ lbase,
+                                    const int32_t* __restrict__ dims, int ntabs, uint32_t* __restrict__ width) {
+  const long n = n_ptr ? (long)*n_ptr : n_fix;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < cap; i += (long)gridDim.x * blockDim.x) {
-    const uint32_t k = i < n ? uk[i] : SH_INVALID;
-    out_local[i] = (k == SH_INVALID || k == 0) ? SH_INVALID : (uniq_okeys[k - 1] & mask);
+    uint32_t wd = 0;
+    if (i < n && keys[i] != SH_INVALID) {
+      const uint32_t lk = keys[i] & mask;
+      int a = 0, b = ntabs;
+      while (b - a > 1) {
+        const int mid = (a + b) >> 1;
+        if (lbase[mid] <= lk) a = mid; else b = mid;
+      }
+      wd = (uint32_t)dims[a];
+    }
+    width[i] = wd;
   }
 }
 
-// owner w's fetched-row ids are the run [1 + sum_{v<w} fwd_counts[v], + fwd_counts[w])
-__global__ void shard_route_counts_kernel(const uint32_t* __restrict__ uk, const uint32_t* __restrict__ nu,
-                                          const long long* __restrict__ fwd_counts, int world,
+// per-owner float counts of the owner-major unique keys: the width sums over each owner's run
+__global__ void shard_float_counts_kernel(const uint32_t* __restrict__ uniq, const uint32_t* __restrict__ n_uniq,
+                                          const uint32_t* __restrict__ offsets, int world, int lbits,
                                           long long* __restrict__ counts) {
   const int w = threadIdx.x;
   if (w >= world) return;
-  long long lo = 1;
-  for (int v = 0; v < w; ++v) lo += fwd_counts[v];
-  const long long hi = lo + fwd_counts[w];
-  const uint32_t n = *nu;
-  counts[w] = (long long)lower_bound_u32(uk, n, (uint64_t)hi) - (long long)lower_bound_u32(uk, n, (uint64_t)lo);
+  const uint32_t n = *n_uniq;
+  const uint32_t a = lower_bound_u32(uniq, n, (uint64_t)w << lbits);
+  const uint32_t b = lower_bound_u32(uniq, n, (uint64_t)(w + 1) << lbits);
+  counts[w] = (long long)offsets[b] - (long long)offsets[a];
+}
+
+// rows (n, ld) -> packed[off_i .. off_{i+1}) (row i's first off_{i+1} - off_i floats)
+__global__ void shard_pack_kernel(const float* __restrict__ rows, int ld, long n, const uint32_t* __restrict__ off,
+                                  float* __restrict__ packed) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n * ld; q += (long)gridDim.x * blockDim.x) {
+    const long i = q / ld;
+    const uint32_t k = (uint32_t)(q - i * ld), o = off[i], w = off[i + 1] - o;
+    if (k < w) packed[o + k] = rows[q];
+  }
+}
+
+// packed -> rows (row0 + i, out_ld), zero-padded past each row's width
+__global__ void shard_unpack_kernel(const float* __restrict__ packed, const uint32_t* __restrict__ off, long n,
+                                    float* __restrict__ out, int out_ld) {
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n * out_ld; q += (long)gridDim.x * blockDim.x) {
+    const long i = q / out_ld;
+    const uint32_t k = (uint32_t)(q - i * out_ld), o = off[i], w = off[i + 1] - o;
+    out[q] = k < w ? packed[o + k] : 0.f;
+  }
 }
 
 struct PlanWs {
@@ -231,12 +265,46 @@ extern "C" int ctr_shard_gather(const int32_t* local, long n, int mode, const ct
   return check_launch("shard_gather");
 }
 
-extern "C" int ctr_shard_route(const uint32_t* uk, const uint32_t* nu, long cap, const uint32_t* uniq_okeys,
-                               const long long* fwd_counts, int world, uint32_t mask, uint32_t* out_local,
-                               long long* counts, void* stream) {
-  CTR_REQUIRE(world >= 1 && world <= 64, "world must be in [1, 64]");
+extern "C" size_t ctr_shard_offsets_ws_size(long cap) {
+  size_t t = 0;
+  (void)rocprim::exclusive_scan(nullptr, t, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)cap + 1,
+                                rocprim::plus<uint32_t>());
+  return al256(t) + al256(((size_t)cap + 1) * sizeof(uint32_t));
+}
+
+extern "C" int ctr_shard_offsets(const uint32_t* keys, const uint32_t* n_ptr, long n, long cap, uint32_t mask,
+                                 const uint32_t* lbase, const int32_t* dims, int ntabs, uint32_t* offsets, int world,
+                                 int lbits, long long* float_counts, void* ws, size_t ws_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (cap > 0) shard_route_keys_kernel<<<grid_for(cap), 256, 0, s>>>(uk, nu, cap, uniq_okeys, mask, out_local);
-  shard_route_counts_kernel<<<1, 64, 0, s>>>(uk, nu, fwd_counts, world, counts);
-  return check_launch("shard_route");
+  CTR_REQUIRE(cap >= 0 && ntabs >= 1, "ctr_shard_offsets: bad sizes");
+  CTR_REQUIRE(ws_bytes >= ctr_shard_offsets_ws_size(cap), "ctr_shard_offsets: workspace too small");
+  CTR_REQUIRE(!float_counts || (n_ptr && world >= 1 && world <= 64), "ctr_shard_offsets: per-owner counts need n_uniq");
+  size_t tb = 0;
+  (void)rocprim::exclusive_scan(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)cap + 1,
+                                rocprim::plus<uint32_t>());
+  char* base = (char*)ws;
+  uint32_t* width = (uint32_t*)(base + al256(tb));
+  // cap + 1 widths (the last one 0) -> cap + 1 exclusive offsets: offsets[i + 1] - offsets[i] = width i
+  shard_widths_kernel<<<grid_for(cap + 1), 256, 0, s>>>(keys, n_ptr, n, cap + 1, mask, lbase, dims, ntabs, width);
+  size_t t2 = al256(tb);
+  hipError_t e = rocprim::exclusive_scan(base, t2, (const uint32_t*)width, offsets, 0u, (size_t)cap + 1,
+                                         rocprim::plus<uint32_t>(), s);
+  CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
+  if (float_counts) shard_float_counts_kernel<<<1, 64, 0, s>>>(keys, n_ptr, offsets, world, lbits, float_counts);
+  return check_launch("shard_offsets");
+}
+
+extern "C" int ctr_shard_pack(const float* rows, int ld, long n, const uint32_t* offsets, float* packed, void* stream) {
+  CTR_REQUIRE(ld >= 1 && ld <= 64, "ctr_shard_pack: ld must be in [1, 64]");
+  if (n <= 0) return 0;
+  shard_pack_kernel<<<grid_for(n * ld), 256, 0, (hipStream_t)stream>>>(rows, ld, n, offsets, packed);
+  return check_launch("shard_pack");
+}
+
+extern "C" int ctr_shard_unpack(const float* packed, const uint32_t* offsets, long n, float* out, int out_ld,
+                                void* stream) {
+  CTR_REQUIRE(out_ld >= 1 && out_ld <= 64, "ctr_shard_unpack: out_ld must be in [1, 64]");
+  if (n <= 0) return 0;
+  shard_unpack_kernel<<<grid_for(n * out_ld), 256, 0, (hipStream_t)stream>>>(packed, offsets, n, out, out_ld);
+  return check_launch("shard_unpack");
 }

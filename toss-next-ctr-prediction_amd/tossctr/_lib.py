@@ -114,7 +114,10 @@ SIGS = {
     "ctr_shard_plan": (i, [p, l, i, i, i, p, i, i, i, p, p, p, p, p, z, p]),
     "ctr_shard_strip": (i, [p, l, u, p, p]),
     "ctr_shard_gather": (i, [p, l, i, p, i, p, p, p, i, p]),
-    "ctr_shard_route": (i, [p, p, l, p, p, i, u, p, p, p]),
+    "ctr_shard_offsets_ws_size": (z, [l]),
+    "ctr_shard_offsets": (i, [p, p, l, l, u, p, p, i, p, i, i, p, p, z, p]),
+    "ctr_shard_pack": (i, [p, i, l, p, p, p]),
+    "ctr_shard_unpack": (i, [p, p, l, p, i, p]),
     "ctr_calibrate": (i, [p, i, f, i, p, p, i, p, p]),
     "ctr_ensemble": (i, [p, i, i, i, p, i, p, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),

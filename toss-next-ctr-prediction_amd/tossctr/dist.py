@@ -29,6 +29,17 @@ def allreduce_sum_(t: torch.Tensor, group=None):
     return t
 
 
+def allreduce_sum_async(t: torch.Tensor, group=None):
+    """Start an in-place sum across ranks and return its handle (``wait()`` makes the current stream wait
+    for it; None when it already completed).  Under RCCL the collective runs on the process group's own
+    stream after everything queued so far on the current stream, i.e. beside the kernels issued after
+    this call -- the bucketed overlap of DDP.  gloo (host-staged) completes it here."""
+    if _needs_host_staging(group, t):
+        allreduce_sum_(t, group)
+        return None
+    return dist.all_reduce(t, group=group, async_op=True)
+
+
 def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None):
     """out = concat over ranks (rank order) of inp; out.numel() == world * inp.numel()."""
     if _needs_host_staging(group, inp):

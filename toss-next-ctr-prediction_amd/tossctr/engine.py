@@ -151,6 +151,7 @@ class Engine:
         self._gen = 0
         self.stream = None
         self.last = None
+        self.grad_ready = None   # data parallel: called once the head's dense grads are final (bucket 1)
         self.lazy = None     # a lazy FusedAdamW: table rows are brought current before they are read
         # fused FFN kernels (ffn.hip) when the shape allows; the GEMM path otherwise
         # row-streaming in/out-projection kernels (rowgemm.hip) for the D they are built for
@@ -517,9 +518,10 @@ class Engine:
         return out, dz, (dza if self.a.aux_w > 0 else None)
 
     # ------------------------------------------------------------------ backward
-    def backward(self, sv, dlogits, daux):
+    def backward(self, sv, dlogits, daux, overlap=True):
         """Backward of the whole model.  Dense grads -> arena.grad; table grads -> compact
-        (sorted unique keys, summed rows, count) in self.tg for the optimizer stream."""
+        (sorted unique keys, summed rows, count) in self.tg for the optimizer stream.  ``overlap``: let a
+        data-parallel optimizer start the head bucket's all-reduce mid-backward (grad_ready)."""
         if sv["gen"] != self._gen:
             raise RuntimeError("backward() must follow the most recent training forward (buffers are reused)")
         a, P, G, st = self.a, self.P, self.G, self.s()
@@ -542,6 +544,10 @@ class Engine:
             dxF.zero_()
             dfc = self._fc_backward(sv, dlogits)
             du_ptr, du_ld = ptr(dfc), dfc.shape[1]
+        if overlap and self.grad_ready is not None:
+            # the head's grads (the last dense params of the arena: qnn.* / fc.*) are final: their
+            # all-reduce runs beside the rest of the backward
+            self.grad_ready()
         # ---------------- pool + aux head
         dx = W.get("dx_a", (B, K, D))
         dvals = W.get("dvals", (B, K))

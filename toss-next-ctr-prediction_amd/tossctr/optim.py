@@ -176,10 +176,40 @@ class FusedAdamW:
         object.__setattr__(model, "_fused_opt", self)
         self.engine.lazy = self if self.lazy else None
         self.shards = self.engine.shards
+        # data parallel: the dense grads are all-reduced in two buckets -- the head (qnn.* / fc.*: the last
+        # dense params of the arena and ~98 % of their bytes at cfg2), started by the engine as soon as
+        # the head's backward is done and overlapped with the DARE backward, then the rest
+        self._early, self._early_started = None, False
+        self._head_lo = self._head_offset()
+        if process_group is not None and self._head_lo is not None:
+            self.engine.grad_ready = self._head_ready
         if self.shards is not None:
             if process_group is None:
                 raise ValueError("row-sharded tables need the process_group they are sharded over")
             self.shards.lazy = self if self.lazy else None
+
+    def _head_offset(self):
+        ar = self.arena
+        offs = [ar.offsets[k] for k in ar.order if ar.kind[k] == "dense" and k.split(".")[0] in ("qnn", "fc")
+                and ar.offsets[k] < ar.n_dense_grad]
+        return min(offs) if offs else None
+
+    def _head_ready(self):
+        from . import dist as D
+        self._early_started = True
+        self._early = D.allreduce_sum_async(self.arena.grad[self._head_lo:self.arena.n_dense_grad], self.pg)
+
+    def _reduce_dense(self):
+        """Sum the dense grads over the ranks: the head bucket was started during the backward (when the
+        engine reached that point), the rest now; the current stream then waits for both."""
+        from . import dist as D
+        g, n = self.arena.grad, self.arena.n_dense_grad
+        started, work = self._early_started, self._early
+        self._early_started, self._early = False, None
+        lo = self._head_lo if started else n
+        D.allreduce_sum_(g[:lo], self.pg)
+        if work is not None:
+            work.wait()
 
     # -------------------------------------------------------------- layout
     def _segments(self, tg):
@@ -354,7 +384,7 @@ class FusedAdamW:
         rank applies the same global row grads (replicated tables stay bitwise identical)."""
         from . import dist as D
         eng = self.engine
-        D.allreduce_sum_(self.arena.grad[:self.arena.n_dense_grad], self.pg)
+        self._reduce_dense()
         out = {}
         st = eng.s()
         W = eng.ws(-1, -1)
@@ -393,8 +423,7 @@ class FusedAdamW:
         """clip (if max_grad_norm > 0) -> AdamW -> EMA (if bound and due at global_step)."""
         tg = tg if tg is not None else self.engine.tg
         if self.shards is not None:
-            from . import dist as D
-            D.allreduce_sum_(self.arena.grad[:self.arena.n_dense_grad], self.pg)
+            self._reduce_dense()
             tg = self.shards.route(tg, tg["fx"])
             self.engine.tg = tg
         elif self.pg is not None:

@@ -13,9 +13,10 @@ are all 1/world per GPU), and a step exchanges only the rows a batch uses:
            owner runs -> all-to-all of (local key, grad row) -> the owner's second dedup merges the
            ranks' contributions in rank order (deterministic) -> clip / AdamW / EMA on local rows.
 
-Per rank and step that is the batch's unique rows twice (rows out, grads back) instead of
-world x (all ranks' grads) for the replicated all-gather.  Two host reads of per-owner counts per
-step (forward and backward) size the all-to-alls.
+Per rank and step that is the batch's unique rows twice (rows out, grads back; categorical rows at their
+table's width d_c) instead of world x (all ranks' grads) for the replicated all-gather.  One host read of
+per-owner counts per step (forward) sizes every all-to-all of the step: the grads go back along the
+forward's request splits.
 
 The pad token's rows are never fetched: fetched row 0 is zero, which is what ``padding_idx`` keeps
 the pad rows at (zero init, zero grad, so AdamW/EMA leave them at zero).
@@ -78,7 +79,7 @@ class _Grow:
 class TableShards:
     """Owner map, fetch (forward) and grad routing (backward) for one CTRModel's tables."""
 
-    CAT_LD = 64    # fetched categorical rows are zero-padded to 64 floats (d_c <= 64)
+    CAT_LD = 64    # fetched categorical rows are zero-padded to 64 floats in HBM (d_c <= 64); packed on the wire
 
     def __init__(self, arch, group, rank: int, world: int, device):
         self.a = arch
@@ -104,6 +105,7 @@ class TableShards:
         self.cat_lbase = torch.from_numpy(self.cat_lbase_np.view(np.int32)).to(device)
         self.cat_zero_off = torch.zeros(arch.Fc, dtype=torch.int64, device=device)
         self.cat_zero_base = torch.zeros(arch.Fc, dtype=torch.int32, device=device)
+        self.cat_dims = torch.tensor(arch.cat_dims, dtype=torch.int32, device=device)
         self.buf = _Grow(device)
         self.lazy = None        # FusedAdamW (lazy) bound by the optimizer: owners bring rows current
         self.tabs_seq = None    # device ctr_lazy_tab_t arrays of the local shards (set by the engine)
@@ -132,28 +134,42 @@ class TableShards:
         else:
             call("ctr_shard_plan", _ptr(X), n, ncols, 1, 0, _ptr(self.cat_lbase), self.world, self.cat_lbits,
                  self.cat_kbits, _ptr(uniq), _ptr(nu), _ptr(remap), _ptr(cnt), _ptr(ws), wsz, self._stream())
-        return uniq, remap.view(X.shape), cnt
+        return uniq, nu, remap.view(X.shape), cnt
 
-    def _counts(self, name, a, b):
-        """All-to-all of two per-owner count vectors; one host read returns (send_a, send_b, recv_a, recv_b)."""
-        W = self.world
-        send = self.buf.get(f"{name}_csend", 2 * W, dtype=torch.int64).view(W, 2)
-        send[:, 0].copy_(a)
-        send[:, 1].copy_(b)
-        recv = self.buf.get(f"{name}_crecv", 2 * W, dtype=torch.int64)
-        D.all_to_all_var(recv, send.view(-1), [2] * W, [2] * W, self.group)
-        h = torch.cat([send.view(-1), recv]).cpu().tolist()      # the phase's one host sync
-        return h[0:2 * W:2], h[1:2 * W:2], h[2 * W::2], h[2 * W + 1::2]
+    def _offsets(self, name, keys, n_ptr, n, cap, counts=None):
+        """Offsets of categorical keys' rows at their table widths (and per-owner float counts)."""
+        off = self.buf.get(f"{name}_off", cap + 1, dtype=torch.int32)
+        wsz = _lib.query("ctr_shard_offsets_ws_size", cap)
+        ws = self.buf.get("off_ws", wsz, dtype=torch.uint8)
+        call("ctr_shard_offsets", _ptr(keys), _ptr(n_ptr), n, cap, self._mask(self.cat_lbits), _ptr(self.cat_lbase),
+             _ptr(self.cat_dims), self.a.Fc, _ptr(off), self.world, self.cat_lbits, _ptr(counts), _ptr(ws), wsz,
+             self._stream())
+        return off
+
+    def _counts(self, name, *vecs):
+        """All-to-all of per-owner count vectors; ONE host read returns, per vector, (what this rank sends to
+        each owner, what it receives from each rank) -- the only host synchronisation of a step."""
+        W, k = self.world, len(vecs)
+        send = self.buf.get(f"{name}_csend", k * W, dtype=torch.int64).view(W, k)
+        for j, v in enumerate(vecs):
+            send[:, j].copy_(v)
+        recv = self.buf.get(f"{name}_crecv", k * W, dtype=torch.int64)
+        D.all_to_all_var(recv, send.view(-1), [k] * W, [k] * W, self.group)
+        h = torch.cat([send.view(-1), recv]).cpu().tolist()
+        return [h[j:k * W:k] for j in range(k)], [h[k * W + j::k] for j in range(k)]
 
     # ------------------------------------------------------------------ forward
     def fetch(self, X_cat, seq):
         """Rows the batch reads, fetched from their owners.  Returns the remapped batch (fetched-row
-        ids; 0 = pad) and the compact tables: att/rep (1 + n_uniq, D) with row 0 zero, cat (1 + n, 64)."""
+        ids; 0 = pad) and the compact tables: att/rep (1 + n_uniq, D) with row 0 zero, cat (1 + n, 64).
+        Categorical rows travel at their table's width d_c (packed), not as 64-float rows."""
         a, st = self.a, self._stream()
-        Dm = a.D
-        uniq_s, seq_c, cnt_s = self._plan("seq", seq, 1, 0)
-        uniq_c, xcat_c, cnt_c = self._plan("cat", X_cat, X_cat.shape[1], 1)
-        send_s, send_c, recv_s, recv_c = self._counts("fwd", cnt_s, cnt_c)
+        Dm, LD = a.D, self.CAT_LD
+        uniq_s, _, seq_c, cnt_s = self._plan("seq", seq, 1, 0)
+        uniq_c, nu_c, xcat_c, cnt_c = self._plan("cat", X_cat, X_cat.shape[1], 1)
+        fcnt = self.buf.get("fcnt_c", self.world, dtype=torch.int64)
+        off_c = self._offsets("req", uniq_c, nu_c, 0, X_cat.numel(), fcnt)
+        (send_s, send_c, send_f), (recv_s, recv_c, recv_f) = self._counts("fwd", cnt_s, cnt_c, fcnt)
         ns, nc = sum(send_s), sum(send_c)
         rs, rc = sum(recv_s), sum(recv_c)
         # requested keys -> owners
@@ -161,7 +177,7 @@ class TableShards:
         req_c = self.buf.get("req_c", rc, dtype=torch.int32)
         D.all_to_all_var(req_s, uniq_s[:ns], recv_s, send_s, self.group)
         D.all_to_all_var(req_c, uniq_c[:nc], recv_c, send_c, self.group)
-        # owner side: local keys, rows brought current, rows gathered
+        # owner side: local keys, rows brought current, rows gathered (categorical ones packed at d_c)
         loc_s = self.buf.get("loc_s", rs, dtype=torch.int32)
         loc_c = self.buf.get("loc_c", rc, dtype=torch.int32)
         call("ctr_shard_strip", _ptr(req_s), rs, self._mask(self.seq_lbits), _ptr(loc_s), st)
@@ -171,20 +187,26 @@ class TableShards:
         arena = self.arena_buf
         out_att = self.buf.get("out_att", rs, Dm)
         out_rep = self.buf.get("out_rep", rs, Dm)
-        out_cat = self.buf.get("out_cat", rc, self.CAT_LD)
+        out_cat = self.buf.get("out_cat", rc, LD)
         tabs, nt = self.tabs_seq
         call("ctr_shard_gather", _ptr(loc_s), rs, 0, _ptr(tabs), nt, _ptr(arena), _ptr(out_att), _ptr(out_rep), Dm, st)
         tabs, nt = self.tabs_cat
-        call("ctr_shard_gather", _ptr(loc_c), rc, 1, _ptr(tabs), nt, _ptr(arena), _ptr(out_cat), None, self.CAT_LD, st)
+        call("ctr_shard_gather", _ptr(loc_c), rc, 1, _ptr(tabs), nt, _ptr(arena), _ptr(out_cat), None, LD, st)
+        off_o = self._offsets("own", req_c, None, rc, rc)
+        pk_o = self.buf.get("cat_pk_o", sum(recv_f))
+        call("ctr_shard_pack", _ptr(out_cat), LD, rc, _ptr(off_o), _ptr(pk_o), st)
         # rows back, in the requester's unique-key order (fetched row u + 1 = unique key u)
         att = self.buf.get("att", 1 + seq.numel(), Dm, zero=True)
         rep = self.buf.get("rep", 1 + seq.numel(), Dm, zero=True)
-        cat = self.buf.get("cat", 1 + X_cat.numel(), self.CAT_LD, zero=True)
+        cat = self.buf.get("cat", 1 + X_cat.numel(), LD, zero=True)
+        pk_r = self.buf.get("cat_pk_r", sum(send_f))
         D.all_to_all_var(att[1:1 + ns], out_att, send_s, recv_s, self.group)
         D.all_to_all_var(rep[1:1 + ns], out_rep, send_s, recv_s, self.group)
-        D.all_to_all_var(cat[1:1 + nc], out_cat, send_c, recv_c, self.group)
-        return dict(seq=seq_c, xcat=xcat_c, att=att, rep=rep, cat=cat, uniq_s=uniq_s, uniq_c=uniq_c, cnt_s=cnt_s,
-                    cnt_c=cnt_c, n_seq=seq.numel(), n_cat=X_cat.numel())
+        D.all_to_all_var(pk_r, pk_o, send_f, recv_f, self.group)
+        call("ctr_shard_unpack", _ptr(pk_r), _ptr(off_c), nc, _ptr(cat, LD), LD, st)
+        return dict(seq=seq_c, xcat=xcat_c, att=att, rep=rep, cat=cat, n_seq=seq.numel(), n_cat=X_cat.numel(),
+                    splits=(send_s, recv_s, send_c, recv_c, send_f, recv_f), loc_s=loc_s, loc_c=loc_c, off_c=off_c,
+                    off_o=off_o)
 
     # ------------------------------------------------------------------ backward
     def _rowgrad(self, name, keys, rows, n, width, bits):
@@ -211,34 +233,36 @@ class TableShards:
 
     def route(self, tg, fx):
         """Compact grads on fetched-row ids (tg from Engine.backward) -> the owners' merged grads on
-        local keys: {"att", "rep", "cat"} in the layout the optimizer consumes."""
+        local keys: {"att", "rep", "cat"} in the layout the optimizer consumes.
+
+        The grads are scattered to the fetched-row order first (a fetched row without a gradient -- a
+        token outside every top-K -- stays 0, which AdamW steps exactly like an untouched row), so they
+        go back along the forward's request splits: no second count exchange, no host read."""
         st = self._stream()
-        W = self.world
+        LD = self.CAT_LD
         ta, tr, tc = tg["att"], tg["rep"], tg["cat"]
-        # att and rep were deduplicated from the same keys (top-K tokens): one key order for both
-        ks = self.buf.get("rk_s", ta["n"], dtype=torch.int32)
-        kc = self.buf.get("rk_c", tc["n"], dtype=torch.int32)
-        cs = self.buf.get("rcnt_s", W, dtype=torch.int64)
-        cc = self.buf.get("rcnt_c", W, dtype=torch.int64)
-        call("ctr_shard_route", _ptr(ta["keys"]), _ptr(ta["n_uniq"]), ta["n"], _ptr(fx["uniq_s"]), _ptr(fx["cnt_s"]), W,
-             self._mask(self.seq_lbits), _ptr(ks), _ptr(cs), st)
-        call("ctr_shard_route", _ptr(tc["keys"]), _ptr(tc["n_uniq"]), tc["n"], _ptr(fx["uniq_c"]), _ptr(fx["cnt_c"]), W,
-             self._mask(self.cat_lbits), _ptr(kc), _ptr(cc), st)
-        send_s, send_c, recv_s, recv_c = self._counts("bwd", cs, cc)
+        send_s, recv_s, send_c, recv_c, send_f, recv_f = fx["splits"]
         ns, nc, rs, rc = sum(send_s), sum(send_c), sum(recv_s), sum(recv_c)
         Dm = ta["width"]
-        rk_s = self.buf.get("gk_s", rs, dtype=torch.int32)
+        ga = self.buf.get("dg_att", ns, Dm)
+        gr = self.buf.get("dg_rep", ns, Dm)
+        gc = self.buf.get("dg_cat", nc, LD)
+        for dst, t, w in ((ga, ta, Dm), (gr, tr, Dm), (gc, tc, LD)):
+            dst.zero_()
+            call("ctr_scatter_rows", _ptr(t["keys"]), _ptr(t["G"]), _ptr(t["n_uniq"]), t["n"], w, t["G"].shape[1], 1,
+                 dst.shape[0], _ptr(dst), st)
+        pk = self.buf.get("dg_cat_pk", sum(send_f))
+        call("ctr_shard_pack", _ptr(gc), LD, nc, _ptr(fx["off_c"]), _ptr(pk), st)
         rg_a = self.buf.get("ga_s", rs, Dm)
         rg_r = self.buf.get("gr_s", rs, Dm)
-        rk_c = self.buf.get("gk_c", rc, dtype=torch.int32)
-        rg_c = self.buf.get("gc_c", rc, tc["width"])
-        D.all_to_all_var(rk_s, ks[:ns], recv_s, send_s, self.group)
-        D.all_to_all_var(rg_a, ta["G"][:ns], recv_s, send_s, self.group)
-        D.all_to_all_var(rg_r, tr["G"][:ns], recv_s, send_s, self.group)
-        D.all_to_all_var(rk_c, kc[:nc], recv_c, send_c, self.group)
-        D.all_to_all_var(rg_c, tc["G"][:nc], recv_c, send_c, self.group)
-        att, rep = self._rowgrad2("sh_seq", rk_s, rg_a, rg_r, rs, Dm, self.seq_lbits)
-        return {"att": att, "rep": rep, "cat": self._rowgrad("sh_cat", rk_c, rg_c, rc, tc["width"], self.cat_lbits)}
+        rg_p = self.buf.get("gc_pk", sum(recv_f))
+        D.all_to_all_var(rg_a, ga, recv_s, send_s, self.group)
+        D.all_to_all_var(rg_r, gr, recv_s, send_s, self.group)
+        D.all_to_all_var(rg_p, pk, recv_f, send_f, self.group)
+        rg_c = self.buf.get("gc_c", rc, LD)
+        call("ctr_shard_unpack", _ptr(rg_p), _ptr(fx["off_o"]), rc, _ptr(rg_c), LD, st)
+        att, rep = self._rowgrad2("sh_seq", fx["loc_s"], rg_a, rg_r, rs, Dm, self.seq_lbits)
+        return {"att": att, "rep": rep, "cat": self._rowgrad("sh_cat", fx["loc_c"], rg_c, rc, LD, self.cat_lbits)}
 
     # ------------------------------------------------------------------ full-table views (checkpoints)
     def gather_full(self, local: torch.Tensor, rows: int) -> torch.Tensor:

@@ -132,6 +132,7 @@ def release(model, opt, ema):
     reference goes, not at some later gen-2 collection (src/train.py:280-316 _free_fold)."""
     model.__dict__.pop("_fused_opt", None)
     model.engine.lazy = None
+    model.engine.grad_ready = None
     model.engine.last = None
     if model.shards is not None:
         model.shards.lazy = None

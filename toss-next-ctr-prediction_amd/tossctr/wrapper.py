@@ -53,7 +53,7 @@ class _CTRFunction(torch.autograd.Function):
             p = sv["prob"]
             dz = dz + g_prob * p * (1 - p)
         daux = None if g_aux is None else g_aux.float().contiguous()
-        eng.backward(sv, dz, daux)
+        eng.backward(sv, dz, daux, overlap=False)     # torch reads the grads right after: no async reduce
         grads = []
         for k in model.arena.order:
             if model.arena.kind[k] == "table":
