@@ -284,6 +284,9 @@ def main():
                     help="launch an empty step_marker_kernel around the timed region (tools/prof_summary.py)")
     ap.add_argument("--dense-opt", action="store_true",
                     help="step the tables in the dense AdamW/EMA stream instead of the exact lazy path")
+    ap.add_argument("--amp", choices=("none", "bf16"), default="none",
+                    help="cfg['amp'] (src/train.py:133-139): bf16 = bf16 MFMA operands, fp32 accumulation, fp32 "
+                         "master weights / optimizer state / tables")
     ap.add_argument("--tables", choices=("sharded", "replicated"), default="sharded",
                     help="N > 1: row-shard the embedding tables over the ranks (all-to-all row fetch / grad "
                          "routing) or replicate them (all-gather of row grads)")
@@ -310,6 +313,7 @@ def main():
     if args.seq_len is None:
         args.seq_len = int(cfg["sequence"]["max_len"])
     cfg["sequence"]["max_len"] = args.seq_len
+    cfg["amp"] = args.amp
     cards = cat_cardinals(cfg)
     cols = list(cfg["data"]["cat_cols"])
     vocab = 10_000_000                                   # src/train.py:116
@@ -406,7 +410,7 @@ def main():
                       + ("" if args.config == "cfg2" else f" [{args.config}: not the headline config]"),
             "value": round(samples, 1), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp32", "data": "synthetic (SURVEY 8(d) distributions), HBM-resident",
+            "vs_baseline": None, "dtype": "fp32" if args.amp == "none" else "bf16 (fp32 accumulate, fp32 master)", "data": "synthetic (SURVEY 8(d) distributions), HBM-resident",
             "config": {"workload": WORKLOADS[args.config].format(B=args.batch, L=args.seq_len,
                                                                  P=sum(int(np.prod(sh)) for _, sh, _ in
                                                                        a.param_shapes()) / 1e9),

@@ -73,6 +73,13 @@ int ctr_gemm(int M, int N, int K, const float* A, int lda, int ta, const float* 
 int ctr_gemm_seg(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
                  float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
                  void* stream);
+/* ctr_gemm_seg with flags (seg nullable).  CTR_GEMM_BF16: the operands are rounded to bf16 (RNE) and
+ * multiplied on v_mfma_f32_16x16x32_bf16 with fp32 accumulation -- the reference's
+ * torch.autocast(bfloat16) matmul (src/train.py:133-139,158-164; amp: bf16); C and epilogues fp32.     */
+#define CTR_GEMM_BF16 1
+int ctr_gemm_ex(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
+                int flags, void* stream);
 
 
 /* Row-streaming GEMMs of the DARE encoder layer (MHA in_proj / out_proj, src/models/dare.py:53-62, and

@@ -22,6 +22,7 @@ Usage:  python tests/golden/gen_golden.py            (writes tests/golden/*.npz)
 from __future__ import annotations
 
 import ast
+import contextlib
 import copy
 import json
 import os
@@ -190,8 +191,16 @@ def put_allow(store, name, allow, rows, shape):
 
 
 def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, store_params, train_cfg,
-             y_override=None, lognormal=False):
+             y_override=None, lognormal=False, amp_twin=None):
+    """One fixture.  ``amp_twin``: the name of the fp32 fixture this case repeats (same inputs, seeds and
+    parameters) under ``amp: bf16`` -- the forward and the loss run inside
+    ``torch.autocast("cpu", dtype=torch.bfloat16)`` as src/train.py:158-164 wraps them in
+    ``torch.cuda.amp.autocast(dtype=bfloat16)`` (CPU autocast here: no GPU in the generating container);
+    backward, clip, AdamW and EMA outside it, on the fp32 master parameters."""
     CTRModel, ref_dare, build_ema, cosine_warmup_lr, bce_wll_style = load_ref()
+    if amp_twin is not None:
+        cfg = dict(cfg, amp="bf16")
+    amp_ctx = (lambda: torch.autocast("cpu", dtype=torch.bfloat16)) if amp_twin else contextlib.nullcontext
     cat_cols = list(cat_cards)
     A = make_arch(cfg, vocab, Fn, Fm, cat_cards, cat_cols)
     torch.manual_seed(0)
@@ -206,7 +215,7 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
     store = {}
     meta = dict(name=name, cfg=cfg, B=B, L=L, vocab=vocab, Fn=Fn, Fm=Fm, cat_cards=cat_cards,
                 steps=steps, pseed=pseed, bseed=bseed, store_params=store_params, train=train_cfg,
-                lrs=[], seeds=[])
+                lrs=[], seeds=[], amp="bf16" if amp_twin else "none", twin=amp_twin)
     if store_params:
         for k, v in P0.items():
             store[f"p0/{k}"] = v
@@ -261,12 +270,12 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
             opt.param_groups[0]["lr"] = lr
             opt.zero_grad(set_to_none=True)
             patch.seed, patch.calls = seed, 0
-            with patch:
+            with patch, amp_ctx():
                 logits, prob, aux = model(batch)
+                loss = bce_wll_style(logits, y)
+                if aux_w > 0:
+                    loss = loss + aux_w * bce_wll_style(aux, y)
             assert patch.calls == len(patch.sites), (patch.calls, patch.sites)
-            loss = bce_wll_style(logits, y)
-            if aux_w > 0:
-                loss = loss + aux_w * bce_wll_style(aux, y)
             loss.backward()
             if t == 0:   # raw (pre-clip) grads of the first step
                 names = []
@@ -277,14 +286,14 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
                     put(store, f"grad0/{k}", p.grad.numpy().copy(), rows=touched.get(k))
                 meta["grad_keys"] = names
             gn = nn.utils.clip_grad_norm_(model.parameters(), train_cfg["clip"]) if train_cfg["clip"] > 0 else None
-            store[f"out{t}/logits"] = logits.detach().numpy()
-            store[f"out{t}/prob"] = prob.detach().numpy()
-            store[f"out{t}/aux"] = aux.detach().numpy()
+            store[f"out{t}/logits"] = logits.detach().float().numpy()
+            store[f"out{t}/prob"] = prob.detach().float().numpy()
+            store[f"out{t}/aux"] = aux.detach().float().numpy()
             store[f"out{t}/loss"] = np.float64(loss.item())
             store[f"out{t}/gnorm"] = np.float64(float(gn) if gn is not None else -1.0)
             store[f"out{t}/topk_idx"] = topk_rec["idx"].numpy().astype(np.int32)
-            store[f"out{t}/topk_vals"] = topk_rec["vals"].numpy()
-            store[f"out{t}/query"] = topk_rec["query"].numpy()
+            store[f"out{t}/topk_vals"] = topk_rec["vals"].float().numpy()
+            store[f"out{t}/query"] = topk_rec["query"].float().numpy()
             gsteps.append({k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None})
             opt.step()
             if ema is not None:
@@ -295,8 +304,10 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
         mT = {k: opt.state[p]["exp_avg"].numpy() for k, p in model.named_parameters() if p in opt.state and opt.state[p]}
         vT = {k: opt.state[p]["exp_avg_sq"].numpy() for k, p in model.named_parameters()
               if p in opt.state and opt.state[p]}
-        allow = update_allowance(P0, gsteps, meta["lrs"], train_cfg["wd"], cfg.get("ema") if ema else None,
-                                 pT, {k: v.numpy() for k, v in shadow.items()}, mT, vT)
+        # bf16 twins are compared through their bf16-vs-fp32 noise band, not the replay allowances
+        allow = {} if amp_twin else update_allowance(P0, gsteps, meta["lrs"], train_cfg["wd"],
+                                                     cfg.get("ema") if ema else None, pT,
+                                                     {k: v.numpy() for k, v in shadow.items()}, mT, vT)
         for kind, d in allow.items():
             if kind not in ("dT", "demaT"):     # moments are compared without an allowance
                 continue
@@ -318,9 +329,10 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
         # eval forward with the final params on the last batch
         model.eval()
         patch.calls = 0
-        with torch.no_grad():
+        with torch.no_grad(), amp_ctx():
             z, p_, a_ = model(batch)
-        store["eval/logits"], store["eval/prob"], store["eval/aux"] = z.numpy(), p_.numpy(), a_.numpy()
+        store["eval/logits"], store["eval/prob"], store["eval/aux"] = (z.float().numpy(), p_.float().numpy(),
+                                                                        a_.float().numpy())
     finally:
         ref_dare.DARE.topk_select = orig_topk
     store["meta"] = np.array(json.dumps(meta))
@@ -465,6 +477,9 @@ def main():
     if "--infer-only" in sys.argv:
         gen_infer()
         return
+    if "--bf16-only" in sys.argv:
+        gen_bf16()
+        return
     tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
     cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
     run_case("tiny_concat", tiny_cfg(), B=64, L=32, vocab=5000, Fn=6, Fm=6, cat_cards=cards, steps=3,
@@ -493,6 +508,23 @@ def main():
     run_case("k120", cfg5, B=6, L=150, vocab=2000, Fn=10, Fm=10, cat_cards={c: 100 for c in cols5[:6]},
              steps=2, pseed=51, bseed=800, store_params=False, train_cfg=big_tr)
     gen_infer()
+    gen_bf16()
+
+
+def gen_bf16():
+    """amp: bf16 twins of three fp32 fixtures (same inputs, seeds, parameters): the noise band the
+    parity tests compare the bf16 build against is the reference's own bf16-vs-fp32 deviation."""
+    tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
+    cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
+    run_case("tiny_concat_bf16", tiny_cfg(), B=64, L=32, vocab=5000, Fn=6, Fm=6, cat_cards=cards, steps=3,
+             pseed=11, bseed=100, store_params=True, train_cfg=tr, amp_twin="tiny_concat")
+    big_tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=0, epochs=8)
+    cfg2, cols = cfg2_cfg()
+    run_case("cfg2_dims_bf16", cfg2, B=8, L=100, vocab=3000, Fn=82, Fm=82, cat_cards={c: 200 for c in cols},
+             steps=2, pseed=21, bseed=500, store_params=False, train_cfg=big_tr, amp_twin="cfg2_dims")
+    cfg4, cols4 = k148_cfg()
+    run_case("k148_bf16", cfg4, B=4, L=160, vocab=2000, Fn=10, Fm=10, cat_cards={c: 100 for c in cols4[:6]},
+             steps=2, pseed=31, bseed=600, store_params=False, train_cfg=big_tr, amp_twin="k148")
 
 
 if __name__ == "__main__":

@@ -12,6 +12,20 @@ from oracle.model import make_arch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["tiny_concat", "tiny_s1_relu", "tiny_s2", "base_fc", "cfg2_dims", "cfg3_dims", "k148", "k120"]
+# amp: bf16 twins (gen_golden.gen_bf16): the reference under torch.autocast(bfloat16) on the inputs,
+# seeds and parameters of the fp32 fixture named in meta["twin"]
+BF16_CASES = ["tiny_concat_bf16", "cfg2_dims_bf16", "k148_bf16"]
+BF16_BAND = 3.0      # bf16 tolerance: within 3x the reference's own bf16-vs-fp32 deviation ...
+BF16_FLOOR = 1e-4    # ... or 1e-4 of the tensor's norm, whichever is larger
+# scalars (loss, grad norm): one draw of the bf16 rounding says little about its spread, so the floor is
+# 4 bf16 unit roundoffs (4 x 2^-9) of the value
+BF16_SCALAR_FLOOR = 4 * 2.0 ** -9
+# tensors of fewer than BF16_FEW elements (the output layers' biases, ...): their gradients are batch sums
+# of per-sample terms of both signs (sum of dlogits over 8 samples), where bf16 rounding of the terms is
+# amplified by the cancellation -- measured: 4.8% between the bf16 build and the reference's bf16 run on
+# the final bias's Adam moment, 3.9% against its fp32 run; the floor there is 10% of the value
+BF16_FEW = 64
+BF16_FEW_FLOOR = 0.1
 
 
 def key_bias_mask(arch, key):
@@ -145,6 +159,65 @@ class Fixture:
         if rtol is None:
             rtol = 2e-4 if kind == "mT" else 4e-4
         return self.check(f"{kind}/{key}", got, rtol, 0.0)
+
+
+def _exact_subset(fx, name):
+    """(index array or None = all, exact reference values there) of a stored tensor: the whole tensor
+    when stored in full, else the fingerprint's sampled elements plus the touched rows' elements."""
+    if name in fx.z.files:
+        return None, np.asarray(fx.z[name], np.float64).ravel()
+    idx = fx.z[f"{name}@idx"].astype(np.int64)
+    vals = fx.z[f"{name}@vals"].astype(np.float64)
+    if f"{name}@rows" in fx.z.files:
+        rows = fx.z[f"{name}@rows"].astype(np.int64)
+        rv = fx.z[f"{name}@rowvals"].astype(np.float64)
+        w = rv.shape[1]
+        ridx = (rows[:, None] * w + np.arange(w)[None, :]).ravel()
+        keep = ~np.isin(idx, ridx)
+        idx = np.concatenate([idx[keep], ridx])
+        vals = np.concatenate([vals[keep], rv.ravel()])
+    return idx, vals
+
+
+def check_bf16_band(fx16, fx32, name, got, label=None):
+    """amp: bf16 parity.  ``got`` (the build under amp: bf16) is compared with the reference run under
+    autocast(bfloat16) (``fx16``) and in fp32 (``fx32``, the twin fixture): the norm of the difference
+    to EACH must stay within BF16_BAND x the reference's own bf16-vs-fp32 deviation, or BF16_FLOOR of
+    the tensor's norm.  Norms over the whole tensor when it is stored in full, else over the exact
+    sampled elements + touched rows (the same subset for all three), and the projected whole-tensor
+    estimate within twice that bound."""
+    label = label or f"{fx16.name}:{name}"
+    if isinstance(got, torch.Tensor):
+        got = got.detach().cpu().double().numpy()
+    got = np.asarray(got, np.float64).ravel()
+    idx, r16 = _exact_subset(fx16, name)
+    idx32, r32 = _exact_subset(fx32, name)
+    if idx is not None:
+        assert idx32 is not None, label
+        pos = {int(i): j for j, i in enumerate(idx32)}
+        sel = np.array([pos.get(int(i), -1) for i in idx])
+        have = sel >= 0
+        idx, r16, r32 = idx[have], r16[have], r32[sel[have]]
+    g = got if idx is None else got[idx]
+    assert g.shape == r16.shape == r32.shape, (label, g.shape, r16.shape, r32.shape)
+    band = float(np.linalg.norm(r32 - r16))
+    nrm = max(float(np.linalg.norm(r16)), float(np.linalg.norm(r32)))
+    tol = BF16_BAND * band + (BF16_FLOOR if got.size >= BF16_FEW else BF16_FEW_FLOOR) * nrm + 1e-30
+    e16, e32 = float(np.linalg.norm(g - r16)), float(np.linalg.norm(g - r32))
+    assert e16 <= tol and e32 <= tol, (
+        f"{label}: |got - ref_bf16| {e16:.3e}, |got - ref_fp32| {e32:.3e} vs band |ref_fp32 - ref_bf16| "
+        f"{band:.3e} (tol {tol:.3e}, |ref| {nrm:.3e})")
+    if idx is not None:          # whole tensor through the projections (chi-square estimates: 2x slack)
+        p16 = fx16.z[f"{name}@projs"].astype(np.float64)
+        p32 = fx32.z[f"{name}@projs"].astype(np.float64)
+        pg = synth.project(got)
+        est = lambda d: float(np.sqrt(np.mean(d * d)))    # noqa: E731
+        nb = np.sqrt(max(float(fx16.z[f"{name}@sumsq"]), float(fx32.z[f"{name}@sumsq"])))
+        ptol = 2 * (BF16_BAND * est(p32 - p16) + BF16_FLOOR * nb) + 1e-30
+        assert est(pg - p16) <= ptol and est(pg - p32) <= ptol, (
+            f"{label}: projected |got - ref_bf16| {est(pg - p16):.3e}, |got - ref_fp32| {est(pg - p32):.3e} vs "
+            f"band {est(p32 - p16):.3e} (tol {ptol:.3e})")
+    return e16, e32, band
 
 
 def close_enough(got, ref, rtol, atol, label, ulp=None, elem_rtol=None):

@@ -42,6 +42,62 @@ def test_gemm_vs_torch(M, N, K, ta, tb, splits):
     assert rel(C.double(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K,ta,tb", [(300, 96, 32, 0, 1), (257, 384, 45, 0, 1), (130, 32, 384, 0, 1),
+                                         (64, 512, 7552, 0, 1), (384, 32, 5000, 1, 0), (33, 70, 19, 1, 1),
+                                         (1, 32, 4096, 1, 0), (4096, 1, 256, 0, 1), (200, 130, 64, 0, 0),
+                                         (4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0)])
+@pytest.mark.parametrize("splits", [1, 7])
+def test_gemm_bf16_vs_torch(M, N, K, ta, tb, splits):
+    """ctr_gemm_ex(CTR_GEMM_BF16) -- amp: bf16 -- against the fp64 product of the bf16-ROUNDED operands
+    (torch's round-to-nearest-even .bfloat16()): bf16 x bf16 products are exact in fp32, so only the fp32
+    accumulation order separates them (1e-5).  Shapes include the QNN MLP's forward / dW / dX."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + 1)
+    A = torch.randn((K, M) if ta else (M, K), device="cuda", generator=g)
+    B = torch.randn((N, K) if tb else (K, N), device="cuda", generator=g)
+    C = torch.empty(M, N, device="cuda")
+    ws = torch.empty(splits * M * N + 16, device="cuda")
+    L.call("ctr_gemm_ex", M, N, K, ptr(A), A.shape[1], ta, ptr(B), B.shape[1], tb, ptr(C), N, None, splits, ptr(ws),
+           None, 1, stream())
+    Ab, Bb = A.bfloat16().double(), B.bfloat16().double()
+    ref = (Ab.t() if ta else Ab) @ (Bb.t() if tb else Bb)
+    assert rel(C.double(), ref) < 1e-5
+
+
+def test_gemm_bf16_epilogues_and_segments():
+    """bf16 operands under the fused epilogues the model uses (bias + ReLU + dropout with the pre-activation
+    stored; residual + RMSNorm) and the [z | inter] operand / result segments of the QNN MLP."""
+    L = _lib()
+    from tossctr.rng import drop_args
+    M, N, K, kc = 700, 384, 200, 128
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A1 = torch.randn(M, kc, device="cuda", generator=g)
+    A2 = torch.randn(M, K - kc, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * 0.1
+    b = torch.randn(N, device="cuda", generator=g)
+    out, pre = torch.empty(M, N, device="cuda"), torch.empty(M, N, device="cuda")
+    dk = drop_args(77, 3, 0.2, True)
+    epi = L.GemmEpi(bias=ptr(b), act=1, pre=ptr(pre), drop_key=dk[0], drop_thresh=dk[1], drop_scale=dk[2])
+    L.call("ctr_gemm_ex", M, N, K, ptr(A1), kc, 0, ptr(W), K, 1, ptr(out), N, epi, 1, None,
+           L.GemmSeg(A2=ptr(A2), lda2=K - kc, ka=kc), 1, stream())
+    Ab = torch.cat([A1, A2], 1).bfloat16().double()
+    pre_ref = Ab @ W.bfloat16().double().t() + b.double()
+    assert rel(pre.double(), pre_ref) < 1e-5
+    ref_relu = torch.relu(pre_ref)
+    kept = out != 0
+    assert rel(out.double()[kept], (ref_relu * dk[2])[kept]) < 1e-5
+    D = 32
+    W2 = torch.randn(D, N, device="cuda", generator=g) * 0.05
+    resid = torch.randn(M, D, device="cuda", generator=g)
+    nw = torch.rand(D, device="cuda", generator=g) + 0.5
+    y, h, r = torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda")
+    epi2 = L.GemmEpi(resid=ptr(resid), ld_resid=D, norm_w=ptr(nw), norm_h=ptr(h), norm_r=ptr(r), norm_eps=1e-6)
+    L.call("ctr_gemm_ex", M, D, N, ptr(out), N, 0, ptr(W2), N, 1, ptr(y), D, epi2, 1, None, None, 1, stream())
+    h_ref = resid.double() + out.bfloat16().double() @ W2.bfloat16().double().t()
+    y_ref = nw.double() * h_ref * torch.rsqrt(h_ref.pow(2).mean(-1, keepdim=True) + 1e-6)
+    assert rel(h.double(), h_ref) < 1e-5 and rel(y.double(), y_ref) < 1e-5
+
+
 def test_gemm_epilogues():
     L = _lib()
     M, N, K = 517, 384, 32

@@ -8,12 +8,19 @@
 //
 // f32-input MFMA is bit-for-bit a k-ordered fmaf chain per lane; results differ from the reference's
 // MKL sgemm only by summation order (covered by the 1e-4 parity tolerance).
+//
+// BF = true (amp: bf16, the reference's torch.autocast(bfloat16) Linear / matmul): the same loaders read
+// fp32 from HBM, the staging store rounds to bf16 (v_cvt_pk_bf16_f32, round-to-nearest-even) into
+// [row][k] LDS tiles of BK = 32, and v_mfma_f32_16x16x32_bf16 accumulates in fp32 -- one MFMA per
+// 16x16 block and k-slice where the fp32 form issues eight.  Outputs and epilogues stay fp32.
 #include "common.h"
 #include "ctr_hip.h"
 
 namespace ctr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 struct GemmArgs {
   int M, N, K;
@@ -62,14 +69,15 @@ __device__ __forceinline__ float epi_elem(const ctr_gemm_epi_t& e, float v, int 
   return v;
 }
 
-template <int BM, int BN, bool TA, bool TB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gemm_kernel(GemmArgs g) {
-  constexpr int BK = 16;
+template <int BM, int BN, bool TA, bool TB, bool BF = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 2 : 4))) void gemm_kernel(GemmArgs g) {
+  constexpr int BK = BF ? 32 : 16;
   constexpr int SA = BM + 16, SB = BN + 16;
+  constexpr int SK = BK + 8;                 // bf16 tiles: [row][k] rows of 40 bf16 (80 B: conflict-free b128)
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int SC = BN + 4;
-  constexpr int LDS_K = 2 * BK * (SA + SB);
+  constexpr int LDS_K = BF ? (2 * (BM + BN) * SK + 1) / 2 : 2 * BK * (SA + SB);
   // only the fused residual+RMSNorm epilogue (BN <= 64 tiles) stages the tile through LDS; every other
   // epilogue runs straight from the accumulator registers (keeps big tiles at 4 workgroups / CU)
   constexpr int LDS_E = BN <= 64 ? BM * SC : 0;
@@ -77,9 +85,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   __shared__ __attribute__((aligned(16))) float smem[LDS];
   float* As = smem;
   float* Bs = smem + 2 * BK * SA;
+  __bf16* Ah = (__bf16*)smem;                // BF: [2][BM][SK]
+  __bf16* Bh = Ah + 2 * BM * SK;             // BF: [2][BN][SK]
 
   constexpr int A_V = BM * BK / 4, B_V = BN * BK / 4;           // float4 slots per tile
-  constexpr int A_IT = (A_V + 255) / 256, B_IT = (B_V + 255) / 256;
+  // BF with the operand stored k-major (A: TA, B: !TB): each thread loads a 4k x 4row block (four float4
+  // rows, lanes of one row block cover its eight k blocks: 128-B lines) and stores it transposed as four
+  // 8-byte bf16x4 row segments -- [row][k] tiles without 2-byte scattered stores (16-way bank conflicts)
+  constexpr bool A_BLK = BF && TA, B_BLK = BF && !TB;
+  constexpr int A_NB = BM * BK / 16, B_NB = BN * BK / 16;       // 4x4 blocks per tile
+  constexpr int A_IT = A_BLK ? 4 * ((A_NB + 255) / 256) : (A_V + 255) / 256;
+  constexpr int B_IT = B_BLK ? 4 * ((B_NB + 255) / 256) : (B_V + 255) / 256;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = (wid >> 1) * WM, wn = (wid & 1) * WN;
@@ -91,6 +107,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
   f32x4 ra[A_IT], rb[B_IT];
 
   auto load_a = [&](int k0) {
+    if constexpr (A_BLK) {      // A stored [k][m]: block (kb, ib) = k 4kb.., rows 4ib..
+#pragma unroll
+      for (int bi = 0; bi < A_IT / 4; ++bi) {
+        const int e = tid + bi * 256, kb = e % (BK / 4), ib = e / (BK / 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          const int kk = k0 + 4 * kb + t, m = m0 + 4 * ib;
+          if (e < A_NB && kk < kz1) {
+            const float* p = g.A + (long)kk * g.lda + m;
+            if (g.vecA && m + 3 < g.M) v = *(const f32x4*)p;
+            else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (m + j < g.M) ? p[j] : 0.f;
+            }
+          }
+          ra[4 * bi + t] = v;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int e = tid + it * 256;
@@ -139,6 +176,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     }
   };
   auto load_b = [&](int k0) {
+    if constexpr (B_BLK) {      // B stored [k][n] (n columns 0..nb from B, past nb from B2)
+#pragma unroll
+      for (int bi = 0; bi < B_IT / 4; ++bi) {
+        const int e = tid + bi * 256, kb = e % (BK / 4), nbk = e / (BK / 4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
+          const int kk = k0 + 4 * kb + t, n = n0 + 4 * nbk;
+          if (e < B_NB && kk < kz1) {
+            if (g.B2 == nullptr || n + 3 < g.nb) {
+              const float* p = g.B + (long)kk * g.ldb + n;
+              if (g.vecB && n + 3 < g.N) v = *(const f32x4*)p;
+              else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? p[j] : 0.f;
+              }
+            } else if (n >= g.nb) {
+              const float* p = g.B2 + (long)kk * g.ldb2 + (n - g.nb);
+              if (g.vecB && n + 3 < g.N) v = *(const f32x4*)p;
+              else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) v[j] = (n + j < g.N) ? p[j] : 0.f;
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                const int nn = n + j;
+                v[j] = nn >= g.N ? 0.f : nn < g.nb ? g.B[(long)kk * g.ldb + nn] : g.B2[(long)kk * g.ldb2 + (nn - g.nb)];
+              }
+            }
+          }
+          rb[4 * bi + t] = v;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int e = tid + it * 256;
@@ -186,7 +259,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       rb[it] = v;
     }
   };
+  auto store_ab_bf = [&](int buf) {
+    __bf16* a = Ah + buf * BM * SK;
+    __bf16* b = Bh + buf * BN * SK;
+    // a 4k x 4row block -> four bf16x4 row segments (row 4ib + j: k 4kb .. 4kb + 3)
+    auto put_block = [&](__bf16* dst, const f32x4* r, int e, int nblk) {
+      if (e >= nblk) return;
+      const int kb = e % (BK / 4), ib = e / (BK / 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *(bf16x4*)&dst[(4 * ib + j) * SK + 4 * kb] = bf16x4{(__bf16)r[0][j], (__bf16)r[1][j], (__bf16)r[2][j], (__bf16)r[3][j]};
+    };
+    if constexpr (A_BLK) {
+#pragma unroll
+      for (int bi = 0; bi < A_IT / 4; ++bi) put_block(a, &ra[4 * bi], tid + bi * 256, A_NB);
+    }
+    if constexpr (B_BLK) {
+#pragma unroll
+      for (int bi = 0; bi < B_IT / 4; ++bi) put_block(b, &rb[4 * bi], tid + bi * 256, B_NB);
+    }
+#pragma unroll
+    for (int it = 0; it < (A_BLK ? 0 : A_IT); ++it) {
+      const int e = tid + it * 256;
+      if (e < A_V) {
+        if (!TA) {
+          const int i = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+          *(bf16x4*)&a[i * SK + kq] = __builtin_convertvector(ra[it], bf16x4);
+        } else {
+          const int k = e / (BM / 4), iq = (e % (BM / 4)) * 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[(iq + j) * SK + k] = (__bf16)ra[it][j];
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < (B_BLK ? 0 : B_IT); ++it) {
+      const int e = tid + it * 256;
+      if (e < B_V) {
+        if (!TB) {
+          const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[(nq + j) * SK + k] = (__bf16)rb[it][j];
+        } else {
+          const int n = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+          *(bf16x4*)&b[n * SK + kq] = __builtin_convertvector(rb[it], bf16x4);
+        }
+      }
+    }
+  };
   auto store_ab = [&](int buf) {
+    if constexpr (BF) {
+      store_ab_bf(buf);
+      return;
+    }
     float* a = As + buf * BK * SA;
     float* b = Bs + buf * BK * SB;
 #pragma unroll
@@ -237,6 +362,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       load_a(kz0 + (kt + 1) * BK);
       load_b(kz0 + (kt + 1) * BK);
     }
+    if constexpr (BF) {
+      // lane (g, c) reads row 16i + c, k = 8g .. 8g + 7 of the A tile (row 16j + c of the B tile)
+      const __bf16* a = Ah + cur * BM * SK + (lane & 15) * SK + 8 * (lane >> 4);
+      const __bf16* b = Bh + cur * BN * SK + (lane & 15) * SK + 8 * (lane >> 4);
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(a + (wm + i * 16) * SK);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *(const bf16x8*)(b + (wn + j * 16) * SK);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
     const float* a = As + cur * BK * SA;
     const float* b = Bs + cur * BK * SB;
 #pragma unroll
@@ -251,6 +391,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
     }
     if (kt + 1 < nkt) store_ab(cur ^ 1);
     __syncthreads();
@@ -391,13 +532,19 @@ __global__ void gemm_smallk_kernel(GemmArgs g, int ta, int tb) {
   }
 }
 
-template <int BM, int BN>
-static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s) {
+template <int BM, int BN, bool BF>
+static void launch_tile_t(GemmArgs& g, int ta, int tb, int splits, hipStream_t s) {
   dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), splits);
-  if (!ta && !tb) gemm_kernel<BM, BN, false, false><<<grid, 256, 0, s>>>(g);
-  else if (!ta && tb) gemm_kernel<BM, BN, false, true><<<grid, 256, 0, s>>>(g);
-  else if (ta && !tb) gemm_kernel<BM, BN, true, false><<<grid, 256, 0, s>>>(g);
-  else gemm_kernel<BM, BN, true, true><<<grid, 256, 0, s>>>(g);
+  if (!ta && !tb) gemm_kernel<BM, BN, false, false, BF><<<grid, 256, 0, s>>>(g);
+  else if (!ta && tb) gemm_kernel<BM, BN, false, true, BF><<<grid, 256, 0, s>>>(g);
+  else if (ta && !tb) gemm_kernel<BM, BN, true, false, BF><<<grid, 256, 0, s>>>(g);
+  else gemm_kernel<BM, BN, true, true, BF><<<grid, 256, 0, s>>>(g);
+}
+
+template <int BM, int BN>
+static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s, bool bf) {
+  if (bf) launch_tile_t<BM, BN, true>(g, ta, tb, splits, s);
+  else launch_tile_t<BM, BN, false>(g, ta, tb, splits, s);
 }
 
 }  // namespace ctr
@@ -410,7 +557,7 @@ extern "C" size_t ctr_gemm_ws_size(int M, int N, int splits) {
 
 static int gemm_core(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
                      float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
-                     void* stream) {
+                     void* stream, bool bf = false) {
   CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative dims");
   if (M == 0 || N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -444,7 +591,7 @@ static int gemm_core(int M, int N, int K, const float* A, int lda, int ta, const
     }
     if (seg->C2) { g.C2 = seg->C2; g.ldc2 = seg->ldc2; g.nc = seg->nc; }
   }
-  const int BK = 16;
+  const int BK = bf ? 32 : 16;
   int klen = K;
   if (splits > 1) {
     klen = ((K + splits - 1) / splits + BK - 1) / BK * BK;
@@ -452,26 +599,26 @@ static int gemm_core(int M, int N, int K, const float* A, int lda, int ta, const
   }
   g.klen = klen > 0 ? klen : 1;
   g.ws = ws;
-  if (K <= 4 && !g.epi.norm_w && splits == 1 && !seg) {
+  if (K <= 4 && !g.epi.norm_w && splits == 1 && !seg && !bf) {
     const long MN = (long)M * N;
     gemm_smallk_kernel<<<(int)std::min<long>((MN + 255) / 256, 8192), 256, 0, s>>>(g, ta, tb);
     return check_launch("ctr_gemm");
   }
   if (g.epi.norm_w) {
-    if (N <= 32) launch_tile<128, 32>(g, ta, tb, 1, s);
-    else launch_tile<128, 64>(g, ta, tb, 1, s);
+    if (N <= 32) launch_tile<128, 32>(g, ta, tb, 1, s, bf);
+    else launch_tile<128, 64>(g, ta, tb, 1, s, bf);
   } else if (N <= 32) {
-    launch_tile<128, 32>(g, ta, tb, splits, s);
+    launch_tile<128, 32>(g, ta, tb, splits, s, bf);
   } else if (N <= 64) {
-    launch_tile<128, 64>(g, ta, tb, splits, s);
+    launch_tile<128, 64>(g, ta, tb, splits, s, bf);
   } else if (N <= 96) {
-    launch_tile<128, 96>(g, ta, tb, splits, s);
+    launch_tile<128, 96>(g, ta, tb, splits, s, bf);
   } else if (M <= 64) {
-    launch_tile<64, 128>(g, ta, tb, splits, s);
+    launch_tile<64, 128>(g, ta, tb, splits, s, bf);
   } else if ((long)((M + 127) / 128) * ((N + 127) / 128) * splits < 512) {
-    launch_tile<64, 64>(g, ta, tb, splits, s);     // too few 128x128 tiles to fill the chip
+    launch_tile<64, 64>(g, ta, tb, splits, s, bf);     // too few 128x128 tiles to fill the chip
   } else {
-    launch_tile<128, 128>(g, ta, tb, splits, s);
+    launch_tile<128, 128>(g, ta, tb, splits, s, bf);
   }
   if (splits > 1) {
     const long MN = (long)M * N;
@@ -490,4 +637,11 @@ extern "C" int ctr_gemm_seg(int M, int N, int K, const float* A, int lda, int ta
                             float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws,
                             const ctr_gemm_seg_t* seg, void* stream) {
   return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, stream);
+}
+
+extern "C" int ctr_gemm_ex(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
+                           float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
+                           int flags, void* stream) {
+  CTR_REQUIRE((flags & ~CTR_GEMM_BF16) == 0, "ctr_gemm_ex: unknown flags");
+  return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, stream, (flags & CTR_GEMM_BF16) != 0);
 }

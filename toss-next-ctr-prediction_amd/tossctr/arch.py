@@ -51,6 +51,7 @@ class Arch:
     use_residual: bool = True
     pair_grouping: str = "all"
     qnn_norm: str = "rms"
+    amp: str = "none"          # cfg["amp"] (src/train.py:133-139): "none" (fp32) or "bf16"
 
     @property
     def Fc(self):
@@ -93,6 +94,7 @@ class Arch:
             ffn_p=float(t.get("ffn_dropout", 0.1)), add_pos=bool(t.get("add_positional_bias", True)),
             gating=t.get("gating", "softmax") if t else "softmax", norm=str(t.get("norm", "rms")),
             use_qnn=bool(qa["enabled"]), aux_w=float(qa.get("aux_head_weight", 0.0)),
+            amp=str(cfg.get("amp", "none") or "none").lower(),
         )
         if a.use_qnn:
             a.qh, a.qr, a.qP = int(qa["heads"]), int(qa["rank"]), int(qa["proj_dim"])
@@ -117,6 +119,8 @@ class Arch:
             raise NotImplementedError("only QNN norm: rms is implemented (all reference configs use rms)")
         if self.use_qnn and self.pair_grouping != "all":
             raise NotImplementedError("pair_grouping 'block' is not implemented (no reference config uses it)")
+        if self.amp not in ("none", "bf16"):
+            raise NotImplementedError(f"amp: {self.amp!r} -- the MI355X path runs fp32 or bf16 (amp: bf16)")
         if self.gating not in ("softmax", "relu"):
             raise ValueError(f"unknown gating {self.gating}")
         if self.D % 4 or self.D > 64:

@@ -152,6 +152,11 @@ class Engine:
         self.stream = None
         self.last = None
         self.grad_ready = None   # data parallel: called once the head's dense grads are final (bucket 1)
+        # amp: bf16 (src/train.py:133-139,158-164, torch.autocast(bfloat16)): every GEMM-shaped product on the
+        # gemm kernel takes bf16-rounded operands on bf16 MFMA with fp32 accumulation; parameters, optimizer
+        # state, tables and the element-wise math stay fp32
+        self.bf16 = a.amp == "bf16"
+        self.gemm_flags = 1 if self.bf16 else 0     # CTR_GEMM_BF16
         self.lazy = None     # a lazy FusedAdamW: table rows are brought current before they are read
         # fused FFN kernels (ffn.hip) when the shape allows; the GEMM path otherwise
         # row-streaming in/out-projection kernels (rowgemm.hip) for the D they are built for
@@ -221,10 +226,8 @@ class Engine:
         wsp = None
         if splits > 1:
             wsp = ptr(self.splitk_ws(splits * M * N))
-        if seg is not None:
-            call("ctr_gemm_seg", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg, self.s())
-        else:
-            call("ctr_gemm", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, self.s())
+        call("ctr_gemm_ex", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg, self.gemm_flags,
+             self.s())
 
     @staticmethod
     def _split_factor(M, N, K, min_depth):

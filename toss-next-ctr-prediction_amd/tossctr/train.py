@@ -55,7 +55,7 @@ def check_supported(cfg):
     """Refuse configuration the fused path does not implement instead of silently training something
     else: ``sampler.type: balanced`` (src/train.py:95-106; no reference yaml enables it) and an ``amp``
     mode other than none/bf16 (fp16 + GradScaler, src/train.py:133-139,185-190)."""
-    amp = str(cfg.get("amp", "none")).lower()
+    amp = str(cfg.get("amp", "none") or "none").lower()
     if amp not in ("none", "bf16"):
         raise NotImplementedError(f"amp: {cfg.get('amp')!r} -- the fused MI355X step runs fp32 or bf16 (amp: bf16)")
     if str((cfg.get("sampler", {}) or {}).get("type", "") or "").lower() == "balanced":
