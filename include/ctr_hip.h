@@ -178,20 +178,26 @@ int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K
  * (ffn = Linear(D,FF) -> GELU -> Dropout -> Linear(FF,D); x2 = norm2(x1 + ffn(x1)))       (ffn.hip)
  * The FF-wide activations never reach HBM: the backward recomputes them from x1.
  * ------------------------------------------------------------------------------------------- */
-int ctr_ffn_supported(int D, int FF);          /* D in {16, 32, 64}, FF % 16 == 0 */
-int ctr_ffn_slab_rows(int M, int D);           /* workgroups of ctr_ffn_bwd = rows of its grad slab */
+/* flags: CTR_FFN_BF16 (amp: bf16, src/train.py:158-164) -- both products on bf16 MFMA (bf16-rounded operands,
+ * fp32 accumulate), GELU / dropout / residual / norms fp32; D in {32, 64}, FF % 32 == 0; the keep-bit
+ * mask in the bf16 kernels' own layout (a bf16 forward pairs with a bf16 backward).  wbf: 3*FF*D bf16
+ * (6*FF*D bytes) the bf16 forward fills with weight images (W1 | W2^T | W1^T) for the bf16 backward
+ * (nullable in an inference-only forward; ignored without the flag)                                    */
+#define CTR_FFN_BF16 1
+int ctr_ffn_supported(int D, int FF, int flags);   /* fp32: D in {16, 32, 64}, FF % 16 == 0 */
+int ctr_ffn_slab_rows(int M, int D, int flags);    /* workgroups of ctr_ffn_bwd = rows of its grad slab */
 int ctr_ffn_mask_words(int M, int FF);         /* uint32 words of the dropout keep-bit mask (16 bits per 16 cols) */
 /* y = norm_w * h * r, h = x + (gelu(x W1^T + b1) [dropout] W2^T + b2), r = 1/rms(h).  mask (nullable
  * without dropout) receives the keep bits, chunk-major (FF/16, M) uint16.                           */
 int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
                 const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
-                float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* stream);
+                float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* wbf, int flags, void* stream);
 /* dh = grad wrt h (after ctr_rmsnorm_bwd).  dx = dh + (dact W1); per-workgroup weight-grad slab rows
  * (ld_slab floats): dW1 (FF, D) at 0, db1 (FF) at o_b1, dW2 (D, FF) at o_w2 -- colsum them (the
  * offsets may match the arena layout so one ctr_colsum lands in the grad buffer).  db2 = colsum(dh). */
 int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
                 const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const uint32_t* mask,
-                float* dx, float* slab, long ld_slab, int o_b1, int o_w2, void* stream);
+                float* dx, float* slab, long ld_slab, int o_b1, int o_w2, const void* wbf, int flags, void* stream);
 /* The FFN backward fused with the transformer layer's two RMSNorm backwards (x1 = norm1(h1),
  * h2 = x1 + FFN(x1), x2 = norm2(h2); src/models/dare.py TransformerEncoderLayer norm_first=False):
  * dy = grad wrt x2 -> dh1 = grad wrt h1.  Slab rows (ld_slab floats) hold d norm1.w at o_n1, dW1 at o_w1,
@@ -201,7 +207,7 @@ int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h2, const fl
                       const float* h1, const float* r1, const float* nw1, int M, int D, int FF, const float* W1,
                       const float* b1, const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale,
                       const uint32_t* mask, float* dh1, float* slab, long ld_slab, int o_n1, int o_w1, int o_b1,
-                      int o_w2, int o_b2, int o_n2, void* stream);
+                      int o_w2, int o_b2, int o_n2, const void* wbf, int flags, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Row / column ops                                                                (rowops.hip)

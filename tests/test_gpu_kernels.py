@@ -342,7 +342,7 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     y, h, r = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
     fmask = torch.zeros(L.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
     L.call("ctr_ffn_fwd", ptr(x), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(nw), 1e-6, key, thresh, scale,
-           ptr(fmask), ptr(y), ptr(h), ptr(r), stream())
+           ptr(fmask), ptr(y), ptr(h), ptr(r), None, 0, stream())
     mask = torch.from_numpy(keep_mask(seed, site, p, (M, FF)).astype(np.float32)).cuda() if p > 0 else \
         torch.ones(M, FF, device="cuda")
     xr, W1r, b1r, W2r = (t.detach().double().requires_grad_() for t in (x, W1, b1, W2))
@@ -359,13 +359,13 @@ def test_fused_ffn_vs_torch(M, D, FF, p):
     dh = torch.randn(M, D, device="cuda", generator=g)
     hr.backward(dh.double())
     dx = torch.empty(M, D, device="cuda")
-    nb = L.query("ctr_ffn_slab_rows", M, D)
+    nb = L.query("ctr_ffn_slab_rows", M, D, 0)
     o_b1 = FF * D
     o_w2 = o_b1 + (FF + 63) // 64 * 64
     ld = o_w2 + D * FF
     slab = torch.zeros(nb, ld, device="cuda")
     L.call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask),
-           ptr(dx), ptr(slab), ld, o_b1, o_w2, stream())
+           ptr(dx), ptr(slab), ld, o_b1, o_w2, None, 0, stream())
     red = slab.double().sum(0)
     assert rel(dx.double(), xr.grad) < 1e-5
     assert rel(red[:FF * D].view(FF, D), W1r.grad) < 1e-5
@@ -399,7 +399,7 @@ def test_ffn_bwd_norms_vs_torch(M, D, FF, p):
     x2, h2, r2 = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
     fmask = torch.zeros(L.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
     L.call("ctr_ffn_fwd", ptr(x1), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(n2), 1e-6, key, thresh, scale,
-           ptr(fmask), ptr(x2), ptr(h2), ptr(r2), stream())
+           ptr(fmask), ptr(x2), ptr(h2), ptr(r2), None, 0, stream())
     mask = torch.from_numpy(keep_mask(seed, site, p, (M, FF)).astype(np.float32)).cuda() if p > 0 else \
         torch.ones(M, FF, device="cuda")
     h1r, W1r, b1r, W2r, b2r, n1r, n2r = (t.detach().double().requires_grad_() for t in (h1, W1, b1, W2, b2, n1, n2))
@@ -418,12 +418,12 @@ def test_ffn_bwd_norms_vs_torch(M, D, FF, p):
     o_b2 = al(o_w2 + D * FF)
     o_n2 = al(o_b2 + D)
     ld = o_n2 + D
-    nb = L.query("ctr_ffn_slab_rows", M, D)
+    nb = L.query("ctr_ffn_slab_rows", M, D, 0)
     slab = torch.zeros(nb, ld, device="cuda")
     dh1 = torch.empty(M, D, device="cuda")
     L.call("ctr_ffn_bwd_norms", ptr(x1), ptr(dy), ptr(h2), ptr(r2), ptr(n2), ptr(h1), ptr(r1), ptr(n1), M, D, FF,
            ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask), ptr(dh1), ptr(slab), ld,
-           o_n1, o_w1, o_b1, o_w2, o_b2, o_n2, stream())
+           o_n1, o_w1, o_b1, o_w2, o_b2, o_n2, None, 0, stream())
     red = slab.double().sum(0)
     assert rel(dh1.double(), h1r.grad) < 1e-5
     assert rel(red[o_n1:o_n1 + D], n1r.grad) < 1e-5
@@ -437,6 +437,157 @@ def test_ffn_bwd_norms_vs_torch(M, D, FF, p):
         used[o:o + n] = True
     gaps = slab[:, ~used.cuda()]
     assert gaps.numel() == 0 or float(gaps.abs().max()) == 0.0
+
+
+def ffn_keep_bits_bf(fmask, M, FF):
+    """(M, FF) keep bits of the amp bf16 FFN kernels (ffn.hip "row words"): word
+    (chunk * nb16 + row // 16) * 16 + row % 16 holds bit f for column 32 chunk + f."""
+    nb16 = (M + 15) // 16
+    words = fmask.cpu().numpy().view(np.uint32)[:FF // 32 * nb16 * 16].reshape(FF // 32, nb16 * 16)
+    rows, cols = np.arange(M), np.arange(FF)
+    w = words[(cols // 32)[None, :], rows[:, None]]
+    return ((w >> (cols % 32).astype(np.uint32)[None, :]) & 1).astype(bool)
+
+
+def _bfr(t):
+    return t.to(torch.bfloat16).double()
+
+
+def ffn_ref_bf16(x, W1, b1, W2, b2, keep, dh):
+    """fp64 reference of the amp bf16 FFN: every product's operands rounded to bf16 (RNE), exact GELU,
+    fp32-kept residual; returns h and, for the grad dh wrt h, (dx, dW1, db1, dW2)."""
+    pre = _bfr(x) @ _bfr(W1).t() + b1.double()
+    cdf = 0.5 * (1 + torch.special.erf(pre / math.sqrt(2.0)))
+    fo = pre * cdf * keep
+    h = x.double() + (_bfr(fo) @ _bfr(W2).t() + b2.double())
+    dfo = _bfr(dh) @ _bfr(W2)
+    gg = cdf + pre * torch.exp(-0.5 * pre * pre) / math.sqrt(2 * math.pi)
+    da = dfo * keep * gg
+    # db1 sums the bf16-rounded dact, as the reference's bias grad sums its bf16 grad_output
+    return h, (_bfr(da) @ _bfr(W1) + dh.double(), _bfr(da).t() @ _bfr(x), _bfr(da).sum(0), _bfr(dh).t() @ _bfr(fo))
+
+
+BF_TOL = 2e-4     # bf16 emulation: only rare rounding-boundary flips of an operand element differ
+
+
+@pytest.mark.parametrize("M,D,FF,p", [(300, 32, 384, 0.1), (130, 64, 384, 0.15), (4097, 32, 384, 0.0),
+                                      (517, 32, 64, 0.2), (64, 32, 32, 0.5), (70001, 32, 384, 0.1),
+                                      (140003, 64, 96, 0.1)])
+def test_fused_ffn_bf16_vs_emulation(M, D, FF, p):
+    """amp bf16 FFN kernels (CTR_FFN_BF16) vs an fp64 emulation with bf16-rounded product operands; the
+    persistent backward (M > 512 tiles: several tiles per workgroup, slab rows accumulated) included."""
+    from oracle.rng import keep_mask
+    from tossctr.rng import drop_args
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M + D + FF + 1)
+    x = torch.randn(M, D, device="cuda", generator=g)
+    W1 = torch.randn(FF, D, device="cuda", generator=g) / math.sqrt(D)
+    b1 = torch.randn(FF, device="cuda", generator=g) * 0.1
+    W2 = torch.randn(D, FF, device="cuda", generator=g) / math.sqrt(FF)
+    b2 = torch.randn(D, device="cuda", generator=g) * 0.1
+    nw = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    seed, site = (5 << 32) | 9, 4
+    key, thresh, scale = drop_args(seed, site, p, True)
+    y, h, r = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
+    fmask = torch.zeros(L.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
+    wbf = torch.empty(3 * FF * D, dtype=torch.bfloat16, device="cuda")
+    L.call("ctr_ffn_fwd", ptr(x), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(nw), 1e-6, key, thresh, scale,
+           ptr(fmask), ptr(y), ptr(h), ptr(r), ptr(wbf), 1, stream())
+    # the weight images the backward reads
+    assert torch.equal(wbf[:FF * D].view(FF, D), W1.to(torch.bfloat16))
+    assert torch.equal(wbf[FF * D:2 * FF * D].view(FF, D), W2.t().to(torch.bfloat16))
+    assert torch.equal(wbf[2 * FF * D:].view(D, FF), W1.t().to(torch.bfloat16))
+    km = keep_mask(seed, site, p, (M, FF)) if p > 0 else np.ones((M, FF), bool)
+    keep = torch.from_numpy(km.astype(np.float64)).cuda() * float(np.float32(scale if p > 0 else 1.0))
+    dh = torch.randn(M, D, device="cuda", generator=g)
+    hr, (dxr, dW1r, db1r, dW2r) = ffn_ref_bf16(x, W1, b1, W2, b2, keep, dh)
+    rr = 1.0 / torch.sqrt((hr * hr).mean(1) + 1e-6)
+    assert rel(h.double(), hr) < BF_TOL
+    assert rel(r.double(), rr) < BF_TOL
+    assert rel(y.double(), nw.double() * hr * rr[:, None]) < BF_TOL
+    if p > 0:
+        assert np.array_equal(ffn_keep_bits_bf(fmask, M, FF), km)
+    dx = torch.empty(M, D, device="cuda")
+    nb = L.query("ctr_ffn_slab_rows", M, D, 1)
+    assert nb <= 512
+    o_b1 = FF * D
+    o_w2 = o_b1 + (FF + 63) // 64 * 64
+    ld = o_w2 + D * FF
+    slab = torch.full((nb, ld), float("nan"), device="cuda")       # every used entry must be written
+    slab[:, o_b1 + FF:o_w2] = 0
+    L.call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask),
+           ptr(dx), ptr(slab), ld, o_b1, o_w2, ptr(wbf), 1, stream())
+    red = slab.double().sum(0)
+    assert rel(dx.double(), dxr) < BF_TOL
+    assert rel(red[:FF * D].view(FF, D), dW1r) < BF_TOL
+    assert rel(red[o_b1:o_b1 + FF], db1r) < BF_TOL
+    assert rel(red[o_w2:o_w2 + D * FF].view(D, FF), dW2r) < BF_TOL
+    # deterministic: a second run is bitwise identical
+    slab2 = torch.empty_like(slab)
+    slab2[:, o_b1 + FF:o_w2] = 0
+    dx2 = torch.empty_like(dx)
+    L.call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask),
+           ptr(dx2), ptr(slab2), ld, o_b1, o_w2, ptr(wbf), 1, stream())
+    assert torch.equal(dx, dx2) and torch.equal(slab, slab2)
+
+
+@pytest.mark.parametrize("M,D,FF,p", [(300, 32, 384, 0.1), (130, 64, 384, 0.15), (70001, 32, 384, 0.1),
+                                      (70001, 64, 64, 0.0)])
+def test_ffn_bwd_norms_bf16_vs_emulation(M, D, FF, p):
+    """ctr_ffn_bwd_norms with CTR_FFN_BF16: norm2 backward -> bf16 FFN backward -> norm1 backward, the six
+    parameter grads accumulated over each persistent workgroup's tiles."""
+    from oracle.rng import keep_mask
+    from tossctr.rng import drop_args
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(7 * M + D + FF + 1)
+    h1 = torch.randn(M, D, device="cuda", generator=g) * 1.5
+    W1 = torch.randn(FF, D, device="cuda", generator=g) / math.sqrt(D)
+    b1 = torch.randn(FF, device="cuda", generator=g) * 0.1
+    W2 = torch.randn(D, FF, device="cuda", generator=g) / math.sqrt(FF)
+    b2 = torch.randn(D, device="cuda", generator=g) * 0.1
+    n1 = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    n2 = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    seed, site = (3 << 32) | 11, 6
+    key, thresh, scale = drop_args(seed, site, p, True)
+    r1 = 1.0 / torch.sqrt((h1 * h1).mean(1) + 1e-6)
+    x1 = (n1 * h1 * r1[:, None]).contiguous()
+    x2, h2, r2 = (torch.empty(M, D, device="cuda"), torch.empty(M, D, device="cuda"), torch.empty(M, device="cuda"))
+    fmask = torch.zeros(L.query("ctr_ffn_mask_words", M, FF), dtype=torch.int32, device="cuda")
+    wbf = torch.empty(3 * FF * D, dtype=torch.bfloat16, device="cuda")
+    L.call("ctr_ffn_fwd", ptr(x1), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(n2), 1e-6, key, thresh, scale,
+           ptr(fmask), ptr(x2), ptr(h2), ptr(r2), ptr(wbf), 1, stream())
+    km = keep_mask(seed, site, p, (M, FF)) if p > 0 else np.ones((M, FF), bool)
+    keep = torch.from_numpy(km.astype(np.float64)).cuda() * float(np.float32(scale if p > 0 else 1.0))
+    dy = torch.randn(M, D, device="cuda", generator=g)
+    # norm2 backward in fp64 on the kernel's own h2 (its forward is checked above)
+    h2v, n2r = h2.double().requires_grad_(), n2.double().requires_grad_()
+    (n2r * h2v / torch.sqrt((h2v * h2v).mean(1, keepdim=True) + 1e-6)).backward(dy.double())
+    dh2 = h2v.grad
+    _, (dx1, dW1r, db1r, dW2r) = ffn_ref_bf16(x1, W1, b1, W2, b2, keep, dh2)
+    h1r, n1r = h1.double().requires_grad_(), n1.double().requires_grad_()
+    (n1r * h1r / torch.sqrt((h1r * h1r).mean(1, keepdim=True) + 1e-6)).backward(dx1)
+    al = lambda v: (v + 63) // 64 * 64
+    o_n1 = 0
+    o_w1 = al(o_n1 + D)
+    o_b1 = al(o_w1 + FF * D)
+    o_w2 = al(o_b1 + FF)
+    o_b2 = al(o_w2 + D * FF)
+    o_n2 = al(o_b2 + D)
+    ld = o_n2 + D
+    nb = L.query("ctr_ffn_slab_rows", M, D, 1)
+    slab = torch.zeros(nb, ld, device="cuda")
+    dh1 = torch.empty(M, D, device="cuda")
+    L.call("ctr_ffn_bwd_norms", ptr(x1), ptr(dy), ptr(h2), ptr(r2), ptr(n2), ptr(h1), ptr(r1), ptr(n1), M, D, FF,
+           ptr(W1), ptr(b1), ptr(W2), key, thresh, scale, ptr(fmask), ptr(dh1), ptr(slab), ld,
+           o_n1, o_w1, o_b1, o_w2, o_b2, o_n2, ptr(wbf), 1, stream())
+    red = slab.double().sum(0)
+    assert rel(dh1.double(), h1r.grad) < BF_TOL
+    assert rel(red[o_n1:o_n1 + D], n1r.grad) < BF_TOL
+    assert rel(red[o_w1:o_w1 + FF * D].view(FF, D), dW1r) < BF_TOL
+    assert rel(red[o_b1:o_b1 + FF], db1r) < BF_TOL
+    assert rel(red[o_w2:o_w2 + D * FF].view(D, FF), dW2r) < BF_TOL
+    assert rel(red[o_b2:o_b2 + D], dh2.sum(0)) < BF_TOL
+    assert rel(red[o_n2:o_n2 + D], n2r.grad) < BF_TOL
 
 
 @pytest.mark.parametrize("B,F,D,QR", [(37, 23, 16, 8), (64, 200, 32, 96), (9, 27, 64, 96), (5, 3, 32, 20)])

@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--H", type=int, default=8)
     ap.add_argument("--p", type=float, default=0.1, help="dropout probability (0: no dropout)")
     ap.add_argument("--nobias", action="store_true", help="attn: no positional bias")
+    ap.add_argument("--bf16", action="store_true", help="ffn: the amp bf16 kernels (CTR_FFN_BF16)")
     ap.add_argument("--shapes", default="", help="gemm: comma-separated indices of the shape list")
     args = ap.parse_args()
     torch.manual_seed(0)
@@ -64,12 +65,14 @@ def main():
         dh, dx = torch.randn(M, D, device="cuda"), torch.empty(M, D, device="cuda")
         o_b1, o_w2 = FF * D, FF * D + FF
         ld = (o_w2 + D * FF + 3) // 4 * 4
-        nb = _lib.query("ctr_ffn_slab_rows", M, D)
+        fl = 1 if args.bf16 else 0
+        wbf = torch.empty(3 * FF * D, dtype=torch.bfloat16, device="cuda") if fl else None
+        nb = _lib.query("ctr_ffn_slab_rows", M, D, fl)
         slab = torch.zeros(nb, ld, device="cuda")
         fwd = lambda: call("ctr_ffn_fwd", ptr(x), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(nw), 1e-6, 12345,
-                           thr, 1.0 / 0.9, ptr(mask), ptr(y), ptr(h), ptr(r), st)
+                           thr, 1.0 / 0.9, ptr(mask), ptr(y), ptr(h), ptr(r), ptr(wbf), fl, st)
         bwd = lambda: call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), 12345, thr, 1.0 / 0.9,
-                           ptr(mask), ptr(dx), ptr(slab), ld, o_b1, o_w2, st)
+                           ptr(mask), ptr(dx), ptr(slab), ld, o_b1, o_w2, ptr(wbf), fl, st)
         tf = timeit(fwd, args.iters)
         tb = timeit(bwd, args.iters)
         print(f"ffn_fwd M={M} D={D} FF={FF}: {tf * 1e3:.1f} us  {4.0 * M * FF * D / tf / 1e9:.1f} TF/s")

@@ -63,6 +63,7 @@ struct FfnArgs {
   const float* r1;
   const float* nw1;
   float* dh1;          // (M, D) output: grad wrt h1
+  __bf16* wbf;         // amp bf16: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF) in bf16, written by the forward
 };
 
 template <int D>
@@ -163,6 +164,39 @@ __device__ __forceinline__ void fcontract(const float* st, const float (&bw)[Ffn
 }
 
 // ---------------------------------------------------------------- forward
+// h = x + (y + b2); RMSNorm over the row (the row's D values sit in the 16 lanes of one lane group).
+// yacc[i][j][rr]: row 16i + 4g + rr of this wave's rows (first row mw, LDS rows xw), column 16j + c.
+template <int D, class T>
+__device__ __forceinline__ void ffn_fwd_epilogue(const FfnArgs& a, const f32x4 (&yacc)[T::NI][T::NJ], const float* xw,
+                                                 int mw) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * i + 4 * g + rr, m = mw + row;
+      float hv[T::NJ];
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) {
+        const int d = 16 * j + c;
+        hv[j] = xw[row * T::S + d] + (yacc[i][j][rr] + a.b2[d]);
+        ss += hv[j] * hv[j];
+      }
+      ss = group_sum<16>(ss);
+      const float rs = 1.0f / sqrtf(ss / (float)D + a.eps);
+      if (m < a.M) {
+        if (c == 0) a.r[m] = rs;
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) {
+          const int d = 16 * j + c;
+          a.h[(long)m * D + d] = hv[j];
+          a.y[(long)m * D + d] = a.nw[d] * hv[j] * rs;
+        }
+      }
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
   using T = FfnTile<D>;
@@ -267,32 +301,7 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
   }
   if (f0 < a.FF) chunk(f0, wa);               // odd chunk count: wa holds chunk FF-16
 
-  // h = x + (y + b2); RMSNorm over the row (the row's D values sit in the 16 lanes of one lane group)
-#pragma unroll
-  for (int i = 0; i < T::NI; ++i)
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int row = 16 * i + 4 * g + rr, m = m0 + w * T::RW + row;
-      float hv[T::NJ];
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j) {
-        const int d = 16 * j + c;
-        hv[j] = xw[row * T::S + d] + (yacc[i][j][rr] + a.b2[d]);
-        ss += hv[j] * hv[j];
-      }
-      ss = group_sum<16>(ss);
-      const float rs = 1.0f / sqrtf(ss / (float)D + a.eps);
-      if (m < a.M) {
-        if (c == 0) a.r[m] = rs;
-#pragma unroll
-        for (int j = 0; j < T::NJ; ++j) {
-          const int d = 16 * j + c;
-          a.h[(long)m * D + d] = hv[j];
-          a.y[(long)m * D + d] = a.nw[d] * hv[j] * rs;
-        }
-      }
-    }
+  ffn_fwd_epilogue<D, T>(a, yacc, xw, m0 + w * T::RW);
 }
 
 // ---------------------------------------------------------------- backward
@@ -300,9 +309,8 @@ __global__ __launch_bounds__(256) void ffn_fwd_kernel(FfnArgs a) {
 // tile (rmsnorm_bwd_small's formula: dh = w dy r - h r^3/D sum_k w_k dy_k h_k); the workgroup's
 // column sums of dh2 (ffn.3.bias grad) and of dy h2 r2 (norm2.w grad) go to the slab.  `red` holds
 // 2 * 256 * 4 floats of scratch.
-template <int D, bool PERM = false>
-__device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, float* slab) {
-  using T = FfnTile<D>;
+template <int D, bool PERM = false, class T = FfnTile<D>>
+__device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, float* slab, bool acc = false) {
   constexpr int TPR = D / 4;                  // threads per row (one float4 each)
   float cb[4] = {0.f, 0.f, 0.f, 0.f}, cn[4] = {0.f, 0.f, 0.f, 0.f};
   const int c4 = (threadIdx.x % TPR) * 4;
@@ -343,7 +351,8 @@ __device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, 
     const int sub = col / 4 % TPR, t = col % 4;
     float sum = 0.f;
     for (int u = sub; u < 256; u += TPR) sum += red[which * 1024 + u * 4 + t];
-    slab[(which ? a.o_n2 : a.o_b2) + col] = sum;
+    float* dstp = slab + (which ? a.o_n2 : a.o_b2) + col;
+    *dstp = acc ? *dstp + sum : sum;
   }
   __syncthreads();
 }
@@ -351,10 +360,10 @@ __device__ void load_dh_norm2(const FfnArgs& a, int m0, float* dst, float* red, 
 // dx = dact W1 (complete over FF) + dh (residual path) for this wave's RW rows (dx[i][j][rr]: row
 // 16i+4g+rr, col 16j+c; dw = the wave's rows of the dh tile); NORMS: the norm1 backward.  `scratch`:
 // 4*D floats of LDS no wave still reads.
-template <int D, bool NORMS, bool PERM = false>
-__device__ __forceinline__ void ffn_bwd_epilogue(const FfnArgs& a, const f32x4 (&dxacc)[FfnTile<D>::NI][FfnTile<D>::NJ],
-                                                 const float* dw, int m0, float* slab, float* scratch) {
-  using T = FfnTile<D>;
+template <int D, bool NORMS, bool PERM = false, class T = FfnTile<D>>
+__device__ __forceinline__ void ffn_bwd_epilogue(const FfnArgs& a, const f32x4 (&dxacc)[T::NI][T::NJ],
+                                                 const float* dw, int m0, float* slab, float* scratch,
+                                                 bool acc = false) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   if (!NORMS) {
 #pragma unroll
@@ -427,7 +436,10 @@ __device__ __forceinline__ void ffn_bwd_epilogue(const FfnArgs& a, const f32x4 (
 #pragma unroll
     for (int j = 0; j < T::NJ; ++j) red[w * D + 16 * j + c] = cn1[j];
   __syncthreads();
-  if (tid < D) slab[a.o_n1 + tid] = ((red[tid] + red[D + tid]) + red[2 * D + tid]) + red[3 * D + tid];
+  if (tid < D) {
+    const float v = ((red[tid] + red[D + tid]) + red[2 * D + tid]) + red[3 * D + tid];
+    slab[a.o_n1 + tid] = acc ? slab[a.o_n1 + tid] + v : v;
+  }
 }
 
 template <int D, bool NORMS>
@@ -785,6 +797,501 @@ __global__ __launch_bounds__(256) void ffn_bwd_cols_kernel(FfnArgs a) {
   ffn_bwd_epilogue<D, NORMS, true>(a, dxs, dht + w * T::RW * T::S, m0, slab, xt);
 }
 
+// ---------------------------------------------------------------- amp: bf16
+// The reference under autocast(bfloat16) runs both FFN Linears as bf16 matmuls (src/train.py:158-164).
+// Here every product is v_mfma_f32_16x16x32_bf16 (bf16-rounded operands, fp32 accumulation); GELU, the
+// dropout, the residual and both RMSNorms stay fp32.  At bf16 MFMA rates the products cost ~1/16 of the
+// fp32 form, so these kernels are bound by the element-wise GELU / dropout VALU work: it runs on packed
+// fp32 pairs (v_pk_fma_f32 / v_pk_mul_f32: two elements per issue) with a 5-term erfc (cdf_as2).  The
+// layouts are chosen so no product needs a transpose except the backward's dact W1:
+//   * forward, pre^T = W1 x^T (A = W1 rows, B = x rows: both 8 contiguous d per lane) leaves ff on the
+//     accumulator's row axis, so fo feeds y = fo W2^T as the A operand directly (k-set of lane group g:
+//     ff {4g..4g+3} of the chunk's first 16 columns, then of its second 16);
+//   * backward, pre = x W1^T / dfo = dh W2 leave the rows on the accumulator's row axis, so fo and dact of
+//     two 16-row blocks feed the row contractions dW2^T = fo^T dh and dW1 = dact^T x directly (k-set:
+//     rows {4g..4g+3} of block 0, then of block 1); dact goes through a wave-private LDS staging block
+//     for dx = dact W1.
+// The forward also writes the bf16 weight images the backward's operands read with one 16-byte load each
+// (wbf: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF)); the weights do not change between the two.
+// Keep bits (layout "row words"): word (chunk * nb16 + blk) * 16 + row16 holds bit f of 32-column chunk
+// `chunk`, column f, of row 16 blk + row16 -- the forward assembles a row's word across the four lane
+// groups, the backward reads the words of its rows.  The dropout decisions themselves are the fp32
+// path's (drop_pair_bits of the element pair), so both modes drop the same elements.
+// Backward weight grads: persistent workgroups (ctr_ffn_slab_rows: <= 512, two per CU) walk row tiles
+// t = blockIdx.x, + gridDim.x, ...; per 32-column chunk the four waves' partials are summed in a fixed
+// order and added into the workgroup's own slab row (first tile: stored), so the slab has one row per
+// workgroup instead of one per tile -- deterministic.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int D>
+struct FfnBf {
+  static_assert(D == 32 || D == 64, "bf16 FFN: D in {32, 64}");
+  static constexpr int RT = 128, RW = 32, NI = 2;   // rows per tile / per wave, 16-row blocks per wave
+  static constexpr int KH = D / 32;                 // k steps of a D-contraction
+  static constexpr int NJ = D / 16;                 // 16-col blocks of D
+  static constexpr int S = D + 4;                   // fp32 tile row stride
+  static constexpr int TILE = RT * S;
+  static constexpr int SST = 32;                    // dact staging: [32 rows][32 cols] bf16, 16-B chunks swizzled
+  static constexpr int STG = 2 * 16 * SST;          // bf16 elements per wave
+  static constexpr int ES = D + 4;                  // exchange, dW1 half: [32 ff][ES] (+ 32 db1)
+  static constexpr int E2S = 36;                    // exchange, dW2 half: [D][E2S]
+  static constexpr int XCH = (32 * ES + 32) > (D * E2S) ? (32 * ES + 32) : (D * E2S);   // floats per wave
+  // two exchange buffers (one barrier per half) while two workgroups still fit a CU's 160 KB
+  static constexpr int NBUF = D <= 32 ? 2 : 1;
+};
+
+__device__ __forceinline__ f32x4 mfma_bf(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 pack8(f32x4 lo, f32x4 hi) {
+  const bf16x4 l = __builtin_convertvector(lo, bf16x4), h = __builtin_convertvector(hi, bf16x4);
+  return bf16x8{l[0], l[1], l[2], l[3], h[0], h[1], h[2], h[3]};
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+__device__ __forceinline__ bf16x8 buf_ld_bf8(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st_u32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, 0, 0);
+}
+// workgroup barrier ordering LDS only (the exchange's global slab updates need no cross-wave order)
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Phi(z) and exp(-z^2/2) of two elements for the bf16 path: Abramowitz-Stegun 7.1.26 (|erf error| <=
+// 1.5e-7, so Phi to 7.5e-8 absolute -- far below the 2^-9 relative rounding the bf16 product applies to
+// the activation); 5 coefficients instead of norm_cdf's 9, packed, and the exponential doubles as the
+// GELU derivative's pdf.
+__device__ __forceinline__ f32x2 cdf_as2(f32x2 z, f32x2& e) {
+  const f32x2 x = f32x2{fabsf(z.x), fabsf(z.y)} * 0.70710678118654752f;
+  const f32x2 d = x * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * (0.5f * 1.061405429f) + (0.5f * -1.453152027f);
+  p = p * t + (0.5f * 1.421413741f);
+  p = p * t + (0.5f * -0.284496736f);
+  p = p * t + (0.5f * 0.254829592f);
+  const f32x2 ar = z * z * -0.72134752044448170f;
+  e = f32x2{__builtin_amdgcn_exp2f(ar.x), __builtin_amdgcn_exp2f(ar.y)};
+  const f32x2 h = p * t * e;
+  const f32x2 q = 1.0f - h;
+  return f32x2{z.x < 0.f ? h.x : q.x, z.y < 0.f ? h.y : q.y};
+}
+
+// rows [m0, m0 + RT) of a (M, D) matrix -> fp32 LDS tile, row stride D + 4 (zero rows past M)
+template <int D, int RT>
+__device__ __forceinline__ void load_rows(const float* __restrict__ src, int M, int m0, float* dst) {
+  for (int q = threadIdx.x; q < RT * D / 4; q += 256) {
+    const int i = q / (D / 4), c4 = (q % (D / 4)) * 4;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (m0 + i < M) v = *(const f32x4*)(src + (long)(m0 + i) * D + c4);
+    *(f32x4*)(dst + i * (D + 4) + c4) = v;
+  }
+}
+
+__device__ __forceinline__ uint32_t rw_word(int chunk, int nb16, int blk, int row16) {
+  return ((uint32_t)(chunk * nb16 + blk) * 16 + row16);
+}
+
+template <int D, bool DROP>
+__global__ __launch_bounds__(256) void ffn_fwd_bf_kernel(FfnArgs a) {
+  using T = FfnBf<D>;
+  __shared__ __attribute__((aligned(16))) float xt[T::TILE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int m0 = blockIdx.x * T::RT, rb = w * T::RW;
+  // bf16 weight images for the backward: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF)
+  if (a.wbf) {
+    const int n = a.FF * D;
+    for (int e = blockIdx.x * 256 + tid; e < 3 * n; e += gridDim.x * 256) {
+      float v;
+      if (e < n) {
+        v = a.W1[e];
+      } else if (e < 2 * n) {
+        const int q = e - n;
+        v = a.W2[(q % D) * a.FF + q / D];
+      } else {
+        const int q = e - 2 * n;
+        v = a.W1[(q % a.FF) * D + q / a.FF];
+      }
+      a.wbf[e] = (__bf16)v;
+    }
+  }
+  load_rows<D, T::RT>(a.x, a.M, m0, xt);
+  __syncthreads();
+  const float* xw = xt + rb * T::S;
+  // B operand of pre^T = W1 x^T: x[row 16i + c][32kh + 8g .. +7]
+  bf16x8 xf[T::NI][T::KH];
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int kh = 0; kh < T::KH; ++kh) {
+      const float* p = xw + (16 * i + c) * T::S + 32 * kh + 8 * g;
+      xf[i][kh] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 4));
+    }
+  f32x4 yacc[T::NI][T::NJ];
+#pragma unroll
+  for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nb16 = (a.M + 15) / 16;
+  const auto rW1 = buf_rsrc(a.W1, (uint32_t)a.FF * D * 4);
+  const auto rW2 = buf_rsrc(a.W2, (uint32_t)a.FF * D * 4);
+  const auto rb1 = buf_rsrc(a.b1, (uint32_t)a.FF * 4);
+  const auto rmask = buf_rsrc(a.mask, DROP ? (uint32_t)nb16 * 16 * (a.FF / 32) * 4 : 0u);
+  const uint32_t thr = a.drop.thresh;
+  const float dsc = a.drop.scale;
+  struct Wc {
+    bf16x8 w1[2][T::KH], w2[T::NJ];
+    f32x4 b[2];
+  };
+  auto load_w = [&](int f0, Wc& W) {
+    const uint32_t s1 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * D * 4);
+    const uint32_t s2 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * 4);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int kh = 0; kh < T::KH; ++kh) {      // A of pre^T: W1[f0 + 16s + c][32kh + 8g .. +7]
+        const uint32_t vo = (uint32_t)((16 * s + c) * D + 32 * kh + 8 * g) * 4;
+        W.w1[s][kh] = pack8(buf_ld4(rW1, vo, s1), buf_ld4(rW1, vo + 16, s1));
+      }
+#pragma unroll
+    for (int j = 0; j < T::NJ; ++j) {          // B of y: W2[16j + c][f0 + 4g .. +3], [f0 + 16 + 4g .. +3]
+      const uint32_t vo = (uint32_t)((16 * j + c) * a.FF + 4 * g) * 4;
+      W.w2[j] = pack8(buf_ld4(rW2, vo, s2), buf_ld4(rW2, vo + 64, s2));
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) W.b[s] = buf_ld4(rb1, (uint32_t)(16 * s + 4 * g) * 4, s2);
+  };
+  auto chunk = [&](int f0, const Wc& W) {
+    // all of the chunk's pre^T products first: the element-wise work of block 0 covers their latency
+    f32x4 p[T::NI][2];
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        p[i][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < T::KH; ++kh) p[i][s] = mfma_bf(W.w1[s][kh], xf[i][kh], p[i][s]);
+      }
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i) {
+      // p[i][s][r] = pre[row 16i + c][ff f0 + 16s + 4g + r]; elements (r = 0,1), (2,3) share a hash
+      const uint32_t m = (uint32_t)(m0 + rb + 16 * i + c);
+      uint32_t kb = 0;              // keep bit of element (s, r) at 4s + r
+      f32x4 fo[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const f32x2 z = {p[i][s][2 * q] + W.b[s][2 * q], p[i][s][2 * q + 1] + W.b[s][2 * q + 1]};
+          f32x2 e;
+          f32x2 v = z * cdf_as2(z, e);
+          if (DROP) {
+            const uint32_t hb = drop_pair_bits(a.drop, (m * (uint32_t)a.FF + f0 + 16 * s + 4 * g + 2 * q) >> 1);
+            const bool k0 = (hb & 0xFFFFu) >= thr, k1 = (hb >> 16) >= thr;
+            v = v * f32x2{k0 ? dsc : 0.f, k1 ? dsc : 0.f};
+            kb |= (k0 ? 1u : 0u) << (4 * s + 2 * q);
+            kb |= (k1 ? 1u : 0u) << (4 * s + 2 * q + 1);
+          }
+          fo[s][2 * q] = v.x;
+          fo[s][2 * q + 1] = v.y;
+        }
+      const bf16x8 af = pack8(fo[0], fo[1]);
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) yacc[i][j] = mfma_bf(af, W.w2[j], yacc[i][j]);
+      if (DROP) {     // the row's word: bits 4g .. 4g+3 and 16+4g .. +3 from each lane group, stored by group 0
+        uint32_t kw = ((kb & 0xFu) << (4 * g)) | ((kb >> 4) << (16 + 4 * g));
+        kw |= (uint32_t)__shfl_xor((int)kw, 16, 64);
+        kw |= (uint32_t)__shfl_xor((int)kw, 32, 64);
+        const uint32_t wi = rw_word(f0 >> 5, nb16, (m0 + rb) / 16 + i, c);
+        buf_st_u32(kw, rmask, (g == 0 && (int)m < a.M) ? wi * 4 : BUF_OOB);
+      }
+    }
+  };
+  Wc wa, wb;
+  load_w(0, wa);
+  int f0 = 0;
+  for (; f0 + 64 <= a.FF; f0 += 64) {
+    load_w(f0 + 32, wb);
+    chunk(f0, wa);
+    __builtin_amdgcn_sched_barrier(0);
+    load_w(min(f0 + 64, a.FF - 32), wa);     // past the end: a harmless reload of the last chunk
+    chunk(f0 + 32, wb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (f0 < a.FF) chunk(f0, wa);
+  ffn_fwd_epilogue<D, T>(a, yacc, xw, m0 + rb);
+}
+
+// Backward tile: D = 32 takes 128-row tiles (32 rows per wave), D = 64 64-row tiles (16 per wave) so two
+// workgroups fit a CU's LDS.  Per 32-column chunk every wave writes its fo / dact rows as bf16 [ff][rows]
+// images; after one barrier each wave reads its dact rows back transposed (ds_read_b64_tr_b16) for
+// dx = dact W1 and computes its share of the chunk's weight-grad tiles over ALL the tile's rows (K = RT)
+// from the images and the tile's x^T / dh^T images -- complete tiles, no cross-wave partial sums -- and
+// adds them into the workgroup's slab row.  The images alternate between two buffers: one barrier a chunk.
+template <int D>
+struct FfnBb {
+  static_assert(D == 32 || D == 64, "bf16 FFN: D in {32, 64}");
+  static constexpr int RT = D <= 32 ? 128 : 64;
+  static constexpr int RW = RT / 4, NI = RW / 16;
+  static constexpr int KH = D / 32, NJ = D / 16;
+  static constexpr int S = D + 4;                   // fp32 tile row stride
+  static constexpr int TILE = RT * S;
+  static constexpr int RS = RT + 8;                 // bf16 image row stride (rows of a [col][row] image)
+  static constexpr int IMG = 32 * RS;               // one [32 ff][RT] image, bf16 elements
+  static constexpr int CIMG = D * RS;               // one [D][RT] image, bf16 elements
+  static constexpr int NT = 2 * NJ / 4;             // dW1 (and dW2^T) 16x16 tiles per wave and chunk
+  // the fo / dact image buffers (2 x 2 images) share their LDS with the x tile + the norm loader scratch
+  static constexpr int RREG = 2 * IMG > TILE + 2048 ? 2 * IMG : TILE + 2048;   // floats
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+// 4 rows x 16 columns of 16-bit elements, delivered transposed (MI355X ds_read_b64_tr_b16): lane 4q + p of
+// each 16-lane group addresses row q, columns 4p .. 4p+3; lane i receives column i, row q in element q
+__device__ __forceinline__ bf16x4 lds_tr4(const __bf16* p) {
+  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p));
+}
+
+template <int D, bool NORMS, bool DROP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffn_bwd_bf_kernel(FfnArgs a) {
+  using T = FfnBb<D>;
+  // [H: dh tile (fp32; residual / norm1 epilogue) | R: x tile + loader scratch, then 2 x {fo, dact} images |
+  //  XC, HC: x^T and dh^T images of the tile (bf16)]
+  __shared__ __attribute__((aligned(16))) float smem[T::TILE + T::RREG + T::CIMG];
+  float* H = smem;
+  float* X = smem + T::TILE;
+  __bf16* IM = (__bf16*)X;
+  __bf16* XC = (__bf16*)(smem + T::TILE + T::RREG);
+  __bf16* HC = XC + T::CIMG;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int rb = w * T::RW;
+  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
+  const int nb16 = (a.M + 15) / 16;
+  const int ntiles = (a.M + T::RT - 1) / T::RT;
+  const int FF = a.FF;
+  const auto rw = buf_rsrc(a.wbf, (uint32_t)(3 * FF * D) * 2);
+  const auto rb1 = buf_rsrc(a.b1, (uint32_t)FF * 4);
+  const auto rmask = buf_rsrc(a.mask, DROP ? (uint32_t)nb16 * 16 * (FF / 32) * 4 : 0u);
+  const float dsc = a.drop.scale;
+  const uint32_t vw1 = (uint32_t)(c * D + 8 * g) * 2;          // W1 / W2^T rows f0 + c (+16s), d 8g..
+  const uint32_t vw1t = (uint32_t)(c * FF + 8 * g) * 2;         // W1^T rows d = c (+16j), ff f0 + 8g..
+  // this wave's weight-grad tiles of each chunk: (s, j) for j in js0 .. js0 + NT - 1; db1 with the j = 0 tile
+  const int ts = w >> 1, js0 = (w & 1) * T::NT;
+  const bool has_db = js0 == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  struct Wc {
+    bf16x8 w1[2][T::KH], w2[2][T::KH];
+    float b[2];
+    uint32_t mk[T::NI][4];
+  };
+
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const bool acc = t != (int)blockIdx.x;      // later tiles add into the workgroup's slab row
+    const int m0 = t * T::RT;
+    const int blk0 = (m0 + rb) / 16;
+    __syncthreads();                            // the previous tile is done with every region
+    load_rows<D, T::RT>(a.x, a.M, m0, X);
+    if (NORMS) load_dh_norm2<D, false, T>(a, m0, H, X + T::TILE, slab, acc);
+    else load_rows<D, T::RT>(a.dh, a.M, m0, H);
+    __syncthreads();
+    // row fragments (A of pre / dfo: 8 contiguous d of row 16i + c) and the x^T / dh^T images
+    bf16x8 xr[T::NI][T::KH], hr[T::NI][T::KH];
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int kh = 0; kh < T::KH; ++kh) {
+        const int o = (rb + 16 * i + c) * T::S + 32 * kh + 8 * g;
+        xr[i][kh] = pack8(*(const f32x4*)(X + o), *(const f32x4*)(X + o + 4));
+        hr[i][kh] = pack8(*(const f32x4*)(H + o), *(const f32x4*)(H + o + 4));
+      }
+    for (int q = tid; q < T::RT * D / 4; q += 256) {
+      const int row = q % T::RT, d4 = (q / T::RT) * 4;
+      const f32x4 vx = *(const f32x4*)(X + row * T::S + d4), vh = *(const f32x4*)(H + row * T::S + d4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        XC[(d4 + k) * T::RS + row] = (__bf16)vx[k];
+        HC[(d4 + k) * T::RS + row] = (__bf16)vh[k];
+      }
+    }
+    __syncthreads();                            // X becomes the image buffers
+
+    f32x4 dxacc[T::NI][T::NJ];
+#pragma unroll
+    for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto load_w = [&](int f0, Wc& W) {
+      const uint32_t s1 = __builtin_amdgcn_readfirstlane((uint32_t)f0 * D * 2);
+      const uint32_t s2 = __builtin_amdgcn_readfirstlane((uint32_t)(FF * D + f0 * D) * 2);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int kh = 0; kh < T::KH; ++kh) {
+          // B of pre: W1[f0 + 16s + c][32kh + 8g .. +7];  B of dfo: W2^T[f0 + 16s + c][32kh + 8g .. +7]
+          const uint32_t vo = vw1 + (uint32_t)(16 * s * D + 32 * kh) * 2;
+          W.w1[s][kh] = buf_ld_bf8(rw, vo, s1);
+          W.w2[s][kh] = buf_ld_bf8(rw, vo, s2);
+        }
+      const uint32_t sb = __builtin_amdgcn_readfirstlane((uint32_t)f0 * 4);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) W.b[s] = buf_ld(rb1, (uint32_t)(16 * s + c) * 4, sb);
+      if (DROP) {
+        // keep words of rows 16i + 4g + r, pre-shifted to this lane's column; rows past M read 0 (their dh
+        // is 0 anyway)
+        const uint32_t sm = __builtin_amdgcn_readfirstlane((uint32_t)(f0 >> 5) * nb16 * 16 * 4);
+#pragma unroll
+        for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            W.mk[i][r] = __builtin_bit_cast(uint32_t, buf_ld(rmask, (uint32_t)((blk0 + i) * 16 + 4 * g + r) * 4, sm)) >> c;
+      }
+    };
+
+    // slab entries this lane owns in a chunk (fixed over tiles, so a later tile's read-modify-write sees
+    // this lane's own earlier store): dW1 rows f0 + 16 ts + 4g + r, column 16j + c; dW2 row 16j + c,
+    // columns f0 + 16 ts + 4g + r; db1 f0 + 16 ts + 4g + r (lanes c = 0 of the db owners)
+    auto p_w1 = [&](int f0, int jj, int r) { return slab + a.o_w1 + (long)(f0 + 16 * ts + 4 * g + r) * D + 16 * (js0 + jj) + c; };
+    auto p_w2 = [&](int f0, int jj, int r) { return slab + a.o_w2 + (long)(16 * (js0 + jj) + c) * FF + f0 + 16 * ts + 4 * g + r; };
+    auto p_b1 = [&](int f0, int r) { return slab + a.o_b1 + f0 + 16 * ts + 4 * g + r; };
+
+    auto chunk = [&](int f0, int bsel, const Wc& W) {
+      __bf16* FO = IM + bsel * 2 * T::IMG;
+      __bf16* DA = FO + T::IMG;
+      // B of dx: W1^T[16j + c][f0 + 8g .. +7] (first used after the element-wise work)
+      bf16x8 w1d[T::NJ];
+      const uint32_t s3 = __builtin_amdgcn_readfirstlane((uint32_t)(2 * FF * D + f0) * 2);
+#pragma unroll
+      for (int j = 0; j < T::NJ; ++j) w1d[j] = buf_ld_bf8(rw, vw1t + (uint32_t)(16 * j * FF) * 2, s3);
+      // later tiles: the slab values this chunk's tiles add to, loaded now (their latency under the chunk)
+      float o1[T::NT][4], o2[T::NT][4], ob[4];
+#pragma unroll
+      for (int jj = 0; jj < T::NT; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o1[jj][r] = acc ? *p_w1(f0, jj, r) : 0.f;
+          o2[jj][r] = acc ? *p_w2(f0, jj, r) : 0.f;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ob[r] = (acc && has_db && c == 0) ? *p_b1(f0, r) : 0.f;
+      // the chunk's D-contractions (their latency under the element-wise work)
+      f32x4 pre[T::NI][2], dfo[T::NI][2];
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          pre[i][s] = dfo[i][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kh = 0; kh < T::KH; ++kh) {
+            pre[i][s] = mfma_bf(xr[i][kh], W.w1[s][kh], pre[i][s]);
+            dfo[i][s] = mfma_bf(hr[i][kh], W.w2[s][kh], dfo[i][s]);
+          }
+        }
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          // pre[i][s][r], dfo[i][s][r]: row rb + 16i + 4g + r, column f0 + 16s + c
+          f32x4 fv, dv;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const f32x2 z = f32x2{pre[i][s][2 * q], pre[i][s][2 * q + 1]} + W.b[s];
+            f32x2 e;
+            const f32x2 cdf = cdf_as2(z, e);
+            const f32x2 gg = z * e * 0.39894228040143268f + cdf;
+            f32x2 sc = {1.f, 1.f};
+            if (DROP)
+              sc = f32x2{((W.mk[i][2 * q] >> (16 * s)) & 1u) ? dsc : 0.f, ((W.mk[i][2 * q + 1] >> (16 * s)) & 1u) ? dsc : 0.f};
+            const f32x2 fo = z * cdf * sc;
+            const f32x2 da = f32x2{dfo[i][s][2 * q], dfo[i][s][2 * q + 1]} * sc * gg;
+            fv[2 * q] = fo.x;
+            fv[2 * q + 1] = fo.y;
+            dv[2 * q] = da.x;
+            dv[2 * q + 1] = da.y;
+          }
+          // the [ff][rows] images: 4 consecutive rows of column 16s + c
+          const int o = (16 * s + c) * T::RS + rb + 16 * i + 4 * g;
+          *(bf16x4*)(FO + o) = __builtin_convertvector(fv, bf16x4);
+          *(bf16x4*)(DA + o) = __builtin_convertvector(dv, bf16x4);
+        }
+      lds_sync();
+      // dx[rows 16i..] += dact W1 over the chunk: A = dact[row 16i + c][ff 8g .. +7], transposed reads
+#pragma unroll
+      for (int i = 0; i < T::NI; ++i) {
+        const __bf16* base = DA + (8 * g + (lane & 15) / 4) * T::RS + rb + 16 * i + 4 * (lane & 3);
+        const bf16x8 av = cat8(lds_tr4(base), lds_tr4(base + 4 * T::RS));
+#pragma unroll
+        for (int j = 0; j < T::NJ; ++j) dxacc[i][j] = mfma_bf(av, w1d[j], dxacc[i][j]);
+      }
+      // this wave's weight-grad tiles over the tile's RT rows (C[ff 16 ts + 4g + r][d 16j + c])
+      f32x4 t1[T::NT], t2[T::NT], tb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int jj = 0; jj < T::NT; ++jj) t1[jj] = t2[jj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < T::RT / 32; ++kk) {
+        const bf16x8 ad = *(const bf16x8*)(DA + (16 * ts + c) * T::RS + 32 * kk + 8 * g);
+        const bf16x8 af = *(const bf16x8*)(FO + (16 * ts + c) * T::RS + 32 * kk + 8 * g);
+#pragma unroll
+        for (int jj = 0; jj < T::NT; ++jj) {
+          const int o = (16 * (js0 + jj) + c) * T::RS + 32 * kk + 8 * g;
+          t1[jj] = mfma_bf(ad, *(const bf16x8*)(XC + o), t1[jj]);
+          t2[jj] = mfma_bf(af, *(const bf16x8*)(HC + o), t2[jj]);
+        }
+        if (has_db) tb = mfma_bf(ad, ones, tb);
+      }
+#pragma unroll
+      for (int jj = 0; jj < T::NT; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          *p_w1(f0, jj, r) = o1[jj][r] + t1[jj][r];
+          *p_w2(f0, jj, r) = o2[jj][r] + t2[jj][r];
+        }
+      if (has_db && c == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) *p_b1(f0, r) = ob[r] + tb[r];
+    };
+
+    if constexpr (D <= 32) {     // weights of the next chunk prefetched into the other register set
+      Wc wa, wb;
+      load_w(0, wa);
+      int f0 = 0;
+      for (; f0 + 64 <= FF; f0 += 64) {
+        load_w(f0 + 32, wb);
+        chunk(f0, 0, wa);
+        __builtin_amdgcn_sched_barrier(0);
+        load_w(min(f0 + 64, FF - 32), wa);
+        chunk(f0 + 32, 1, wb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (f0 < FF) chunk(f0, 0, wa);
+    } else {
+      for (int f0 = 0; f0 < FF; f0 += 32) {
+        Wc wa;
+        load_w(f0, wa);
+        chunk(f0, (f0 >> 5) & 1, wa);
+      }
+    }
+    ffn_bwd_epilogue<D, NORMS, false, T>(a, dxacc, H + rb * T::S, m0, slab, X, acc);
+  }
+}
+
+// persistent backward grid: at most 512 workgroups (two per CU), tiles split as evenly as possible
+static int ffn_bf_grid(long M, int D) {
+  const long rt = D <= 32 ? 128 : 64;
+  const long nt = (M + rt - 1) / rt;
+  const long per = (nt + 511) / 512;
+  return (int)((nt + per - 1) / per);
+}
+
 template <int D>
 static void launch_ffn(const FfnArgs& a, bool bwd, hipStream_t s) {
   const int blocks = cdiv(a.M, FfnTile<D>::RT);
@@ -804,6 +1311,7 @@ static void launch_ffn(const FfnArgs& a, bool bwd, hipStream_t s) {
 }
 
 static bool ffn_shape_ok(int D, int FF) { return (D == 16 || D == 32 || D == 64) && FF > 0 && FF % 16 == 0; }
+static bool ffn_bf_shape_ok(int D, int FF) { return (D == 32 || D == 64) && FF > 0 && FF % 32 == 0; }
 
 // buffer resources carry 32-bit byte extents: (M, D) activations, (FF, D) weights, the keep-bit words
 static bool ffn_extent_ok(long M, int D, int FF) {
@@ -811,7 +1319,30 @@ static bool ffn_extent_ok(long M, int D, int FF) {
   return M * D * 4 < lim && (long)FF * D * 4 < lim && M * (FF / 16) * 2 < lim;
 }
 
-static int ffn_dispatch(const FfnArgs& a, int D, bool bwd, hipStream_t s) {
+template <int D>
+static void launch_ffn_bf(const FfnArgs& a, bool bwd, hipStream_t s) {
+  const bool drop = a.drop.thresh != 0;
+  if (!bwd) {
+    if (drop) ffn_fwd_bf_kernel<D, true><<<cdiv(a.M, 128), 256, 0, s>>>(a);
+    else ffn_fwd_bf_kernel<D, false><<<cdiv(a.M, 128), 256, 0, s>>>(a);
+    return;
+  }
+  const int grid = ffn_bf_grid(a.M, D);
+  if (a.dy) {
+    if (drop) ffn_bwd_bf_kernel<D, true, true><<<grid, 256, 0, s>>>(a);
+    else ffn_bwd_bf_kernel<D, true, false><<<grid, 256, 0, s>>>(a);
+  } else {
+    if (drop) ffn_bwd_bf_kernel<D, false, true><<<grid, 256, 0, s>>>(a);
+    else ffn_bwd_bf_kernel<D, false, false><<<grid, 256, 0, s>>>(a);
+  }
+}
+
+static int ffn_dispatch(const FfnArgs& a, int D, bool bwd, int flags, hipStream_t s) {
+  if (flags & CTR_FFN_BF16) {
+    if (D == 32) launch_ffn_bf<32>(a, bwd, s);
+    else launch_ffn_bf<64>(a, bwd, s);
+    return check_launch(bwd ? "ffn_bwd_bf16" : "ffn_fwd_bf16");
+  }
   switch (D) {
     case 16: launch_ffn<16>(a, bwd, s); break;
     case 32: launch_ffn<32>(a, bwd, s); break;
@@ -824,9 +1355,14 @@ static int ffn_dispatch(const FfnArgs& a, int D, bool bwd, hipStream_t s) {
 
 using namespace ctr;
 
-extern "C" int ctr_ffn_supported(int D, int FF) { return ffn_shape_ok(D, FF) ? 1 : 0; }
+extern "C" int ctr_ffn_supported(int D, int FF, int flags) {
+  return ((flags & CTR_FFN_BF16) ? ffn_bf_shape_ok(D, FF) : ffn_shape_ok(D, FF)) ? 1 : 0;
+}
 
-extern "C" int ctr_ffn_slab_rows(int M, int D) { return cdiv(M, D >= 64 ? 64 : 128); }
+extern "C" int ctr_ffn_slab_rows(int M, int D, int flags) {
+  if (flags & CTR_FFN_BF16) return ffn_bf_grid(M, D);
+  return cdiv(M, D >= 64 ? 64 : 128);
+}
 
 // enough for either keep-bit layout (FfnTile::LW)
 extern "C" int ctr_ffn_mask_words(int M, int FF) {
@@ -836,8 +1372,10 @@ extern "C" int ctr_ffn_mask_words(int M, int FF) {
 
 extern "C" int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1, const float* b1, const float* W2,
                            const float* b2, const float* norm_w, float eps, uint32_t drop_key, uint32_t drop_thresh,
-                           float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* stream) {
+                           float drop_scale, uint32_t* mask, float* y, float* h, float* r, void* wbf, int flags,
+                           void* stream) {
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_fwd: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(!(flags & CTR_FFN_BF16) || ffn_bf_shape_ok(D, FF), "ctr_ffn_fwd bf16: needs D in {32,64} and FF % 32 == 0");
   CTR_REQUIRE(ffn_extent_ok(M, D, FF), "ctr_ffn_fwd: M x D too large for 32-bit buffer offsets");
   if (M <= 0) return 0;
   FfnArgs a = {};
@@ -845,15 +1383,18 @@ extern "C" int ctr_ffn_fwd(const float* x, int M, int D, int FF, const float* W1
   a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = (uint16_t*)mask;
   a.y = y; a.h = h; a.r = r;
-  return ffn_dispatch(a, D, false, (hipStream_t)stream);
+  a.wbf = (flags & CTR_FFN_BF16) ? (__bf16*)wbf : nullptr;
+  return ffn_dispatch(a, D, false, flags, (hipStream_t)stream);
 }
 
 extern "C" int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF, const float* W1, const float* b1,
                            const float* W2, uint32_t drop_key, uint32_t drop_thresh, float drop_scale,
                            const uint32_t* mask, float* dx, float* slab, long ld_slab, int o_b1, int o_w2,
-                           void* stream) {
+                           const void* wbf, int flags, void* stream) {
+  CTR_REQUIRE(!(flags & CTR_FFN_BF16) || wbf, "ctr_ffn_bwd bf16 needs the forward's bf16 weight images (wbf)");
   CTR_REQUIRE(!drop_thresh || mask, "ctr_ffn_bwd with dropout needs the forward's keep bits");
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(!(flags & CTR_FFN_BF16) || ffn_bf_shape_ok(D, FF), "ctr_ffn_bwd bf16: needs D in {32,64} and FF % 32 == 0");
   CTR_REQUIRE(ffn_extent_ok(M, D, FF), "ctr_ffn_bwd: M x D too large for 32-bit buffer offsets");
   CTR_REQUIRE(o_b1 >= FF * D && o_w2 >= o_b1 + FF && ld_slab >= (long)o_w2 + (long)D * FF, "ctr_ffn_bwd: slab layout");
   if (M <= 0) return 0;
@@ -862,7 +1403,8 @@ extern "C" int ctr_ffn_bwd(const float* x, const float* dh, int M, int D, int FF
   a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = (uint16_t*)const_cast<uint32_t*>(mask);
   a.dh = dh; a.dx = dx; a.slab = slab; a.ld_slab = ld_slab; a.o_b1 = o_b1; a.o_w2 = o_w2;
-  return ffn_dispatch(a, D, true, (hipStream_t)stream);
+  a.wbf = (__bf16*)const_cast<void*>(wbf);
+  return ffn_dispatch(a, D, true, flags, (hipStream_t)stream);
 }
 
 extern "C" int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h2, const float* r2, const float* nw2,
@@ -870,9 +1412,12 @@ extern "C" int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h
                                  const float* W1, const float* b1, const float* W2, uint32_t drop_key,
                                  uint32_t drop_thresh, float drop_scale, const uint32_t* mask, float* dh1,
                                  float* slab, long ld_slab, int o_n1, int o_w1, int o_b1, int o_w2, int o_b2, int o_n2,
-                                 void* stream) {
+                                 const void* wbf, int flags, void* stream) {
+  CTR_REQUIRE(!(flags & CTR_FFN_BF16) || wbf, "ctr_ffn_bwd_norms bf16 needs the forward's bf16 weight images (wbf)");
   CTR_REQUIRE(!drop_thresh || mask, "ctr_ffn_bwd_norms with dropout needs the forward's keep bits");
   CTR_REQUIRE(ffn_shape_ok(D, FF), "ctr_ffn_bwd_norms: needs D in {16,32,64} and FF % 16 == 0");
+  CTR_REQUIRE(!(flags & CTR_FFN_BF16) || ffn_bf_shape_ok(D, FF),
+              "ctr_ffn_bwd_norms bf16: needs D in {32,64} and FF % 32 == 0");
   CTR_REQUIRE(ffn_extent_ok(M, D, FF), "ctr_ffn_bwd_norms: M x D too large for 32-bit buffer offsets");
   CTR_REQUIRE(dy && h2 && r2 && nw2 && h1 && r1 && nw1 && dh1, "ctr_ffn_bwd_norms: missing norm operands");
   CTR_REQUIRE(o_n1 + D <= o_w1 && o_w1 + FF * D <= o_b1 && o_b1 + FF <= o_w2 && o_w2 + D * FF <= o_b2 &&
@@ -886,5 +1431,6 @@ extern "C" int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h
   a.slab = slab; a.ld_slab = ld_slab; a.o_b1 = o_b1; a.o_w2 = o_w2;
   a.o_w1 = o_w1; a.o_b2 = o_b2; a.o_n1 = o_n1; a.o_n2 = o_n2;
   a.dy = dy; a.h2 = h2; a.r2 = r2; a.nw2 = nw2; a.h1 = h1; a.r1 = r1; a.nw1 = nw1; a.dh1 = dh1;
-  return ffn_dispatch(a, D, true, (hipStream_t)stream);
+  a.wbf = (__bf16*)const_cast<void*>(wbf);
+  return ffn_dispatch(a, D, true, flags, (hipStream_t)stream);
 }

@@ -71,13 +71,13 @@ SIGS = {
     "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
     "ctr_attn_bwd_nparts": (i, [i, i, i]),
     "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
-    "ctr_ffn_supported": (i, [i, i]),
-    "ctr_ffn_slab_rows": (i, [i, i]),
+    "ctr_ffn_supported": (i, [i, i, i]),
+    "ctr_ffn_slab_rows": (i, [i, i, i]),
     "ctr_ffn_mask_words": (i, [i, i]),
-    "ctr_ffn_fwd": (i, [p, i, i, i, p, p, p, p, p, f, u, u, f, p, p, p, p, p]),
-    "ctr_ffn_bwd": (i, [p, p, i, i, i, p, p, p, u, u, f, p, p, p, l, i, i, p]),
+    "ctr_ffn_fwd": (i, [p, i, i, i, p, p, p, p, p, f, u, u, f, p, p, p, p, p, i, p]),
+    "ctr_ffn_bwd": (i, [p, p, i, i, i, p, p, p, u, u, f, p, p, p, l, i, i, p, i, p]),
     "ctr_ffn_bwd_norms": (i, [p, p, p, p, p, p, p, p, i, i, i, p, p, p, u, u, f, p, p, p, l,
-                              i, i, i, i, i, i, p]),
+                              i, i, i, i, i, i, p, i, p]),
     "ctr_rmsnorm_fwd": (i, [p, l, i, i, p, f, p, l, p, p]),
     "ctr_rmsnorm_bwd_nparts": (i, [i, i]),
     "ctr_rmsnorm_bwd": (i, [p, l, p, l, p, p, i, i, p, l, p, l, p, p]),

@@ -162,8 +162,12 @@ class Engine:
         # row-streaming in/out-projection kernels (rowgemm.hip) for the D they are built for
         self.rowgemm = a.n_layers > 0 and all(bool(_lib.query("ctr_rowgemm_supported", k, n))
                                               for k, n in ((a.D, 3 * a.D), (a.D, a.D), (3 * a.D, a.D)))
-        self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden)) and \
+        self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden, 0)) and \
             self._ffn_contiguous()
+        # amp: bf16 -> the fused FFN's bf16-MFMA kernels where their shape constraints hold (D in {32, 64},
+        # FF % 32 == 0); other shapes keep the fp32 kernels (more precise than the reference's bf16)
+        self.ffn_flags = 1 if (self.bf16 and self.ffn_fused and
+                               _lib.query("ctr_ffn_supported", a.D, a.ffn_hidden, 1)) else 0   # CTR_FFN_BF16
 
     def _tab_array(self, keys, bases):
         """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
@@ -365,9 +369,11 @@ class Engine:
                 # Linear -> GELU -> Dropout -> Linear -> +x1 -> RMSNorm in one kernel (ffn.hip)
                 fmask = W.get(f"fmask{li}", (_lib.query("ctr_ffn_mask_words", M, FF),), torch.int32) \
                     if dfk[1] else None
+                # bf16 weight images for the bf16 backward (W1 | W2^T | W1^T), written by the forward
+                fwbf = W.get(f"fwbf{li}", (3 * FF * D,), torch.bfloat16) if self.ffn_flags else None
                 call("ctr_ffn_fwd", ptr(x1), M, D, FF, ptr(P[pre + "ffn.0.weight"]), ptr(P[pre + "ffn.0.bias"]),
                      ptr(P[pre + "ffn.3.weight"]), ptr(P[pre + "ffn.3.bias"]), ptr(P[pre + "norm2.w"]), 1e-6, *dfk,
-                     ptr(fmask), ptr(x2), ptr(h2), ptr(r2), st)
+                     ptr(fmask), ptr(x2), ptr(h2), ptr(r2), ptr(fwbf), self.ffn_flags, st)
             else:
                 act = W.get(f"ffa{li}", (M, FF))
                 fo = W.get(f"ffo{li}", (M, FF))
@@ -378,7 +384,7 @@ class Engine:
                           GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
                                   norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
             Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, amask=amask, h1=h1, r1=r1, x1=x1,
-                      act=act, fo=fo, fmask=fmask,
+                      act=act, fo=fo, fmask=fmask, fwbf=fwbf if self.ffn_fused else None,
                       h2=h2, r2=r2)
             layers.append(Ls)
             xs.append(x2)
@@ -658,13 +664,13 @@ class Engine:
                                              "norm2.w")]
             n_sl = o[5] + D
             ld_sl = (n_sl + 3) // 4 * 4
-            nb = _lib.query("ctr_ffn_slab_rows", M, D)
+            nb = _lib.query("ctr_ffn_slab_rows", M, D, self.ffn_flags)
             slab = W.get_zeroed("ffn_slab", (nb, ld_sl))
             dh1 = W.get("dh1", (M, D))
             call("ctr_ffn_bwd_norms", ptr(Ls["x1"]), ptr(dx2), ptr(Ls["h2"]), ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]),
                  ptr(Ls["h1"]), ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
                  ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dh1),
-                 ptr(slab), ld_sl, *o, st)
+                 ptr(slab), ld_sl, *o, ptr(Ls["fwbf"]), self.ffn_flags, st)
             self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
         else:
             # x2 = norm2(x1 + ffn(x1))
