@@ -20,6 +20,37 @@ CAT_DIMS_NEXT = {
 N_NUM_NEXT = 82   # cfgs/dare_qnn_next.yaml:52-134 num_cols_explicit (82 columns) -> X_num / X_mask width
 
 
+def dare_base(**over):
+    """BASELINE config 1: cfgs/dare_base.yaml (DARE only: S1 query on inventory_id, no encoder block, fc
+    head, emb_dim 64, L = 400, K = 80), restated value for value; ``over`` replaces top-level sections."""
+    cfg = {
+        "exp_name": "dare_base", "seed": 777, "device": "cuda", "deterministic": True, "amp": "none",   # l.1-5
+        "use_compile": False,
+        "data": {"train_path": "/path/to/train.parquet", "test_path": "/path/to/test.parquet",          # l.8-24
+                 "cache_dir": "./cache/dare_base", "use_cache": True, "chunked_build": True, "add_isna_mask": True,
+                 "impute_strategy": "median",
+                 "cat_cols": ["gender", "age_group", "inventory_id", "day_of_week", "hour", "l_feat_14"],
+                 "hash_buckets": {"gender": 16, "age_group": 64, "day_of_week": 8, "hour": 32,
+                                  "inventory_id": 2_000_000, "l_feat_14": 1_000_000},
+                 "num_patterns": ["feat_*", "history_*", "l_feat_*"]},
+        "sequence": {"col": "seq", "max_len": 400, "pad_id": 0, "top_k": 80, "recency_tau": 256,         # l.26-34
+                     "query_mode": "S1", "query_key": "inventory_id", "transformer_block": False},
+        "model": {"emb_dim": 64, "dare_dropout": 0.1, "qnn_alpha": {"enabled": False}},                # l.36-40
+        "train": {"batch_size": 16384, "epochs": 10, "optimizer": "adamw", "lr": 0.001, "weight_decay": 0.0001,
+                  "warmup_epochs": 1, "cosine": True, "early_stop_patience": 3, "grad_clip_norm": 1.0},  # l.42-51
+        "cv": {"n_splits": 5, "group_key": "inventory_id", "stratify_target": "clicked"},              # l.53-56
+        "eval": {"monitor": "score", "maximize": True},                                                # l.58-60
+        "calibration": {"enabled": True, "method": "temperature", "lr": 0.05, "iters": 200},           # l.62-66
+        "logging": {"log_dir": "./runs", "tb": True, "csv_log": True, "verbose_steps": 100},           # l.68-72
+    }
+    for k, v in over.items():
+        if isinstance(v, dict) and isinstance(cfg.get(k), dict):
+            cfg[k] = {**cfg[k], **v}
+        else:
+            cfg[k] = v
+    return cfg
+
+
 def dare_qnn_next(emb_dim=32, max_len=100, batch_size=4096, hash_buckets=1_000_000):
     """BASELINE config 2: cfgs/dare_qnn_next.yaml with hash_buckets=1e6, emb_dim=32, seq_len=100, bs=4096."""
     cat_cols = list(CAT_DIMS_NEXT)

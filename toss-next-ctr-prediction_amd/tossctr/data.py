@@ -163,7 +163,9 @@ class DeviceShards:
             parts = []
             for m in man["shards"]:
                 a = np.load(m[k]["path"], mmap_mode="r")
-                parts.append(torch.from_numpy(np.ascontiguousarray(a).astype(dt, copy=False)))
+                # a read-only mmap stays read-only through astype(copy=False): copy it (it is staged to the
+                # device right after, so the host copy is transient)
+                parts.append(torch.from_numpy(np.array(a, dtype=dt, copy=True)))
             host = torch.cat(parts) if parts else torch.zeros(0)
             if host.dim() == 1:
                 host = host[:, None]
