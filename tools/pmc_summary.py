@@ -6,7 +6,7 @@ non-PMC kernel duration from a kernel-trace summary (PMC runs serialise dispatch
 timestamps are not used).  Derived columns:
   * HBM bytes  = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024; gfx950 FETCH_SIZE counts half of wide
     streaming reads, MI355X_MICROARCH.md "HBM")
-  * MFMA TF/s  = SQ_INSTS_VALU_MFMA_MOPS_F32 x 512 FLOP / duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
+  * MFMA TF/s  = (SQ_INSTS_VALU_MFMA_MOPS_F32 + _BF16 when collected) x 512 FLOP / duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
     (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
   * LDS conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS-array cycle)
   * wave-time split = SQ_WAIT_ANY, SQ_WAIT_INST_ANY (of which SQ_WAIT_INST_LDS) over SQ_WAVE_CYCLES
@@ -86,7 +86,8 @@ def main():
         us = dur.get(k[:110])
         hb = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024 / 1e6 if "FETCH_SIZE" in c and "WRITE_SIZE" in c else None
         wr = c["WRITE_SIZE"] * 1024 / 1e6 if "WRITE_SIZE" in c else None
-        tf = c["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512 / (us * 1e-6) / 1e12 if us and "SQ_INSTS_VALU_MFMA_MOPS_F32" in c else None
+        mops = [c[n] for n in ("SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_INSTS_VALU_MFMA_MOPS_BF16") if n in c]
+        tf = sum(mops) * 512 / (us * 1e-6) / 1e12 if us and mops else None
         busy = (c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * 1024)
                 if c.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in c else None)
         lds = (c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"] if c.get("SQ_LDS_IDX_ACTIVE") else None)
