@@ -107,7 +107,7 @@ def main():
             t = timeit(fn, args.iters)
             print(f"rowgemm_wgrad {no}x{ni} M={M}: {t * 1e3:.1f} us  {4 * M * (no + ni) / t / 1e6:.0f} GB/s")
     if "gemm" in which:        # the QNN MLP's big GEMMs at each split-K factor
-        shapes = [(4096, 512, 6400, 0, 1), (512, 6400, 4096, 1, 0), (4096, 6400, 512, 0, 0),
+        shapes = [(4096, 512, 6400, 0, 1), (4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0), (512, 6400, 4096, 1, 0), (4096, 6400, 512, 0, 0),
                   (4096, 1152, 512, 0, 0), (4096, 512, 1152, 0, 1), (512, 1152, 4096, 1, 0),
                   (32, 96, 4096, 1, 0), (1, 256, 4096, 1, 0), (1, 32, 4096, 1, 0), (96, 1152, 4096, 1, 0),
                   (256, 512, 4096, 1, 0), (1024, 96, 4096, 1, 0), (32, 96, 245760, 1, 0)]
@@ -118,17 +118,23 @@ def main():
             Bg = torch.randn((Ng, Kg) if tb else (Kg, Ng), device="cuda")
             Cg = torch.empty(Mg, Ng, device="cuda")
             res = []
-            for sp in (1, 2, 4, 6, 8, 16, 32, 64):
-                if sp > max(1, Kg // 64):
-                    continue
-                ws = torch.empty(sp * Mg * Ng + 16, device="cuda")
-                fn = lambda: call("ctr_gemm", Mg, Ng, Kg, ptr(Ag), Ag.shape[1], ta, ptr(Bg), Bg.shape[1], tb, ptr(Cg), Ng,
-                                  None, sp, ptr(ws), st)
-                t = timeit(fn, args.iters)
-                res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
+            for fl in ((1, 3) if args.bf16 else (0,)):
+                for sp in (1, 2, 3, 4, 5, 6, 8, 12):
+                    if sp > max(1, Kg // 64):
+                        continue
+                    ws = torch.empty(sp * Mg * Ng + 16, device="cuda")
+                    fn = lambda: call("ctr_gemm_ex", Mg, Ng, Kg, ptr(Ag), Ag.shape[1], ta, ptr(Bg), Bg.shape[1], tb,
+                                      ptr(Cg), Ng, None, sp, ptr(ws), None, fl, st)
+                    t = timeit(fn, args.iters)
+                    res.append(f"f{fl}s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
             torch.backends.cuda.matmul.allow_tf32 = False      # the library's fp32 path, for reference
             a_op, b_op = (Ag.t() if ta else Ag), (Bg.t() if tb else Bg)
-            t = timeit(lambda: torch.matmul(a_op, b_op, out=Cg), args.iters)
+            if args.bf16:
+                a_op, b_op = a_op.bfloat16(), b_op.bfloat16()
+                Cb = torch.empty(Mg, Ng, device="cuda", dtype=torch.bfloat16)
+                t = timeit(lambda: torch.matmul(a_op, b_op, out=Cb), args.iters)
+            else:
+                t = timeit(lambda: torch.matmul(a_op, b_op, out=Cg), args.iters)
             res.append(f"torch:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
             print(f"gemm M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
     if "attn" in which:

@@ -69,9 +69,10 @@ __device__ __forceinline__ float epi_elem(const ctr_gemm_epi_t& e, float v, int 
   return v;
 }
 
-template <int BM, int BN, bool TA, bool TB, bool BF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 2 : 4))) void gemm_kernel(GemmArgs g) {
-  constexpr int BK = BF ? 32 : 16;
+template <int BM, int BN, bool TA, bool TB, int BFK = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BFK ? 2 : 4))) void gemm_kernel(GemmArgs g) {
+  constexpr bool BF = BFK > 0;               // BFK: bf16 k-slice depth (32 or 64), 0 = fp32
+  constexpr int BK = BF ? BFK : 16;
   constexpr int SA = BM + 16, SB = BN + 16;
   constexpr int SK = BK + 8;                 // bf16 tiles: [row][k] rows of 40 bf16 (80 B: conflict-free b128)
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -364,8 +365,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 2 : 4)
     }
     if constexpr (BF) {
       // lane (g, c) reads row 16i + c, k = 8g .. 8g + 7 of the A tile (row 16j + c of the B tile)
-      const __bf16* a = Ah + cur * BM * SK + (lane & 15) * SK + 8 * (lane >> 4);
-      const __bf16* b = Bh + cur * BN * SK + (lane & 15) * SK + 8 * (lane >> 4);
+#pragma unroll
+      for (int ks = 0; ks < BK; ks += 32) {
+      const __bf16* a = Ah + cur * BM * SK + (lane & 15) * SK + 8 * (lane >> 4) + ks;
+      const __bf16* b = Bh + cur * BN * SK + (lane & 15) * SK + 8 * (lane >> 4) + ks;
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) af[i] = *(const bf16x8*)(a + (wm + i * 16) * SK);
@@ -376,6 +379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 2 : 4)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
     const float* a = As + cur * BK * SA;
     const float* b = Bs + cur * BK * SB;
@@ -532,7 +536,7 @@ __global__ void gemm_smallk_kernel(GemmArgs g, int ta, int tb) {
   }
 }
 
-template <int BM, int BN, bool BF>
+template <int BM, int BN, int BF>
 static void launch_tile_t(GemmArgs& g, int ta, int tb, int splits, hipStream_t s) {
   dim3 grid(cdiv(g.M, BM), cdiv(g.N, BN), splits);
   if (!ta && !tb) gemm_kernel<BM, BN, false, false, BF><<<grid, 256, 0, s>>>(g);
@@ -542,9 +546,10 @@ static void launch_tile_t(GemmArgs& g, int ta, int tb, int splits, hipStream_t s
 }
 
 template <int BM, int BN>
-static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s, bool bf) {
-  if (bf) launch_tile_t<BM, BN, true>(g, ta, tb, splits, s);
-  else launch_tile_t<BM, BN, false>(g, ta, tb, splits, s);
+static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s, int bf) {
+  if (bf == 64) launch_tile_t<BM, BN, 64>(g, ta, tb, splits, s);
+  else if (bf) launch_tile_t<BM, BN, 32>(g, ta, tb, splits, s);
+  else launch_tile_t<BM, BN, 0>(g, ta, tb, splits, s);
 }
 
 }  // namespace ctr
@@ -557,7 +562,7 @@ extern "C" size_t ctr_gemm_ws_size(int M, int N, int splits) {
 
 static int gemm_core(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
                      float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
-                     void* stream, bool bf = false) {
+                     void* stream, int bf = 0) {
   CTR_REQUIRE(M >= 0 && N >= 0 && K >= 0, "negative dims");
   if (M == 0 || N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
@@ -591,7 +596,7 @@ static int gemm_core(int M, int N, int K, const float* A, int lda, int ta, const
     }
     if (seg->C2) { g.C2 = seg->C2; g.ldc2 = seg->ldc2; g.nc = seg->nc; }
   }
-  const int BK = bf ? 32 : 16;
+  const int BK = bf ? bf : 16;
   int klen = K;
   if (splits > 1) {
     klen = ((K + splits - 1) / splits + BK - 1) / BK * BK;
@@ -642,6 +647,7 @@ extern "C" int ctr_gemm_seg(int M, int N, int K, const float* A, int lda, int ta
 extern "C" int ctr_gemm_ex(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
                            float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
                            int flags, void* stream) {
-  CTR_REQUIRE((flags & ~CTR_GEMM_BF16) == 0, "ctr_gemm_ex: unknown flags");
-  return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, stream, (flags & CTR_GEMM_BF16) != 0);
+  CTR_REQUIRE((flags & ~(CTR_GEMM_BF16 | 2)) == 0, "ctr_gemm_ex: unknown flags");
+  const int bf = (flags & CTR_GEMM_BF16) ? ((flags & 2) ? 64 : 32) : 0;
+  return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, stream, bf);
 }
