@@ -80,6 +80,17 @@ int ctr_gemm_seg(int M, int N, int K, const float* A, int lda, int ta, const flo
 int ctr_gemm_ex(int M, int N, int K, const float* A, int lda, int ta, const float* B, int ldb, int tb,
                 float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
                 int flags, void* stream);
+/* bf16-operand GEMM (amp: bf16 -- the reference's torch.autocast(bfloat16) nn.Linear of the QNN MLP,
+ * src/models/qnn_alpha.py:120-124, src/train.py:133-139): A, B are bf16 images already in HBM (ta / tb as
+ * in ctr_gemm: A (M, K) or stored (K, M); B (N, K) when tb, else (K, N)), fp32 accumulation on
+ * v_mfma_f32_16x16x32_bf16, C and the epilogue fp32 (no fused RMSNorm; seg: the C2 result segment only).
+ * ctr_gemm_bf16_ok: K % 64 == 0, leading dims % 8 == 0, M % 8 (ta) / N % 8 (!tb) == 0.
+ * ctr_to_bf16: fp32 (rows, cols), row stride lds -> bf16 row stride ldd, round-to-nearest-even.     */
+int ctr_gemm_bf16_ok(int M, int N, int K, int lda, int ta, int ldb, int tb, int splits);
+int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta, const void* B, int ldb, int tb,
+                  float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
+                  void* stream);
+int ctr_to_bf16(const float* src, long lds, int rows, int cols, void* dst, long ldd, void* stream);
 
 
 /* Row-streaming GEMMs of the DARE encoder layer (MHA in_proj / out_proj, src/models/dare.py:53-62, and

@@ -137,6 +137,19 @@ def main():
                 t = timeit(lambda: torch.matmul(a_op, b_op, out=Cg), args.iters)
             res.append(f"torch:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
             print(f"gemm M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
+    if "gemmbf" in which:      # ctr_gemm_bf16 (bf16 operands in HBM) on the QNN MLP's three big products
+        for (Mg, Ng, Kg, ta, tb) in [(4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0)]:
+            Ag = torch.randn((Kg, Mg) if ta else (Mg, Kg), device="cuda").bfloat16()
+            Bg = torch.randn((Ng, Kg) if tb else (Kg, Ng), device="cuda").bfloat16()
+            Cg = torch.empty(Mg, Ng, device="cuda")
+            res = []
+            for sp in (1, 2, 3, 4, 6, 8):
+                ws = torch.empty(sp * Mg * Ng + 16, device="cuda")
+                fn = lambda: call("ctr_gemm_bf16", Mg, Ng, Kg, ptr(Ag), Ag.shape[1], ta, ptr(Bg), Bg.shape[1], tb,
+                                  ptr(Cg), Ng, None, sp, ptr(ws), None, st)
+                t = timeit(fn, args.iters)
+                res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}({t * 1e3:.0f}us)")
+            print(f"gemm_bf16 M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
     if "attn" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1

@@ -552,6 +552,182 @@ static void launch_tile(GemmArgs& g, int ta, int tb, int splits, hipStream_t s, 
   else launch_tile_t<BM, BN, 0>(g, ta, tb, splits, s);
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16-operand GEMM (amp: bf16; operands already bf16 in HBM, e.g. the QNN MLP's [z | inter] image).
+// 128 x 128 tile, 256 threads (2 x 2 waves of 64 x 64), BK = 64, both operand tiles staged by
+// global_load_lds (16 B per lane, no VGPR round trip) into two LDS buffers -- the next k-slice's DMA is in
+// flight while the current one is multiplied; one barrier per k-slice.  Operand layouts in LDS:
+//   k-contiguous operand (A[m][k] / B[n][k]): [128 rows][64 k] with 128-B rows, the 16-B chunk c of row r
+//     stored at chunk c ^ ((r >> 1) & 7) (the swizzle is applied to the per-lane GLOBAL address: the
+//     DMA writes lane-linear); fragments are ds_read_b128 -- the 16 rows a read touches land on 16
+//     different 16-B bank groups;
+//   k-major operand (A[k][m] / B[k][n]): [8 k-blocks][8 col-blocks][8 k][16 cols] 256-B blocks, rows 0-3 and
+//     4-7 of odd k-blocks swapped; fragments are two ds_read_b64_tr_b16 (4 k x 16 cols, transposed).
+// Rows / columns past M / N are clamped to the last valid one (their results are never stored); K must
+// be a multiple of 64 per split.  blockIdx -> (split, m-tile, n-tile) runs n fastest after a bijective
+// XCD remap, so the n-tiles sharing an A slab run on one XCD (one L2).
+struct GemmBfArgs {
+  GemmArgs g;            // shapes, C / C2, epilogue, split-K slabs (A/B fields unused)
+  const __bf16* A;
+  const __bf16* B;
+  int mt, nt;            // tiles along M, N
+};
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
+                                   (void __attribute__((address_space(3)))*)lds, 16, 0, 0);
+}
+
+typedef short s16x4_g __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x4 lds_tr4_g(const __bf16* p) {
+  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                                        (__attribute__((address_space(3))) s16x4_g*)p));
+}
+
+// stage rows [r0, r0 + 128) x k [k0, k0 + 64) of a k-contiguous operand; wave w issues 4 x 1 KB
+__device__ __forceinline__ void stage_kc(const __bf16* __restrict__ src, long ld, int r0, int nvalid, int k0,
+                                         __bf16* tile, int w, int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int q = w * 4 + t, r = q * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(r0 + r, nvalid - 1);
+    glds16(src + (long)gr * ld + k0 + 8 * kc, tile + q * 512);
+  }
+}
+
+// stage k [k0, k0 + 64) x cols [c0, c0 + 128) of a k-major operand; wave w issues 4 x 1 KB (instruction q:
+// k-block q / 2, col-blocks 4 (q % 2) .. +3; lane: block + lane / 16, row (lane % 16) / 2, half lane % 2)
+__device__ __forceinline__ void stage_km(const __bf16* __restrict__ src, long ld, int c0, int nvalid, int k0,
+                                         __bf16* tile, int w, int lane) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int q = w * 4 + t, kb = q >> 1, cb = 4 * (q & 1) + (lane >> 4);
+    const int row = ((lane & 15) >> 1) ^ (4 * (kb & 1));
+    const int col = min(c0 + 16 * cb + 8 * (lane & 1), nvalid - 8);
+    glds16(src + (long)(k0 + 8 * kb + row) * ld + col, tile + q * 512);
+  }
+}
+
+// fragment (16 rows/cols x 32 k) of k-slice ks (0/1) at tile row/col base rb: lane (g, c) gets row rb + c,
+// k 32 ks + 8 g .. + 7
+__device__ __forceinline__ bf16x8 frag_kc(const __bf16* tile, int rb, int ks, int lane) {
+  const int r = rb + (lane & 15), kc = 4 * ks + (lane >> 4);
+  return *(const bf16x8*)(tile + r * 64 + 8 * (kc ^ ((r >> 1) & 7)));
+}
+__device__ __forceinline__ bf16x8 frag_km(const __bf16* tile, int cb16, int ks, int lane) {
+  const int kb = 4 * ks + (lane >> 4), l = lane & 15;
+  const __bf16* blk = tile + (kb * 8 + cb16) * 128;
+  const int sw = 4 * (kb & 1);
+  const __bf16* p0 = blk + ((l >> 2) ^ sw) * 16 + 4 * (l & 3);          // k rows 0..3
+  const __bf16* p1 = blk + (((l >> 2) + 4) ^ sw) * 16 + 4 * (l & 3);    // k rows 4..7
+  const bf16x4 lo = lds_tr4_g(p0), hi = lds_tr4_g(p1);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <bool TA, bool TB>
+__global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 128 * 64];     // [stage][A | B][128 x 64]
+  const GemmArgs& g = p.g;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // bijective XCD remap: consecutive ids (same XCD: dispatch is round-robin over 8 XCDs)
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int nt_i = id % p.nt, rest = id / p.nt, mt_i = rest % p.mt, z = rest / p.mt;
+  const int m0 = mt_i * 128, n0 = nt_i * 128;
+  const int kz0 = z * g.klen, kz1 = min(g.K, kz0 + g.klen);
+  const int nkt = kz1 > kz0 ? (kz1 - kz0) / 64 : 0;
+  const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
+  const long lda = g.lda, ldb = g.ldb;
+
+  auto stage = [&](int buf, int k0) {
+    __bf16* ta = smem + buf * 2 * 8192;
+    __bf16* tb = ta + 8192;
+    if (TA) stage_km(p.A, lda, m0, g.M, k0, ta, w, lane);
+    else stage_kc(p.A, lda, m0, g.M, k0, ta, w, lane);
+    if (TB) stage_kc(p.B, ldb, n0, g.N, k0, tb, w, lane);
+    else stage_km(p.B, ldb, n0, g.N, k0, tb, w, lane);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nkt > 0) {
+    stage(0, kz0);
+    __builtin_amdgcn_s_waitcnt(0);       // vmcnt(0) lgkmcnt(0)...: the DMA has landed
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) stage(cur ^ 1, kz0 + (kt + 1) * 64);
+    const __bf16* ta = smem + cur * 2 * 8192;
+    const __bf16* tb = ta + 8192;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = TA ? frag_km(ta, (wm >> 4) + i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = TB ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_km(tb, (wn >> 4) + j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);       // the next slice's DMA (and this slice's reads) complete
+    __syncthreads();
+  }
+
+  const ctr_gemm_epi_t& e = g.epi;
+  const int lrow = wm + (lane >> 4) * 4, lcol = wn + (lane & 15);
+  if (g.ws) {   // split-K partial: raw slab, the reduce kernel applies the epilogue
+    float* slab = g.ws + (long)z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + lcol + j * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + lrow + i * 16 + r;
+          if (m < g.M && n < g.N) slab[(long)m * g.N + n] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + lcol + j * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + lrow + i * 16 + r;
+        if (m < g.M && n < g.N) *cptr(g, m, n) = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
+      }
+    }
+}
+
+// fp32 (rows, cols) with row stride lds -> bf16 with row stride ldd (RNE); 4 elements per thread
+__global__ void to_bf16_kernel(const float* __restrict__ src, long lds, int rows, int cols, __bf16* __restrict__ dst,
+                               long ldd) {
+  const int cq = (cols + 3) / 4;
+  const long n = (long)rows * cq;
+  for (long q = blockIdx.x * 256L + threadIdx.x; q < n; q += (long)gridDim.x * 256) {
+    const int r = (int)(q / cq), c = (int)(q % cq) * 4;
+    const float* s = src + r * lds + c;
+    __bf16* d = dst + r * ldd + c;
+    if (c + 3 < cols && ((((uintptr_t)s) & 15) == 0) && ((((uintptr_t)d) & 7) == 0)) {
+      *(bf16x4*)d = __builtin_convertvector(*(const f32x4*)s, bf16x4);
+    } else {
+      for (int j = 0; j < 4 && c + j < cols; ++j) d[j] = (__bf16)s[j];
+    }
+  }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
@@ -650,4 +826,69 @@ extern "C" int ctr_gemm_ex(int M, int N, int K, const float* A, int lda, int ta,
   CTR_REQUIRE((flags & ~(CTR_GEMM_BF16 | 2)) == 0, "ctr_gemm_ex: unknown flags");
   const int bf = (flags & CTR_GEMM_BF16) ? ((flags & 2) ? 64 : 32) : 0;
   return gemm_core(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, stream, bf);
+}
+
+extern "C" int ctr_to_bf16(const float* src, long lds, int rows, int cols, void* dst, long ldd, void* stream) {
+  CTR_REQUIRE(rows >= 0 && cols >= 0 && lds >= cols && ldd >= cols, "ctr_to_bf16: bad shape");
+  if (rows == 0 || cols == 0) return 0;
+  const long n = (long)rows * ((cols + 3) / 4);
+  to_bf16_kernel<<<(int)std::min<long>((n + 255) / 256, 8192), 256, 0, (hipStream_t)stream>>>(src, lds, rows, cols,
+                                                                                          (__bf16*)dst, ldd);
+  return check_launch("ctr_to_bf16");
+}
+
+extern "C" int ctr_gemm_bf16_ok(int M, int N, int K, int lda, int ta, int ldb, int tb, int splits) {
+  if (M < 8 || N < 8 || K <= 0 || K % 64) return 0;
+  if (splits < 1) splits = 1;
+  const int klen = ((K + splits - 1) / splits + 63) / 64 * 64;
+  (void)klen;
+  // 16-byte aligned rows (glds); k-major operands need 8-column groups inside the row
+  if ((lda % 8) || (ldb % 8)) return 0;
+  if (ta && M % 8) return 0;
+  if (!tb && N % 8) return 0;
+  return 1;
+}
+
+extern "C" int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta, const void* B, int ldb, int tb,
+                             float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws,
+                             const ctr_gemm_seg_t* seg, void* stream) {
+  CTR_REQUIRE(ctr_gemm_bf16_ok(M, N, K, lda, ta, ldb, tb, splits), "ctr_gemm_bf16: unsupported shape / layout");
+  CTR_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "ctr_gemm_bf16: operands need 16-byte alignment");
+  CTR_REQUIRE(!seg || (!seg->A2 && !seg->B2), "ctr_gemm_bf16: only the C2 result segment is supported");
+  GemmBfArgs p = {};
+  GemmArgs& g = p.g;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  ctr_gemm_epi_t zero = {};
+  g.epi = epi ? *epi : zero;
+  CTR_REQUIRE(!(g.epi.dact && !g.epi.aux), "dact needs aux");
+  CTR_REQUIRE(!g.epi.norm_w, "ctr_gemm_bf16: no fused RMSNorm epilogue");
+  g.C2 = nullptr; g.ldc2 = 0; g.nc = N;
+  if (seg && seg->C2) {
+    CTR_REQUIRE(seg->nc >= 0 && seg->nc <= N && !g.epi.aux && !g.epi.pre && !g.epi.add,
+                "ctr_gemm_bf16: C2 needs no row-indexed epilogue operand");
+    g.C2 = seg->C2; g.ldc2 = seg->ldc2; g.nc = seg->nc;
+  }
+  if (splits < 1) splits = 1;
+  int klen = ((K + splits - 1) / splits + 63) / 64 * 64;
+  splits = (K + klen - 1) / klen;
+  g.klen = klen;
+  CTR_REQUIRE(splits == 1 || ws, "ctr_gemm_bf16: split-K needs ws");
+  g.ws = splits > 1 ? ws : nullptr;
+  p.A = (const __bf16*)A;
+  p.B = (const __bf16*)B;
+  p.mt = cdiv(M, 128);
+  p.nt = cdiv(N, 128);
+  const int grid = p.mt * p.nt * splits;
+  hipStream_t s = (hipStream_t)stream;
+  if (!ta && tb) gemm_bf_kernel<false, true><<<grid, 256, 0, s>>>(p);
+  else if (!ta && !tb) gemm_bf_kernel<false, false><<<grid, 256, 0, s>>>(p);
+  else if (ta && !tb) gemm_bf_kernel<true, false><<<grid, 256, 0, s>>>(p);
+  else gemm_bf_kernel<true, true><<<grid, 256, 0, s>>>(p);
+  if (splits > 1) {
+    const long MN = (long)M * N;
+    int blocks = (int)std::min<long>((MN + 255) / 256, 4096);
+    g.ws = ws;
+    splitk_reduce_kernel<<<blocks, 256, 0, s>>>(g, splits);
+  }
+  return check_launch("ctr_gemm_bf16");
 }

@@ -49,6 +49,9 @@ SIGS = {
     "ctr_gemm": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, p]),
     "ctr_gemm_seg": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), p]),
     "ctr_gemm_ex": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), i, p]),
+    "ctr_gemm_bf16_ok": (i, [i, i, i, i, i, i, i, i]),
+    "ctr_gemm_bf16": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), p]),
+    "ctr_to_bf16": (i, [p, l, i, i, p, l, p]),
     "ctr_rowgemm_supported": (i, [i, i]),
     "ctr_rowgemm": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
     "ctr_rowgemm_wgrad_rows": (i, [i]),

@@ -233,6 +233,25 @@ class Engine:
         call("ctr_gemm_ex", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg, self.gemm_flags,
              self.s())
 
+    def bf_image(self, W, name, src, ld, rows, cols, out=None, off=0, ld_out=None):
+        """bf16 (RNE) image of a fp32 (rows, cols) operand for ctr_gemm_bf16 (workspace buffer `name`)."""
+        ld_out = ld_out or cols
+        if out is None:
+            out = W.get(name, (rows, ld_out), torch.bfloat16)
+        call("ctr_to_bf16", src, ld, rows, cols, ptr(out, off), ld_out, self.s())
+        return out
+
+    def gemm_bf(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, seg=None):
+        """C = op(A) op(B) on bf16 operand images (ctr_gemm_bf16, amp: bf16); split-K so that the
+        (tiles x splits) grid stays within one wave of 2 workgroups per CU."""
+        tiles = math.ceil(M / 128) * math.ceil(N / 128)
+        splits = max(1, min(512 // max(tiles, 1), K // 512))
+        wsp = ptr(self.splitk_ws(splits * M * N)) if splits > 1 else None
+        call("ctr_gemm_bf16", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg, self.s())
+
+    def bf_ok(self, M, N, K, lda, ta, ldb, tb):
+        return self.bf16 and bool(_lib.query("ctr_gemm_bf16_ok", M, N, K, lda, ta, ldb, tb, 1))
+
     @staticmethod
     def _split_factor(M, N, K, min_depth):
         """Split-K factor: ~1024 workgroups (4 resident per CU), at most 8 splits once the grid has >= 32
@@ -481,7 +500,14 @@ class Engine:
             dm = (0, 0, 1.0) if last else drop_args(seed, SITE_MLP0 + j, a.qnn_p, training)
             epi = GemmEpi(bias=ptr(P[bkey]), act=0 if last else 1, pre=ptr(pre), drop_key=dm[0], drop_thresh=dm[1],
                           drop_scale=dm[2])
-            if j == 0:
+            if j == 0 and self.bf_ok(B, n_out, din, din, 0, din, 1) and FD % 8 == 0:
+                # amp: bf16 images of [z | inter] (one (B, FD + C) buffer, also the weight grad's operand)
+                # and of W0; the bf16-operand GEMM (glds-staged MFMA tiles)
+                zi_bf = self.bf_image(W, "zi_bf", ptr(z), FD, B, FD, ld_out=din)
+                self.bf_image(W, None, ptr(inter), C, B, C, out=zi_bf, off=FD, ld_out=din)
+                w0_bf = self.bf_image(W, "w0_bf", ptr(W0), din, n_out, din)
+                self.gemm_bf(B, n_out, din, ptr(zi_bf), din, 0, ptr(w0_bf), din, 1, ptr(out), n_out, epi)
+            elif j == 0:
                 # input [z | inter] (qnn_alpha.py:120-124): one GEMM over both K segments
                 self.gemm(B, n_out, FD + C, ptr(z), FD, 0, ptr(W0), din, 1, ptr(out), n_out, epi,
                           seg=_lib.GemmSeg(A2=ptr(inter), lda2=C, ka=FD))
@@ -492,7 +518,8 @@ class Engine:
                 hs.append(out)
                 acts.append(pre)
         return dict(z=z, rq=rq, ucat=ucat, zsum=zsum, gram=gram, vfull=vfull, S=S, quad=quad, inter_pre=inter_pre,
-                    mean=mean, g1=g1, gate=gate, inter=inter, hs=hs, acts=acts)
+                    mean=mean, g1=g1, gate=gate, inter=inter, hs=hs, acts=acts,
+                    zi_bf=W.t.get("zi_bf") if self.bf16 else None, w0_bf=W.t.get("w0_bf") if self.bf16 else None)
 
     def _fc_forward(self, W, fcin, ctx, cat_e, B, seed, training, logits):
         """QNN disabled: fc head on [u, mean(num_e), mean(mask_e), cat_embs] (wrapper.py:95-100,167-173)."""
@@ -741,6 +768,7 @@ class Engine:
         nh = len(a.mlp_hidden)
         # MLP, last layer first; dact epilogues fold relu' and the dropout mask in
         dcur, ncur = dlogits, 1
+        dcur_bf = None
         for j in reversed(range(nh + 1)):
             wkey, bkey = f"qnn.mlp.{3 * j}.weight", f"qnn.mlp.{3 * j}.bias"
             if j > 0:
@@ -753,6 +781,11 @@ class Engine:
                           GemmEpi(dact=1, aux=ptr(q["acts"][j - 1]), drop_key=dm[0], drop_thresh=dm[1],
                                   drop_scale=dm[2]))
                 dcur, ncur = dprev, kin
+            elif q.get("zi_bf") is not None and self.bf_ok(ncur, din, B, ncur, 1, din, 0):
+                # amp: dW0 = dcur^T [z | inter] on the forward's bf16 image (both operands k-major)
+                dcur_bf = self.bf_image(W, "dcur_bf", ptr(dcur), ncur, B, ncur)
+                self.gemm_bf(ncur, din, B, ptr(dcur_bf), ncur, 1, ptr(q["zi_bf"]), din, 0, ptr(G[wkey]), din)
+                self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
             else:
                 # first layer: W0 = [W0a (over z) | W0b (over inter)]
                 self.gemm(ncur, FD + C, B, ptr(dcur), ncur, 1, ptr(q["z"]), FD, 0, ptr(G[wkey]), din, None,
@@ -761,7 +794,11 @@ class Engine:
         W0 = P["qnn.mlp.0.weight"]
         dinter = W.get("dinter", (B, C))
         dz_mlp = W.get("dz_mlp", (B, FD))
-        if a.use_residual:     # [dz | dinter] = dcur W0: one GEMM, output split at column FD
+        bf_da = q.get("w0_bf") is not None and dcur_bf is not None and self.bf_ok(B, din, ncur, ncur, 0, din, 0)
+        if a.use_residual and bf_da:   # amp: [dz | dinter] = dcur W0 on bf16 images (W0 k-major: transposed reads)
+            self.gemm_bf(B, din, ncur, ptr(dcur_bf), ncur, 0, ptr(q["w0_bf"]), din, 0, ptr(dz_mlp), FD,
+                         seg=_lib.GemmSeg(C2=ptr(dinter), ldc2=C, nc=FD))
+        elif a.use_residual:     # [dz | dinter] = dcur W0: one GEMM, output split at column FD
             self.gemm(B, FD + C, ncur, ptr(dcur), ncur, 0, ptr(W0), din, 0, ptr(dz_mlp), FD,
                       seg=_lib.GemmSeg(C2=ptr(dinter), ldc2=C, nc=FD))
         else:
