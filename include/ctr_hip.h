@@ -174,6 +174,7 @@ int ctr_pos_bias_grad(const float* part, int nparts, int H, int n, float* drel, 
  * the recompute backward; drel_part (B*nparts, 2tk+1) positional-bias grad partials.
  * ------------------------------------------------------------------------------------------- */
 int ctr_attn_mask_words(int B, int K, int H);   /* uint32 words of the dropout keep-bit mask */
+void ctr_attn_set_generic(int on);   /* test hook: 1 = the unpacked forward even where the packed one applies */
 /* mask (nullable without dropout): the forward stores the keep bits of p~, row ((b*H+h)*K + i),
  * ceil(K/32) words per row; the backward reads them instead of re-evaluating the hash.             */
 int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,

@@ -178,8 +178,10 @@ def test_rowgrad_dedup_matches_numpy():
                                      # waves, exactly full waves, the K = 100 / 120 configs), dh = 16 tile
                                      (100, 8, 32, 0.1), (120, 8, 64, 0.15), (65, 2, 16, 0.0), (128, 16, 32, 0.2),
                                      (200, 4, 8, 0.1), (256, 8, 64, 0.1), (100, 4, 64, 0.1)])
-def test_attention_fwd_bwd_vs_torch(K, H, D, p):
+@pytest.mark.parametrize("generic", [0, 1])      # 0: the packed forward where it applies (K <= 64 even, dh 4/8)
+def test_attention_fwd_bwd_vs_torch(K, H, D, p, generic):
     L = _lib()
+    L.query("ctr_attn_set_generic", generic)
     from tossctr.rng import drop_args
     import sys, os
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -198,6 +200,7 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p):
     mask = torch.zeros(L.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
     L.call("ctr_attn_fwd", ptr(qkv), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mask), ptr(o), ptr(mrow),
            ptr(lrow), stream())
+    L.query("ctr_attn_set_generic", 0)
     # torch reference (MHA explicit path semantics)
     q, k, v = qkv.view(B, K, 3 * D).split(D, -1)
     q = q.reshape(B, K, H, dh).transpose(1, 2)

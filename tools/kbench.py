@@ -167,10 +167,13 @@ def main():
                            ptr(o), ptr(mrow), ptr(lrow), st)
         bwd = lambda: call("ctr_attn_bwd", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(rel), K, scale, 777, thr,
                            1.0 / 0.9, ptr(amask), ptr(mrow), ptr(lrow), ptr(dqkv), ptr(drp), st)
-        tf = timeit(fwd, args.iters)
-        tb = timeit(bwd, args.iters)
-        print(f"attn_fwd B={B} K={K} H={H} D={D}: {tf * 1e3:.1f} us")
-        print(f"attn_bwd B={B} K={K} H={H} D={D}: {tb * 1e3:.1f} us")
+        for generic in (0, 1):      # the packed kernels (where they apply), then the generic ones
+            _lib.query("ctr_attn_set_generic", generic)
+            tf = timeit(fwd, args.iters)
+            tb = timeit(bwd, args.iters)
+            print(f"attn_fwd{' generic' if generic else ''} B={B} K={K} H={H} D={D}: {tf * 1e3:.1f} us")
+            print(f"attn_bwd{' generic' if generic else ''} B={B} K={K} H={H} D={D}: {tb * 1e3:.1f} us")
+        _lib.query("ctr_attn_set_generic", 0)
 
 
 if __name__ == "__main__":

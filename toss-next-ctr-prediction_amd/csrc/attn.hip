@@ -17,6 +17,7 @@
 namespace ctr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct AttnArgs {
   const float* qkv;     // (B*K, 3D)
@@ -119,6 +120,120 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int c = 0; c < DH; ++c) a.o[((long)b * K + i) * D + h * DH + c] = acc[c] * inv;
   a.mrow[r] = m;
+  a.lrow[r] = l;
+}
+
+// Packed forward for K <= 64, K even, dh in {4, 8} (cfg2: K = 60, dh = 4).  Same thread mapping as
+// attn_fwd_kernel (thread = query row i of one head), but every per-element step runs on key PAIRS in
+// packed f32 (v_pk_fma / v_pk_add / v_pk_mul: two scores per instruction): K is stored pair-interleaved
+// ([j/2][c][2]) so one ds_read_b128 yields (k_j,c, k_j+1,c) pairs; the scores stay in registers between
+// the max and the exp pass (no second QK product); scores live in log2 units (q pre-scaled by
+// sqrt(1/dh) log2(e), the bias by log2(e)), so p = exp2(s - m) is one subtract and one v_exp; the pair's
+// dropout hash is the pair's own (K even: element 2k of a row is always even); 1/(1-p) and 1/l are applied
+// once per row.  mrow is stored in natural units (m ln 2) for the backward's recompute.
+template <int DH, bool BIAS, bool DROP>
+__global__ __launch_bounds__(256) void attn_fwd_pk_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  constexpr float L2E = 1.4426950408889634f;
+  const int K = a.K, D = a.D, G = a.G, KP = K >> 1;
+  const int b = blockIdx.x, hg = blockIdx.y;
+  const int nrel = 2 * a.tk + 1, nr2 = (nrel + 2) & ~1;
+  float* sk = sm;                       // [G][K/2][DH][2]
+  float* sv = sk + G * K * DH;          // [G][K][DH]
+  float* s0 = sv + G * K * DH;          // [nr2] rel * log2e
+  float* s1 = s0 + nr2;                 // [nr2] shifted by one: s1[e] = rel[e + 1] * log2e
+  const float* base = a.qkv + (long)b * K * 3 * D;
+  for (int e = threadIdx.x; e < G * K * DH; e += blockDim.x) {
+    const int g = e / (K * DH), r = e % (K * DH), j = r / DH, c = r % DH;
+    const int col = (hg * G + g) * DH + c;
+    sk[g * K * DH + (j >> 1) * 2 * DH + 2 * c + (j & 1)] = base[(long)j * 3 * D + D + col];
+    sv[e] = base[(long)j * 3 * D + 2 * D + col];
+  }
+  if (BIAS)
+    for (int e = threadIdx.x; e < nr2; e += blockDim.x) {
+      s0[e] = e < nrel ? a.relmean[e] * L2E : 0.f;
+      s1[e] = e + 1 < nrel ? a.relmean[e + 1] * L2E : 0.f;
+    }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= G * K) return;
+  const int g = t / K, i = t % K, h = hg * G + g;
+  const float qsc = a.scale * L2E;
+  f32x2 q2[DH];
+#pragma unroll
+  for (int c = 0; c < DH; ++c) {
+    const float v = base[(long)i * 3 * D + h * DH + c] * qsc;
+    q2[c] = f32x2{v, v};
+  }
+  const float* kg = sk + g * K * DH;
+  const float* vg = sv + g * K * DH;
+  const int bi = a.tk - i;                               // bias index of key 0
+  const float* rbp = (bi & 1) ? s1 + (bi - 1) : s0 + bi;  // pair jp: rbp[2 jp], rbp[2 jp + 1], 8-byte aligned
+  f32x2 sc[32];
+  f32x2 mx = {-INFINITY, -INFINITY};
+#pragma unroll
+  for (int jp = 0; jp < 32; ++jp) {
+    if (jp < KP) {
+      const f32x4* kp = (const f32x4*)(kg + jp * 2 * DH);
+      f32x2 acc = BIAS ? *(const f32x2*)(rbp + 2 * jp) : f32x2{0.f, 0.f};
+#pragma unroll
+      for (int c2 = 0; c2 < DH / 2; ++c2) {
+        const f32x4 kk = kp[c2];
+        acc = q2[2 * c2] * f32x2{kk[0], kk[1]} + acc;
+        acc = q2[2 * c2 + 1] * f32x2{kk[2], kk[3]} + acc;
+      }
+      sc[jp] = acc;
+      mx = f32x2{fmaxf(mx.x, acc.x), fmaxf(mx.y, acc.y)};
+    }
+  }
+  const float m = fmaxf(mx.x, mx.y);
+  f32x2 l2 = {0.f, 0.f};
+  f32x2 acc[DH / 2];
+#pragma unroll
+  for (int c2 = 0; c2 < DH / 2; ++c2) acc[c2] = f32x2{0.f, 0.f};
+  const long r = ((long)b * a.H + h) * K + i;
+  const uint32_t pair0 = (uint32_t)(r * K) >> 1;
+  uint32_t w0 = 0, w1 = 0;
+  const uint32_t thr = a.drop.thresh;
+#pragma unroll
+  for (int jp = 0; jp < 32; ++jp) {
+    if (jp < KP) {
+      const f32x2 e = {__builtin_amdgcn_exp2f(sc[jp].x - m), __builtin_amdgcn_exp2f(sc[jp].y - m)};
+      l2 += e;
+      f32x2 w = e;
+      if (DROP) {
+        const uint32_t hb = drop_pair_bits(a.drop, pair0 + jp);
+        const bool k0 = (hb & 0xFFFFu) >= thr, k1 = (hb >> 16) >= thr;
+        w = f32x2{k0 ? e.x : 0.f, k1 ? e.y : 0.f};
+        const uint32_t bits = (k0 ? 1u : 0u) | (k1 ? 2u : 0u);
+        if (jp < 16) w0 |= bits << (2 * jp);
+        else w1 |= bits << (2 * jp - 32);
+      }
+      const f32x4* v0 = (const f32x4*)(vg + 2 * jp * DH);
+      const f32x4* v1 = (const f32x4*)(vg + (2 * jp + 1) * DH);
+#pragma unroll
+      for (int c4 = 0; c4 < DH / 4; ++c4) {
+        const f32x4 a0 = v0[c4], a1 = v1[c4];
+        acc[2 * c4] = f32x2{w.x, w.x} * f32x2{a0[0], a0[1]} + acc[2 * c4];
+        acc[2 * c4 + 1] = f32x2{w.x, w.x} * f32x2{a0[2], a0[3]} + acc[2 * c4 + 1];
+        acc[2 * c4] = f32x2{w.y, w.y} * f32x2{a1[0], a1[1]} + acc[2 * c4];
+        acc[2 * c4 + 1] = f32x2{w.y, w.y} * f32x2{a1[2], a1[3]} + acc[2 * c4 + 1];
+      }
+    }
+  }
+  const float l = l2.x + l2.y;
+  const float inv = (DROP ? a.drop.scale : 1.0f) / l;
+  float* op = a.o + ((long)b * K + i) * D + h * DH;
+#pragma unroll
+  for (int c4 = 0; c4 < DH / 4; ++c4)
+    *(f32x4*)(op + 4 * c4) = f32x4{acc[2 * c4].x * inv, acc[2 * c4].y * inv, acc[2 * c4 + 1].x * inv,
+                                   acc[2 * c4 + 1].y * inv};
+  if (DROP) {
+    uint32_t* mb = a.mask + r * a.KW;
+    mb[0] = w0;
+    if (K > 32) mb[1] = w1;
+  }
+  a.mrow[r] = m * 0.69314718055994531f;
   a.lrow[r] = l;
 }
 
@@ -704,6 +819,24 @@ static void launch_fwd3(const AttnArgs& a, size_t sm, hipStream_t s) {
   attn_fwd_kernel<DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), (a.G * a.K + 63) / 64 * 64, sm, s>>>(a);
 }
 
+// the packed forward: K <= 64 and even, dh in {4, 8}, the output rows 16-byte aligned
+static bool fwd_use_pk(int K, int dh, int D) { return K <= 64 && (K & 1) == 0 && (dh == 4 || dh == 8) && D % 4 == 0; }
+
+template <int DH, bool BIAS, bool DROP>
+static void launch_fwd_pk3(const AttnArgs& a, hipStream_t s) {
+  const size_t sm = ((size_t)2 * a.G * a.K * DH + 2 * (size_t)((2 * a.tk + 3) & ~1)) * sizeof(float);
+  attn_fwd_pk_kernel<DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), (a.G * a.K + 63) / 64 * 64, sm, s>>>(a);
+}
+
+template <int DH>
+static void launch_fwd_pk(const AttnArgs& a, hipStream_t s) {
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  if (bias && drop) launch_fwd_pk3<DH, true, true>(a, s);
+  else if (bias) launch_fwd_pk3<DH, true, false>(a, s);
+  else if (drop) launch_fwd_pk3<DH, false, true>(a, s);
+  else launch_fwd_pk3<DH, false, false>(a, s);
+}
+
 template <int DH>
 static void launch_fwd(const AttnArgs& a, size_t sm, hipStream_t s) {
   const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
@@ -744,6 +877,10 @@ static void launch_bwd(const AttnArgs& a, size_t sm, hipStream_t s) {
 
 using namespace ctr;
 
+// test hook: 1 = always the generic (unpacked) forward, so tests can compare the two forms
+static int ctr_attn_force_generic = 0;
+extern "C" void ctr_attn_set_generic(int on) { ctr_attn_force_generic = on; }
+
 extern "C" int ctr_attn_mask_words(int B, int K, int H) { return B * H * K * ((K + 31) / 32); }
 
 extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
@@ -763,6 +900,11 @@ extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const 
   a.o = o; a.mrow = mrow; a.lrow = lrow;
   const size_t sm = ((size_t)2 * G * K * dh + 2 * tk + 1) * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
+  if (fwd_use_pk(K, dh, D) && !ctr_attn_force_generic) {
+    if (dh == 4) launch_fwd_pk<4>(a, s);
+    else launch_fwd_pk<8>(a, s);
+    return check_launch("attn_fwd");
+  }
   switch (dh) {
     case 2: launch_fwd<2>(a, sm, s); break;
     case 4: launch_fwd<4>(a, sm, s); break;
