@@ -147,8 +147,12 @@ class Engine:
             raise NotImplementedError("cat_cols_order must match the cat_cardinals order")
         self._decay = {}
         self._ws = {}
-        self._splitk = None
+        self._splitk = {}
         self._gen = 0
+        # backward side stream: weight / bias grads whose inputs are final run beside the input-grad chain
+        # (one stream per engine; joined before the optimizer and before a data-parallel bucket hand-off)
+        self._side = None
+        self.side_stream = True
         self.stream = None
         self.last = None
         self.grad_ready = None   # data parallel: called once the head's dense grads are final (bucket 1)
@@ -211,9 +215,50 @@ class Engine:
         return self._decay[L]
 
     def splitk_ws(self, nfloats):
-        if self._splitk is None or self._splitk.numel() < nfloats:
-            self._splitk = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=self.device)
-        return self._splitk
+        """Split-K / colsum scratch, one buffer per stream (the side stream's kernels run concurrently)."""
+        st = self.s()
+        buf = self._splitk.get(st)
+        if buf is None or buf.numel() < nfloats:
+            buf = torch.empty(max(nfloats, 1 << 20), dtype=torch.float32, device=self.device)
+            self._splitk[st] = buf
+        return buf
+
+    class _Side:
+        def __init__(self, eng):
+            self.eng = eng
+
+        def __enter__(self):
+            e = self.eng
+            if not e.side_stream:
+                return self
+            if e._side is None:
+                e._side = torch.cuda.Stream(device=e.device)
+            self.main = torch.cuda.current_stream(e.device)
+            ev = torch.cuda.Event()
+            ev.record(self.main)
+            e._side.wait_event(ev)
+            self.ctx = torch.cuda.stream(e._side)
+            self.ctx.__enter__()
+            e._side_used = True
+            return self
+
+        def __exit__(self, *exc):
+            if self.eng.side_stream:
+                self.ctx.__exit__(*exc)
+            return False
+
+    def side(self):
+        """Context: the enclosed launches go to the side stream, after everything issued so far on the
+        current stream.  Their inputs must not be overwritten by later main-stream work before join()."""
+        return Engine._Side(self)
+
+    def join(self):
+        """Current stream waits for the side stream's work."""
+        if self._side is not None and getattr(self, "_side_used", False):
+            ev = torch.cuda.Event()
+            ev.record(self._side)
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            self._side_used = False
 
     @staticmethod
     def _tiles(M, N):
@@ -273,7 +318,7 @@ class Engine:
         call("ctr_rowgemm", M, K, N, A, K, W, tb, C, N, bias, add, N if add else 0, resid, N if resid else 0, norm_w,
              norm_h, norm_r, 1e-6, self.s())
 
-    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey):
+    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey, tag=""):
         """dW = dY^T X and db = colsum(dY) of one nn.Linear in one pass (rowgemm.hip): per-wave partial
         slab rows laid out like the grad arena from the weight on, reduced by one fixed-order colsum."""
         o0 = self.arena.offsets[wkey]
@@ -281,7 +326,7 @@ class Engine:
         n_sl = o_db + n_out
         ld = (n_sl + 3) // 4 * 4
         rows = _lib.query("ctr_rowgemm_wgrad_rows", M)
-        slab = W.get_zeroed(f"wg_slab_{n_out}x{n_in}", (rows, ld))     # padding columns stay zero
+        slab = W.get_zeroed(f"wg_slab_{n_out}x{n_in}_{tag}", (rows, ld))     # padding columns stay zero
         call("ctr_rowgemm_wgrad", dY, n_out, X, n_in, M, n_out, n_in, ptr(slab), ld, o_db, self.s())
         self.colsum(ptr(slab), ld, rows, n_sl, ptr(self.arena.grad, o0))
 
@@ -583,6 +628,7 @@ class Engine:
         if overlap and self.grad_ready is not None:
             # the head's grads (the last dense params of the arena: qnn.* / fc.*) are final: their
             # all-reduce runs beside the rest of the backward
+            self.join()
             self.grad_ready()
         # ---------------- pool + aux head
         dx = W.get("dx_a", (B, K, D))
@@ -646,6 +692,7 @@ class Engine:
              ptr(self.cat_proj_off), ptr(self.cat_dims_t), tv["cat_ld"], D, ptr(dcat), tv["row_base"], ptr(cat_c),
              ptr(cat_k), ptr(self.arena.grad), ptr(self.cat_proj_off), ptr(cws), st)
         tg["cat"] = self._rowgrad(W, "cat", cat_k, cat_c, n_cat, 64, 64, tv["cat_bits"])
+        self.join()
         return tg
 
     def _rowgrad(self, W, name, keys, contrib, n, width, ld, key_bits):
@@ -692,13 +739,14 @@ class Engine:
             n_sl = o[5] + D
             ld_sl = (n_sl + 3) // 4 * 4
             nb = _lib.query("ctr_ffn_slab_rows", M, D, self.ffn_flags)
-            slab = W.get_zeroed("ffn_slab", (nb, ld_sl))
-            dh1 = W.get("dh1", (M, D))
+            slab = W.get_zeroed(f"ffn_slab{li}", (nb, ld_sl))
+            dh1 = W.get(f"dh1_{li}", (M, D))
             call("ctr_ffn_bwd_norms", ptr(Ls["x1"]), ptr(dx2), ptr(Ls["h2"]), ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]),
                  ptr(Ls["h1"]), ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
                  ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dh1),
                  ptr(slab), ld_sl, *o, ptr(Ls["fwbf"]), self.ffn_flags, st)
-            self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
+            with self.side():
+                self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
         else:
             # x2 = norm2(x1 + ffn(x1))
             dh2 = W.get("dh2", (M, D))
@@ -727,27 +775,32 @@ class Engine:
         # out_proj
         do = W.get("do", (M, D))
         if self.rowgemm:
-            self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight", pre + "mha.out_proj.bias")
+            with self.side():
+                self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
+                                pre + "mha.out_proj.bias", tag=li)
             self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
         else:
             self.wgrad(ptr(dh1), D, ptr(Ls["o"]), D, M, D, D, ptr(G[pre + "mha.out_proj.weight"]),
                        bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
             self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
         # attention core
-        dqkv = W.get("dqkv", (M, 3 * D))
+        dqkv = W.get(f"dqkv{li}", (M, 3 * D))
         nparts = _lib.query("ctr_attn_bwd_nparts", a.H, K, D) * B
         nrel = 2 * a.top_k + 1
-        drp = W.get("drel_part", (nparts, nrel))
+        drp = W.get(f"drel_part{li}", (nparts, nrel))
         da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
         scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
         call("ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale,
              *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
-        if a.add_pos:
-            call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), st)
-        # in_proj
         x_in = sv["xs"][li]
+        with self.side():
+            if a.add_pos:
+                call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), self.s())
+            if self.rowgemm:
+                self.wgrad_rows(W, ptr(dqkv), ptr(x_in), M, 3 * D, D, pre + "mha.in_proj_weight",
+                                pre + "mha.in_proj_bias", tag=li)
+        # in_proj
         if self.rowgemm:
-            self.wgrad_rows(W, ptr(dqkv), ptr(x_in), M, 3 * D, D, pre + "mha.in_proj_weight", pre + "mha.in_proj_bias")
             self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
                               add=ptr(dh1))
         else:
@@ -773,8 +826,9 @@ class Engine:
             wkey, bkey = f"qnn.mlp.{3 * j}.weight", f"qnn.mlp.{3 * j}.bias"
             if j > 0:
                 kin = a.mlp_hidden[j - 1]
-                self.wgrad(ptr(dcur), ncur, ptr(q["hs"][j - 1]), kin, B, ncur, kin, ptr(G[wkey]),
-                           bias_grad=ptr(G[bkey]))
+                with self.side():
+                    self.wgrad(ptr(dcur), ncur, ptr(q["hs"][j - 1]), kin, B, ncur, kin, ptr(G[wkey]),
+                               bias_grad=ptr(G[bkey]))
                 dprev = W.get(f"dmlp_a{j - 1}", (B, kin))
                 dm = drop_args(seed, SITE_MLP0 + j - 1, a.qnn_p, training)
                 self.gemm(B, kin, ncur, ptr(dcur), ncur, 0, ptr(P[wkey]), kin, 0, ptr(dprev), kin,
@@ -784,13 +838,15 @@ class Engine:
             elif q.get("zi_bf") is not None and self.bf_ok(ncur, din, B, ncur, 1, din, 0):
                 # amp: dW0 = dcur^T [z | inter] on the forward's bf16 image (both operands k-major)
                 dcur_bf = self.bf_image(W, "dcur_bf", ptr(dcur), ncur, B, ncur)
-                self.gemm_bf(ncur, din, B, ptr(dcur_bf), ncur, 1, ptr(q["zi_bf"]), din, 0, ptr(G[wkey]), din)
-                self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
+                with self.side():
+                    self.gemm_bf(ncur, din, B, ptr(dcur_bf), ncur, 1, ptr(q["zi_bf"]), din, 0, ptr(G[wkey]), din)
+                    self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
             else:
                 # first layer: W0 = [W0a (over z) | W0b (over inter)]
-                self.gemm(ncur, FD + C, B, ptr(dcur), ncur, 1, ptr(q["z"]), FD, 0, ptr(G[wkey]), din, None,
-                          self.wgrad_splits(ncur, FD + C, B), seg=_lib.GemmSeg(B2=ptr(q["inter"]), ldb2=C, nb=FD))
-                self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
+                with self.side():
+                    self.gemm(ncur, FD + C, B, ptr(dcur), ncur, 1, ptr(q["z"]), FD, 0, ptr(G[wkey]), din, None,
+                              self.wgrad_splits(ncur, FD + C, B), seg=_lib.GemmSeg(B2=ptr(q["inter"]), ldb2=C, nb=FD))
+                    self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
         W0 = P["qnn.mlp.0.weight"]
         dinter = W.get("dinter", (B, C))
         dz_mlp = W.get("dz_mlp", (B, FD))
@@ -816,28 +872,31 @@ class Engine:
         dquad = W.get("qdquad", (B, QR))
         self.gemm(B, QR, C, ptr(dinter_pre), C, 0, ptr(q["vfull"]), C, 1, ptr(dquad), QR)
         dvfull = W.get("qdvfull", (QR, C))
-        self.gemm(QR, C, B, ptr(q["quad"]), QR, 1, ptr(dinter_pre), C, 0, ptr(dvfull), C, None,
-                  self.wgrad_splits(QR, C, B))
-        call("ctr_qnn_vfull", ptr(dvfull), a.qh, a.qr, a.qP, ptr(G["qnn.V"]), 1, st)
+        with self.side():
+            self.gemm(QR, C, B, ptr(q["quad"]), QR, 1, ptr(dinter_pre), C, 0, ptr(dvfull), C, None,
+                      self.wgrad_splits(QR, C, B))
+            call("ctr_qnn_vfull", ptr(dvfull), a.qh, a.qr, a.qP, ptr(G["qnn.V"]), 1, self.s())
         dz = W.get("dz", (B, FD))
         DS = W.get("qDS", (B, QR))
         call("ctr_qnn_gram_bwd", ptr(q["z"]), B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]), ptr(dquad),
              ptr(dz_mlp) if a.use_residual else None, ptr(dz), ptr(DS), st)
         # dUcat = 2 (zsum^T DS - sum_b G_b Ucat diag(dquad_b))
         T1 = W.get("qT1", (D, QR))
-        self.gemm(D, QR, B, ptr(q["zsum"]), D, 1, ptr(DS), QR, 0, ptr(T1), QR, None, self.wgrad_splits(D, QR, B))
         T = W.get("qT", (D * D, QR))
-        self.gemm(D * D, QR, B, ptr(q["gram"]), D * D, 1, ptr(dquad), QR, 0, ptr(T), QR, None,
-                  self.wgrad_splits(D * D, QR, B))
         ducat = W.get("ducat", (D, QR))
-        call("ctr_qnn_du_combine", ptr(T1), ptr(T), ptr(q["ucat"]), D, QR, ptr(ducat), st)
-        call("ctr_qnn_ucat", ptr(ducat), a.qh, D, a.qr, ptr(G["qnn.U"]), 1, st)
+        with self.side():
+            self.gemm(D, QR, B, ptr(q["zsum"]), D, 1, ptr(DS), QR, 0, ptr(T1), QR, None, self.wgrad_splits(D, QR, B))
+            self.gemm(D * D, QR, B, ptr(q["gram"]), D * D, 1, ptr(dquad), QR, 0, ptr(T), QR, None,
+                      self.wgrad_splits(D * D, QR, B))
+            call("ctr_qnn_du_combine", ptr(T1), ptr(T), ptr(q["ucat"]), D, QR, ptr(ducat), self.s())
+            call("ctr_qnn_ucat", ptr(ducat), a.qh, D, a.qr, ptr(G["qnn.U"]), 1, self.s())
         # pre-norm
         npart = _lib.query("ctr_rmsnorm_bwd_nparts", B, FD)
         dwp = W.get("dwq_part", (npart, FD))
         call("ctr_rmsnorm_bwd", ptr(dz), FD, ptr(sv["xF"]), FD, ptr(q["rq"]), ptr(P["qnn.pre_norm.w"]), B, FD,
              ptr(dxF), FD, None, 0, ptr(dwp), st)
-        self.colsum(ptr(dwp), FD, npart, FD, ptr(G["qnn.pre_norm.w"]))
+        with self.side():
+            self.colsum(ptr(dwp), FD, npart, FD, ptr(G["qnn.pre_norm.w"]))
 
     def _fc_backward(self, sv, dlogits):
         a, P, G, st = self.a, self.P, self.G, self.s()
