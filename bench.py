@@ -190,8 +190,8 @@ def pmc_traffic(name):
     corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE counts half of wide streaming reads:
     x2).  None when the summaries are absent."""
     import csv
-    bwd = ("ffn_bwd_cols_kernel", "ffn_bwd_kernel")       # the entry point's kernels, preferred first
-    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_kernel",)}.get(name)
+    bwd = ("ffn_bwd_bf_kernel", "ffn_bwd_cols_kernel", "ffn_bwd_kernel")   # the entry point's kernels, preferred first
+    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bf_kernel", "ffn_fwd_kernel")}.get(name)
     if kerns is None:
         return None
     base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS

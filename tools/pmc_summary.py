@@ -8,6 +8,8 @@ timestamps are not used).  Derived columns:
     streaming reads, MI355X_MICROARCH.md "HBM")
   * MFMA TF/s  = (SQ_INSTS_VALU_MFMA_MOPS_F32 + _BF16 when collected) x 512 FLOP / duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
     (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
+  * VALU issue = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction on a 32-wide SIMD) / (duration x
+    2.4 GHz x 1024 SIMDs): the fraction of the chip's VALU issue slots the kernel's vector instructions fill
   * LDS conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS-array cycle)
   * wave-time split = SQ_WAIT_ANY, SQ_WAIT_INST_ANY (of which SQ_WAIT_INST_LDS) over SQ_WAVE_CYCLES
 
@@ -79,8 +81,8 @@ def main():
     print("Counters: averages per dispatch over the timed steps of each pass (tools/pmc_summary.py).  "
           "Duration: the non-PMC kernel trace.\n")
     print("| kernel | avg us | HBM MB (2F+W) | write MB | MFMA TF/s | MFMA busy | LDS confl | VALU insts/wave | "
-          "wait-mem | wait-issue (LDS) |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
+          "VALU issue | wait-mem | wait-issue (LDS) |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for k in keys[:args.top]:
         c = data[k]
         us = dur.get(k[:110])
@@ -92,13 +94,15 @@ def main():
                 if c.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in c else None)
         lds = (c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"] if c.get("SQ_LDS_IDX_ACTIVE") else None)
         valu = c["SQ_INSTS_VALU"] / c["SQ_WAVES"] if c.get("SQ_WAVES") and "SQ_INSTS_VALU" in c else None
+        # VALU issue fraction: wave64 VALU instructions x 2 cycles over (duration x 2.4 GHz x 1024 SIMDs)
+        vis = c["SQ_INSTS_VALU"] * 2 / (us * 1e-6 * 2.4e9 * 1024) if us and "SQ_INSTS_VALU" in c else None
         wc = c.get("SQ_WAVE_CYCLES")
         wmem = c["SQ_WAIT_ANY"] / wc if wc and "SQ_WAIT_ANY" in c else None
         wiss = (f"{c['SQ_WAIT_INST_ANY'] / wc:.2f} ({c['SQ_WAIT_INST_LDS'] / wc:.2f})"
                 if wc and "SQ_WAIT_INST_ANY" in c and "SQ_WAIT_INST_LDS" in c else "")
         f = lambda v, fmt: "" if v is None else format(v, fmt)     # noqa: E731
         print(f"| `{short(k)}` | {f(us, '.1f')} | {f(hb, '.1f')} | {f(wr, '.1f')} | {f(tf, '.1f')} | {f(busy, '.2f')} | "
-              f"{f(lds, '.3f')} | {f(valu, '.0f')} | {f(wmem, '.2f')} | {wiss} |")
+              f"{f(lds, '.3f')} | {f(valu, '.0f')} | {f(vis, '.2f')} | {f(wmem, '.2f')} | {wiss} |")
 
 
 if __name__ == "__main__":

@@ -304,14 +304,17 @@ __global__ __launch_bounds__(256) void matvec_cols_kernel(const float* __restric
 
 // out[b,c] = drop(x[b,c] * gate[c])   (gate nullable: no SE)
 __global__ void scale_drop_kernel(const float* __restrict__ x, int B, int C, const float* __restrict__ gate,
-                                  Drop drop, float* __restrict__ out, long out_ld) {
+                                  Drop drop, float* __restrict__ out, long out_ld, __bf16* __restrict__ obf = nullptr,
+                                  long obf_ld = 0) {
   const long n = (long)B * C;
   for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
     const int c = (int)(q % C);
     const long b = q / C;
     float v = x[q];
     if (gate) v = v * gate[c];
-    out[b * out_ld + c] = drop_apply(drop, (uint32_t)q, v);
+    const float o = drop_apply(drop, (uint32_t)q, v);
+    out[b * out_ld + c] = o;
+    if (obf) obf[b * obf_ld + c] = (__bf16)o;     // amp: the GEMM's bf16 image
   }
 }
 
@@ -466,6 +469,16 @@ extern "C" int ctr_scale_drop(const float* x, int B, int C, const float* gate, u
   scale_drop_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, B, C, gate, Drop{drop_key, drop_thresh, drop_scale},
                                                              out, out_ld);
   return check_launch("scale_drop");
+}
+
+extern "C" int ctr_scale_drop_bf(const float* x, int B, int C, const float* gate, uint32_t drop_key, uint32_t drop_thresh,
+                                 float drop_scale, float* out, long out_ld, void* obf, long obf_ld, void* stream) {
+  if (B == 0) return 0;
+  long n = (long)B * C;
+  int blocks = (int)std::min<long>((n + 255) / 256, 16384);
+  scale_drop_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(x, B, C, gate, Drop{drop_key, drop_thresh, drop_scale},
+                                                             out, out_ld, (__bf16*)obf, obf_ld);
+  return check_launch("scale_drop_bf");
 }
 
 constexpr int SE_RPB = 32;     // rows per se_bwd_partial workgroup (B = 4096: 5 x 128 workgroups)

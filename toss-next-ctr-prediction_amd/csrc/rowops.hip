@@ -30,8 +30,10 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big(const float* __restrict__
 template <int NQ>
 __global__ __launch_bounds__(256) void rmsnorm_fwd_big_vec(const float* __restrict__ x, long ldx, int N,
                                                            const float* __restrict__ w, float eps,
-                                                           float* __restrict__ y, long ldy, float* __restrict__ r) {
+                                                           float* __restrict__ y, long ldy, float* __restrict__ r,
+                                                           __bf16* __restrict__ ybf = nullptr, long ldybf = 0) {
   typedef float f4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 b4 __attribute__((ext_vector_type(4)));
   __shared__ float red[4];
   const long row = blockIdx.x;
   const f4* xr = (const f4*)(x + row * ldx);
@@ -58,7 +60,11 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big_vec(const float* __restri
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
     const int j = threadIdx.x + 256 * k;
-    if (j < n4) yr[j] = w4[j] * v[k] * rr;
+    if (j < n4) {
+      const f4 o = w4[j] * v[k] * rr;
+      yr[j] = o;
+      if (ybf) *(b4*)(ybf + row * ldybf + 4 * j) = __builtin_convertvector(o, b4);   // amp: the GEMM's bf16 image
+    }
   }
 }
 
@@ -386,6 +392,19 @@ extern "C" int ctr_rmsnorm_fwd(const float* x, long ldx, int M, int N, const flo
   else
     rmsnorm_fwd_big<<<M, 256, 0, (hipStream_t)stream>>>(x, ldx, N, w, eps, y, ldy, r);
   return check_launch("rmsnorm_fwd");
+}
+
+extern "C" int ctr_rmsnorm_fwd_bf(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy,
+                                  float* r, void* ybf, long ldybf, void* stream) {
+  if (M == 0) return 0;
+  const bool vec = (N % 4) == 0 && (ldx % 4) == 0 && (ldy % 4) == 0 && (ldybf % 4) == 0 &&
+                   ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)w)) & 15) == 0 && (((uintptr_t)ybf) & 7) == 0;
+  CTR_REQUIRE(vec && N <= 1024 * 16, "ctr_rmsnorm_fwd_bf: needs N % 4 == 0, N <= 16384 and aligned rows");
+  if (N <= 1024 * 8)
+    rmsnorm_fwd_big_vec<8><<<M, 256, 0, (hipStream_t)stream>>>(x, ldx, N, w, eps, y, ldy, r, (__bf16*)ybf, ldybf);
+  else
+    rmsnorm_fwd_big_vec<16><<<M, 256, 0, (hipStream_t)stream>>>(x, ldx, N, w, eps, y, ldy, r, (__bf16*)ybf, ldybf);
+  return check_launch("rmsnorm_fwd_bf");
 }
 
 // big rows: ~512 workgroups (2 per CU), at least 2 rows each
