@@ -227,6 +227,9 @@ int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h2, const fl
 /* RMSNorm.forward for long rows (QNN pre_norm, src/models/qnn_alpha.py:110-113) */
 int ctr_rmsnorm_fwd(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy, float* r,
                     void* stream);
+/* ... also writing y's bf16 (RNE) image, row stride ldybf (amp: the QNN MLP's [z | inter] GEMM operand) */
+int ctr_rmsnorm_fwd_bf(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy, float* r,
+                       void* ybf, long ldybf, void* stream);
 int ctr_rmsnorm_bwd_nparts(int M, int N);
 /* RMSNorm backward: dh = w*dy*r - h*r^3/N*sum(w*dy*h) (+ add); dw partials (nparts, N) */
 int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long ldh, const float* r, const float* w, int M, int N,
@@ -262,6 +265,8 @@ int ctr_se_fwd_gate(const float* mean, int C, int Cr, const float* W1, const flo
                     const float* b2, float* g1, float* gate, void* stream);
 int ctr_scale_drop(const float* x, int B, int C, const float* gate, uint32_t drop_key, uint32_t drop_thresh,
                    float drop_scale, float* out, long out_ld, void* stream);
+int ctr_scale_drop_bf(const float* x, int B, int C, const float* gate, uint32_t drop_key, uint32_t drop_thresh,
+                      float drop_scale, float* out, long out_ld, void* obf, long obf_ld, void* stream);
 size_t ctr_se_bwd_ws(int B, int C);
 int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, int Cr, const float* gate,
                const float* g1, const float* mean, const float* W1, const float* W2, uint32_t drop_key,

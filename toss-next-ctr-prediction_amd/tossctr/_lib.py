@@ -83,6 +83,7 @@ SIGS = {
     "ctr_ffn_bwd_norms": (i, [p, p, p, p, p, p, p, p, i, i, i, p, p, p, u, u, f, p, p, p, l,
                               i, i, i, i, i, i, p, i, p]),
     "ctr_rmsnorm_fwd": (i, [p, l, i, i, p, f, p, l, p, p]),
+    "ctr_rmsnorm_fwd_bf": (i, [p, l, i, i, p, f, p, l, p, p, l, p]),
     "ctr_rmsnorm_bwd_nparts": (i, [i, i]),
     "ctr_rmsnorm_bwd": (i, [p, l, p, l, p, p, i, i, p, l, p, l, p, p]),
     "ctr_colsum_ws_size": (z, [i, i]),
@@ -95,6 +96,7 @@ SIGS = {
     "ctr_qnn_du_combine": (i, [p, p, p, i, i, p, p]),
     "ctr_se_fwd_gate": (i, [p, i, i, p, p, p, p, p, p, p]),
     "ctr_scale_drop": (i, [p, i, i, p, u, u, f, p, l, p]),
+    "ctr_scale_drop_bf": (i, [p, i, i, p, u, u, f, p, l, p, l, p]),
     "ctr_se_bwd_ws": (z, [i, i]),
     "ctr_se_bwd": (i, [p, l, p, i, i, i, p, p, p, p, p, u, u, f, p, p, p, p, p, p, p]),
     "ctr_rowgrad_ws_size": (z, [i]),

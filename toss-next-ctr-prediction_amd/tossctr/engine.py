@@ -505,7 +505,16 @@ class Engine:
         FD, C, QR = F * D, a.C, a.qh * a.qr
         z = W.get("z", (B, FD))
         rq = W.get("rq", (B,))
-        call("ctr_rmsnorm_fwd", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq), st)
+        H0 = a.mlp_hidden[0] if a.mlp_hidden else 1
+        din = FD + C
+        # amp: the MLP's first GEMM runs on a bf16 image of [z | inter], written by z's and inter's producers
+        zi_bf = W.get("zi_bf", (B, din), torch.bfloat16) if (self.bf_ok(B, H0, din, din, 0, din, 1) and
+                                                              FD % 8 == 0 and FD % 4 == 0) else None
+        if zi_bf is not None:
+            call("ctr_rmsnorm_fwd_bf", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq),
+                 ptr(zi_bf), din, st)
+        else:
+            call("ctr_rmsnorm_fwd", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq), st)
         ucat = W.get("ucat", (D, QR))
         call("ctr_qnn_ucat", ptr(P["qnn.U"]), a.qh, D, a.qr, ptr(ucat), 0, st)
         # pair interaction through per-sample Gram matrices: A = z @ Ucat is never formed (qnn.hip)
@@ -529,12 +538,13 @@ class Engine:
                  ptr(P["qnn.se.fc.2.weight"]), ptr(P["qnn.se.fc.2.bias"]), ptr(g1), ptr(gate), st)
         inter = W.get("inter", (B, C))
         dq_ = drop_args(seed, SITE_QNN, a.qnn_p, training)
-        call("ctr_scale_drop", ptr(inter_pre), B, C, ptr(gate), *dq_, ptr(inter), C, st)
+        if zi_bf is not None:
+            call("ctr_scale_drop_bf", ptr(inter_pre), B, C, ptr(gate), *dq_, ptr(inter), C, ptr(zi_bf, FD), din, st)
+        else:
+            call("ctr_scale_drop", ptr(inter_pre), B, C, ptr(gate), *dq_, ptr(inter), C, st)
         # MLP on cat[z, inter] without materialising the concat: W0 = [W0a | W0b]
         hs, acts = [], []
-        din = FD + C
         W0 = P["qnn.mlp.0.weight"]
-        H0 = a.mlp_hidden[0] if a.mlp_hidden else 1
         nh = len(a.mlp_hidden)
         for j in range(nh + 1):
             last = j == nh
@@ -545,11 +555,9 @@ class Engine:
             dm = (0, 0, 1.0) if last else drop_args(seed, SITE_MLP0 + j, a.qnn_p, training)
             epi = GemmEpi(bias=ptr(P[bkey]), act=0 if last else 1, pre=ptr(pre), drop_key=dm[0], drop_thresh=dm[1],
                           drop_scale=dm[2])
-            if j == 0 and self.bf_ok(B, n_out, din, din, 0, din, 1) and FD % 8 == 0:
-                # amp: bf16 images of [z | inter] (one (B, FD + C) buffer, also the weight grad's operand)
+            if j == 0 and zi_bf is not None:
+                # amp: the bf16 image of [z | inter] (one (B, FD + C) buffer, also the weight grad's operand)
                 # and of W0; the bf16-operand GEMM (glds-staged MFMA tiles)
-                zi_bf = self.bf_image(W, "zi_bf", ptr(z), FD, B, FD, ld_out=din)
-                self.bf_image(W, None, ptr(inter), C, B, C, out=zi_bf, off=FD, ld_out=din)
                 w0_bf = self.bf_image(W, "w0_bf", ptr(W0), din, n_out, din)
                 self.gemm_bf(B, n_out, din, ptr(zi_bf), din, 0, ptr(w0_bf), din, 1, ptr(out), n_out, epi)
             elif j == 0:
@@ -564,7 +572,7 @@ class Engine:
                 acts.append(pre)
         return dict(z=z, rq=rq, ucat=ucat, zsum=zsum, gram=gram, vfull=vfull, S=S, quad=quad, inter_pre=inter_pre,
                     mean=mean, g1=g1, gate=gate, inter=inter, hs=hs, acts=acts,
-                    zi_bf=W.t.get("zi_bf") if self.bf16 else None, w0_bf=W.t.get("w0_bf") if self.bf16 else None)
+                    zi_bf=zi_bf, w0_bf=W.t.get("w0_bf") if zi_bf is not None else None)
 
     def _fc_forward(self, W, fcin, ctx, cat_e, B, seed, training, logits):
         """QNN disabled: fc head on [u, mean(num_e), mean(mask_e), cat_embs] (wrapper.py:95-100,167-173)."""
