@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--p", type=float, default=0.1, help="dropout probability (0: no dropout)")
     ap.add_argument("--nobias", action="store_true", help="attn: no positional bias")
     ap.add_argument("--bf16", action="store_true", help="ffn: the amp bf16 kernels (CTR_FFN_BF16)")
+    ap.add_argument("--norms", action="store_true", help="ffn: the norm-fused backward (ctr_ffn_bwd_norms, as the step)")
     ap.add_argument("--shapes", default="", help="gemm: comma-separated indices of the shape list")
     args = ap.parse_args()
     torch.manual_seed(0)
@@ -73,6 +74,15 @@ def main():
                            thr, 1.0 / 0.9, ptr(mask), ptr(y), ptr(h), ptr(r), ptr(wbf), fl, st)
         bwd = lambda: call("ctr_ffn_bwd", ptr(x), ptr(dh), M, D, FF, ptr(W1), ptr(b1), ptr(W2), 12345, thr, 1.0 / 0.9,
                            ptr(mask), ptr(dx), ptr(slab), ld, o_b1, o_w2, ptr(wbf), fl, st)
+        if args.norms:
+            h1, r1 = torch.randn(M, D, device="cuda"), torch.rand(M, device="cuda") + 0.5
+            h2, r2 = torch.randn(M, D, device="cuda"), torch.rand(M, device="cuda") + 0.5
+            o = [0, D, D + FF * D, D + FF * D + FF, D + 2 * FF * D + FF, 2 * D + 2 * FF * D + FF]
+            ldn = (o[-1] + D + 3) // 4 * 4
+            slab = torch.zeros(nb, ldn, device="cuda")
+            bwd = lambda: call("ctr_ffn_bwd_norms", ptr(x), ptr(dh), ptr(h2), ptr(r2), ptr(nw), ptr(h1), ptr(r1), ptr(nw),
+                               M, D, FF, ptr(W1), ptr(b1), ptr(W2), 12345, thr, 1.0 / 0.9, ptr(mask), ptr(dx), ptr(slab),
+                               ldn, *o, ptr(wbf), fl, st)
         tf = timeit(fwd, args.iters)
         tb = timeit(bwd, args.iters)
         print(f"ffn_fwd M={M} D={D} FF={FF}: {tf * 1e3:.1f} us  {4.0 * M * FF * D / tf / 1e9:.1f} TF/s")

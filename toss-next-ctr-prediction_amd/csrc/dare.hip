@@ -262,8 +262,14 @@ __global__ __launch_bounds__(256) void pos_bias_grad_kernel(const float* __restr
                                                             float* __restrict__ drel) {
   __shared__ float red[4];
   const int d = blockIdx.x;
-  float s = 0.f;
-  for (int p = threadIdx.x; p < nparts; p += 256) s += part[(long)p * n + d];
+  // eight independent partial sums per thread (eight strided loads in flight), combined in a fixed order
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int p = threadIdx.x;
+  for (; p + 7 * 256 < nparts; p += 8 * 256)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += part[(long)(p + u * 256) * n + d];
+  for (int u = 0; p < nparts; p += 256, ++u) acc[u] += part[(long)p * n + d];
+  float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   s = block_sum(s, red);
   if (threadIdx.x < H) drel[(long)d * H + threadIdx.x] = s / (float)H;
 }

@@ -1164,7 +1164,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     auto p_w2 = [&](int f0, int jj, int r) { return slab + a.o_w2 + (long)(16 * (js0 + jj) + c) * FF + f0 + 16 * ts + 4 * g + r; };
     auto p_b1 = [&](int f0, int r) { return slab + a.o_b1 + f0 + 16 * ts + 4 * g + r; };
 
-    auto chunk = [&](int f0, int bsel, const Wc& W) {
+    // the slab values a chunk's tiles add to (later tiles only); loaded one chunk ahead, so a chunk's wait
+    // for them does not also wait for the previous chunk's slab stores (loads and stores retire in order)
+    struct Os {
+      float o1[T::NT][4], o2[T::NT][4], ob[4];
+    };
+    auto load_o = [&](int f0, Os& O) {
+#pragma unroll
+      for (int jj = 0; jj < T::NT; ++jj)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          O.o1[jj][r] = acc ? *p_w1(f0, jj, r) : 0.f;
+          O.o2[jj][r] = acc ? *p_w2(f0, jj, r) : 0.f;
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) O.ob[r] = (acc && has_db && c == 0) ? *p_b1(f0, r) : 0.f;
+    };
+
+    auto chunk = [&](int f0, int bsel, const Wc& W, const Os& O, Os& On, int fn) {
       __bf16* FO = IM + bsel * 2 * T::IMG;
       __bf16* DA = FO + T::IMG;
       // B of dx: W1^T[16j + c][f0 + 8g .. +7] (first used after the element-wise work)
@@ -1172,17 +1189,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
       const uint32_t s3 = __builtin_amdgcn_readfirstlane((uint32_t)(2 * FF * D + f0) * 2);
 #pragma unroll
       for (int j = 0; j < T::NJ; ++j) w1d[j] = buf_ld_bf8(rw, vw1t + (uint32_t)(16 * j * FF) * 2, s3);
-      // later tiles: the slab values this chunk's tiles add to, loaded now (their latency under the chunk)
-      float o1[T::NT][4], o2[T::NT][4], ob[4];
-#pragma unroll
-      for (int jj = 0; jj < T::NT; ++jj)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          o1[jj][r] = acc ? *p_w1(f0, jj, r) : 0.f;
-          o2[jj][r] = acc ? *p_w2(f0, jj, r) : 0.f;
-        }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ob[r] = (acc && has_db && c == 0) ? *p_b1(f0, r) : 0.f;
+      if (fn >= 0) load_o(fn, On);
       // the chunk's D-contractions (their latency under the element-wise work)
       f32x4 pre[T::NI][2], dfo[T::NI][2];
 #pragma unroll
@@ -1252,32 +1259,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
       for (int jj = 0; jj < T::NT; ++jj)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          *p_w1(f0, jj, r) = o1[jj][r] + t1[jj][r];
-          *p_w2(f0, jj, r) = o2[jj][r] + t2[jj][r];
+          *p_w1(f0, jj, r) = O.o1[jj][r] + t1[jj][r];
+          *p_w2(f0, jj, r) = O.o2[jj][r] + t2[jj][r];
         }
       if (has_db && c == 0)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) *p_b1(f0, r) = ob[r] + tb[r];
+        for (int r = 0; r < 4; ++r) *p_b1(f0, r) = O.ob[r] + tb[r];
     };
 
+    Os oa, ob;
+    load_o(0, oa);
     if constexpr (D <= 32) {     // weights of the next chunk prefetched into the other register set
       Wc wa, wb;
       load_w(0, wa);
       int f0 = 0;
       for (; f0 + 64 <= FF; f0 += 64) {
         load_w(f0 + 32, wb);
-        chunk(f0, 0, wa);
+        chunk(f0, 0, wa, oa, ob, f0 + 32);
         __builtin_amdgcn_sched_barrier(0);
         load_w(min(f0 + 64, FF - 32), wa);
-        chunk(f0 + 32, 1, wb);
+        chunk(f0 + 32, 1, wb, ob, oa, f0 + 64 < FF ? f0 + 64 : -1);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (f0 < FF) chunk(f0, 0, wa);
+      if (f0 < FF) chunk(f0, 0, wa, oa, ob, -1);
     } else {
-      for (int f0 = 0; f0 < FF; f0 += 32) {
+      for (int f0 = 0; f0 < FF; f0 += 32) {     // D = 64: no register room for a second slab set
         Wc wa;
         load_w(f0, wa);
-        chunk(f0, (f0 >> 5) & 1, wa);
+        if (f0 > 0) load_o(f0, oa);
+        chunk(f0, (f0 >> 5) & 1, wa, oa, ob, -1);
       }
     }
     ffn_bwd_epilogue<D, NORMS, false, T>(a, dxacc, H + rb * T::S, m0, slab, X, acc);

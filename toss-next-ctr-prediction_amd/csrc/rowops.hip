@@ -296,6 +296,17 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
   if (ty == 0 && n < N) part[(long)blockIdx.y * N + n] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
 }
 
+// few partials (a slab of a few hundred rows): one thread per column, partials summed in order, the
+// loads of a partial row coalesced across the threads
+__global__ __launch_bounds__(256) void colsum_final_cols(const float* __restrict__ part, int nparts, int N, float div,
+                                                         float* __restrict__ out) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(long)p * N + n];
+  out[n] = div == 1.0f ? s : s / div;
+}
+
 // one wave per column: lanes stride the partials, fixed xor-tree combine
 __global__ __launch_bounds__(64) void colsum_final(const float* __restrict__ part, int nparts, int N, float div,
                                                    float* __restrict__ out) {
@@ -453,7 +464,8 @@ extern "C" int ctr_colsum(const float* X, long ld, int M, int N, float div, floa
   const int rpb = std::min(4096, std::max(64, cdiv((long)M * ctiles, 1024)));   // ~1024 blocks
   const int np = M > 0 ? cdiv(M, rpb) : 0;
   if (np > 0) colsum_partial<<<dim3(ctiles, np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
-  colsum_final<<<N, 64, 0, s>>>(ws, np, N, div, out);
+  if (np <= 16) colsum_final_cols<<<cdiv(N, 256), 256, 0, s>>>(ws, np, N, div, out);
+  else colsum_final<<<N, 64, 0, s>>>(ws, np, N, div, out);
   return check_launch("colsum");
 }
 

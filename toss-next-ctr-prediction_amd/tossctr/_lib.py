@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libctrhip.so")
+# CTR_LIB_PATH: an alternative build of the same library (kernel A/B experiments, tools/ only)
+LIB_PATH = os.environ.get("CTR_LIB_PATH") or os.path.join(_HERE, "libctrhip.so")
 
 p, i, l, f, u, z = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint32, C.c_size_t
 
