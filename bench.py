@@ -68,6 +68,9 @@ MFMA_F32_PEAK_TFS = 157.3   # MI355X dense fp32 MFMA (v_mfma_f32_16x16x4_f32), M
 MFMA_BF16_PEAK_TFS = 16 * MFMA_F32_PEAK_TFS   # dense bf16 MFMA = 16x the fp32 rate (~2.5 PF), same guide
 
 
+PROFILE_STEPS = 5       # untimed steps after the timed region that fill the per-kernel table
+
+
 def kernel_work(name, a, B, ffn_M):
     """(bound, algorithmic units per launch, unit) of the timed entry points -- SURVEY §8(d) per-unit
     figures x the units one launch processes ("Roofline accounting")."""
@@ -281,6 +284,8 @@ def main():
     ap.add_argument("--config", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2",
                     help="BASELINE.json config (the metric is quoted on cfg2; cfg5 needs 8 GPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-events", choices=("all", "none"), default="all",
+                    help="HIP events around the big kernels' calls in the timed steps (none: no roofline)")
     ap.add_argument("--markers", action="store_true",
                     help="launch an empty step_marker_kernel around the timed region (tools/prof_summary.py)")
     ap.add_argument("--dense-opt", action="store_true",
@@ -347,11 +352,16 @@ def main():
     if pg is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    opt.time_kernels(True)
     from tossctr import _lib
-    timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
-             "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_update", "ctr_lazy_update_pair", "ctr_adamw_ema")
-    _lib.time_calls(timed)
+    # HIP events cost host time per bracketed call (~0.1 ms per step for the whole list below when the step is
+    # host-issue sensitive), so the timed steps bracket only the roofline candidates (the kernels with an
+    # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
+    roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd")
+    timed = roof_timed + ("ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
+                          "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_update", "ctr_lazy_update_pair",
+                          "ctr_adamw_ema")
+    if args.kernel_events == "all":
+        _lib.time_calls(roof_timed)
     if args.markers:
         _lib.call("ctr_step_marker", 1, torch.cuda.current_stream(dev).cuda_stream)
     t0 = time.perf_counter()
@@ -370,11 +380,21 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    opt_ms = opt.kernel_ms()
     flush_ms = fl[0].elapsed_time(fl[1])
-    opt.time_kernels(False)
-    kstats = _lib.timed_ms()
+    kstats_timed = _lib.timed_ms()
     _lib.time_calls(())
+    opt_ms, kstats = None, {}
+    if args.kernel_events == "all":      # per-kernel table: a few more steps, every listed call bracketed
+        opt.time_kernels(True)
+        _lib.time_calls(timed)
+        for _ in range(PROFILE_STEPS):
+            run(g, g)
+            g += 1
+        model.sync()
+        opt_ms = opt.kernel_ms()
+        opt.time_kernels(False)
+        kstats = _lib.timed_ms()
+        _lib.time_calls(())
     # U of the exact-lazy byte count: the unique rows of the last timed step's batch and gradients
     U = measure_unique(model, data[(g - 1) % nb][0], model.engine.tg) if world == 1 else None
     if pg is not None:
@@ -389,16 +409,17 @@ def main():
         # dominant timed kernel (by device time per step) and its roofline
         a = model.arch
         ffn_M = args.batch * a.K_eff(args.seq_len)
-        per_step = {n: c * ms / args.steps for n, (c, ms) in kstats.items()}
-        kernels = {n: {"calls_per_step": round(kstats[n][0] / args.steps, 2), "avg_launch_ms": round(kstats[n][1], 4),
+        per_step = {n: c * ms / PROFILE_STEPS for n, (c, ms) in kstats.items()}
+        kernels = {n: {"calls_per_step": round(kstats[n][0] / PROFILE_STEPS, 2), "avg_launch_ms": round(kstats[n][1], 4),
                        "ms_per_step": round(per_step[n], 4)} for n in kstats}
+        per_step_t = {n: c * ms / args.steps for n, (c, ms) in kstats_timed.items()}
         roof = None
-        for n in sorted(per_step, key=per_step.get, reverse=True):
+        for n in sorted(per_step_t, key=per_step_t.get, reverse=True):
             w = kernel_work(n, a, args.batch, ffn_M)
             if w is None:
                 continue
             bound, work, unit = w
-            ach = work / (kstats[n][1] * 1e-3) / 1e12
+            ach = work / (kstats_timed[n][1] * 1e-3) / 1e12
             # amp bf16: the FFN kernels' products run on bf16 MFMA -> priced against the bf16 dense peak
             bf = args.amp == "bf16" and n.startswith("ctr_ffn") and model.engine.ffn_flags
             peak = MFMA_BF16_PEAK_TFS if bf else MFMA_F32_PEAK_TFS
@@ -406,8 +427,8 @@ def main():
                     "unit": "TFLOP/s", "frac": round(ach / peak, 4), "mfma_dtype": "bf16" if bf else "f32",
                     "traffic": pmc_traffic(n) if args.config == "cfg2" else None, "work_per_launch": work,
                     "work_unit": unit,
-                    "avg_launch_ms": round(kstats[n][1], 4), "ms_per_step": round(per_step[n], 4),
-                    "share_of_step": round(per_step[n] / ms, 4)}
+                    "avg_launch_ms": round(kstats_timed[n][1], 4), "ms_per_step": round(per_step_t[n], 4),
+                    "share_of_step": round(per_step_t[n] / ms, 4), "timing": "HIP events in the timed steps"}
             break
         rec = {
             "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref"
@@ -427,7 +448,9 @@ def main():
                                                      f", tables {'row-sharded' if shard else 'replicated'}")},
             "roofline": roof,
             "kernels": kernels,
-            "opt_ms_per_step": round(opt_ms, 3),
+            "kernels_note": f"HIP events on {PROFILE_STEPS} extra steps after the timed region (the flush: once, over those "
+                            f"{PROFILE_STEPS} ticks; the timed region's flush is flush_ms)",
+            "opt_ms_per_step": round(opt_ms, 3) if opt_ms is not None else None,
             "table_update": "dense stream" if args.dense_opt else "exact lazy (replay on read/grad; final flush timed)",
             "flush_ms": round(flush_ms, 3),
         }

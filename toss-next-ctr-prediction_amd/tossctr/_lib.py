@@ -192,19 +192,24 @@ def timed_ms():
     return out
 
 
+_fns = {}      # name -> bound ctypes function (one dict lookup per call on the launch path)
+
+
 def call(name, *args):
-    lib = load()
-    ev = None
-    if name in _timed:
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(load(), name)
+    if _timed and name in _timed:
         import torch
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
-    rc = getattr(lib, name)(*args)
-    if ev is not None:
+        rc = fn(*args)
         ev[1].record()
         _timed[name].append(ev)
+    else:
+        rc = fn(*args)
     if rc != 0:
-        raise CtrError(f"{name} failed ({rc}): {lib.ctr_last_error().decode()}")
+        raise CtrError(f"{name} failed ({rc}): {_lib.ctr_last_error().decode()}")
     return rc
 
 

@@ -346,9 +346,12 @@ class FusedAdamW:
         self._flushed_tick = self.tick
 
     def _segs_device(self, tg):
-        segs = self._segments(tg)
-        key = tuple((s.get("keys"), s.get("G"), s.get("n_uniq")) for s in segs)
-        if key != self._seg_key:
+        # the table segments only change when the compact grad buffers do: key on their pointers (building
+        # the segment list every step cost ~0.25 ms of host time, exposed when the host is behind)
+        key = tuple((ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["G"].shape[1])
+                    for t in (tg.get(n) for n in ("att", "rep", "cat")) if t) if tg else None
+        if key != self._seg_key or self._segs_dev is None:
+            segs = self._segments(tg)
             arr = (OptSeg * len(segs))()
             for i, s in enumerate(segs):
                 o = arr[i]
