@@ -320,11 +320,14 @@ __device__ __forceinline__ int flush_lg(int width) {
 
 // Persistent grid over (table, chunk of 256/lg rows) work items.  Per chunk everything (table, lg, nq)
 // is workgroup-uniform; every lane enters the wave replay (rows past the table or already current are
-// dead lanes), whose tick loop is wave-uniform.
+// dead lanes), whose tick loop is wave-uniform.  The chunk's rows are first ordered zero-moment rows
+// first, stepped rows last (LDS), so a wave's rows are of one kind and take the short or the full replay
+// -- in table order a wave almost always held a stepped row and ran the full replay for all of them.
 __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
                                                          float* P, float* M, float* V, float* E,
                                                          const OptScalars* __restrict__ hist, int tick) {
   __shared__ long chunk0[FLUSH_MAXTABS + 1];
+  __shared__ int ord_row[256], ord_w[256], n_lo, n_hi;
   const int tid = threadIdx.x;
   if (tid == 0) {
     long c = 0;
@@ -344,9 +347,21 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
     }
     const ctr_lazy_tab_t tb = tabs[a];
     const int lg = flush_lg(tb.width);
-    const long row = (c - chunk0[a]) * (256 / lg) + tid / lg;
+    const int nrow = 256 / lg;
+    const long row0 = (c - chunk0[a]) * nrow;
+    if (tid == 0) n_lo = n_hi = 0;
+    __syncthreads();
+    if (tid < nrow) {
+      const long rr = row0 + tid;
+      const int wr = rr < tb.rows ? tb.last[rr] : tick;
+      const int pos = (wr & LAST_NZ) ? nrow - 1 - atomicAdd(&n_hi, 1) : atomicAdd(&n_lo, 1);
+      ord_row[pos] = tid;
+      ord_w[pos] = wr;
+    }
+    __syncthreads();
+    const long row = row0 + ord_row[tid / lg];
     const bool in = row < tb.rows;
-    const int w = in ? tb.last[row] : tick;
+    const int w = in ? ord_w[tid / lg] : tick;
     const int s = ltick(w);
     const bool nzr = (w & LAST_NZ) != 0;
     const bool live = in && s < tick;
@@ -357,6 +372,7 @@ __global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* _
     else
       replay_rows_wave<false>(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), live, s, nzr, hist, tick);
     if (live && l == 0) tb.last[row] = tick | (w & LAST_NZ);
+    __syncthreads();      // the order arrays are refilled by the next chunk
   }
 }
 
@@ -597,6 +613,127 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_kernel(const ctr_lazy_tab
   }
 }
 
+// Flush of the DARE table pair, classified (W % 4 == 0, 128 % W == 0).  A workgroup takes CH consecutive row
+// pairs, sorts the ones behind `tick` into a zero-moment and a stepped list in LDS, and each wave replays
+// list entries in groups of 2 x (128 / W) row pairs: W / 4 lanes hold a table row (a float4 each, element
+// pairs in packed f32), one tick loop for the whole group, a lane applying tick k only past its own row's
+// tick.  A wave's rows then all take the short (zero-moment: decay + EMA) or all the full replay, and the
+// per-tick scalar work (history loads, flag branches) is shared by 2 x (128 / W) row pairs instead of being
+// paid per pair: the one-wave-per-pair kernel spent ~0.17 ms per replayed tick at cfg2 whatever the rows'
+// class.  Same adam.h arithmetic per element (packed halves are the same IEEE operations), so the result
+// is bit-identical to the dense stream.  List order inside a workgroup is arbitrary; rows are independent.
+template <int W>
+__global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs, float* P,
+                                                                  float* M, float* V, float* E,
+                                                                  const OptScalars* __restrict__ hist, int tick) {
+  constexpr int CH = 1024;                 // row pairs per workgroup iteration
+  constexpr int LPT = W / 4;               // lanes per table row
+  constexpr int LPP = 2 * LPT;             // lanes per row pair
+  constexpr int PPS = 64 / LPP;            // row pairs per slot
+  constexpr int NS = 2;                    // slots per lane
+  constexpr int GRP = PPS * NS;            // row pairs per wave group
+  __shared__ int lrow[2][CH];
+  __shared__ int ls[2][CH];
+  __shared__ int cnt[2];
+  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int u = lane / LPP, c = lane % LPP;
+  const bool is_b = c >= LPT;
+  const long tab_off = is_b ? tb.p_off : ta.p_off;
+  const int e0 = 4 * (is_b ? c - LPT : c);
+  const long rows = ta.rows;
+  for (long r0 = (long)blockIdx.x * CH; r0 < rows; r0 += (long)gridDim.x * CH) {
+    if (tid < 2) cnt[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < CH; i += 256) {
+      const long r = r0 + i;
+      if (r < rows) {
+        const int w = ta.last[r];
+        const int st = ltick(w);
+        if (st < tick) {
+          const int cl = (w & LAST_NZ) ? 1 : 0;
+          const int pos = atomicAdd(&cnt[cl], 1);
+          lrow[cl][pos] = i;
+          ls[cl][pos] = st;
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+      const int n = cnt[cl];
+      for (int g0 = wv * GRP; g0 < n; g0 += 4 * GRP) {
+        long off[NS], row[NS];
+        int s[NS];
+        bool live[NS];
+        f32x2 p[NS][2], m[NS][2], v[NS][2], e[NS][2];
+        int smin = tick;
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+          const int idx = g0 + q * PPS + u;
+          live[q] = idx < n;
+          row[q] = r0 + (live[q] ? lrow[cl][idx] : 0);
+          s[q] = live[q] ? ls[cl][idx] : tick;
+          off[q] = tab_off + row[q] * W + e0;
+          const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+          f32x4 pv = z4, mv = z4, vv = z4, ev = z4;
+          if (live[q]) {
+            pv = *(const f32x4*)(P + off[q]);
+            if (cl) {
+              mv = *(const f32x4*)(M + off[q]);
+              vv = *(const f32x4*)(V + off[q]);
+            }
+            if (E) ev = *(const f32x4*)(E + off[q]);
+          }
+          p[q][0] = f32x2{pv[0], pv[1]}; p[q][1] = f32x2{pv[2], pv[3]};
+          m[q][0] = f32x2{mv[0], mv[1]}; m[q][1] = f32x2{mv[2], mv[3]};
+          v[q][0] = f32x2{vv[0], vv[1]}; v[q][1] = f32x2{vv[2], vv[3]};
+          e[q][0] = f32x2{ev[0], ev[1]}; e[q][1] = f32x2{ev[2], ev[3]};
+          smin = min(smin, s[q]);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
+        smin = __builtin_amdgcn_readfirstlane(smin);
+        for_ticks(hist, smin + 1, tick, [&](const OptScalars& sc, int k) {
+#pragma unroll
+          for (int q = 0; q < NS; ++q) {
+            if (k > s[q]) {
+              if (sc.do_adam) {
+                if (cl) {
+                  idle_adam_pk(sc, p[q][0], m[q][0], v[q][0]);
+                  idle_adam_pk(sc, p[q][1], m[q][1], v[q][1]);
+                } else {
+                  p[q][0] = p[q][0] * splat2(sc.decay_mul);
+                  p[q][1] = p[q][1] * splat2(sc.decay_mul);
+                }
+              }
+              if (sc.do_ema) {
+                ema_pk(sc, p[q][0], e[q][0]);
+                ema_pk(sc, p[q][1], e[q][1]);
+              }
+            }
+          }
+        });
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+          if (!live[q]) continue;
+          *(f32x4*)(P + off[q]) = f32x4{p[q][0].x, p[q][0].y, p[q][1].x, p[q][1].y};
+          if (cl) {
+            *(f32x4*)(M + off[q]) = f32x4{m[q][0].x, m[q][0].y, m[q][1].x, m[q][1].y};
+            *(f32x4*)(V + off[q]) = f32x4{v[q][0].x, v[q][0].y, v[q][1].x, v[q][1].y};
+          }
+          if (E) *(f32x4*)(E + off[q]) = f32x4{e[q][0].x, e[q][0].y, e[q][1].x, e[q][1].y};
+          if (c == 0) {
+            ta.last[row[q]] = tick | (cl ? LAST_NZ : 0);
+            tb.last[row[q]] = tick | (cl ? LAST_NZ : 0);
+          }
+        }
+      }
+    }
+    __syncthreads();      // the lists are refilled by the next iteration
+  }
+}
+
 }  // namespace ctr
 
 using namespace ctr;
@@ -678,6 +815,17 @@ extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long r
                                    float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_flush_pair: two tables of width <= 64");
   if (tick <= 0 || rows <= 0) return 0;
+  const int cgrid = (int)std::max<long>(1, std::min<long>((rows + 1023) / 1024, 256L * 8));
+  const OptScalars* h = (const OptScalars*)hist;
+  hipStream_t s = (hipStream_t)stream;
+  switch (width) {      // the classified flush for the widths whose rows split into float4 lanes
+    case 4: lazy_flush_pair_cls_kernel<4><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 8: lazy_flush_pair_cls_kernel<8><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 16: lazy_flush_pair_cls_kernel<16><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 32: lazy_flush_pair_cls_kernel<32><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 64: lazy_flush_pair_cls_kernel<64><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    default: break;
+  }
   if (width <= 32)
     lazy_flush_pair_kernel<1><<<pair_grid(rows), 256, 0, (hipStream_t)stream>>>(tabs, P, M, V, E,
                                                                                  (const OptScalars*)hist, tick);

@@ -337,12 +337,16 @@ class FusedAdamW:
         exactly what the dense stream would (call before reading them as a whole)."""
         if not self.lazy or self.tick == self._flushed_tick:
             return
-        st = self.engine.s()
-        call("ctr_lazy_flush_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, self._seq_rows,
-             ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
+        # the DARE pair and the categorical tables are disjoint rows: their flushes run side by side (both
+        # are bound by memory latency and replay issue, neither fills the chip alone)
+        with self.engine.side():
+            call("ctr_lazy_flush_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, self._seq_rows,
+                 ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
+                 self.engine.s())
         tabs, n = self._lazy_tabs["cat"]
         call("ctr_lazy_flush", ptr(tabs), n, self._lazy_max_rows, ptr(self.arena.buf), ptr(self.m), ptr(self.v),
-             self._ema_ptr(), ptr(self.hist), self.tick, st)
+             self._ema_ptr(), ptr(self.hist), self.tick, self.engine.s())
+        self.engine.join()
         self._flushed_tick = self.tick
 
     def _segs_device(self, tg):
