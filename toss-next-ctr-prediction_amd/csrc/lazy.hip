@@ -613,39 +613,117 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_kernel(const ctr_lazy_tab
   }
 }
 
-// Flush of the DARE table pair, classified (W % 4 == 0, 128 % W == 0).  A workgroup takes CH consecutive row
-// pairs, sorts the ones behind `tick` into a zero-moment and a stepped list in LDS, and each wave replays
-// list entries in groups of 2 x (128 / W) row pairs: W / 4 lanes hold a table row (a float4 each, element
-// pairs in packed f32), one tick loop for the whole group, a lane applying tick k only past its own row's
-// tick.  A wave's rows then all take the short (zero-moment: decay + EMA) or all the full replay, and the
-// per-tick scalar work (history loads, flag branches) is shared by 2 x (128 / W) row pairs instead of being
-// paid per pair: the one-wave-per-pair kernel spent ~0.17 ms per replayed tick at cfg2 whatever the rows'
-// class.  Same adam.h arithmetic per element (packed halves are the same IEEE operations), so the result
-// is bit-identical to the dense stream.  List order inside a workgroup is arbitrary; rows are independent.
-template <int W>
-__global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs, float* P,
-                                                                  float* M, float* V, float* E,
-                                                                  const OptScalars* __restrict__ hist, int tick) {
-  constexpr int CH = 1024;                 // row pairs per workgroup iteration
+// Classified replay of DARE table-pair rows (W % 4 == 0, 128 % W == 0).  The rows to bring current sit in a
+// zero-moment and a stepped list in LDS (absolute row, last tick); each wave replays list entries in groups
+// of 2 x (128 / W) row pairs: W / 4 lanes hold a table row (a float4 each, element pairs in packed f32), one
+// tick loop for the whole group, a lane applying tick k only past its own row's tick.  A wave's rows all take
+// the short (zero-moment: decay + EMA) or all the full replay, and the per-tick scalar work (history loads,
+// flag branches) is shared by 2 x (128 / W) row pairs instead of being paid per pair: the one-wave-per-pair
+// kernels spent ~0.17 ms per replayed tick of a cfg2 flush whatever the rows' class.  Same adam.h arithmetic
+// per element (packed halves are the same IEEE operations): bit-identical to the dense stream.  List order is
+// arbitrary; rows are independent.  Rows end at `tick`; both tables' state words are written when write_a,
+// else only the rep table's (the att word was claimed by CAS).
+template <int W, int CL>
+__device__ __forceinline__ void replay_pair_list(const ctr_lazy_tab_t& ta, const ctr_lazy_tab_t& tb,
+                                                 const int* lrow, const int* ls, int n, float* P, float* M,
+                                                 float* V, float* E, const OptScalars* __restrict__ hist, int tick,
+                                                 bool write_a) {
   constexpr int LPT = W / 4;               // lanes per table row
   constexpr int LPP = 2 * LPT;             // lanes per row pair
   constexpr int PPS = 64 / LPP;            // row pairs per slot
   constexpr int NS = 2;                    // slots per lane
   constexpr int GRP = PPS * NS;            // row pairs per wave group
-  __shared__ int lrow[2][CH];
-  __shared__ int ls[2][CH];
-  __shared__ int cnt[2];
-  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int u = lane / LPP, c = lane % LPP;
   const bool is_b = c >= LPT;
   const long tab_off = is_b ? tb.p_off : ta.p_off;
   const int e0 = 4 * (is_b ? c - LPT : c);
+  for (int g0 = wv * GRP; g0 < n; g0 += nw * GRP) {
+    long off[NS], row[NS];
+    int s[NS];
+    bool live[NS];
+    f32x2 p[NS][2], m[NS][2], v[NS][2], e[NS][2];
+    int smin = tick;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const int idx = g0 + q * PPS + u;
+      live[q] = idx < n;
+      row[q] = live[q] ? lrow[idx] : 0;
+      s[q] = live[q] ? ls[idx] : tick;
+      off[q] = tab_off + row[q] * W + e0;
+      const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 pv = z4, mv = z4, vv = z4, ev = z4;
+      if (live[q]) {
+        pv = *(const f32x4*)(P + off[q]);
+        if (CL) {
+          mv = *(const f32x4*)(M + off[q]);
+          vv = *(const f32x4*)(V + off[q]);
+        }
+        if (E) ev = *(const f32x4*)(E + off[q]);
+      }
+      p[q][0] = f32x2{pv[0], pv[1]}; p[q][1] = f32x2{pv[2], pv[3]};
+      m[q][0] = f32x2{mv[0], mv[1]}; m[q][1] = f32x2{mv[2], mv[3]};
+      v[q][0] = f32x2{vv[0], vv[1]}; v[q][1] = f32x2{vv[2], vv[3]};
+      e[q][0] = f32x2{ev[0], ev[1]}; e[q][1] = f32x2{ev[2], ev[3]};
+      smin = min(smin, s[q]);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
+    smin = __builtin_amdgcn_readfirstlane(smin);
+    for_ticks(hist, smin + 1, tick, [&](const OptScalars& sc, int k) {
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (k > s[q]) {
+          if (sc.do_adam) {
+            if (CL) {
+              idle_adam_pk(sc, p[q][0], m[q][0], v[q][0]);
+              idle_adam_pk(sc, p[q][1], m[q][1], v[q][1]);
+            } else {
+              p[q][0] = p[q][0] * splat2(sc.decay_mul);
+              p[q][1] = p[q][1] * splat2(sc.decay_mul);
+            }
+          }
+          if (sc.do_ema) {
+            ema_pk(sc, p[q][0], e[q][0]);
+            ema_pk(sc, p[q][1], e[q][1]);
+          }
+        }
+      }
+    });
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      if (!live[q]) continue;
+      *(f32x4*)(P + off[q]) = f32x4{p[q][0].x, p[q][0].y, p[q][1].x, p[q][1].y};
+      if (CL) {
+        *(f32x4*)(M + off[q]) = f32x4{m[q][0].x, m[q][0].y, m[q][1].x, m[q][1].y};
+        *(f32x4*)(V + off[q]) = f32x4{v[q][0].x, v[q][0].y, v[q][1].x, v[q][1].y};
+      }
+      if (E) *(f32x4*)(E + off[q]) = f32x4{e[q][0].x, e[q][0].y, e[q][1].x, e[q][1].y};
+      if (c == 0) {
+        if (write_a) ta.last[row[q]] = tick | (CL ? LAST_NZ : 0);
+        tb.last[row[q]] = tick | (CL ? LAST_NZ : 0);
+      }
+    }
+  }
+}
+
+constexpr int CLS_CH = 1024;     // rows (flush) / token positions (touch) per workgroup iteration
+
+// flush of the DARE table pair: a workgroup sorts CLS_CH consecutive row pairs behind `tick` into the lists
+template <int W>
+__global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs, float* P,
+                                                                  float* M, float* V, float* E,
+                                                                  const OptScalars* __restrict__ hist, int tick) {
+  __shared__ int lrow[2][CLS_CH];
+  __shared__ int ls[2][CLS_CH];
+  __shared__ int cnt[2];
+  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
+  const int tid = threadIdx.x;
   const long rows = ta.rows;
-  for (long r0 = (long)blockIdx.x * CH; r0 < rows; r0 += (long)gridDim.x * CH) {
+  for (long r0 = (long)blockIdx.x * CLS_CH; r0 < rows; r0 += (long)gridDim.x * CLS_CH) {
     if (tid < 2) cnt[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < CH; i += 256) {
+    for (int i = tid; i < CLS_CH; i += 256) {
       const long r = r0 + i;
       if (r < rows) {
         const int w = ta.last[r];
@@ -653,84 +731,55 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy
         if (st < tick) {
           const int cl = (w & LAST_NZ) ? 1 : 0;
           const int pos = atomicAdd(&cnt[cl], 1);
-          lrow[cl][pos] = i;
+          lrow[cl][pos] = (int)r;
           ls[cl][pos] = st;
         }
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int cl = 0; cl < 2; ++cl) {
-      const int n = cnt[cl];
-      for (int g0 = wv * GRP; g0 < n; g0 += 4 * GRP) {
-        long off[NS], row[NS];
-        int s[NS];
-        bool live[NS];
-        f32x2 p[NS][2], m[NS][2], v[NS][2], e[NS][2];
-        int smin = tick;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-          const int idx = g0 + q * PPS + u;
-          live[q] = idx < n;
-          row[q] = r0 + (live[q] ? lrow[cl][idx] : 0);
-          s[q] = live[q] ? ls[cl][idx] : tick;
-          off[q] = tab_off + row[q] * W + e0;
-          const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
-          f32x4 pv = z4, mv = z4, vv = z4, ev = z4;
-          if (live[q]) {
-            pv = *(const f32x4*)(P + off[q]);
-            if (cl) {
-              mv = *(const f32x4*)(M + off[q]);
-              vv = *(const f32x4*)(V + off[q]);
-            }
-            if (E) ev = *(const f32x4*)(E + off[q]);
-          }
-          p[q][0] = f32x2{pv[0], pv[1]}; p[q][1] = f32x2{pv[2], pv[3]};
-          m[q][0] = f32x2{mv[0], mv[1]}; m[q][1] = f32x2{mv[2], mv[3]};
-          v[q][0] = f32x2{vv[0], vv[1]}; v[q][1] = f32x2{vv[2], vv[3]};
-          e[q][0] = f32x2{ev[0], ev[1]}; e[q][1] = f32x2{ev[2], ev[3]};
-          smin = min(smin, s[q]);
-        }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
-        smin = __builtin_amdgcn_readfirstlane(smin);
-        for_ticks(hist, smin + 1, tick, [&](const OptScalars& sc, int k) {
-#pragma unroll
-          for (int q = 0; q < NS; ++q) {
-            if (k > s[q]) {
-              if (sc.do_adam) {
-                if (cl) {
-                  idle_adam_pk(sc, p[q][0], m[q][0], v[q][0]);
-                  idle_adam_pk(sc, p[q][1], m[q][1], v[q][1]);
-                } else {
-                  p[q][0] = p[q][0] * splat2(sc.decay_mul);
-                  p[q][1] = p[q][1] * splat2(sc.decay_mul);
-                }
-              }
-              if (sc.do_ema) {
-                ema_pk(sc, p[q][0], e[q][0]);
-                ema_pk(sc, p[q][1], e[q][1]);
-              }
-            }
-          }
-        });
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {
-          if (!live[q]) continue;
-          *(f32x4*)(P + off[q]) = f32x4{p[q][0].x, p[q][0].y, p[q][1].x, p[q][1].y};
-          if (cl) {
-            *(f32x4*)(M + off[q]) = f32x4{m[q][0].x, m[q][0].y, m[q][1].x, m[q][1].y};
-            *(f32x4*)(V + off[q]) = f32x4{v[q][0].x, v[q][0].y, v[q][1].x, v[q][1].y};
-          }
-          if (E) *(f32x4*)(E + off[q]) = f32x4{e[q][0].x, e[q][0].y, e[q][1].x, e[q][1].y};
-          if (c == 0) {
-            ta.last[row[q]] = tick | (cl ? LAST_NZ : 0);
-            tb.last[row[q]] = tick | (cl ? LAST_NZ : 0);
+    replay_pair_list<W, 0>(ta, tb, lrow[0], ls[0], cnt[0], P, M, V, E, hist, tick, true);
+    replay_pair_list<W, 1>(ta, tb, lrow[1], ls[1], cnt[1], P, M, V, E, hist, tick, true);
+    __syncthreads();      // the lists are refilled by the next iteration
+  }
+}
+
+// forward read of tokens X[0, n): a workgroup claims the rows of CLS_CH token positions (CAS on the att
+// row's state word: a token read many times is caught up once; a token equal to its predecessor is that
+// position's job) into the lists, then replays them
+template <int W>
+__global__ __launch_bounds__(256) void lazy_touch_pair_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
+                                                                  const int32_t* __restrict__ X, long n, float* P,
+                                                                  float* M, float* V, float* E,
+                                                                  const OptScalars* __restrict__ hist, int tick) {
+  __shared__ int lrow[2][CLS_CH];
+  __shared__ int ls[2][CLS_CH];
+  __shared__ int cnt[2];
+  const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
+  const int tid = threadIdx.x;
+  for (long p0 = (long)blockIdx.x * CLS_CH; p0 < n; p0 += (long)gridDim.x * CLS_CH) {
+    if (tid < 2) cnt[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < CLS_CH; i += 256) {
+      const long pos = p0 + i;
+      if (pos < n) {
+        const long row = X[pos];
+        const bool dup = pos > 0 && X[pos - 1] == row;
+        if (!dup && row >= 0 && row < ta.rows) {
+          int* lp = ta.last + row;
+          const int w = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (ltick(w) < tick && atomicCAS(lp, w, tick | (w & LAST_NZ)) == w) {
+            const int cl = (w & LAST_NZ) ? 1 : 0;
+            const int q = atomicAdd(&cnt[cl], 1);
+            lrow[cl][q] = (int)row;
+            ls[cl][q] = ltick(w);
           }
         }
       }
     }
-    __syncthreads();      // the lists are refilled by the next iteration
+    __syncthreads();
+    replay_pair_list<W, 0>(ta, tb, lrow[0], ls[0], cnt[0], P, M, V, E, hist, tick, false);
+    replay_pair_list<W, 1>(ta, tb, lrow[1], ls[1], cnt[1], P, M, V, E, hist, tick, false);
+    __syncthreads();
   }
 }
 
@@ -788,6 +837,19 @@ extern "C" int ctr_lazy_touch_pair(const ctr_lazy_tab_t* tabs, int width, const 
                                    float* M, float* V, float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_touch_pair: two tables of width <= 64");
   if (tick <= 0 || n <= 0) return 0;
+  {
+    const int cgrid = (int)std::max<long>(1, std::min<long>((n + CLS_CH - 1) / CLS_CH, 256L * 8));
+    const OptScalars* h = (const OptScalars*)hist;
+    hipStream_t s = (hipStream_t)stream;
+    switch (width) {      // the classified touch for the widths whose rows split into float4 lanes
+      case 4: lazy_touch_pair_cls_kernel<4><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 8: lazy_touch_pair_cls_kernel<8><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 16: lazy_touch_pair_cls_kernel<16><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 32: lazy_touch_pair_cls_kernel<32><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 64: lazy_touch_pair_cls_kernel<64><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      default: break;
+    }
+  }
   if (width <= 32)
     lazy_touch_pair_kernel<1><<<pair_grid(n), 256, 0, (hipStream_t)stream>>>(tabs, X, n, P, M, V, E,
                                                                              (const OptScalars*)hist, tick);
@@ -815,7 +877,7 @@ extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long r
                                    float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_flush_pair: two tables of width <= 64");
   if (tick <= 0 || rows <= 0) return 0;
-  const int cgrid = (int)std::max<long>(1, std::min<long>((rows + 1023) / 1024, 256L * 8));
+  const int cgrid = (int)std::max<long>(1, std::min<long>((rows + CLS_CH - 1) / CLS_CH, 256L * 8));
   const OptScalars* h = (const OptScalars*)hist;
   hipStream_t s = (hipStream_t)stream;
   switch (width) {      // the classified flush for the widths whose rows split into float4 lanes
