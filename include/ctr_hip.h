@@ -166,7 +166,8 @@ int ctr_pool_bwd(const float* x, const float* vals, const float* w, int B, int K
                  const float* daux, float* dx, float* dvals, void* stream);
 /* PositionalBias + head mean, src/models/dare.py:29-37,56-60: out[d] = mean_h rel[d,h] */
 int ctr_pos_bias_mean(const float* rel, int H, int n, float* out, void* stream);
-int ctr_pos_bias_grad(const float* part, int nparts, int H, int n, float* drel, void* stream);
+/* drel[d, h] = sum_p part[p, d] / H; part (the attention backward's diagonal partials) is scratch, reduced in place */
+int ctr_pos_bias_grad(float* part, int nparts, int H, int n, float* drel, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Attention core of DAREEncoderLayer (MHA explicit path), src/models/dare.py:53-62    (attn.hip)

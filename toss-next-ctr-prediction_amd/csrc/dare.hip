@@ -258,20 +258,27 @@ __global__ void pos_bias_mean_kernel(const float* __restrict__ rel, int H, int n
 }
 
 // drel[d, h] = (sum_p part[p, d]) / H ; one workgroup per distance d, fixed-order block reduction
-__global__ __launch_bounds__(256) void pos_bias_grad_kernel(const float* __restrict__ part, int nparts, int H, int n,
-                                                            float* __restrict__ drel) {
+// drel[d, h] = (sum_p part[p, d]) / H for every head h (the head-mean bias), in two passes over the
+// (nparts, n) partials: pass 1, block (column d, row split s) sums rows [s*PB_ROWS, ...) of column d in a
+// fixed order and writes the sum over the split's first row, column d (that block is the only reader /
+// writer of that column in those rows: the partials are scratch); pass 2 sums the splits in order.
+constexpr int PB_ROWS = 512;
+__global__ __launch_bounds__(256) void pos_bias_grad_part(float* __restrict__ part, int nparts, int n) {
   __shared__ float red[4];
-  const int d = blockIdx.x;
-  // eight independent partial sums per thread (eight strided loads in flight), combined in a fixed order
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int p = threadIdx.x;
-  for (; p + 7 * 256 < nparts; p += 8 * 256)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += part[(long)(p + u * 256) * n + d];
-  for (int u = 0; p < nparts; p += 256, ++u) acc[u] += part[(long)p * n + d];
-  float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  const int d = blockIdx.x, p0 = blockIdx.y * PB_ROWS, p1 = min(nparts, p0 + PB_ROWS);
+  float s = 0.f;
+  for (int p = p0 + threadIdx.x; p < p1; p += 256) s += part[(long)p * n + d];
   s = block_sum(s, red);
-  if (threadIdx.x < H) drel[(long)d * H + threadIdx.x] = s / (float)H;
+  if (threadIdx.x == 0) part[(long)p0 * n + d] = s;
+}
+
+__global__ __launch_bounds__(256) void pos_bias_grad_kernel(const float* __restrict__ part, int nsplit, int H, int n,
+                                                            float* __restrict__ drel) {
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) s += part[(long)k * PB_ROWS * n + d];
+  for (int h = 0; h < H; ++h) drel[(long)d * H + h] = s / (float)H;
 }
 
 }  // namespace ctr
@@ -339,8 +346,12 @@ extern "C" int ctr_pos_bias_mean(const float* rel, int H, int n, float* out, voi
   return check_launch("pos_bias_mean");
 }
 
-extern "C" int ctr_pos_bias_grad(const float* part, int nparts, int H, int n, float* drel, void* stream) {
+extern "C" int ctr_pos_bias_grad(float* part, int nparts, int H, int n, float* drel, void* stream) {
   CTR_REQUIRE(H <= 256, "H > 256");
-  pos_bias_grad_kernel<<<n, 256, 0, (hipStream_t)stream>>>(part, nparts, H, n, drel);
+  if (n <= 0) return 0;
+  const int nsplit = std::max(1, cdiv(nparts, PB_ROWS));
+  // the partials are the attention backward's per-(sample, head group) scratch: reduced in place
+  if (nparts > 0) pos_bias_grad_part<<<dim3(n, nsplit), 256, 0, (hipStream_t)stream>>>(part, nparts, n);
+  pos_bias_grad_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(part, nparts > 0 ? nsplit : 0, H, n, drel);
   return check_launch("pos_bias_grad");
 }
