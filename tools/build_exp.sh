@@ -7,5 +7,5 @@ name=$1; src=$2; shift 2
 mkdir -p ../exp/obj
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I../include -Wall -Wno-unused-function "$@" \
     -c csrc/$src -o ../exp/obj/$name.o
-objs=$(ls build/*.o | grep -v "build/$src.o")
+objs=$(ls build/*.o | grep -v "build/${EXP_REPLACES:-$src}.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o ../exp/lib_$name.so $objs ../exp/obj/$name.o
