@@ -358,7 +358,7 @@ def main():
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd")
     timed = roof_timed + ("ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
-                          "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_update", "ctr_lazy_update_pair",
+                          "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
                           "ctr_adamw_ema")
     if args.kernel_events == "all":
         _lib.time_calls(roof_timed)

@@ -366,6 +366,10 @@ int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_rows, float* 
  * keys with att grads Ga and rep grads Gb (same keys, as ctr_rowgrad2 produces); flush: all rows.   */
 int ctr_lazy_touch_pair(const ctr_lazy_tab_t* tabs, int width, const int32_t* X, long n, float* P, float* M, float* V,
                         float* E, const void* hist, int tick, void* stream);
+/* the same with hot_row (>= 0; -1: none): a row most sequences hold (the padding token), claimed once instead of
+ * at every position that holds it (widths 4/8/16/32/64; other widths ignore it)                              */
+int ctr_lazy_touch_pair_hot(const ctr_lazy_tab_t* tabs, int width, const int32_t* X, long n, int hot_row, float* P,
+                            float* M, float* V, float* E, const void* hist, int tick, void* stream);
 int ctr_lazy_update_pair(const ctr_lazy_tab_t* tabs, int width, const uint32_t* keys, const float* Ga, const float* Gb,
                          int g_ld, const uint32_t* n_uniq, long cap, const float* coef, float* P, float* M, float* V,
                          float* E, const void* hist, int tick, void* stream);

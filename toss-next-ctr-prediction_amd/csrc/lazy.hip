@@ -707,7 +707,11 @@ __device__ __forceinline__ void replay_pair_list(const ctr_lazy_tab_t& ta, const
   }
 }
 
-constexpr int CLS_CH = 1024;     // rows (flush) / token positions (touch) per workgroup iteration
+constexpr int CLS_CH = 1024;     // rows per workgroup iteration of the flush
+// token positions per workgroup of the touch: its claims (a load and a CAS per position) and its row gathers
+// are dependent memory round trips, so many small workgroups beat few large ones (one of 1024 positions per
+// workgroup: 400 workgroups at cfg2, 141 us; 256: 1600 workgroups)
+constexpr int TOUCH_CH = 256;
 
 // flush of the DARE table pair: a workgroup sorts CLS_CH consecutive row pairs behind `tick` into the lists
 template <int W>
@@ -746,24 +750,37 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy
 // forward read of tokens X[0, n): a workgroup claims the rows of CLS_CH token positions (CAS on the att
 // row's state word: a token read many times is caught up once; a token equal to its predecessor is that
 // position's job) into the lists, then replays them
+// hot (>= 0): a row most sequences hold (the padding token of the left-padded histories): claimed once,
+// by the first workgroup, and skipped at every position -- 4096 CAS attempts on one word per step otherwise
+// serialise at its L2 channel (~40 us of the touch at cfg2)
 template <int W>
 __global__ __launch_bounds__(256) void lazy_touch_pair_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs,
-                                                                  const int32_t* __restrict__ X, long n, float* P,
-                                                                  float* M, float* V, float* E,
+                                                                  const int32_t* __restrict__ X, long n, int hot,
+                                                                  float* P, float* M, float* V, float* E,
                                                                   const OptScalars* __restrict__ hist, int tick) {
-  __shared__ int lrow[2][CLS_CH];
-  __shared__ int ls[2][CLS_CH];
+  __shared__ int lrow[2][TOUCH_CH];
+  __shared__ int ls[2][TOUCH_CH];
   __shared__ int cnt[2];
   const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
   const int tid = threadIdx.x;
-  for (long p0 = (long)blockIdx.x * CLS_CH; p0 < n; p0 += (long)gridDim.x * CLS_CH) {
+  for (long p0 = (long)blockIdx.x * TOUCH_CH; p0 < n; p0 += (long)gridDim.x * TOUCH_CH) {
     if (tid < 2) cnt[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < CLS_CH; i += 256) {
+    if (p0 == 0 && tid == 0 && hot >= 0 && hot < ta.rows) {
+      int* lp = ta.last + hot;
+      const int w = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ltick(w) < tick && atomicCAS(lp, w, tick | (w & LAST_NZ)) == w) {
+        const int cl = (w & LAST_NZ) ? 1 : 0;
+        const int q = atomicAdd(&cnt[cl], 1);
+        lrow[cl][q] = hot;
+        ls[cl][q] = ltick(w);
+      }
+    }
+    for (int i = tid; i < TOUCH_CH; i += 256) {
       const long pos = p0 + i;
       if (pos < n) {
         const long row = X[pos];
-        const bool dup = pos > 0 && X[pos - 1] == row;
+        const bool dup = (pos > 0 && X[pos - 1] == row) || row == hot;
         if (!dup && row >= 0 && row < ta.rows) {
           int* lp = ta.last + row;
           const int w = __hip_atomic_load(lp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -835,18 +852,24 @@ static bool pair_ok(const ctr_lazy_tab_t* tabs_host_view) { return tabs_host_vie
 
 extern "C" int ctr_lazy_touch_pair(const ctr_lazy_tab_t* tabs, int width, const int32_t* X, long n, float* P,
                                    float* M, float* V, float* E, const void* hist, int tick, void* stream) {
+  return ctr_lazy_touch_pair_hot(tabs, width, X, n, -1, P, M, V, E, hist, tick, stream);
+}
+
+extern "C" int ctr_lazy_touch_pair_hot(const ctr_lazy_tab_t* tabs, int width, const int32_t* X, long n, int hot_row,
+                                       float* P, float* M, float* V, float* E, const void* hist, int tick,
+                                       void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_touch_pair: two tables of width <= 64");
   if (tick <= 0 || n <= 0) return 0;
   {
-    const int cgrid = (int)std::max<long>(1, std::min<long>((n + CLS_CH - 1) / CLS_CH, 256L * 8));
+    const int cgrid = (int)std::max<long>(1, std::min<long>((n + TOUCH_CH - 1) / TOUCH_CH, 256L * 16));
     const OptScalars* h = (const OptScalars*)hist;
     hipStream_t s = (hipStream_t)stream;
     switch (width) {      // the classified touch for the widths whose rows split into float4 lanes
-      case 4: lazy_touch_pair_cls_kernel<4><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
-      case 8: lazy_touch_pair_cls_kernel<8><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
-      case 16: lazy_touch_pair_cls_kernel<16><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
-      case 32: lazy_touch_pair_cls_kernel<32><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
-      case 64: lazy_touch_pair_cls_kernel<64><<<cgrid, 256, 0, s>>>(tabs, X, n, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 4: lazy_touch_pair_cls_kernel<4><<<cgrid, 256, 0, s>>>(tabs, X, n, hot_row, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 8: lazy_touch_pair_cls_kernel<8><<<cgrid, 256, 0, s>>>(tabs, X, n, hot_row, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 16: lazy_touch_pair_cls_kernel<16><<<cgrid, 256, 0, s>>>(tabs, X, n, hot_row, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 32: lazy_touch_pair_cls_kernel<32><<<cgrid, 256, 0, s>>>(tabs, X, n, hot_row, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
+      case 64: lazy_touch_pair_cls_kernel<64><<<cgrid, 256, 0, s>>>(tabs, X, n, hot_row, P, M, V, E, h, tick); return check_launch("lazy_touch_pair");
       default: break;
     }
   }

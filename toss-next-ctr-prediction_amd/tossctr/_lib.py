@@ -116,6 +116,7 @@ SIGS = {
     "ctr_lazy_update": (i, [p, i, p, p, i, p, l, p, p, p, p, p, p, i, p]),
     "ctr_lazy_flush": (i, [p, i, l, p, p, p, p, p, i, p]),
     "ctr_lazy_touch_pair": (i, [p, i, p, l, p, p, p, p, p, i, p]),
+    "ctr_lazy_touch_pair_hot": (i, [p, i, p, l, i, p, p, p, p, p, i, p]),
     "ctr_lazy_update_pair": (i, [p, i, p, p, p, i, p, l, p, p, p, p, p, p, i, p]),
     "ctr_lazy_flush_pair": (i, [p, i, l, p, p, p, p, p, i, p]),
     "ctr_shard_plan_ws_size": (z, [l]),

@@ -306,10 +306,11 @@ class FusedAdamW:
         row of both DARE tables."""
         if self.tick == self._flushed_tick:
             return
-        if group == "seq":      # both DARE tables of each token: one wave per token (lazy.hip, pair kernels)
-            call("ctr_lazy_touch_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, ptr(X), X.numel(),
-                 ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
-                 self.engine.s())
+        if group == "seq":      # both DARE tables of each token (lazy.hip, pair kernels); the padding token,
+            # which most left-padded histories hold, is claimed once
+            call("ctr_lazy_touch_pair_hot", ptr(self._lazy_tabs["seq"][0]), self._seq_width, ptr(X), X.numel(),
+                 int(self.engine.a.pad_id), ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(),
+                 ptr(self.hist), self.tick, self.engine.s())
             return
         tabs, n = self._lazy_tabs[group]
         call("ctr_lazy_touch", ptr(tabs), n, ptr(X), X.shape[0], X.shape[1], 1,
