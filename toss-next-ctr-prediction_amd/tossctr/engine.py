@@ -679,8 +679,10 @@ class Engine:
         tg["fx"] = tv["fx"]
         call("ctr_dare_topk_bwd", ptr(sv["tok"]), B, K, ptr(sv["query"]), tv["att"], D, ptr(dvals), tv["pad"], ptr(dq),
              ptr(att_c), ptr(att_k), ptr(rep_k), st)
-        # att and rep contributions share their keys (the top-K tokens): one sort for both
-        tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"])
+        # att and rep contributions share their keys (the top-K tokens): one sort for both, on the side
+        # stream beside the context / embedding backward (its inputs are final; its own sort workspace)
+        with self.side():
+            tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
         # ---------------- context / query
         mode = QUERY_MODES[a.query_mode]
         dcat = W.get("dcat", (B, a.Fc, D))
@@ -730,14 +732,13 @@ class Engine:
              rws.numel(), self.s())
         return dict(keys=uk, G=ug, n_uniq=nu, width=width, n=n)
 
-    def _rowgrad2(self, W, keys, contrib_a, contrib_b, n, width, key_bits, name="seq"):
+    def _rowgrad2(self, W, keys, contrib_a, contrib_b, n, width, key_bits, name="seq", ws="rowgrad_ws"):
         uk = W.get(f"{name}_uk", (n,), torch.int32)
         ua = W.get(f"{name}_ug_a", (n, width))
         ub = W.get(f"{name}_ug_b", (n, width))
         nu = W.get(f"{name}_nu", (1,), torch.int32)
         wsz = _lib.query("ctr_rowgrad_ws_size", n)
-        rws = W.get("rowgrad_ws", (max(wsz, W.t["rowgrad_ws"].numel() if "rowgrad_ws" in W.t else 0),),
-                    torch.uint8)
+        rws = W.get(ws, (max(wsz, W.t[ws].numel() if ws in W.t else 0),), torch.uint8)
         call("ctr_rowgrad2", ptr(keys), ptr(contrib_a), ptr(contrib_b), n, width, width, key_bits, ptr(uk), ptr(ua),
              ptr(ub), ptr(nu), ptr(rws), rws.numel(), self.s())
         return (dict(keys=uk, G=ua, n_uniq=nu, width=width, n=n), dict(keys=uk, G=ub, n_uniq=nu, width=width, n=n))
