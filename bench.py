@@ -359,7 +359,7 @@ def main():
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd")
     timed = roof_timed + ("ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
-                          "ctr_adamw_ema")
+                          "ctr_adamw_ema", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
     if args.kernel_events == "all":
         _lib.time_calls(roof_timed)
     if args.markers:

@@ -226,13 +226,17 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
     f32x4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the lane's four A values of a 16-column block are contiguous: one 16-byte load per block
+    f32x4 zq[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+      zq[i] = fa < F ? *(const f32x4*)(zb + (long)fa * D + 16 * i + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float av = fa < F ? zb[(long)fa * D + 16 * i + 4 * g + r] : 0.f;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[j] = mfma4q(av, M[i][j][r], acc[j]);
+        for (int j = 0; j < NT; ++j) acc[j] = mfma4q(zq[i][r], M[i][j][r], acc[j]);
       }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
