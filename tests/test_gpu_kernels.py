@@ -692,6 +692,22 @@ def test_rowgemm_wgrad_vs_torch(NO, NIN, M):
     assert float(out[NO * NIN:o_db].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("M,N,ld", [(1, 4, 4), (7, 3, 3), (4096, 512, 512), (4096, 513, 516), (1023, 8432, 8432),
+                                    (5000, 257, 260), (64, 1, 1), (129, 260, 264), (0, 8, 8)])
+def test_colsum_vs_torch(M, N, ld):
+    """ctr_colsum (out = column sums / div) vs torch fp64: the float4 form (N, ld multiples of 4) and the
+    scalar form, ragged row chunks, few and many partials."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    X = torch.randn(max(M, 1), ld, device="cuda", generator=g)
+    out = torch.full((N,), float("nan"), device="cuda")
+    ws = torch.empty(L.query("ctr_colsum_ws_size", M, N) // 4 + 1, device="cuda")
+    L.call("ctr_colsum", ptr(X), ld, M, N, 3.0, ptr(out), ptr(ws), stream())
+    torch.cuda.synchronize()
+    ref = X[:M, :N].double().sum(0) / 3.0
+    assert rel(out.double(), ref) < 1e-6
+
+
 @pytest.mark.parametrize("M,N,K,cut,splits", [(4096, 512, 7552, 6400, 8), (300, 200, 130, 70, 1),
                                               (257, 130, 99, 33, 3), (64, 7552, 512, 6400, 1)])
 def test_gemm_segments_vs_torch(M, N, K, cut, splits):

@@ -296,6 +296,45 @@ __global__ __launch_bounds__(256) void colsum_partial(const float* __restrict__ 
   if (ty == 0 && n < N) part[(long)blockIdx.y * N + n] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
 }
 
+// same reduction over 256-column tiles, a lane owning four adjacent columns (one 16-byte load per row;
+// X 16-byte aligned, ld and N multiples of 4): each column keeps the scalar kernel's summation order
+__global__ __launch_bounds__(256) void colsum_partial_v4(const float* __restrict__ X, long ld, int M, int N,
+                                                         int rows_per_block, float* __restrict__ part) {
+  __shared__ float4 red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = (blockIdx.x * 64 + tx) * 4;
+  const int m0 = blockIdx.y * rows_per_block, m1 = min(M, m0 + rows_per_block);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    int m = m0 + ty;
+    for (; m + 12 < m1; m += 16) {
+      const float4 a0 = *reinterpret_cast<const float4*>(X + (long)m * ld + n);
+      const float4 a1 = *reinterpret_cast<const float4*>(X + (long)(m + 4) * ld + n);
+      const float4 a2 = *reinterpret_cast<const float4*>(X + (long)(m + 8) * ld + n);
+      const float4 a3 = *reinterpret_cast<const float4*>(X + (long)(m + 12) * ld + n);
+      s.x += a0.x; s.y += a0.y; s.z += a0.z; s.w += a0.w;
+      s.x += a1.x; s.y += a1.y; s.z += a1.z; s.w += a1.w;
+      s.x += a2.x; s.y += a2.y; s.z += a2.z; s.w += a2.w;
+      s.x += a3.x; s.y += a3.y; s.z += a3.z; s.w += a3.w;
+    }
+    for (; m < m1; m += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(X + (long)m * ld + n);
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && n < N) {
+    const float4 r0 = red[0][tx], r1 = red[1][tx], r2 = red[2][tx], r3 = red[3][tx];
+    float4 o;
+    o.x = ((r0.x + r1.x) + r2.x) + r3.x;
+    o.y = ((r0.y + r1.y) + r2.y) + r3.y;
+    o.z = ((r0.z + r1.z) + r2.z) + r3.z;
+    o.w = ((r0.w + r1.w) + r2.w) + r3.w;
+    *reinterpret_cast<float4*>(part + (long)blockIdx.y * N + n) = o;
+  }
+}
+
 // few partials (a slab of a few hundred rows): one thread per column, partials summed in order, the
 // loads of a partial row coalesced across the threads
 __global__ __launch_bounds__(256) void colsum_final_cols(const float* __restrict__ part, int nparts, int N, float div,
@@ -454,16 +493,29 @@ extern "C" int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long l
   return check_launch("rmsnorm_bwd");
 }
 
-extern "C" size_t ctr_colsum_ws_size(int M, int N) { return (size_t)cdiv(M, 64) * N * sizeof(float); }
+// float4 form: target block count and minimum row chunk (multiple of 16)
+#ifndef COLSUM_V4_BLOCKS
+#define COLSUM_V4_BLOCKS 1024
+#endif
+#ifndef COLSUM_V4_MIN_ROWS
+#define COLSUM_V4_MIN_ROWS 64
+#endif
+
+extern "C" size_t ctr_colsum_ws_size(int M, int N) {
+  return (size_t)cdiv(M, std::min(64, COLSUM_V4_MIN_ROWS)) * N * sizeof(float);
+}
 
 // out[n] = (sum_m X[m, n]) / div   (div = 1 for plain sums, B for torch .mean(dim=0))
 extern "C" int ctr_colsum(const float* X, long ld, int M, int N, float div, float* out, float* ws, void* stream) {
   if (N == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  const int ctiles = cdiv(N, 64);
-  const int rpb = std::min(4096, std::max(64, cdiv((long)M * ctiles, 1024)));   // ~1024 blocks
+  const bool v4 = (N % 4) == 0 && (ld % 4) == 0 && (((uintptr_t)X) & 15) == 0;
+  const int ctiles = cdiv(N, v4 ? 256 : 64);
+  const int rpb = v4 ? std::min(4096, std::max(COLSUM_V4_MIN_ROWS, cdiv((long)M * ctiles, COLSUM_V4_BLOCKS)))
+                     : std::min(4096, std::max(64, cdiv((long)M * ctiles, 1024)));   // ~1024 blocks
   const int np = M > 0 ? cdiv(M, rpb) : 0;
-  if (np > 0) colsum_partial<<<dim3(ctiles, np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
+  if (np > 0 && v4) colsum_partial_v4<<<dim3(ctiles, np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
+  else if (np > 0) colsum_partial<<<dim3(ctiles, np), 256, 0, s>>>(X, ld, M, N, rpb, ws);
   if (np <= 16) colsum_final_cols<<<cdiv(N, 256), 256, 0, s>>>(ws, np, N, div, out);
   else colsum_final<<<N, 64, 0, s>>>(ws, np, N, div, out);
   return check_launch("colsum");
