@@ -10,6 +10,7 @@ Buffer names follow the reference's tensors (see the call-stack comments in each
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -17,6 +18,11 @@ import torch
 from . import _lib
 from ._lib import GemmEpi, call
 from .arch import QUERY_MODES, Arch
+# Side-stream issue order: the main stream's next product is queued before the side stream's grads (its
+# event wait then resolves behind queued main-stream work; 4.82 -> 4.79 ms/step).  CTR_SIDE_ORDER=legacy
+# restores the side-first order for A/B runs.
+_REORDER = os.environ.get("CTR_SIDE_ORDER", "main-first") != "legacy"
+
 from .rng import (SITE_DARE, SITE_EMB, SITE_FC, SITE_FFN0, SITE_MLP0, SITE_QNN, SITE_ATTN0, drop_args)
 
 F32 = 4
@@ -681,8 +687,9 @@ class Engine:
              ptr(att_c), ptr(att_k), ptr(rep_k), st)
         # att and rep contributions share their keys (the top-K tokens): one sort for both, on the side
         # stream beside the context / embedding backward (its inputs are final; its own sort workspace)
-        with self.side():
-            tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
+        if not _REORDER:
+            with self.side():
+                tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
         # ---------------- context / query
         mode = QUERY_MODES[a.query_mode]
         dcat = W.get("dcat", (B, a.Fc, D))
@@ -692,6 +699,9 @@ class Engine:
              B, mode, self.qi, ptr(P["ctx_mlp.0.weight"]), ptr(sv["hq"]), ptr(dq),
              ptr(dxF, cat_off) if a.use_qnn else None, FD, *dk, ptr(dfc), dfc.shape[1] if dfc is not None else 0,
              ptr(dxF, num_off), ptr(dxF, mask_off), ptr(dcat), ptr(dpre), st)
+        if _REORDER:     # the side-stream sort after the main stream's next product is queued
+            with self.side():
+                tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
         if mode != 0:
             self.wgrad(ptr(dpre), D, ptr(sv["ctx"]), a.nctx * D, B, D, a.nctx * D, ptr(G["ctx_mlp.0.weight"]),
                        bias_grad=ptr(G["ctx_mlp.0.bias"]))
@@ -770,9 +780,13 @@ class Engine:
                  ptr(Ls["h1"]), ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D, FF, ptr(P[pre + "ffn.0.weight"]),
                  ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dh1),
                  ptr(slab), ld_sl, *o, ptr(Ls["fwbf"]), self.ffn_flags, st)
-            with self.side():
-                self.colsum(ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
+            slab_sum = (ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
+            if not _REORDER:
+                with self.side():
+                    self.colsum(*slab_sum)
+                slab_sum = None
         else:
+            slab_sum = None
             # x2 = norm2(x1 + ffn(x1))
             dh2 = W.get("dh2", (M, D))
             npart = _lib.query("ctr_rmsnorm_bwd_nparts", M, D)
@@ -800,11 +814,21 @@ class Engine:
         # out_proj
         do = W.get("do", (M, D))
         if self.rowgemm:
-            with self.side():
-                self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
-                                pre + "mha.out_proj.bias", tag=li)
-            self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
+            if slab_sum is not None:     # main-stream product first, then the side stream's slab sums
+                self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
+                with self.side():
+                    self.colsum(*slab_sum)
+                    self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
+                                    pre + "mha.out_proj.bias", tag=li)
+            else:
+                with self.side():
+                    self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
+                                    pre + "mha.out_proj.bias", tag=li)
+                self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
         else:
+            if slab_sum is not None:
+                with self.side():
+                    self.colsum(*slab_sum)
             self.wgrad(ptr(dh1), D, ptr(Ls["o"]), D, M, D, D, ptr(G[pre + "mha.out_proj.weight"]),
                        bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
             self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
@@ -818,6 +842,9 @@ class Engine:
         call("ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale,
              *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
         x_in = sv["xs"][li]
+        if self.rowgemm and _REORDER:     # in_proj input grad queued first, then the side stream's grads
+            self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
+                              add=ptr(dh1))
         with self.side():
             if a.add_pos:
                 call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), self.s())
@@ -826,8 +853,9 @@ class Engine:
                                 pre + "mha.in_proj_bias", tag=li)
         # in_proj
         if self.rowgemm:
-            self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
-                              add=ptr(dh1))
+            if not _REORDER:
+                self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
+                                  add=ptr(dh1))
         else:
             self.wgrad(ptr(dqkv), 3 * D, ptr(x_in), D, M, 3 * D, D, ptr(G[pre + "mha.in_proj_weight"]),
                        bias_grad=ptr(G[pre + "mha.in_proj_bias"]))
