@@ -47,9 +47,14 @@ struct RowGemmArgs {
   float eps;
 };
 
+// row blocks of 16 * NI rows per wave iteration
+#ifndef RG_NI
+#define RG_NI 2
+#endif
+
 template <int K, int N, bool SIDE>
 __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
-  constexpr int KQ = K / 4, NJ = N / 16, NI = 2;
+  constexpr int KQ = K / 4, NJ = N / 16, NI = RG_NI;
   constexpr int NS = SIDE ? NJ : 1;      // per-row epilogue operand (add / residual) slots
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
@@ -215,7 +220,7 @@ static int resident_grid(int M) {
       nb = 1;
     per_cu = std::min(nb, 4);
   }
-  const int nblk = (M + 31) / 32;
+  const int nblk = (M + 16 * RG_NI - 1) / (16 * RG_NI);
   return std::max(1, std::min((nblk + 3) / 4, 256 * per_cu));
 }
 
