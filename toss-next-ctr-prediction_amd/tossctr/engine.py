@@ -842,9 +842,7 @@ class Engine:
         call("ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale,
              *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
         x_in = sv["xs"][li]
-        if self.rowgemm and _REORDER:     # in_proj input grad queued first, then the side stream's grads
-            self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
-                              add=ptr(dh1))
+        # (here the side work goes first: queuing the in_proj input grad ahead of it measured 0.02 ms/step slower)
         with self.side():
             if a.add_pos:
                 call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), self.s())
@@ -853,9 +851,8 @@ class Engine:
                                 pre + "mha.in_proj_bias", tag=li)
         # in_proj
         if self.rowgemm:
-            if not _REORDER:
-                self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
-                                  add=ptr(dh1))
+            self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
+                              add=ptr(dh1))
         else:
             self.wgrad(ptr(dqkv), 3 * D, ptr(x_in), D, M, 3 * D, D, ptr(G[pre + "mha.in_proj_weight"]),
                        bias_grad=ptr(G[pre + "mha.in_proj_bias"]))
