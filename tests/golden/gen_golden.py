@@ -342,7 +342,7 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
 
 
 def tiny_cfg(query_mode="concat", gating="softmax", emb_drop=0.0, aux_w=0.1, qnn=True, tb=True,
-             D=16, K=16, H=4, layers=2, ema=True):
+             D=16, K=16, H=4, layers=2, ema=True, ffn_hidden=48):
     dims = {"c0": 8, "c1": 12, "c2": 16, "c3": 4, "c4": 20}
     cfg = {
         "model": {"emb_dim": D, "embedding_dropout": emb_drop, "cat_embedding_dims": dims, "dare_dropout": 0.2,
@@ -350,7 +350,7 @@ def tiny_cfg(query_mode="concat", gating="softmax", emb_drop=0.0, aux_w=0.1, qnn
                                 "mlp_hidden": [32, 16], "dropout": 0.2, "use_se": True, "se_reduction": 4,
                                 "use_residual": True, "norm": "rms", "pair_grouping": "all",
                                 "aux_head_weight": aux_w}},
-        "sequence": {"tfm": {"n_layers": layers, "n_heads": H, "mha_dropout": 0.1, "ffn_hidden": 48,
+        "sequence": {"tfm": {"n_layers": layers, "n_heads": H, "mha_dropout": 0.1, "ffn_hidden": ffn_hidden,
                              "ffn_dropout": 0.1, "norm": "rms", "gating": gating, "add_positional_bias": True},
                      "query_mode": query_mode, "transformer_block": tb, "top_k": K, "recency_tau": 16,
                      "pad_id": 0, "query_key": "c1"},
@@ -378,6 +378,15 @@ def k148_cfg():
     cfg["sequence"]["tfm"]["n_layers"] = 1
     cfg["model"]["qnn_alpha"]["mlp_hidden"] = [64, 32]
     return cfg, list(c["data"]["cat_cols"])
+
+
+def cfg4_full_cfg():
+    """cfgs/v3_k148_s1.yaml as-is (BASELINE config 4): D = 64, L = 400, K = 148, 4 encoder layers, S1, the
+    full QNN head (MLP 13952 -> 512 -> 256 -> 1), EMA off."""
+    import yaml
+    c = yaml.safe_load(open(os.path.join(REF, "cfgs/v3_k148_s1.yaml")))
+    cfg = {"model": copy.deepcopy(c["model"]), "sequence": copy.deepcopy(c["sequence"])}
+    return cfg, list(c["data"]["cat_cols"]), len(c["data"]["num_cols_explicit"])
 
 
 def cfg3_cfg():
@@ -480,6 +489,9 @@ def main():
     if "--bf16-only" in sys.argv:
         gen_bf16()
         return
+    if "--r3" in sys.argv:
+        gen_r3()
+        return
     tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
     cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
     run_case("tiny_concat", tiny_cfg(), B=64, L=32, vocab=5000, Fn=6, Fm=6, cat_cards=cards, steps=3,
@@ -509,6 +521,27 @@ def main():
              steps=2, pseed=51, bseed=800, store_params=False, train_cfg=big_tr)
     gen_infer()
     gen_bf16()
+    gen_r3()
+
+
+def gen_r3():
+    """Round-3 cases: BASELINE config 4 at its true lengths (L = 400, K = 148, D = 64, 4 layers, every
+    categorical and numeric column of the yaml) in fp32 and amp bf16; config 3 (K = 100, S1) in amp bf16;
+    and a two-layer encoder whose FFN width (40) is not a multiple of 16, so the FFN runs as separate
+    GEMMs + RMSNorm backwards instead of the fused kernel."""
+    big_tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=0, epochs=8)
+    cfg4, cols4, nnum = cfg4_full_cfg()
+    kw4 = dict(B=3, L=400, vocab=2000, Fn=nnum, Fm=nnum, cat_cards={c: 100 for c in cols4}, steps=2, pseed=61,
+               bseed=900, store_params=False, train_cfg=big_tr)
+    run_case("cfg4_full", cfg4, **kw4)
+    run_case("cfg4_full_bf16", cfg4, **kw4, amp_twin="cfg4_full")
+    cfg3, cols3 = cfg3_cfg()
+    run_case("cfg3_dims_bf16", cfg3, B=8, L=100, vocab=3000, Fn=82, Fm=82, cat_cards={c: 200 for c in cols3},
+             steps=2, pseed=41, bseed=700, store_params=False, train_cfg=big_tr, amp_twin="cfg3_dims")
+    tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
+    cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
+    run_case("tiny_ffn40", tiny_cfg(D=32, H=4, ffn_hidden=40), B=40, L=28, vocab=3000, Fn=5, Fm=5,
+             cat_cards=cards, steps=2, pseed=15, bseed=1000, store_params=True, train_cfg=tr)
 
 
 def gen_bf16():

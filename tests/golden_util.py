@@ -11,10 +11,11 @@ from oracle import synth
 from oracle.model import make_arch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = ["tiny_concat", "tiny_s1_relu", "tiny_s2", "base_fc", "cfg2_dims", "cfg3_dims", "k148", "k120"]
+CASES = ["tiny_concat", "tiny_s1_relu", "tiny_s2", "base_fc", "cfg2_dims", "cfg3_dims", "k148", "k120", "cfg4_full",
+         "tiny_ffn40"]
 # amp: bf16 twins (gen_golden.gen_bf16): the reference under torch.autocast(bfloat16) on the inputs,
 # seeds and parameters of the fp32 fixture named in meta["twin"]
-BF16_CASES = ["tiny_concat_bf16", "cfg2_dims_bf16", "k148_bf16"]
+BF16_CASES = ["tiny_concat_bf16", "cfg2_dims_bf16", "cfg3_dims_bf16", "k148_bf16", "cfg4_full_bf16"]
 BF16_BAND = 3.0      # bf16 tolerance: within 3x the reference's own bf16-vs-fp32 deviation ...
 BF16_FLOOR = 1e-4    # ... or 1e-4 of the tensor's norm, whichever is larger
 # scalars (loss, grad norm): one draw of the bf16 rounding says little about its spread, so the floor is
@@ -179,7 +180,7 @@ def _exact_subset(fx, name):
     return idx, vals
 
 
-def check_bf16_band(fx16, fx32, name, got, label=None, update=False):
+def check_bf16_band(fx16, fx32, name, got, label=None, update=False, p0=None):
     """amp: bf16 parity.  ``got`` (the build under amp: bf16) is compared with the reference run under
     autocast(bfloat16) (``fx16``) and in fp32 (``fx32``, the twin fixture): the norm of the difference
     to EACH must stay within BF16_BAND x the reference's own bf16-vs-fp32 deviation, or BF16_FLOOR of
@@ -208,6 +209,14 @@ def check_bf16_band(fx16, fx32, name, got, label=None, update=False):
         # bf16 noise of 0 steps either way, and one such flip moves a small tensor's update (or its EMA
         # shadow's) by up to twice its largest element
         floor = max(floor, 2.0 * max(float(np.abs(r16).max(initial=0)), float(np.abs(r32).max(initial=0))))
+    if update and p0 is not None:
+        # an update pT - p0 (or the EMA shadow's) carries the fp32 rounding of the result itself: 2 ulps per
+        # element, as the fp32 checks allow (Fixture.check_update).  Where the reference's bf16 and fp32 runs
+        # round alike (band 0: a parameter without gradient, whose EMA shadow d s + (1 - d) p drifts by
+        # rounding alone) this is the whole tolerance
+        p0 = np.asarray(p0.detach().cpu().double().numpy() if isinstance(p0, torch.Tensor) else p0, np.float64).ravel()
+        p0s = p0 if idx is None else p0[idx]
+        floor += float(np.linalg.norm(2.0 * np.spacing(np.abs(p0s + r32).astype(np.float32)).astype(np.float64)))
     tol = BF16_BAND * band + floor + 1e-30
     e16, e32 = float(np.linalg.norm(g - r16)), float(np.linalg.norm(g - r32))
     assert e16 <= tol and e32 <= tol, (

@@ -65,6 +65,11 @@ def test_rank_slices_cover_epoch_once(n, world):
         if step < steps - 1:
             assert sizes == [bs] * world
     assert sorted(seen) == list(range(n))
+    # the gradient average of each step runs over exactly the ranks that hold rows
+    from tossctr.train import step_contributors
+    for step in range(steps):
+        assert step_contributors(n, bs, world, step) == sum(rank_slice(n, bs, world, r, step)[1] > 0
+                                                            for r in range(world))
     if world == 1:
         assert [rank_slice(n, bs, 1, 0, s) for s in range(steps)] == \
             [(s * bs, min(bs, n - s * bs)) for s in range(steps)]

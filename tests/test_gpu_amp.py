@@ -84,14 +84,14 @@ def test_bf16_fused_steps_within_band(case):
                         f"{case} gnorm {t}")
     sd = model.state_dict()
     for k, v in sd.items():
-        check_bf16_band(f16, f32, f"dT/{k}", v.double().cpu() - p0[k], update=True)
+        check_bf16_band(f16, f32, f"dT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k])
     ar = model.arena
     for k in m["grad_keys"]:
         check_bf16_band(f16, f32, f"mT/{k}", ar._view(opt.m, k))
         check_bf16_band(f16, f32, f"vT/{k}", ar._view(opt.v, k))
     if ema is not None:
         for k, v in ema.shadow_params().items():
-            check_bf16_band(f16, f32, f"demaT/{k}", v.double().cpu() - p0[k], update=True)
+            check_bf16_band(f16, f32, f"demaT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k])
 
 
 def test_bf16_differs_from_fp32_build():

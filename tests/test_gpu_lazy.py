@@ -93,3 +93,36 @@ def test_lazy_state_dict_flushes():
         assert torch.equal(sd_d[k], sd_l[k]), k
     assert ol._flushed_tick == ol.tick == 3
     np.testing.assert_array_equal(ol.last.cpu().numpy() & 0x7FFFFFFF, 3)    # bit 31: row took a grad tick
+
+
+def test_touch_first_chunk_full_class_plus_hot_row():
+    """lazy_touch_pair_cls_kernel's first chunk of TOUCH_CH = 256 token positions: all 256 distinct rows
+    claimed into one class list (rows that took a gradient tick) while the hot (padding) row joins the same
+    class -- 257 entries.  The padding row's state word is given the has-grad bit by hand (its moments are
+    zero, so the full replay is bit-identical to the short one).  Lazy must still equal dense bitwise."""
+    from tossctr import FusedAdamW
+    fx = Fixture("tiny_concat")
+    m, tr = fx.meta, fx.meta["train"]
+    vocab = int(m["vocab"]) * 4
+    cards = dict(fx.cat_cards)
+    md, ml = _models(fx, vocab, cards)
+    od = FusedAdamW(md, lr=1e-3, weight_decay=tr["wd"], max_grad_norm=tr["clip"], lazy=False)
+    ol = FusedAdamW(ml, lr=1e-3, weight_decay=tr["wd"], max_grad_norm=tr["clip"], lazy=True)
+    L = int(m["L"])
+    assert 8 * L == 256
+    toks = np.random.default_rng(5).choice(np.arange(1, vocab), 8 * L, replace=False).astype(np.int32)
+    batches = []
+    for t in range(4):
+        b = make_batch(16, m["Fn"], m["Fm"], list(cards.values()), L, vocab, seed=300 + t)
+        if t in (0, 2):            # tick 1 steps the 256 tokens (every history position takes an att grad);
+            b["seq"][:8] = toks.reshape(8, L)     # tick 3 reads them again first: 256 distinct class-1 rows
+        batches.append(b)
+    for t, b in enumerate(batches):
+        for model, opt in ((md, od), (ml, ol)):
+            if t == 2 and opt is ol:
+                ol.last[0] |= np.int32(-2 ** 31)      # the hot row in the has-grad class as well
+            model.train_step(model.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda(), opt, t + 1,
+                             seed=(3 << 32) | t)
+    ml.sync()
+    assert torch.equal(md.arena.buf, ml.arena.buf)
+    assert torch.equal(od.m, ol.m) and torch.equal(od.v, ol.v)

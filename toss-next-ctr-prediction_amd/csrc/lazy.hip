@@ -758,8 +758,9 @@ __global__ __launch_bounds__(256) void lazy_touch_pair_cls_kernel(const ctr_lazy
                                                                   const int32_t* __restrict__ X, long n, int hot,
                                                                   float* P, float* M, float* V, float* E,
                                                                   const OptScalars* __restrict__ hist, int tick) {
-  __shared__ int lrow[2][TOUCH_CH];
-  __shared__ int ls[2][TOUCH_CH];
+  // TOUCH_CH + 1: in the first chunk the hot row can join TOUCH_CH distinct claimed rows of the same class
+  __shared__ int lrow[2][TOUCH_CH + 1];
+  __shared__ int ls[2][TOUCH_CH + 1];
   __shared__ int cnt[2];
   const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
   const int tid = threadIdx.x;

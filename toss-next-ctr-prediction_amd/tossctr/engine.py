@@ -806,8 +806,9 @@ class Engine:
                        bias_grad=ptr(G[pre + "ffn.0.bias"]))
             self.gemm(M, D, FF, ptr(dact), FF, 0, ptr(P[pre + "ffn.0.weight"]), D, 0, ptr(dx1), D,
                       GemmEpi(add=ptr(dh2), ld_add=D))
-            # x1 = norm1(x + attn(x))
-            dh1 = W.get("dh1", (M, D))
+            # x1 = norm1(x + attn(x)); per layer: the side stream's out_proj weight grad reads it while the
+            # next layer's backward runs on the main stream
+            dh1 = W.get(f"dh1_{li}", (M, D))
             call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,
                  ptr(dh1), D, None, 0, ptr(dwp), st)
             self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))

@@ -151,6 +151,7 @@ class FusedAdamW:
         self.ema = ema
         self.pg = process_group
         self.world = 1
+        self.contributors = None    # ranks contributing to the current step's gradient (None: all)
         if process_group is not None:
             import torch.distributed as dist
             self.world = dist.get_world_size(process_group)
@@ -382,7 +383,10 @@ class FusedAdamW:
         if self.shards is not None:     # each rank holds its own rows' grads: sum the table partials
             from . import dist as D
             D.allreduce_sum_(parts[n:], self.pg)
-        call("ctr_clip_finalize", ptr(parts), 4 * n, self.max_grad_norm, 1.0 / self.world, ptr(self.norm_out), st)
+        # the DDP mean over the ranks that hold rows this step (all of them except on an epoch's short last
+        # step, where tossctr.train.rank_slice leaves some ranks empty: their zero gradients do not count)
+        div = self.world if self.contributors is None else self.contributors
+        call("ctr_clip_finalize", ptr(parts), 4 * n, self.max_grad_norm, 1.0 / div, ptr(self.norm_out), st)
         return self.norm_out
 
     # -------------------------------------------------------------- data parallel

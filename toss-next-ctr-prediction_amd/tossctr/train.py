@@ -156,6 +156,12 @@ def rank_slice(n, bs, world, rank, step):
     return lo + rank * base + min(rank, extra), base + (1 if rank < extra else 0)
 
 
+def step_contributors(n, bs, world, step):
+    """How many ranks hold rows at ``step`` (rank_slice): all of them except on a short last step with
+    fewer rows than ranks.  The all-reduced gradient is averaged over these."""
+    return max(1, min(world, n - step * bs * world))
+
+
 def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None, device=None):
     """src/train.py:92-317 (same signature + optional pre-staged ``store``). Returns (best_state, best_score)."""
     from .configs import cat_cardinals  # noqa: F401
@@ -203,7 +209,11 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
             inputs, y = store.batch(idx)
             opt.param_groups[0]["lr"] = cosine_warmup_lr(epoch - 1, step, steps_per_epoch, cfg["train"]["lr"], warmup,
                                                          epochs)
-            loss_sum += model.train_step(inputs, y, opt, global_step=global_step, contribute=n_rows > 0)[0]
+            # DDP semantics per replica: the mean of the per-rank gradients over the ranks that
+            # hold rows -- on the short last step a rank without rows does not dilute the average
+            n_contrib = step_contributors(len(idx_tr), bs, world, step)
+            loss_sum += model.train_step(inputs, y, opt, global_step=global_step, contribute=n_rows > 0,
+                                         contributors=n_contrib if n_contrib < world else None)[0]
         tr_loss = float(loss_sum.item()) / max(1, steps_per_epoch)
         use_ema_eval = ema is not None and cfg["ema"].get("eval_with_ema", True)
         if use_ema_eval:

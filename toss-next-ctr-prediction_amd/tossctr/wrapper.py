@@ -218,12 +218,14 @@ class CTRModel(nn.Module):
         return logits.clone(), prob.clone(), aux.clone()
 
     # ------------------------------------------------------------------ fused training step
-    def train_step(self, inputs, y, opt, global_step, seed=None, contribute=True):
+    def train_step(self, inputs, y, opt, global_step, seed=None, contribute=True, contributors=None):
         """One reference step (src/train.py:152-199): forward -> bce_wll_style(+aux) -> backward ->
         clip -> AdamW -> EMA, all on device, no host sync.  ``inputs`` = staged (X_num, X_mask, X_cat,
         seq) device tensors (see ``stage``), ``y`` float labels on device.  Returns the loss (device).
         ``contribute=False`` (data parallel: a rank without rows on an epoch's last step) runs the step
-        with a zero loss gradient, so the rank joins the collectives but adds nothing to the gradient."""
+        with a zero loss gradient, so the rank joins the collectives but adds nothing to the gradient;
+        ``contributors`` = how many ranks hold rows this step (the all-reduced gradient is averaged over those,
+        not over the whole world; None: every rank)."""
         seed = self.next_seed() if seed is None else seed
         eng = self.engine
         _, _, _, sv = eng.forward(*inputs, training=True, seed=seed, save=True)
@@ -234,7 +236,11 @@ class CTRModel(nn.Module):
             if daux is not None:
                 daux.zero_()
         tg = eng.backward(sv, dz, daux)
-        opt.step(tg, global_step)
+        opt.contributors = contributors
+        try:
+            opt.step(tg, global_step)
+        finally:
+            opt.contributors = None
         return loss
 
     def stage(self, batch):
