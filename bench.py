@@ -73,12 +73,22 @@ PROFILE_STEPS = 5       # untimed steps after the timed region that fill the per
 
 def kernel_work(name, a, B, ffn_M):
     """(bound, algorithmic units per launch, unit) of the timed entry points -- SURVEY §8(d) per-unit
-    figures x the units one launch processes ("Roofline accounting")."""
+    figures x the units one launch processes ("Roofline accounting").
+    FFN: the four products (8 FF D flop per row backward, 4 forward; the backward's pre-activation
+    recompute not counted).  Attention core (src/models/dare.py:39-70, MHA over K candidates, dh = D / H):
+    per (sample, head) QK^T and PV = 4 K^2 dh flop forward; dP = dO V^T, dV = P^T dO, dQ = dS K,
+    dK = dS^T Q = 8 K^2 dh backward (the score recompute not counted), on the fp32 vector units (dh = 4 / 8
+    is too thin for MFMA tiles) -> priced against the fp32 vector peak."""
     D, FF = a.D, a.ffn_hidden
     if name in ("ctr_ffn_bwd", "ctr_ffn_bwd_norms"):     # dfo = dh W2, dW2 = dh^T fo, dW1 = dact^T x, dx = dact W1 (pre recompute excluded)
         return "mfma", 8.0 * ffn_M * FF * D, "flop"
     if name == "ctr_ffn_fwd":     # pre = x W1^T, y = fo W2^T
         return "mfma", 4.0 * ffn_M * FF * D, "flop"
+    K = ffn_M // max(1, B)
+    if name == "ctr_attn_fwd":
+        return "valu", 4.0 * B * K * K * D, "flop"
+    if name == "ctr_attn_bwd":
+        return "valu", 8.0 * B * K * K * D, "flop"
     return None
 
 
@@ -184,7 +194,7 @@ def opt_algorithmic_bytes(opt, with_ema):
     return b
 
 
-PMC_ROUNDS = ("r02", "r01")      # newest committed PMC summaries first
+PMC_ROUNDS = ("r03", "r02", "r01")      # newest committed PMC summaries first
 
 
 def pmc_traffic(name):
@@ -193,8 +203,10 @@ def pmc_traffic(name):
     corrected as MI355X_MICROARCH.md prescribes (gfx950 FETCH_SIZE counts half of wide streaming reads:
     x2).  None when the summaries are absent."""
     import csv
-    bwd = ("ffn_bwd_bf_kernel", "ffn_bwd_cols_kernel", "ffn_bwd_kernel")   # the entry point's kernels, preferred first
-    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bf_kernel", "ffn_fwd_kernel")}.get(name)
+    bwd = ("ffn_bwd_own_kernel", "ffn_bwd_bf_kernel", "ffn_bwd_cols_kernel", "ffn_bwd_kernel")   # preferred first
+    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bf_kernel", "ffn_fwd_kernel"),
+             "ctr_attn_bwd": ("attn_bwd_wave_kernel", "attn_bwd_kernel"),
+             "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel")}.get(name)
     if kerns is None:
         return None
     base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS
@@ -256,6 +268,7 @@ def cpu_baseline(cfg, B, L, seed=0, timed=3):
             t.uniform_(-0.05, 0.05, generator=gen)
         P[k] = t
     st = TrainState(P, A, 3e-4, 1e-4, 0.5, ema_cfg=cfg["ema"])
+    st.native_dropout = True     # torch's bernoulli dropout, as the reference draws it (the cost, not the masks)
     del P
     batches = synth_batches(1 + timed, B, L, N_NUM_NEXT, N_NUM_NEXT, list(cards.values()), 10_000_000, "cpu",
                             seed + 1)
@@ -269,7 +282,8 @@ def cpu_baseline(cfg, B, L, seed=0, timed=3):
     t = float(np.median(times[1:]))
     return {"value": round(B / t, 2), "unit": "samples/s", "cores": torch.get_num_threads(), "kind": "port",
             "cpu": cpu_model(),
-            "sample": f"oracle fp32 train step (fwd+bwd+clip+AdamW+EMA, 1.24B params) at bs={B}, L={L}: "
+            "sample": f"oracle fp32 train step (fwd+bwd+clip+AdamW+EMA, 1.24B params; torch bernoulli dropout "
+                      f"as the reference; tools/cpu_calibrate.py) at bs={B}, L={L}: "
                       f"1 warm-up + {timed} timed steps, median {t:.1f} s "
                       f"({', '.join(f'{x:.1f}' for x in times[1:])} s)"}
 
@@ -356,8 +370,8 @@ def main():
     # HIP events cost host time per bracketed call (~0.1 ms per step for the whole list below when the step is
     # host-issue sensitive), so the timed steps bracket only the roofline candidates (the kernels with an
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
-    roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd")
-    timed = roof_timed + ("ctr_attn_bwd", "ctr_attn_fwd", "ctr_lazy_flush", "ctr_lazy_flush_pair",
+    roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd")
+    timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
                           "ctr_adamw_ema", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
     if args.kernel_events == "all":
@@ -420,15 +434,29 @@ def main():
                 continue
             bound, work, unit = w
             ach = work / (kstats_timed[n][1] * 1e-3) / 1e12
-            # amp bf16: the FFN kernels' products run on bf16 MFMA -> priced against the bf16 dense peak
+            # amp bf16: the FFN kernels' products run on bf16 MFMA -> priced against the bf16 dense peak; the
+            # attention core runs on the fp32 vector units (its peak = the fp32 rate, 157.3 TF)
             bf = args.amp == "bf16" and n.startswith("ctr_ffn") and model.engine.ffn_flags
             peak = MFMA_BF16_PEAK_TFS if bf else MFMA_F32_PEAK_TFS
             roof = {"bound": bound, "kernel": n, "achieved": round(ach, 2), "peak": round(peak, 1),
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4), "mfma_dtype": "bf16" if bf else "f32",
+                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                    "mfma_dtype": None if bound == "valu" else "bf16" if bf else "f32",
                     "traffic": pmc_traffic(n) if args.config == "cfg2" else None, "work_per_launch": work,
                     "work_unit": unit,
                     "avg_launch_ms": round(kstats_timed[n][1], 4), "ms_per_step": round(per_step_t[n], 4),
                     "share_of_step": round(per_step_t[n] / ms, 4), "timing": "HIP events in the timed steps"}
+            # every priced kernel of the timed steps, dominant first (the roofline object is the first)
+            roof["priced"] = {}
+            for m_ in sorted(per_step_t, key=per_step_t.get, reverse=True):
+                w_ = kernel_work(m_, a, args.batch, ffn_M)
+                if w_ is None:
+                    continue
+                bf_ = args.amp == "bf16" and m_.startswith("ctr_ffn") and model.engine.ffn_flags
+                pk_ = MFMA_BF16_PEAK_TFS if bf_ else MFMA_F32_PEAK_TFS
+                a_ = w_[1] / (kstats_timed[m_][1] * 1e-3) / 1e12
+                roof["priced"][m_] = {"bound": w_[0], "ms_per_step": round(per_step_t[m_], 4),
+                                      "avg_launch_ms": round(kstats_timed[m_][1], 4), "achieved": round(a_, 2),
+                                      "peak": round(pk_, 1), "frac": round(a_ / pk_, 4)}
             break
         rec = {
             "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref"

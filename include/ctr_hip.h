@@ -198,7 +198,7 @@ int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K
  * (nullable in an inference-only forward; ignored without the flag)                                    */
 #define CTR_FFN_BF16 1
 int ctr_ffn_supported(int D, int FF, int flags);   /* fp32: D in {16, 32, 64}, FF % 16 == 0 */
-int ctr_ffn_slab_rows(int M, int D, int flags);    /* workgroups of ctr_ffn_bwd = rows of its grad slab */
+int ctr_ffn_slab_rows(int M, int D, int FF, int flags);   /* workgroups of ctr_ffn_bwd = rows of its grad slab */
 int ctr_ffn_mask_words(int M, int FF);         /* uint32 words of the dropout keep-bit mask (16 bits per 16 cols) */
 /* y = norm_w * h * r, h = x + (gelu(x W1^T + b1) [dropout] W2^T + b2), r = 1/rms(h).  mask (nullable
  * without dropout) receives the keep bits, chunk-major (FF/16, M) uint16.                           */

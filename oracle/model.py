@@ -39,15 +39,20 @@ def site_ffn(i):
 
 @dataclass
 class Dropper:
-    """Applies reference-style dropout ``x * (mask / (1-p))`` with hash masks."""
+    """Applies reference-style dropout ``x * (mask / (1-p))`` with hash masks.  ``native``: torch's own
+    ``F.dropout`` (bernoulli_ masks, the reference's exact op) -- for TIMING the CPU baseline only, where
+    the masks' values do not matter but their cost does (tools/cpu_calibrate.py)."""
     seed: int
     training: bool = True
     double: bool = False
     record: dict = field(default_factory=dict)
+    native: bool = False
 
     def __call__(self, site: int, x: torch.Tensor, p: float) -> torch.Tensor:
         if not self.training or p <= 0.0:
             return x
+        if self.native:
+            return F.dropout(x, p, training=True)
         keep = torch.from_numpy(rng.keep_mask(self.seed, site, p, tuple(x.shape)))
         self.record[site] = keep
         noise = keep.to(x.dtype) / (1.0 - p)            # _dropout_impl: bernoulli_(1-p).div_(1-p)
@@ -364,9 +369,11 @@ class TrainState:
         self.ema_n = 0
         self.shadow = {k: v.detach().clone() for k, v in self.P.items()} if ema_cfg else None
 
+    native_dropout = False      # cpu baseline timing: torch's bernoulli dropout (Dropper.native)
+
     def grads(self, batch, y, seed, record=None):
         """forward -> loss (+aux) -> backward on one batch (src/train.py:158-192): (loss, outputs, grads)."""
-        drop = Dropper(seed, training=True)
+        drop = Dropper(seed, training=True, native=self.native_dropout)
         for p in self.P.values():
             p.grad = None
         logits, prob, aux = forward(self.P, batch, self.A, drop, record=record)

@@ -55,14 +55,40 @@ def thresh16(p: float) -> int:
     return min(1 << 16, max(1, int(round(float(p) * (1 << 16)))))
 
 
+_POOL = None
+
+
+def _pool():
+    global _POOL
+    if _POOL is None:
+        import concurrent.futures
+        import os
+        _POOL = concurrent.futures.ThreadPoolExecutor(max_workers=os.cpu_count() or 1)
+    return _POOL
+
+
 def keep_mask(seed: int, site: int, p: float, shape) -> np.ndarray:
-    """Boolean keep-mask over a tensor of ``shape`` indexed by its C-order linear index."""
+    """Boolean keep-mask over a tensor of ``shape`` indexed by its C-order linear index: one hash per
+    element pair (2k, 2k+1), the low half for the even element and the high half for the odd one.  Large
+    masks are hashed in chunks on a thread pool (numpy's ufunc loops release the GIL), so the CPU baseline
+    that times the oracle's train step is not bound by a single-threaded mask generator."""
     n = int(np.prod(shape))
     key = np.uint32(site_key(seed, site))
-    idx = np.arange(n, dtype=np.uint32)
-    b = mix32_np((idx >> np.uint32(1)) ^ key)
-    u = np.where((idx & np.uint32(1)) != 0, b >> np.uint32(16), b & np.uint32(0xFFFF))
-    return (u >= np.uint32(thresh16(p))).reshape(shape)
+    thr = np.uint32(thresh16(p))
+    npair = (n + 1) // 2
+    out = np.empty(2 * npair, dtype=bool)
+
+    def work(lo, hi):
+        b = mix32_np(np.arange(lo, hi, dtype=np.uint32) ^ key)
+        out[2 * lo:2 * hi:2] = (b & np.uint32(0xFFFF)) >= thr
+        out[2 * lo + 1:2 * hi:2] = (b >> np.uint32(16)) >= thr
+
+    CH = 1 << 20
+    if npair <= CH:
+        work(0, npair)
+    else:
+        list(_pool().map(lambda lo: work(lo, min(npair, lo + CH)), range(0, npair, CH)))
+    return out[:n].reshape(shape)
 
 
 def dropout_scale(p: float) -> np.float32:

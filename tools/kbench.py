@@ -68,7 +68,7 @@ def main():
         ld = (o_w2 + D * FF + 3) // 4 * 4
         fl = 1 if args.bf16 else 0
         wbf = torch.empty(3 * FF * D, dtype=torch.bfloat16, device="cuda") if fl else None
-        nb = _lib.query("ctr_ffn_slab_rows", M, D, fl)
+        nb = _lib.query("ctr_ffn_slab_rows", M, D, FF, fl)
         slab = torch.zeros(nb, ld, device="cuda")
         fwd = lambda: call("ctr_ffn_fwd", ptr(x), M, D, FF, ptr(W1), ptr(b1), ptr(W2), ptr(b2), ptr(nw), 1e-6, 12345,
                            thr, 1.0 / 0.9, ptr(mask), ptr(y), ptr(h), ptr(r), ptr(wbf), fl, st)

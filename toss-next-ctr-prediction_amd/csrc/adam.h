@@ -52,7 +52,11 @@ inline OptScalars make_opt_scalars(float lr, float wd, float beta1, float beta2,
   return s;
 }
 
+// `#pragma clang fp contract(off)` in every element function: a caller's g = grad * coef would otherwise be
+// fused into `g - m` after inlining (fma(grad, coef, -m)) in one caller and not in another, and the dense
+// stream and the lazy replay would round m differently -- the explicit fmaf calls are the only fusions.
 __device__ __forceinline__ void adam_elem(const OptScalars& s, float& p, float& m, float& v, float g) {
+#pragma clang fp contract(off)
   p = p * s.decay_mul;                                  // param.mul_(1 - lr*wd)
   m = fmaf(s.b1w, g - m, m);                            // exp_avg.lerp_(grad, 1-beta1)
   v = fmaf(s.omb2 * g, g, v * s.b2);                    // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
@@ -61,6 +65,7 @@ __device__ __forceinline__ void adam_elem(const OptScalars& s, float& p, float& 
 }
 
 __device__ __forceinline__ void ema_elem(const OptScalars& s, float p, float& e) {
+#pragma clang fp contract(off)
   e = fmaf(e, s.ema_d, s.ema_omd * p);                  // shadow.mul_(d).add_(p, alpha=1-d)
 }
 
@@ -74,6 +79,7 @@ __device__ __forceinline__ void adam_ema_elem(const OptScalars& s, float& p, flo
 // fmaf(b1w, 0 - m, m) == fmaf(b1w, -m, m) (the two differ only in the sign of a zero product, which
 // the addend absorbs) and fmaf(omb2 * 0, 0, v * b2) == v * b2 (v >= 0).
 __device__ __forceinline__ void idle_adam_elem(const OptScalars& s, float& p, float& m, float& v) {
+#pragma clang fp contract(off)
   p = p * s.decay_mul;
   m = fmaf(s.b1w, -m, m);
   v = v * s.b2;
@@ -89,6 +95,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 splat2(float a) { return f32x2{a, a}; }
 
 __device__ __forceinline__ void idle_adam_pk(const OptScalars& s, f32x2& p, f32x2& m, f32x2& v) {
+#pragma clang fp contract(off)
   p = p * splat2(s.decay_mul);
   m = __builtin_elementwise_fma(splat2(s.b1w), -m, m);
   v = v * splat2(s.b2);
@@ -99,6 +106,7 @@ __device__ __forceinline__ void idle_adam_pk(const OptScalars& s, f32x2& p, f32x
 }
 
 __device__ __forceinline__ void ema_pk(const OptScalars& s, f32x2 p, f32x2& e) {
+#pragma clang fp contract(off)
   e = __builtin_elementwise_fma(e, splat2(s.ema_d), splat2(s.ema_omd) * p);
 }
 

@@ -20,6 +20,8 @@
 // Weight / bias grads go to a per-workgroup slab row (rows-per-wave form: the four waves' partials summed
 // in a fixed order per chunk; column-owner form: complete per wave); ctr_colsum (rowops.hip) reduces the
 // slabs in a fixed order -- deterministic.
+#include <cstdlib>
+
 #include "common.h"
 #include "ctr_hip.h"
 
@@ -64,6 +66,7 @@ struct FfnArgs {
   const float* nw1;
   float* dh1;          // (M, D) output: grad wrt h1
   __bf16* wbf;         // amp bf16: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF) in bf16, written by the forward
+  int dbg;             // column-owner backward debug dumps (CTR_FFN_DEBUG), 0 = off
 };
 
 template <int D>
@@ -823,6 +826,7 @@ __global__ __launch_bounds__(256) void ffn_bwd_cols_kernel(FfnArgs a) {
 // workgroup instead of one per tile -- deterministic.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int D>
@@ -1294,6 +1298,451 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
   }
 }
 
+// ---------------------------------------------------------------- amp: bf16, column-owner persistent backward
+// One 512-thread workgroup per CU walks a contiguous range of 32-row steps.  Wave w OWNS the FF columns
+// [16 NT w, 16 NT (w + 1)) (FF = 128 NT) for the whole launch: its dW1 / dW2 / db1 slices are complete over
+// every row the workgroup visits in that wave's registers and are written ONCE, at the end, to the
+// workgroup's slab row (no per-tile slab read-modify-write), and its weight operands stay in registers.
+// The price is the dx = dact W1 contraction over FF, split over the eight waves: each writes its partial
+// for the step's 32 rows to an LDS exchange slot and, after the step's single barrier, every wave sums
+// the eight partials of its own four rows in a fixed order (deterministic) and runs the norm1 backward.
+// Per step a wave loads / prepares four rows of the NEXT step (norm2 backward of dy, bf16 images of x and
+// dh, keep words) while the current step's images are read: images triple-buffered, exchange double-
+// buffered, so one barrier per step orders everything.
+// Products (v_mfma_f32_16x16x32_bf16; the odd tile of the dx contraction on 16x16x16):
+//   pre / dfo = x W1^T / dh W2 (rows on the accumulator's row axis, ff on its column axis);
+//   dW1[ff][d] += dact^T x and dW2[d][ff] += dh^T fo over the step's rows, the row k-set of lane group g
+//   being rows {4g..4g+3} of both 16-row blocks -- dact / fo straight from the accumulator registers,
+//   x / dh from the images by transposed reads (ds_read_b64_tr_b16);
+//   dx += dact W1: dact through a wave-private [ff][row] staging image, read back transposed.
+template <int D, int NT>
+struct FfnOwn {
+  static constexpr int NW = 8;                  // waves per workgroup
+  static constexpr int SR = 32;                 // rows per step
+  static constexpr int KH = D / 32, NJ = D / 16, NP = NT / 2;
+  static constexpr int VPL = D / 16;            // loader / epilogue: floats of a row per lane (16 lanes a row)
+  static constexpr int FF = 128 * NT;
+  static constexpr int NCH = FF / 32;           // 32-column keep-word chunks (<= 16: one word per lane)
+  static constexpr int XRS = D == 32 ? 96 : 160;   // bytes per row of the bf16 x / dh images (conflict-free
+                                                   // ds_read_b128 rows and transposed 4-row reads)
+  static constexpr int O_XB = 0, O_HB = SR * XRS, O_KB = 2 * SR * XRS;
+  static constexpr int IMG = 2 * SR * XRS + NCH * SR * 4;
+  static constexpr int XCS = D + 4;             // floats per exchange row: 4 XCS = 16 mod 32 banks
+  static constexpr int XSLOT = SR * XCS * 4;
+  static constexpr int XCH = NW * XSLOT;
+  static constexpr int S4 = 24;                 // dwords per staging row ([ff][32 rows] bf16, swizzled)
+  static constexpr int STG = 16 * NT * S4 * 4;
+  static constexpr int O_XCH = 3 * IMG, O_STG = O_XCH + 2 * XCH;
+  static constexpr int LDS = O_STG + NW * STG;
+  static_assert(NCH <= 16 && LDS <= 160 * 1024, "FfnOwn: shape");
+};
+
+// staging image byte offset of (ff row, 4 rows from rowM): dword (rowM / 2) ^ f(ff) -- 8-byte stores of
+// four rows and the transposed reads of the dx A operand without bank conflicts on the stores and <= 2-way
+// on the reads
+__device__ __forceinline__ int own_stg(int ffl, int rowM) {
+  const int f = (((ffl >> 2) & 1) << 1) ^ (((ffl >> 3) & 1) << 2);
+  return ffl * (24 * 4) + ((((rowM >> 1)) ^ f) << 2);
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16k(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c,
+                                                   0, 0, 0);
+}
+
+template <int N>
+struct fvec {
+  float v[N];
+};
+// Row segments are read with plain global loads behind a row bound.  Not raw buffer loads: ROCm 7.2's backend
+// miscompiles a buffer load whose result vector is then taken apart element by element (the 8-byte form and
+// a 16-byte load of which two elements are used alike): it shrinks the load to ONE dword and hands that
+// dword out for every element (reproduced stand-alone: buffer_load_dword + v_cvt_pk_bf16_f32 v, v, v).
+template <int N>
+__device__ __forceinline__ fvec<N> ld_row(const float* __restrict__ p, bool ok) {
+  typedef float fv __attribute__((ext_vector_type(N)));
+  fv u = {};
+  if (ok) u = *(const fv*)p;
+  fvec<N> o;
+#pragma unroll
+  for (int i = 0; i < N; ++i) o.v[i] = u[i];
+  return o;
+}
+
+template <int D, int NT, bool NORMS, bool DROP>
+__global__ __launch_bounds__(512) void ffn_bwd_own_kernel(FfnArgs a, int steps_per_wg) {
+  using T = FfnOwn<D, NT>;
+  constexpr int VPL = T::VPL, KH = T::KH, NJ = T::NJ, NP = T::NP, FF = T::FF;
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int M = a.M;
+  const int nsteps = (M + T::SR - 1) / T::SR;
+  const int s0 = blockIdx.x * steps_per_wg, s1 = min(nsteps, s0 + steps_per_wg);
+  const int nb16 = (M + 15) / 16;
+  const int fw = 16 * NT * w;                   // this wave's first FF column
+  const float dsc = a.drop.scale;
+
+  // ---- resident weights (bf16 images written by the forward: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF))
+  const auto rw = buf_rsrc(a.wbf, (uint32_t)(3 * FF * D) * 2);
+  bf16x8 w1b[NT][KH], w2b[NT][KH];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      const uint32_t o = (uint32_t)((fw + 16 * t + c) * D + 32 * kh + 8 * g) * 2;
+      w1b[t][kh] = buf_ld_bf8(rw, o, 0);
+      w2b[t][kh] = buf_ld_bf8(rw, o + (uint32_t)(FF * D) * 2, 0);
+    }
+  bf16x8 w1t32[NP > 0 ? NP : 1][NJ];
+  bf16x4 w1t16[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const uint32_t row = (uint32_t)(2 * FF * D + (16 * j + c) * FF + fw) * 2;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) w1t32[p][j] = buf_ld_bf8(rw, row + (uint32_t)(32 * p + 8 * g) * 2, 0);
+    if constexpr (NT & 1)
+      w1t16[j] = *(const bf16x4*)(a.wbf + 2 * FF * D + (16 * j + c) * FF + fw + 32 * NP + 4 * g);
+  }
+  float b1v[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) b1v[t] = a.b1[fw + 16 * t + c];
+
+  // ---- accumulators over the whole launch
+  f32x4 dw1[NT][NJ], dw2[NT][NJ];
+  float db1[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    db1[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dw1[t][j] = dw2[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float cb2[VPL], cn2[VPL], cn1[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) cb2[v] = cn2[v] = cn1[v] = 0.f;
+
+  // ---- loader / epilogue lane map: row 4w + g of the step, columns c0 .. c0 + VPL - 1
+  const int rl = 4 * w + g, c0 = VPL * c;
+  const uint32_t mbytes = (uint32_t)M * D * 4;
+  const auto rr2 = buf_rsrc(a.r2, NORMS ? (uint32_t)M * 4 : 0u);
+  const auto rr1 = buf_rsrc(a.r1, NORMS ? (uint32_t)M * 4 : 0u);
+  const auto rout = buf_rsrc(NORMS ? a.dh1 : a.dx, mbytes);
+  const auto rmask = buf_rsrc(a.mask, DROP ? (uint32_t)nb16 * 16 * (FF / 32) * 4 : 0u);
+  float nw2[VPL], nw1[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    nw2[v] = NORMS ? a.nw2[c0 + v] : 0.f;
+    nw1[v] = NORMS ? a.nw1[c0 + v] : 0.f;
+  }
+  struct Raw {
+    fvec<VPL> x, dy, h2, h1;
+    float r2, r1;
+    uint32_t kw;
+  };
+  auto issue = [&](int s, Raw& R) {
+    const int m = T::SR * s + rl;
+    const bool ok = m < M;
+    const long e = (long)m * D + c0;
+    const uint32_t offr = ok ? (uint32_t)m * 4 : BUF_OOB;
+    R.x = ld_row<VPL>(a.x + e, ok);
+    R.dy = ld_row<VPL>((NORMS ? a.dy : a.dh) + e, ok);
+    if (NORMS) {
+      R.h2 = ld_row<VPL>(a.h2 + e, ok);
+      R.h1 = ld_row<VPL>(a.h1 + e, ok);
+      R.r2 = buf_ld(rr2, offr);
+      R.r1 = buf_ld(rr1, offr);
+    }
+    if (DROP) {      // keep word of chunk lane / 4, row 4w + lane % 4 (lanes >= 4 NCH idle)
+      const int row = T::SR * s + 4 * w + (lane & 3), ch = lane >> 2;
+      const bool ok = lane < 4 * T::NCH && row < M;
+      R.kw = __builtin_bit_cast(uint32_t, buf_ld(rmask, ok ? rw_word(ch, nb16, row >> 4, row & 15) * 4 : BUF_OOB));
+    }
+  };
+  // norm2 backward of the loaded rows -> dh2 (kept for this row's epilogue) + the images of step s
+  auto prepare = [&](int s, const Raw& R, float (&dh2)[VPL]) {
+    char* img = lds + (s % 3) * T::IMG;
+    if (NORMS) {
+      float dot = 0.f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dot = fmaf(nw2[v] * R.dy.v[v], R.h2.v[v], dot);
+      dot = group_sum<16>(dot);
+      const float rm = R.r2;
+      const float coef = rm * rm * rm / (float)D * dot;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        dh2[v] = nw2[v] * R.dy.v[v] * rm - R.h2.v[v] * coef;
+        cb2[v] += dh2[v];
+        cn2[v] = fmaf(R.dy.v[v] * R.h2.v[v], rm, cn2[v]);
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dh2[v] = R.dy.v[v];
+    }
+    if constexpr (VPL == 2) {
+      *(bf16x2*)(img + T::O_XB + rl * T::XRS + c0 * 2) = bf16x2{(__bf16)R.x.v[0], (__bf16)R.x.v[1]};
+      *(bf16x2*)(img + T::O_HB + rl * T::XRS + c0 * 2) = bf16x2{(__bf16)dh2[0], (__bf16)dh2[1]};
+    } else {
+      *(bf16x4*)(img + T::O_XB + rl * T::XRS + c0 * 2) =
+          bf16x4{(__bf16)R.x.v[0], (__bf16)R.x.v[1], (__bf16)R.x.v[2], (__bf16)R.x.v[3]};
+      *(bf16x4*)(img + T::O_HB + rl * T::XRS + c0 * 2) =
+          bf16x4{(__bf16)dh2[0], (__bf16)dh2[1], (__bf16)dh2[2], (__bf16)dh2[3]};
+    }
+    if (DROP && lane < 4 * T::NCH) *(uint32_t*)(img + T::O_KB + ((lane >> 2) * T::SR + 4 * w + (lane & 3)) * 4) = R.kw;
+  };
+
+  char* stg = lds + T::O_STG + w * T::STG;
+  // the step's products; the dx partial of the step's 32 rows -> exchange slot (s & 1, w)
+  auto compute = [&](int s) {
+    const char* img = lds + (s % 3) * T::IMG;
+    bf16x8 xa[2][KH], ha[2][KH], xt[NJ], ht[NJ];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) {
+        const int o = (16 * b + c) * T::XRS + (32 * kh + 8 * g) * 2;
+        xa[b][kh] = *(const bf16x8*)(img + T::O_XB + o);
+        ha[b][kh] = *(const bf16x8*)(img + T::O_HB + o);
+      }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      // lane 4q + p of group g: row 16b + 4g + q, columns 16j + 4p .. +3 -> lane c gets column 16j + c
+      const int o0 = (4 * g + (c >> 2)) * T::XRS + (16 * j + 4 * (c & 3)) * 2, o1 = o0 + 16 * T::XRS;
+      xt[j] = cat8(lds_tr4((const __bf16*)(img + T::O_XB + o0)), lds_tr4((const __bf16*)(img + T::O_XB + o1)));
+      ht[j] = cat8(lds_tr4((const __bf16*)(img + T::O_HB + o0)), lds_tr4((const __bf16*)(img + T::O_HB + o1)));
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int f0 = fw + 16 * t;
+      f32x4 pre[2], dfo[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        pre[b] = dfo[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh) {
+          pre[b] = mfma_bf(xa[b][kh], w1b[t][kh], pre[b]);
+          dfo[b] = mfma_bf(ha[b][kh], w2b[t][kh], dfo[b]);
+        }
+      }
+      f32x4 fo[2], da[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        u32x4 kw = {0u, 0u, 0u, 0u};
+        if (DROP) kw = *(const u32x4*)(img + T::O_KB + ((f0 >> 5) * T::SR + 16 * b + 4 * g) * 4);
+        const int bit = (f0 & 31) + c;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          // pre[b][r]: row 16b + 4g + r, column f0 + c
+          const f32x2 z = f32x2{pre[b][2 * q], pre[b][2 * q + 1]} + b1v[t];
+          f32x2 e;
+          const f32x2 cdf = cdf_as2(z, e);
+          const f32x2 gg = z * e * 0.39894228040143268f + cdf;
+          f32x2 sc = {1.f, 1.f};
+          if (DROP) sc = f32x2{((kw[2 * q] >> bit) & 1u) ? dsc : 0.f, ((kw[2 * q + 1] >> bit) & 1u) ? dsc : 0.f};
+          const f32x2 fv = z * cdf * sc;
+          const f32x2 dv = f32x2{dfo[b][2 * q], dfo[b][2 * q + 1]} * sc * gg;
+          fo[b][2 * q] = fv.x;
+          fo[b][2 * q + 1] = fv.y;
+          da[b][2 * q] = dv.x;
+          da[b][2 * q + 1] = dv.y;
+        }
+        db1[t] += (da[b][0] + da[b][1]) + (da[b][2] + da[b][3]);
+      }
+      const bf16x8 afo = pack8(fo[0], fo[1]), ada = pack8(da[0], da[1]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        dw1[t][j] = mfma_bf(ada, xt[j], dw1[t][j]);      // C[ff f0 + 4g + r][d 16j + c]
+        dw2[t][j] = mfma_bf(ht[j], afo, dw2[t][j]);      // C[d 16j + 4g + r][ff f0 + c]
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        *(bf16x4*)(stg + own_stg(16 * t + c, 16 * b + 4 * g)) = __builtin_convertvector(da[b], bf16x4);
+    }
+    __builtin_amdgcn_wave_barrier();
+    // dx partial over this wave's FF columns: A = dact[row 16b + c][ff k-set of group g] (transposed reads)
+    float* xs = (float*)(lds + T::O_XCH + (s & 1) * T::XCH + w * T::XSLOT);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      f32x4 dxp[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) dxp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int rm = 16 * b + 4 * (c & 3);
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int fl = 32 * p + 8 * g + (c >> 2);
+        const bf16x8 av = cat8(lds_tr4((const __bf16*)(stg + own_stg(fl, rm))),
+                               lds_tr4((const __bf16*)(stg + own_stg(fl + 4, rm))));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) dxp[j] = mfma_bf(av, w1t32[p][j], dxp[j]);
+      }
+      if constexpr (NT & 1) {
+        const bf16x4 av = lds_tr4((const __bf16*)(stg + own_stg(32 * NP + 4 * g + (c >> 2), rm)));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) dxp[j] = mfma_bf16k(av, w1t16[j], dxp[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xs[(16 * b + 4 * g + r) * T::XCS + 16 * j + c] = dxp[j][r];
+    }
+    __builtin_amdgcn_wave_barrier();     // the staging image is rewritten by the next step
+  };
+
+  // the eight partials of this lane's row (fixed source order) + the residual -> norm1 backward
+  auto epilogue = [&](int s, const float (&dh2)[VPL], const Raw& R) {
+    const float* xs = (const float*)(lds + T::O_XCH + (s & 1) * T::XCH);
+    float dx1[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dx1[v] = 0.f;
+#pragma unroll
+    for (int src = 0; src < T::NW; ++src) {
+      const fvec<VPL> pv = *(const fvec<VPL>*)(xs + src * (T::XSLOT / 4) + rl * T::XCS + c0);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dx1[v] += pv.v[v];
+    }
+    const int m = T::SR * s + rl;
+    const uint32_t off = m < M ? (uint32_t)(m * D + c0) * 4 : BUF_OOB;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dx1[v] += dh2[v];
+    if (!NORMS) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) buf_st(dx1[v], rout, off + 4 * v);
+      return;
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dot = fmaf(nw1[v] * dx1[v], R.h1.v[v], dot);
+    dot = group_sum<16>(dot);
+    const float rm = R.r1;
+    const float coef = rm * rm * rm / (float)D * dot;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      buf_st(nw1[v] * dx1[v] * rm - R.h1.v[v] * coef, rout, off + 4 * v);
+      cn1[v] = fmaf(dx1[v] * R.h1.v[v], rm, cn1[v]);
+    }
+  };
+
+  // ---- the step pipeline
+  Raw rc, rn;
+  float dh2c[VPL], dh2n[VPL];
+  if (s0 < s1) {
+    issue(s0, rc);
+    prepare(s0, rc, dh2c);
+  }
+  __syncthreads();
+  if (a.dbg && blockIdx.x == 0) {      // debug: dump step s0's images / wave 0's first products into dx
+    const char* img = lds + (s0 % 3) * T::IMG;
+    if (a.dbg <= 2) {
+      for (int q = tid; q < 32 * D; q += 512) {
+        const int r = q / D, d = q % D;
+        a.dx[q] = (float)*(const __bf16*)(img + (a.dbg == 1 ? T::O_XB : T::O_HB) + r * T::XRS + d * 2);
+      }
+    } else if (w == 0) {
+      bf16x8 xa = *(const bf16x8*)(img + T::O_XB + c * T::XRS + 8 * g * 2);
+      bf16x8 ha = *(const bf16x8*)(img + T::O_HB + c * T::XRS + 8 * g * 2);
+      f32x4 pre = mfma_bf(xa, w1b[0][0], f32x4{0.f, 0.f, 0.f, 0.f});
+      f32x4 dfo = mfma_bf(ha, w2b[0][0], f32x4{0.f, 0.f, 0.f, 0.f});
+      for (int r = 0; r < 4; ++r) {
+        a.dx[(4 * g + r) * D + c] = pre[r];
+        a.dx[(4 * g + r) * D + 16 + c] = dfo[r];
+        a.dx[(16 + 4 * g + r) * D + c] = (float)w1b[0][0][r];
+        a.dx[(16 + 4 * g + r) * D + 16 + c] = (float)xa[r];
+      }
+    }
+    return;
+  }
+  for (int s = s0; s < s1; ++s) {
+    const bool more = s + 1 < s1;
+    if (more) issue(s + 1, rn);
+    compute(s);
+    if (more) prepare(s + 1, rn, dh2n);
+    __syncthreads();
+    epilogue(s, dh2c, rc);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dh2c[v] = dh2n[v];
+    rc = rn;
+  }
+
+  // ---- the workgroup's slab row, written once
+  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int f0 = fw + 16 * t;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        slab[a.o_w1 + (long)(f0 + 4 * g + r) * D + 16 * j + c] = dw1[t][j][r];
+        slab[a.o_w2 + (long)(16 * j + 4 * g + r) * FF + f0 + c] = dw2[t][j][r];
+      }
+    float v = db1[t];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (g == 0) slab[a.o_b1 + f0 + c] = v;
+  }
+  // column sums of the norm weights / db2: lanes of one column (4 per wave, 8 waves), fixed order
+  __syncthreads();                       // the exchange buffers are free
+  float* red = (float*)(lds + T::O_XCH);   // [wave][3][D]
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    float q[3] = {cb2[v], cn2[v], cn1[v]};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      q[k] += __shfl_xor(q[k], 16, 64);
+      q[k] += __shfl_xor(q[k], 32, 64);
+      if (g == 0) red[(w * 3 + k) * D + c0 + v] = q[k];
+    }
+  }
+  __syncthreads();
+  if (NORMS && tid < 3 * D) {
+    const int k = tid / D, col = tid % D;
+    float sum = 0.f;
+#pragma unroll
+    for (int src = 0; src < T::NW; ++src) sum += red[(src * 3 + k) * D + col];
+    slab[(k == 0 ? a.o_b2 : k == 1 ? a.o_n2 : a.o_n1) + col] = sum;
+  }
+}
+
+// the owner-form shapes: D = 32 (D = 64 needs more registers than two waves per SIMD hold), FF = 128 NT,
+// NT <= 3
+static int ffn_own_nt(int D, int FF) {
+  if (D != 32 || FF % 128 != 0) return 0;
+  const int nt = FF / 128;
+  if (nt < 1 || nt > 3) return 0;      // NT = 4 spills at 256 VGPRs
+  static const bool off = [] {
+    const char* e = getenv("CTR_FFN_BWD_LEGACY");
+    return e && *e && *e != '0';
+  }();
+  return off ? 0 : nt;
+}
+static int ffn_own_steps_per_wg(long M) {
+  const long ns = (M + 31) / 32;
+  const long grid = ns < 256 ? ns : 256;
+  return (int)((ns + grid - 1) / grid);
+}
+static int ffn_own_grid(long M) {
+  const long ns = (M + 31) / 32;
+  const long per = ffn_own_steps_per_wg(M);
+  return (int)((ns + per - 1) / per);
+}
+
+template <int D, int NT>
+static void launch_ffn_own(const FfnArgs& a0, hipStream_t s) {
+  FfnArgs a = a0;
+  static const int dbg = [] {
+    const char* e = getenv("CTR_FFN_DEBUG");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
+  const int per = ffn_own_steps_per_wg(a.M), grid = ffn_own_grid(a.M);
+  const bool drop = a.drop.thresh != 0;
+  if (a.dy) {
+    if (drop) ffn_bwd_own_kernel<D, NT, true, true><<<grid, 512, 0, s>>>(a, per);
+    else ffn_bwd_own_kernel<D, NT, true, false><<<grid, 512, 0, s>>>(a, per);
+  } else {
+    if (drop) ffn_bwd_own_kernel<D, NT, false, true><<<grid, 512, 0, s>>>(a, per);
+    else ffn_bwd_own_kernel<D, NT, false, false><<<grid, 512, 0, s>>>(a, per);
+  }
+}
+
 // persistent backward grid: at most 512 workgroups (two per CU), tiles split as evenly as possible
 static int ffn_bf_grid(long M, int D) {
   const long rt = D <= 32 ? 128 : 64;
@@ -1337,6 +1786,13 @@ static void launch_ffn_bf(const FfnArgs& a, bool bwd, hipStream_t s) {
     else ffn_fwd_bf_kernel<D, false><<<cdiv(a.M, 128), 256, 0, s>>>(a);
     return;
   }
+  if (const int nt = ffn_own_nt(D, a.FF)) {
+    switch (nt) {
+      case 1: launch_ffn_own<32, 1>(a, s); return;
+      case 2: launch_ffn_own<32, 2>(a, s); return;
+      default: launch_ffn_own<32, 3>(a, s); return;
+    }
+  }
   const int grid = ffn_bf_grid(a.M, D);
   if (a.dy) {
     if (drop) ffn_bwd_bf_kernel<D, true, true><<<grid, 256, 0, s>>>(a);
@@ -1369,8 +1825,8 @@ extern "C" int ctr_ffn_supported(int D, int FF, int flags) {
   return ((flags & CTR_FFN_BF16) ? ffn_bf_shape_ok(D, FF) : ffn_shape_ok(D, FF)) ? 1 : 0;
 }
 
-extern "C" int ctr_ffn_slab_rows(int M, int D, int flags) {
-  if (flags & CTR_FFN_BF16) return ffn_bf_grid(M, D);
+extern "C" int ctr_ffn_slab_rows(int M, int D, int FF, int flags) {
+  if (flags & CTR_FFN_BF16) return ffn_own_nt(D, FF) ? ffn_own_grid(M) : ffn_bf_grid(M, D);
   return cdiv(M, D >= 64 ? 64 : 128);
 }
 

@@ -77,7 +77,7 @@ SIGS = {
     "ctr_attn_bwd_nparts": (i, [i, i, i]),
     "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_ffn_supported": (i, [i, i, i]),
-    "ctr_ffn_slab_rows": (i, [i, i, i]),
+    "ctr_ffn_slab_rows": (i, [i, i, i, i]),
     "ctr_ffn_mask_words": (i, [i, i]),
     "ctr_ffn_fwd": (i, [p, i, i, i, p, p, p, p, p, f, u, u, f, p, p, p, p, p, i, p]),
     "ctr_ffn_bwd": (i, [p, p, i, i, i, p, p, p, u, u, f, p, p, p, l, i, i, p, i, p]),

@@ -773,7 +773,7 @@ class Engine:
                                              "norm2.w")]
             n_sl = o[5] + D
             ld_sl = (n_sl + 3) // 4 * 4
-            nb = _lib.query("ctr_ffn_slab_rows", M, D, self.ffn_flags)
+            nb = _lib.query("ctr_ffn_slab_rows", M, D, FF, self.ffn_flags)
             slab = W.get_zeroed(f"ffn_slab{li}", (nb, ld_sl))
             dh1 = W.get(f"dh1_{li}", (M, D))
             call("ctr_ffn_bwd_norms", ptr(Ls["x1"]), ptr(dx2), ptr(Ls["h2"]), ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]),
