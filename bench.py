@@ -89,7 +89,35 @@ def kernel_work(name, a, B, ffn_M):
         return "valu", 4.0 * B * K * K * D, "flop"
     if name == "ctr_attn_bwd":
         return "valu", 8.0 * B * K * K * D, "flop"
+    # amp: the bf16-MFMA attention (attn_mf.hip) -- its products take a few % of the bf16 MFMA peak, so its
+    # roofline is HBM: per (sample, candidate) row the fp32 qkv read (12 D B), o write (4 D), row max / sum
+    # (8 H) and keep bits (8 H: 2 words per head per 64-row tile, 128 per head over <= 64 rows); the backward
+    # reads qkv, o, dO (20 D), the row stats and bits, and writes dqkv (12 D)
+    H = a.H
+    if name == "ctr_attn_fwd_bf":
+        return "hbm", float(B * K * (16 * D + 8 * H) + B * H * 512), "B"
+    if name == "ctr_attn_bwd_bf":
+        return "hbm", float(B * K * (32 * D + 8 * H) + B * H * 512), "B"
     return None
+
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, MI355X_MICROARCH.md
+
+
+def price(name, a, B, ffn_M, amp, ffn_flags, launch_ms):
+    """(bound, work, achieved, peak, unit, mfma dtype) of one timed entry point, or None."""
+    w = kernel_work(name, a, B, ffn_M)
+    if w is None:
+        return None
+    bound, work, _ = w
+    if bound == "hbm":
+        return bound, w, work / (launch_ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", None
+    # amp bf16: the FFN kernels' products run on bf16 MFMA -> priced against the bf16 dense peak; the fp32
+    # attention core runs on the fp32 vector units (its peak = the fp32 rate, 157.3 TF)
+    bf = amp == "bf16" and name.startswith("ctr_ffn") and ffn_flags
+    peak = MFMA_BF16_PEAK_TFS if bf else MFMA_F32_PEAK_TFS
+    return bound, w, work / (launch_ms * 1e-3) / 1e12, peak, "TFLOP/s", (None if bound == "valu" else
+                                                                        "bf16" if bf else "f32")
 
 
 def step_bytes_dense_equiv(a, B, L, with_ema):
@@ -206,7 +234,8 @@ def pmc_traffic(name):
     bwd = ("ffn_bwd_own_kernel", "ffn_bwd_bf_kernel", "ffn_bwd_cols_kernel", "ffn_bwd_kernel")   # preferred first
     kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bf_kernel", "ffn_fwd_kernel"),
              "ctr_attn_bwd": ("attn_bwd_wave_kernel", "attn_bwd_kernel"),
-             "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel")}.get(name)
+             "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel"),
+             "ctr_attn_bwd_bf": ("attn_bwd_mf_kernel",), "ctr_attn_fwd_bf": ("attn_fwd_mf_kernel",)}.get(name)
     if kerns is None:
         return None
     base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS
@@ -370,7 +399,8 @@ def main():
     # HIP events cost host time per bracketed call (~0.1 ms per step for the whole list below when the step is
     # host-issue sensitive), so the timed steps bracket only the roofline candidates (the kernels with an
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
-    roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd")
+    roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd",
+                  "ctr_attn_bwd_bf", "ctr_attn_fwd_bf")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
                           "ctr_adamw_ema", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
@@ -429,18 +459,12 @@ def main():
         per_step_t = {n: c * ms / args.steps for n, (c, ms) in kstats_timed.items()}
         roof = None
         for n in sorted(per_step_t, key=per_step_t.get, reverse=True):
-            w = kernel_work(n, a, args.batch, ffn_M)
-            if w is None:
+            pr = price(n, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, kstats_timed[n][1])
+            if pr is None:
                 continue
-            bound, work, unit = w
-            ach = work / (kstats_timed[n][1] * 1e-3) / 1e12
-            # amp bf16: the FFN kernels' products run on bf16 MFMA -> priced against the bf16 dense peak; the
-            # attention core runs on the fp32 vector units (its peak = the fp32 rate, 157.3 TF)
-            bf = args.amp == "bf16" and n.startswith("ctr_ffn") and model.engine.ffn_flags
-            peak = MFMA_BF16_PEAK_TFS if bf else MFMA_F32_PEAK_TFS
+            bound, (_, work, unit), ach, peak, runit, mdt = pr
             roof = {"bound": bound, "kernel": n, "achieved": round(ach, 2), "peak": round(peak, 1),
-                    "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                    "mfma_dtype": None if bound == "valu" else "bf16" if bf else "f32",
+                    "unit": runit, "frac": round(ach / peak, 4), "mfma_dtype": mdt,
                     "traffic": pmc_traffic(n) if args.config == "cfg2" else None, "work_per_launch": work,
                     "work_unit": unit,
                     "avg_launch_ms": round(kstats_timed[n][1], 4), "ms_per_step": round(per_step_t[n], 4),
@@ -448,15 +472,12 @@ def main():
             # every priced kernel of the timed steps, dominant first (the roofline object is the first)
             roof["priced"] = {}
             for m_ in sorted(per_step_t, key=per_step_t.get, reverse=True):
-                w_ = kernel_work(m_, a, args.batch, ffn_M)
-                if w_ is None:
+                pr_ = price(m_, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, kstats_timed[m_][1])
+                if pr_ is None:
                     continue
-                bf_ = args.amp == "bf16" and m_.startswith("ctr_ffn") and model.engine.ffn_flags
-                pk_ = MFMA_BF16_PEAK_TFS if bf_ else MFMA_F32_PEAK_TFS
-                a_ = w_[1] / (kstats_timed[m_][1] * 1e-3) / 1e12
-                roof["priced"][m_] = {"bound": w_[0], "ms_per_step": round(per_step_t[m_], 4),
-                                      "avg_launch_ms": round(kstats_timed[m_][1], 4), "achieved": round(a_, 2),
-                                      "peak": round(pk_, 1), "frac": round(a_ / pk_, 4)}
+                roof["priced"][m_] = {"bound": pr_[0], "ms_per_step": round(per_step_t[m_], 4),
+                                      "avg_launch_ms": round(kstats_timed[m_][1], 4), "achieved": round(pr_[2], 2),
+                                      "peak": round(pr_[3], 1), "unit": pr_[4], "frac": round(pr_[2] / pr_[3], 4)}
             break
         rec = {
             "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref"
@@ -465,8 +486,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp32" if args.amp == "none" else "bf16",
             "precision": ("fp32 everywhere" if args.amp == "none" else
-                          "amp bf16: bf16 MFMA operands with fp32 accumulation in the FFN and the QNN/head GEMMs; "
-                          "attention, projections, norms, embeddings, optimizer state and master weights fp32"),
+                          "amp bf16: bf16 MFMA operands with fp32 accumulation in the FFN, the QNN/head GEMMs and "
+                          "the attention products" + ("" if model.engine.attn_bf else " (this shape: fp32 attention)")
+                          + "; softmax, projections, norms, embeddings, optimizer state and master weights fp32"),
             "data": "synthetic (SURVEY 8(d) distributions), HBM-resident",
             "config": {"workload": WORKLOADS[args.config].format(B=args.batch, L=args.seq_len,
                                                                  P=sum(int(np.prod(sh)) for _, sh, _ in

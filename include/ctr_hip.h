@@ -185,6 +185,20 @@ int ctr_attn_bwd_nparts(int H, int K, int D);
 int ctr_attn_bwd(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D, const float* relmean,
                  int tk, float scale, uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const uint32_t* mask,
                  const float* mrow, const float* lrow, float* dqkv, float* drel_part, void* stream);
+/* amp: bf16 -- the same attention on bf16 MFMA (attn_mf.hip): products on bf16-rounded q*scale, k, v, dO, p~
+ * and dS with fp32 accumulation, as the reference's autocast(bfloat16) baddbmm / bmm; softmax, dropout and dS
+ * in fp32.  K <= 64 and head dim 4 or 8 (ctr_attn_bf_ok).  Arguments as ctr_attn_fwd / ctr_attn_bwd, except:
+ * mask holds the keep bits in the kernels' lane layout (B*H x 2 x 64 words, <= ctr_attn_mask_words), mrow
+ * the row max in log2 units -- both only meaningful to ctr_attn_bwd_bf; drel_part has B*ctr_attn_bwd_bf_nparts rows. */
+int ctr_attn_bf_ok(int K, int H, int D);
+int ctr_attn_fwd_bf(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
+                    uint32_t drop_key, uint32_t drop_thresh, float drop_scale, uint32_t* mask, float* o, float* mrow,
+                    float* lrow, void* stream);
+int ctr_attn_bwd_bf_nparts(int H);
+int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D,
+                    const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                    float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow, float* dqkv,
+                    float* drel_part, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused position-wise FFN + residual + RMSNorm of DAREEncoderLayer, src/models/dare.py:53-70
@@ -238,6 +252,22 @@ int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long ldh, const f
 size_t ctr_colsum_ws_size(int M, int N);
 /* out[n] = sum_m X[m,n] / div  (bias grads; div = B gives torch .mean(dim=0)) */
 int ctr_colsum(const float* X, long ld, int M, int N, float div, float* out, float* ws, void* stream);
+/* several column sums in one launch pair: out_i[n] = sum_m X_i[m,n] / div_i (div 0 or 1: plain sums) for up to
+ * CTR_COLSUM_MAXSEG segments (the backward's per-layer weight-grad slabs, summed together once the layers
+ * are done).  segs: a HOST array (copied into the launch); every segment needs N and ld multiples of 4 and
+ * a 16-byte aligned X (ctr_colsum_multi_ok); ws: ctr_colsum_multi_ws_size bytes.  Deterministic.  */
+#define CTR_COLSUM_MAXSEG 16
+typedef struct {
+  const float* X;
+  long ld;
+  int M, N;
+  float* out;
+  float div;
+  int pad;
+} ctr_colsum_seg_t;
+int ctr_colsum_multi_ok(const ctr_colsum_seg_t* seg);
+size_t ctr_colsum_multi_ws_size(const ctr_colsum_seg_t* segs, int nseg);
+int ctr_colsum_multi(const ctr_colsum_seg_t* segs, int nseg, float* ws, size_t ws_bytes, void* stream);
 /* bce_wll_style(logits) + aux_w * bce_wll_style(aux) (src/train.py:71-90,165-168) and d/dlogits, d/daux */
 int ctr_loss(const float* z, const float* za, const float* y, int B, float aux_w, float* loss, float* dz, float* dza,
              void* stream);

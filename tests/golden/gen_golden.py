@@ -535,14 +535,18 @@ def gen_r3(only_cfg4=False):
     GEMMs + RMSNorm backwards instead of the fused kernel."""
     big_tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=0, epochs=8)
     cfg4, cols4, nnum = cfg4_full_cfg()
+    # the yaml's own lr (3e-4): at 3e-3 the first update moves this deep (4-layer, D = 64) model so far that the
+    # second step's gradients carry the first step's ill-conditioned AdamW elements (see golden_util.
+    # Fixture.ill_conditioned) into every moment
+    tr4 = dict(big_tr, lr=3e-4)
     kw4 = dict(B=3, L=400, vocab=2000, Fn=nnum, Fm=nnum, cat_cards={c: 100 for c in cols4}, steps=2, pseed=61,
-               bseed=900, store_params=False, train_cfg=big_tr)
+               bseed=900, store_params=False, train_cfg=tr4)
     # B = 3 single-sample categorical rows: many table-grad elements sit near AdamW's eps after the clip,
     # where the update is ill-conditioned -- more replays for a representative allowance
     run_case("cfg4_full", cfg4, **kw4, allow_replays=8)
+    run_case("cfg4_full_bf16", cfg4, **kw4, amp_twin="cfg4_full")
     if only_cfg4:
         return
-    run_case("cfg4_full_bf16", cfg4, **kw4, amp_twin="cfg4_full")
     cfg3, cols3 = cfg3_cfg()
     run_case("cfg3_dims_bf16", cfg3, B=8, L=100, vocab=3000, Fn=82, Fm=82, cat_cards={c: 200 for c in cols3},
              steps=2, pseed=41, bseed=700, store_params=False, train_cfg=big_tr, amp_twin="cfg3_dims")

@@ -63,7 +63,8 @@ class Fixture:
     def has(self, name):
         return name in self.z.files or f"{name}@idx" in self.z.files
 
-    def check(self, name, got, rtol=1e-4, atol=1e-6, what=None, exclude=None, base=None, elem_rtol=None, allow=None):
+    def check(self, name, got, rtol=1e-4, atol=1e-6, what=None, exclude=None, base=None, elem_rtol=None, allow=None,
+              skip=None):
         """Compare ``got`` with the stored full tensor or its fingerprint.
 
         Full tensors: norm-wise relative error <= rtol and elementwise (close_enough).  Fingerprinted
@@ -96,6 +97,7 @@ class Fixture:
             return u
 
         al = self.allowance(allow) if allow else None
+        sk = skip(self) if skip else None      # {"full" | "idx", "rows"}: elements left out of the elementwise test
 
         if name in self.z.files:
             ref = np.asarray(self.z[name], dtype=np.float64).ravel()
@@ -106,21 +108,23 @@ class Fixture:
                 got, ref = got[~exclude], ref[~exclude]
                 b = None if b is None else b[~exclude]
                 a = None if a is None else a[~exclude]
-            close_enough(got, ref, rtol, atol, label, ulp(ref, b, a), elem_rtol)
+            close_enough(got, ref, rtol, atol, label, ulp(ref, b, a), elem_rtol,
+                         None if sk is None or exclude is not None else sk["full"])
             return
         assert exclude is None, label
         fp = {k: self.z[f"{name}@{k}"] for k in ("idx", "vals", "sumsq", "projs")}
         vals = fp["vals"].astype(np.float64)
         close_enough(got[fp["idx"]], vals, rtol, atol, label + "[sampled]",
                      ulp(vals, None if base is None else base[fp["idx"]], None if al is None else al["idx"]),
-                     elem_rtol)
+                     elem_rtol, None if sk is None else sk["idx"])
         if f"{name}@rows" in self.z.files:
             rows = self.z[f"{name}@rows"]
             ref_rows = self.z[f"{name}@rowvals"].astype(np.float64)
             w = ref_rows.shape[1]
             br = None if base is None else base.reshape(-1, w)[rows].ravel()
             close_enough(got.reshape(-1, w)[rows].ravel(), ref_rows.ravel(), rtol, atol, label + "[touched rows]",
-                         ulp(ref_rows.ravel(), br, None if al is None else al["rows"].ravel()), elem_rtol)
+                         ulp(ref_rows.ravel(), br, None if al is None else al["rows"].ravel()), elem_rtol,
+                         None if sk is None or sk["rows"] is None else sk["rows"].ravel())
         sumsq = float(fp["sumsq"])
         slack = (0.0 if base is None else float(np.linalg.norm(ulp(0.0 * base, base)))) + \
             (0.0 if al is None else float(al["norm"]))
@@ -147,7 +151,27 @@ class Fixture:
         norm-wise rtol plus, per element, 2 ulp of the fp32 result and the replayed conditioning
         allowance (gen_golden.update_allowance); elementwise at 1e-2 of the tensor's largest update."""
         return self.check(f"{kind}/{key}", got_delta, rtol, 1e-12, exclude=exclude, base=p0, elem_rtol=1e-2,
-                          allow=f"{kind}allow/{key}")
+                          allow=f"{kind}allow/{key}", skip=lambda fx: fx.ill_conditioned(key))
+
+    def ill_conditioned(self, key, factor=100.0):
+        """Elements whose final AdamW denominator sqrt(v_T / bc2) + eps is dominated by eps: sqrt(v_T / bc2) <
+        factor * eps (the criterion of tests/test_gpu_shard.py's data-parallel check).  There m / denom is
+        a cancellation residue of near-zero gradients -- two fp32 implementations with different summation
+        orders step such an element by different fractions of lr (cfg4_full: a DARE att row whose gradient is
+        a softmax-cancellation residue of ~1e-9, GPU 4x smaller than the reference, update 1/3 of the
+        reference's).  They stay in the norm-wise test; the elementwise test leaves them out.  None when the
+        fixture holds no v_T for ``key`` (no gradient)."""
+        name = f"vT/{key}"
+        if not self.has(name):
+            return None
+        bc2 = 1.0 - 0.999 ** int(self.meta["steps"])
+        lim = (factor * 1e-8) ** 2 * bc2
+        if name in self.z.files:
+            return {"full": np.asarray(self.z[name], np.float64).ravel() < lim}
+        out = {"idx": self.z[f"{name}@vals"].astype(np.float64) < lim, "rows": None}
+        if f"{name}@rowvals" in self.z.files:
+            out["rows"] = self.z[f"{name}@rowvals"].astype(np.float64) < lim
+        return out
 
 
     def check_moment(self, kind, key, got, rtol=None):
@@ -235,9 +259,10 @@ def check_bf16_band(fx16, fx32, name, got, label=None, update=False, p0=None):
     return e16, e32, band
 
 
-def close_enough(got, ref, rtol, atol, label, ulp=None, elem_rtol=None):
+def close_enough(got, ref, rtol, atol, label, ulp=None, elem_rtol=None, skip=None):
     """Norm-wise ||got - ref|| <= rtol ||ref|| (+ ||ulp||) AND elementwise
-    |d| <= atol (+ ulp) + e*(10|ref| + max|ref|) with e = elem_rtol (default rtol)."""
+    |d| <= atol (+ ulp) + e*(10|ref| + max|ref|) with e = elem_rtol (default rtol); ``skip`` (boolean, like
+    ref): elements left out of the elementwise test only."""
     d = np.abs(got - ref)
     nrm = np.linalg.norm(ref)
     u = 0.0 if ulp is None else ulp
@@ -246,6 +271,8 @@ def close_enough(got, ref, rtol, atol, label, ulp=None, elem_rtol=None):
     rel = err / (nrm + 1e-30)
     e = rtol if elem_rtol is None else elem_rtol
     bad = d > atol + u + 10 * e * np.abs(ref) + e * np.abs(ref).max(initial=0)
+    if skip is not None:
+        bad &= ~np.asarray(skip, bool)
     ok_norm = err <= rtol * nrm + un or (nrm == 0 and d.max(initial=0) <= atol)
     assert ok_norm and not bad.any(), (
         f"{label}: normwise rel err {rel:.3e} (rtol {rtol}{'' if ulp is None else f', +ulp {un / (nrm + 1e-30):.1e}'}), "

@@ -218,7 +218,7 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p, generic):
     assert rel(o, o_ref.detach()) < 5e-6
     if p > 0:   # the stored keep bits are exactly the oracle's mask
         km = keep.view(B * H * K, K).cpu().numpy()
-        words = mask.view(B * H * K, -1).cpu().numpy().view(np.uint32)
+        words = mask[:B * H * K * ((K + 31) // 32)].view(B * H * K, -1).cpu().numpy().view(np.uint32)
         bits = (words[:, np.arange(K) // 32] >> (np.arange(K) % 32).astype(np.uint32)) & 1
         assert np.array_equal(bits.astype(bool), km)
     do = torch.randn(B * K, D, device="cuda")
@@ -235,6 +235,98 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p, generic):
         assert drel.abs().max() < 1e-6 and rel_w.grad.abs().max() == 0
     else:
         assert rel(drel, rel_w.grad) < 1e-5
+
+
+def attn_bf_keep_bits(mask, B, H, K):
+    """(B*H, K, K) keep bits from ctr_attn_fwd_bf's lane-layout mask (attn_mf.hip): per head 2 x 64 words,
+    bit 16 (ti & 1) + 4 tj + r of word ti >> 1 in lane 16 g + c <-> (i = 16 ti + c, j = 16 tj + 4 g + r)."""
+    words = mask.cpu().numpy().view(np.uint32)[:B * H * 128].reshape(B * H, 2, 64)
+    i = np.arange(K)[:, None]
+    j = np.arange(K)[None, :]
+    ti, c, tj, g, r = i // 16, i % 16, j // 16, (j % 16) // 4, j % 4
+    bit = (16 * (ti & 1) + 4 * tj + r).astype(np.uint32)
+    w = words[:, ti >> 1, 16 * g + c]
+    return ((w >> bit[None]) & 1).astype(bool)
+
+
+@pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (37, 2, 8, 0.3), (64, 4, 16, 0.2),
+                                     (61, 8, 32, 0.1), (50, 8, 64, 0.1), (64, 8, 64, 0.1), (40, 6, 24, 0.1),
+                                     (1, 8, 32, 0.1), (60, 8, 64, 0.0), (33, 3, 24, 0.1)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_attention_bf16_vs_torch(K, H, D, p, bias):
+    """amp: the bf16-MFMA attention (ctr_attn_fwd_bf / ctr_attn_bwd_bf) against the fp32 torch reference of
+    the MHA explicit path: products on bf16-rounded operands -> tolerances of bf16 operand rounding (rel
+    2e-2 on o, 3e-2 on the gradients; the fp32 kernels' test holds 1e-5); keep bits exactly the oracle's."""
+    L = _lib()
+    assert L.query("ctr_attn_bf_ok", K, H, D) == 1
+    from tossctr.rng import drop_args
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import rng as orng
+    B, dh = 7, D // H
+    tk = K + 3
+    g = torch.Generator(device="cuda").manual_seed(K * 131 + H)
+    qkv = torch.randn(B * K, 3 * D, device="cuda", generator=g).requires_grad_(True)
+    rel_w = (torch.randn(2 * tk + 1, H, device="cuda", generator=g)).requires_grad_(True)
+    dk = drop_args(4321, 9, p, True)
+    relmean = torch.empty(2 * tk + 1, device="cuda")
+    L.call("ctr_pos_bias_mean", ptr(rel_w), H, 2 * tk + 1, ptr(relmean), stream())
+    o = torch.empty(B * K, D, device="cuda")
+    mrow = torch.empty(B * H * K, device="cuda")
+    lrow = torch.empty(B * H * K, device="cuda")
+    scale = float(np.float32(math.sqrt(1.0 / dh)))
+    mask = torch.zeros(L.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
+    rm = ptr(relmean) if bias else None
+    L.call("ctr_attn_fwd_bf", ptr(qkv), B, K, H, D, rm, tk, scale, *dk, ptr(mask), ptr(o), ptr(mrow), ptr(lrow),
+           stream())
+    q, k, v = qkv.view(B, K, 3 * D).split(D, -1)
+    q = q.reshape(B, K, H, dh).transpose(1, 2)
+    k = k.reshape(B, K, H, dh).transpose(1, 2)
+    v = v.reshape(B, K, H, dh).transpose(1, 2)
+    i = torch.arange(K, device="cuda")[:, None]
+    j = torch.arange(K, device="cuda")[None, :]
+    s = (q * scale) @ k.transpose(-1, -2)
+    if bias:
+        s = s + rel_w[(j - i).clamp(-tk, tk) + tk].permute(2, 0, 1).mean(0)
+    a = torch.softmax(s, -1)
+    if p > 0:
+        keep = torch.from_numpy(orng.keep_mask(4321, 9, p, (B * H, K, K))).cuda().view(B, H, K, K)
+        a = a * keep.float() / (1 - p)
+        assert np.array_equal(attn_bf_keep_bits(mask, B, H, K), keep.view(B * H, K, K).cpu().numpy())
+    o_ref = (a @ v).transpose(1, 2).reshape(B * K, D)
+    assert rel(o, o_ref.detach()) < 2e-2
+    do = torch.randn(B * K, D, device="cuda", generator=g)
+    o_ref.backward(do)
+    dqkv = torch.full((B * K, 3 * D), float("nan"), device="cuda")
+    nparts = L.query("ctr_attn_bwd_bf_nparts", H) * B
+    drp = torch.full((nparts, 2 * tk + 1), float("nan"), device="cuda")
+    L.call("ctr_attn_bwd_bf", ptr(qkv), ptr(o), ptr(do), B, K, H, D, rm, tk, scale, *dk, ptr(mask), ptr(mrow),
+           ptr(lrow), ptr(dqkv), ptr(drp), stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(dqkv).all()
+    gq, gk, gv = qkv.grad.split(D, -1)
+    dq, dkk, dv = dqkv.split(D, -1)
+    if K == 1:      # softmax over one key: exact dq = dk = 0; ours the bf16 residue of dp - do.o
+        assert dq.abs().max() < 0.05 and dkk.abs().max() < 0.05 and rel(dv, gv) < 3e-2
+    else:
+        assert rel(dq, gq) < 3e-2 and rel(dkk, gk) < 3e-2 and rel(dv, gv) < 3e-2, (rel(dq, gq), rel(dkk, gk),
+                                                                                  rel(dv, gv))
+    drp_first = drp.clone()           # ctr_pos_bias_grad reduces the partials in place
+    if bias:
+        assert torch.isfinite(drp).all()
+        drel = torch.empty(2 * tk + 1, H, device="cuda")
+        L.call("ctr_pos_bias_grad", ptr(drp), nparts, H, 2 * tk + 1, ptr(drel), stream())
+        if K == 1:      # exact grad 0; ours the bf16 residue of dp - do.o
+            assert drel.abs().max() < 0.1
+        else:
+            assert rel(drel, rel_w.grad) < 3e-2
+    # deterministic: a second backward is bitwise identical
+    dqkv2 = torch.empty_like(dqkv)
+    drp2 = torch.empty_like(drp)
+    L.call("ctr_attn_bwd_bf", ptr(qkv), ptr(o), ptr(do), B, K, H, D, rm, tk, scale, *dk, ptr(mask), ptr(mrow),
+           ptr(lrow), ptr(dqkv2), ptr(drp2), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dqkv, dqkv2) and (not bias or torch.equal(drp_first, drp2))
 
 
 @pytest.mark.parametrize("L_,K,D", [(100, 60, 32), (40, 40, 16), (400, 148, 64), (7, 3, 8)])
@@ -751,3 +843,34 @@ def test_gemm_segments_vs_torch(M, N, K, cut, splits):
                GemmSeg(C2=ptr(C2), ldc2=N - nc, nc=nc), stream())
         ref = A.double() @ Wt.double()
         assert rel(torch.cat([C1, C2], 1).double(), ref) < 1e-5
+
+
+def test_colsum_multi_matches_sums_and_is_deterministic():
+    """ctr_colsum_multi (the backward's deferred slab sums): several segments of different shapes and strides in
+    one launch pair == each segment's fp64 column sum (/ div), bitwise equal on a second run."""
+    import ctypes
+    from tossctr._lib import ColsumSeg
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(17)
+    shapes = [(256, 25088, 25088, 1.0), (1920, 3168, 3172, 1.0), (7, 4, 8, 2.0), (513, 1056, 1056, 4096.0),
+              (64, 260, 264, 1.0)]
+    Xs, outs, segs = [], [], []
+    for M, N, ld, div in shapes:
+        X = torch.randn(M, ld, device="cuda", generator=g)
+        out = torch.full((N + 1,), float("nan"), device="cuda")
+        Xs.append(X)
+        outs.append(out)
+        segs.append(ColsumSeg(ptr(X), ld, M, N, ptr(out), div, 0))
+    arr = (ColsumSeg * len(segs))(*segs)
+    assert all(L.query("ctr_colsum_multi_ok", ctypes.byref(s_)) for s_ in segs)
+    nb = L.query("ctr_colsum_multi_ws_size", arr, len(segs))
+    ws = torch.empty(nb // 4 + 1, device="cuda")
+    L.call("ctr_colsum_multi", arr, len(segs), ptr(ws), nb, stream())
+    first = [o.clone() for o in outs]
+    for (M, N, ld, div), X, o in zip(shapes, Xs, outs):
+        ref = X[:, :N].double().sum(0) / div
+        assert rel(o[:N].double(), ref) < 1e-6
+        assert torch.isnan(o[N])                      # nothing past N is written
+    L.call("ctr_colsum_multi", arr, len(segs), ptr(ws), nb, stream())
+    for a, b in zip(first, outs):
+        assert torch.equal(a[:-1], b[:-1])

@@ -110,6 +110,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--threads", type=int, default=os.cpu_count())
     ap.add_argument("--timed", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=2,
+                    help="reference / oracle phases alternate this many times (host-load drift cancels)")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     from bench import cpu_model
@@ -119,13 +121,17 @@ def main():
     L = int(cfg["sequence"]["max_len"])
     data = batches(cfg, args.batch, L, 1 + args.timed, 1)
     lr = 3e-4
-    res = {}
-    for name, fn in (("reference", time_reference), ("oracle", time_oracle)):
-        ts = fn(cfg, data, lr)
-        med = float(np.median(ts[1:]))
+    res = {"reference": [], "oracle": []}
+    for rd in range(args.rounds):
+        for name, fn in (("reference", time_reference), ("oracle", time_oracle)):
+            ts = fn(cfg, data, lr)
+            res[name] += ts[1:]
+            print(f"round {rd} {name}: steps {', '.join(f'{x:.2f}' for x in ts)} s (first = warm-up)", flush=True)
+    for name in res:
+        med = float(np.median(res[name]))
+        print(f"{name}: median of {len(res[name])} timed steps {med:.2f} s = {args.batch / med:.1f} samples/s",
+              flush=True)
         res[name] = med
-        print(f"{name}: steps {', '.join(f'{x:.2f}' for x in ts)} s (first = warm-up); median {med:.2f} s = "
-              f"{args.batch / med:.1f} samples/s", flush=True)
     ratio = res["oracle"] / res["reference"]
     print(f"cfg2 shape (bs={args.batch}, L={L}, fp32), {torch.get_num_threads()} threads on {cpu_model()}: "
           f"oracle / reference step time = {ratio:.3f} ({'within' if abs(ratio - 1) <= 0.10 else 'OUTSIDE'} 10 %)",

@@ -881,7 +881,11 @@ using namespace ctr;
 static int ctr_attn_force_generic = 0;
 extern "C" void ctr_attn_set_generic(int on) { ctr_attn_force_generic = on; }
 
-extern "C" int ctr_attn_mask_words(int B, int K, int H) { return B * H * K * ((K + 31) / 32); }
+// row layout (this file) or the bf16-MFMA kernels' lane layout (attn_mf.hip: 128 words per head), whichever is larger
+extern "C" int ctr_attn_mask_words(int B, int K, int H) {
+  const int row = K * ((K + 31) / 32);
+  return B * H * (row > 128 ? row : 128);
+}
 
 extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
                             uint32_t drop_key, uint32_t drop_thresh, float drop_scale, uint32_t* mask, float* o,

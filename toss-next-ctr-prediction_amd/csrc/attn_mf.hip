@@ -1,0 +1,595 @@
+// Attention core of DAREEncoderLayer on bf16 MFMA (amp: bf16), K <= 64, head dim dh in {4, 8}.
+// Same algorithm as attn.hip (src/models/dare.py:53-62, torch's MHA explicit path): s_ij = mean_h rel[j-i+tk]
+// + (q_i sqrt(1/dh)) . k_j ; p = softmax_j(s) ; p~ = dropout(p) ; o_i = sum_j p~_ij v_j ; and its backward.
+// Under torch.autocast(bfloat16) the reference runs both attention products (baddbmm(q, k^T) and bmm(p~, v))
+// and their autograd products on bf16 operands with fp32 accumulation; here every product is a
+// v_mfma_f32_16x16x16_bf16 over bf16-rounded q*scale, k, v, dO, p~ and dS, while the softmax, the dropout
+// and dS = p (dp - do.o) stay fp32 (the scores are not rounded to bf16 -- the reference rounds them; ours is
+// the more precise side of that difference).
+//
+// One wave per head, the whole K x K head in registers as 16 x 16 tiles (K padded to 64, nt = ceil(K/16)
+// tiles a side).  Every elementwise step works on the TRANSPOSED score tile S^T = K Q^T, whose MFMA
+// accumulator layout puts key j = 16 tj + 4g + r in register r of lane (g, c) and query i = 16 ti + c in the
+// lane: a softmax row (fixed i) is the lane's registers plus the four lane groups (two permlane swaps), and
+// the tile's registers ARE the B operand of the products that reduce over keys (o^T = v^T p~^T,
+// dq^T = k^T dS^T) -- no data movement.  The products that reduce over queries (dk^T = q^T dS,
+// dv^T = do^T p~) take dS / p~ through a per-wave 16 x 64 LDS image read back with ds_read_b64_tr_b16.
+// Per head: 32 MFMAs forward, 80 backward; per score element ~12 VALU operations (exp, dropout, dS)
+// instead of the ~50 of the VALU kernels (which recompute p in a second pass for dq).
+//
+// Keep bits of p~ (the backward reads them instead of re-hashing) are stored in the lane layout: per head
+// 2 words x 64 lanes, bit 16 (ti & 1) + 4 tj + r of word ti >> 1 in lane (g, c) = element (i = 16 ti + c,
+// j = 16 tj + 4g + r).  The keep decision is the same counter hash as every other dropout site (common.h).
+// mrow holds the row max in log2 units (the forward's and backward's exp2 argument), lrow the row sum.
+#include "common.h"
+#include "ctr_hip.h"
+
+namespace ctr {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int KT = 64;                      // padded K (<= 4 16-key tiles a side)
+constexpr float L2E = 1.4426950408889634f;
+
+struct AttnBfArgs {
+  const float* qkv;      // (B*K, 3D)
+  int B, K, H, D, G, nt, tk;
+  const float* relmean;  // (2tk+1) or null
+  float scale;           // sqrt(1/dh) (the reference's python float in fp32)
+  Drop drop;
+  uint32_t* mask;        // (B*H, 2, 64) keep bits, lane layout
+  float* o;              // (B*K, D)
+  float* mrow;           // (B*H*K) row max, log2 units
+  float* lrow;           // (B*H*K) row sum of exp2(t - max)
+  const float* dO;       // (B*K, D)
+  float* dqkv;           // (B*K, 3D)
+  float* drel_part;      // (B * H/G, 2tk+1)
+};
+
+__device__ __forceinline__ f32x4 mma(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c,
+                                                   0, 0, 0);
+}
+
+// 4 rows x 16 columns of 16-bit elements, transposed (ds_read_b64_tr_b16): lane 4q + p of each 16-lane group
+// addresses row q, columns 4p .. 4p+3; lane i of the group receives column i, row q in element q
+__device__ __forceinline__ bf16x4 tr4(const __bf16* p) {
+  return __builtin_bit_cast(bf16x4,
+                            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p));
+}
+__device__ __forceinline__ bf16x4 ld4(const __bf16* p) { return *(const bf16x4*)p; }
+
+__device__ __forceinline__ bf16x4 to_bf4(f32x4 v) { return __builtin_convertvector(v, bf16x4); }
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// all ones where x's sign bit is set (v_ashrrev_i32 in asm: as C the compiler turns it back into a compare +
+// select, which keeps the lane masks in SGPRs)
+__device__ __forceinline__ uint32_t sign_mask(uint32_t x) {
+  uint32_t m;
+  asm("v_ashrrev_i32 %0, 31, %1" : "=v"(m) : "v"(x));
+  return m;
+}
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// RNE bf16 pairs (v_cvt_pk_bf16_f32 each), as two dwords: one conversion for both the MFMA operand and the
+// LDS image (through to_bf4 the compiler converted twice, differently packed)
+__device__ __forceinline__ u32x2 pk_bf4(f32x4 v) {
+  const bf16x2 lo = __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2), hi = __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2);
+  return u32x2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+}
+
+// all-reduce over the four 16-lane groups (lanes c, c+16, c+32, c+48) by two permlane swaps of two copies of
+// the value: v_permlane16_swap leaves rows (r0 r0 r2 r2) in one copy and (r1 r1 r3 r3) in the other,
+// v_permlane32_swap (lo lo) / (hi hi).  In asm: through __builtin_amdgcn_permlane16/32_swap the compiler
+// (ROCm 7.2) stored the FIRST result for both (measured on gfx950); the s_nop covers the VALU-write ->
+// permlane-read hazard the compiler does not see inside asm.  Same bits in all four lanes (op commutative).
+__device__ __forceinline__ void swap16(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+__device__ __forceinline__ void swap32(float& x, float& y) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y));
+}
+template <class Op>
+__device__ __forceinline__ float grp_reduce(float v, Op op) {
+  float x = v, y = v;
+  swap16(x, y);
+  v = op(x, y);
+  x = v;
+  y = v;
+  swap32(x, y);
+  return op(x, y);
+}
+__device__ __forceinline__ float grp_max(float v) {
+  return grp_reduce(v, [](float p, float q) { return fmaxf(p, q); });
+}
+__device__ __forceinline__ float grp_sum(float v) {
+  return grp_reduce(v, [](float p, float q) { return p + q; });
+}
+
+// Workgroup staging: q * scale, k, v (and dO) of the group's G heads as bf16 [KT][RS] images.  Head u takes
+// HS = dh + 4 slots of a row: its dh dims, then a 4-slot chunk whose first slot carries the padded-key mask
+// through the score product (k: 1 on padded keys j >= K, q: -3e38), zeros elsewhere; rows >= K are zero.
+// An MFMA operand read of lane group g takes slots 4g .. 4g+3 of the head -- groups with 4g >= HS read
+// zeros instead (registers, not LDS) -- so S^T = K Q^T carries -3e38 (-> -inf after the log2 scale) on every
+// padded key and an exact +-0 elsewhere: no per-element masking.
+template <int DH>
+struct Stg {
+  static constexpr int HS = DH + 4;                 // slots per head
+  static constexpr int RS = 4 * HS + 4;             // row stride (bf16 elements), <= 4 heads
+  static constexpr int IM = KT * RS;                // elements per staged operand
+  static constexpr int PAD = 16;                    // transposed reads past the last head of the last row
+  static constexpr int ZOFF = 4 * HS;               // a zero chunk: slots 4 HS .. 4 HS + 3 of row 0
+};
+constexpr float NEG_BIG = -3.0e38f;
+
+template <int DH, bool WITH_DO>
+__device__ __forceinline__ void stage(const AttnBfArgs& a, __bf16* sq, __bf16* sk, __bf16* sv, __bf16* sdo) {
+  using S = Stg<DH>;
+  const int K = a.K, D = a.D, G = a.G, b = blockIdx.x;
+  const float* base = a.qkv + (long)b * K * 3 * D + blockIdx.y * G * DH;
+  const float* dob = WITH_DO ? a.dO + (long)b * K * D + blockIdx.y * G * DH : nullptr;
+  constexpr int NCH = S::HS / 4;                    // 4-slot chunks per head
+  for (int e = threadIdx.x; e < KT * 4 * NCH; e += blockDim.x) {
+    const int ch = e % NCH, ju = e / NCH, u = ju & 3, j = ju >> 2;
+    if (u >= G) continue;
+    f32x4 q = {0.f, 0.f, 0.f, 0.f}, k = q, v = q, d = q;
+    if (4 * ch < DH) {
+      if (j < K) {
+        const float* r = base + (long)j * 3 * D + u * DH + 4 * ch;
+        q = *(const f32x4*)r * a.scale;
+        k = *(const f32x4*)(r + D);
+        v = *(const f32x4*)(r + 2 * D);
+        if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * ch);
+      }
+    } else {                                        // the mask chunk
+      q[0] = NEG_BIG;
+      k[0] = j >= K ? 1.f : 0.f;
+    }
+    const int o = j * S::RS + u * S::HS + 4 * ch;
+    if (e < 1) {                                    // the zero chunk (row 0, past the 4th head)
+      const bf16x4 z4 = {};
+      *(bf16x4*)(sq + S::ZOFF) = z4;
+      *(bf16x4*)(sk + S::ZOFF) = z4;
+      *(bf16x4*)(sv + S::ZOFF) = z4;
+      if (WITH_DO) *(bf16x4*)(sdo + S::ZOFF) = z4;
+    }
+    *(bf16x4*)(sq + o) = to_bf4(q);
+    *(bf16x4*)(sk + o) = to_bf4(k);
+    *(bf16x4*)(sv + o) = to_bf4(v);
+    if (WITH_DO) *(bf16x4*)(sdo + o) = to_bf4(d);
+  }
+}
+
+// positional bias table in LDS, log2 units, padded by RPAD zeros on both sides: the score element
+// (i = 16 ti + c, j = 16 tj + 4g + r) takes rel[j - i + tk] = srel[RPAD + 16 (tj - ti) + 4g + r - c + tk]; the
+// index stays inside the padded table for every padded row / key (whose values are discarded), so each
+// tile's four values are loads at one per-lane base + immediate offsets, no clamping
+constexpr int RPAD = KT;
+__device__ __forceinline__ void stage_rel(const AttnBfArgs& a, float* srel) {
+  const int nrel = 2 * a.tk + 1;
+  for (int e = threadIdx.x; e < nrel + 2 * RPAD; e += blockDim.x) {
+    const int x = e - RPAD;
+    srel[e] = (x >= 0 && x < nrel) ? a.relmean[x] * L2E : 0.f;
+  }
+}
+__host__ __device__ __forceinline__ int rel_floats(int tk) { return (2 * tk + 1 + 2 * RPAD + 3) & ~3; }   // 16-B multiple
+
+// dS / p~ image of one key tile: 64 query rows x 16 keys, bf16, row stride 16; the 4-key chunk ch of row rw
+// stored at chunk ch ^ ((rw >> 2) & 3): the ds_write_b64 of a score tile (16 lanes: rows 16 ti + 0..15, one
+// chunk) and the ds_read_b64_tr_b16 (32 lanes: rows 16 ti + 4g + q, chunks p) are both bank-conflict free
+__device__ __forceinline__ int swz(int rw, int ch) { return rw * 16 + 4 * (ch ^ ((rw >> 2) & 3)); }
+constexpr int IMG = KT * 16;                // bf16 elements per image
+
+// operand reads: row access (lane (g, c) <- slots 4g .. 4g+3 of row `row`; zeros past the head's slots) and
+// transposed column access (lane (g, c) <- column c of rows row0 + 4g .. row0 + 4g + 3)
+// (the row read is unconditional: lanes past the head's slots read the zero chunk at ZOFF of the image)
+template <int DH>
+__device__ __forceinline__ bf16x4 op_row(const __bf16* img, int row, int hs, int g) {
+  return ld4(img + (4 * g < Stg<DH>::HS ? row * Stg<DH>::RS + hs + 4 * g : Stg<DH>::ZOFF));
+}
+template <int DH>
+__device__ __forceinline__ bf16x4 op_col(const __bf16* img, int row0, int hs, int g, int c) {
+  return tr4(img + (row0 + 4 * g + (c >> 2)) * Stg<DH>::RS + hs + 4 * (c & 3));
+}
+
+// ------------------------------------------------------------------------------------------------
+// forward.  NT = the tiles a side (ceil(K / 16)); DROPK: 0 none, 1 K even (pair hashes), 2 K odd
+template <int NT, int DH, bool BIAS, int DROPK>
+__global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
+  using S = Stg<DH>;
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  const int K = a.K, D = a.D, G = a.G;
+  __bf16* sq = smb;
+  __bf16* sk = sq + S::IM;
+  __bf16* sv = sk + S::IM;
+  float* srel = (float*)(sv + S::IM + S::PAD);
+  stage<DH, false>(a, sq, sk, sv, nullptr);
+  if (BIAS) stage_rel(a, srel);
+  __syncthreads();
+  const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = blockIdx.y * G + w, hs = w * S::HS;
+  bf16x4 kop[NT], vtop[NT];
+#pragma unroll
+  for (int tj = 0; tj < NT; ++tj) {
+    kop[tj] = op_row<DH>(sk, 16 * tj + c, hs, g);          // A = k [j][d]
+    vtop[tj] = op_col<DH>(sv, 16 * tj, hs, g, c);          // A = v^T [d][j]
+  }
+  const float* rb = srel + RPAD + a.tk + 4 * g - c;        // + 16 (tj - ti) + r
+  const long hr = ((long)b * a.H + h) * K;                 // (head, row 0)
+  uint32_t words[2] = {0u, 0u};
+  const float dsc = DROPK ? a.drop.scale : 1.0f;
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti) {
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16x4 qop = op_row<DH>(sq, 16 * ti + c, hs, g); // B = q^T [d][i]
+    const int i = 16 * ti + c;
+    f32x4 t[NT];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int tj = 0; tj < NT; ++tj) {
+      const f32x4 s = mma(kop[tj], qop, f32x4{0.f, 0.f, 0.f, 0.f});                    // S^T [j][i]
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        t[tj][r] = BIAS ? fmaf(s[r], L2E, rb[16 * (tj - ti) + r]) : s[r] * L2E;
+        mx = fmaxf(mx, t[tj][r]);
+      }
+    }
+    mx = grp_max(mx);
+    float l = 0.f;
+    uint32_t dropped = 0u;
+    const uint32_t rowbase = (uint32_t)((hr + i) * K);
+    bf16x4 pb[NT];
+#pragma unroll
+    for (int tj = 0; tj < NT; ++tj) {
+      float pe[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pe[r] = __builtin_amdgcn_exp2f(t[tj][r] - mx);
+        l += pe[r];
+      }
+      if (DROPK) {
+        // keep iff the element's 16-bit hash half >= thresh; drop mask m = (half - thresh) >> 31 (arithmetic:
+        // all ones = dropped), p~ = p & ~m, and the dropped-bit word collects m's bit (one v_and_or each) --
+        // integer arithmetic throughout: compares would leave 64 lane masks in SGPRs (spilled).  The masked
+        // values live in a float array: the same and-not on f32x4 elements was miscompiled (ROCm 7.2: every
+        // element masked from element 0's value, found on gfx950 against the torch reference)
+        const uint32_t j0 = 16 * tj + 4 * g;
+        uint32_t half[4];
+        if (DROPK == 1) {     // K even: (j, j+1) for even j is one pair hash
+          const uint32_t h0 = drop_pair_bits(a.drop, (rowbase + j0) >> 1);
+          const uint32_t h1 = drop_pair_bits(a.drop, (rowbase + j0 + 2) >> 1);
+          half[0] = h0 & 0xFFFFu;
+          half[1] = h0 >> 16;
+          half[2] = h1 & 0xFFFFu;
+          half[3] = h1 >> 16;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t idx = rowbase + j0 + r;
+            const uint32_t hb = mix32((idx >> 1) ^ a.drop.key);
+            half[r] = (idx & 1u) ? hb >> 16 : hb & 0xFFFFu;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t m = sign_mask(half[r] - a.drop.thresh);
+          pe[r] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, pe[r]) & ~m);
+          dropped |= m & (1u << (4 * tj + r));
+        }
+      }
+      pb[tj] = __builtin_bit_cast(bf16x4, pk_bf4(f32x4{pe[0], pe[1], pe[2], pe[3]}));
+    }
+    l = grp_sum(l);
+    f32x4 oacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tj = 0; tj < NT; ++tj) oacc = mma(vtop[tj], pb[tj], oacc);               // o^T [d][i]
+    if (i < K) {
+      const float inv = dsc / l;
+      if (4 * g < DH) *(f32x4*)(a.o + ((long)b * K + i) * D + h * DH + 4 * g) = oacc * inv;
+      if (g == 0) {
+        a.mrow[hr + i] = mx;
+        a.lrow[hr + i] = l;
+      }
+    }
+    if (DROPK) words[ti >> 1] |= (~dropped & 0xFFFFu) << (16 * (ti & 1));
+  }
+  if (DROPK) {
+    uint32_t* mk = a.mask + ((long)b * a.H + h) * 128;
+    mk[lane] = words[0];
+    mk[64 + lane] = words[1];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// backward: dq, dk, dv into dqkv; positional-bias grad partials (diagonal sums of dS over the group's heads).
+// Key tiles outer (dk, dv of a key tile complete in its iteration), query tiles inner (dq accumulates).
+template <int NT, int DH, bool BIAS, bool DROP>
+__global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
+  using S = Stg<DH>;
+  constexpr int ND = 2 * NT - 1;
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  const int K = a.K, D = a.D, G = a.G;
+  __bf16* sq = smb;
+  __bf16* sk = sq + S::IM;
+  __bf16* sv = sk + S::IM;
+  __bf16* sdo = sv + S::IM;
+  __bf16* simg = sdo + S::IM + S::PAD;              // per wave: dS image, p~ image
+  float* srel = (float*)(simg + 4 * 2 * IMG);
+  stage<DH, true>(a, sq, sk, sv, sdo);
+  if (BIAS) stage_rel(a, srel);
+  __syncthreads();
+  const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = blockIdx.y * G + w, hs = w * S::HS;
+  __bf16* ids = simg + w * 2 * IMG;
+  __bf16* ipt = ids + IMG;
+  const float* rb = srel + RPAD + a.tk + 4 * g - c;
+  const long hr = ((long)b * a.H + h) * K;
+  // per query row i (lane): {max (log2), 1 / sum, D_i = do_i . o_i} in the wave's LDS row table, read back
+  // per score tile (padded rows: p = 0, D = 0)
+  f32x4* stw = (f32x4*)(srel + rel_floats(BIAS ? a.tk : 0)) + w * KT;
+  {
+    f32x4 st = {0.f, 0.f, 0.f, 0.f};
+    if (lane < K) {
+      const float* dp = a.dO + ((long)b * K + lane) * D + h * DH;
+      const float* op = a.o + ((long)b * K + lane) * D + h * DH;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) {
+        const f32x4 x = *(const f32x4*)(dp + 4 * q), y = *(const f32x4*)(op + 4 * q);
+        s = fmaf(x[0], y[0], s);
+        s = fmaf(x[1], y[1], s);
+        s = fmaf(x[2], y[2], s);
+        s = fmaf(x[3], y[3], s);
+      }
+      st = f32x4{a.mrow[hr + lane], 1.0f / a.lrow[hr + lane], s, 0.f};
+    }
+    stw[lane] = st;
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint32_t words[2] = {0u, 0u};
+  if (DROP) {
+    const uint32_t* mk = a.mask + ((long)b * a.H + h) * 128;
+    words[0] = mk[lane];
+    words[1] = mk[64 + lane];
+  }
+  const uint32_t dsc_bits = __builtin_bit_cast(uint32_t, DROP ? a.drop.scale : 1.0f);
+  f32x4 dq[NT];
+  float dg[ND][4];
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti) dq[ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dg[dt][r] = 0.f;
+#pragma unroll
+  for (int tj = 0; tj < NT; ++tj) {
+    __builtin_amdgcn_sched_barrier(0);     // one key tile at a time: bounds the live registers
+    const int j = 16 * tj + c;
+    const bf16x4 kop = op_row<DH>(sk, j, hs, g);                                       // A = k [j][d]
+    const bf16x4 vop = op_row<DH>(sv, j, hs, g);                                       // A = v [j][d]
+    const bf16x4 ktop = op_col<DH>(sk, 16 * tj, hs, g, c);                             // A = k^T [d][j]
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+      const int i = 16 * ti + c;
+      const bf16x4 qop = op_row<DH>(sq, i, hs, g);                                     // B = q^T [d][i]
+      const bf16x4 doop = op_row<DH>(sdo, i, hs, g);                                   // B = do^T [d][i]
+      const f32x4 s = mma(kop, qop, f32x4{0.f, 0.f, 0.f, 0.f});                       // S^T [j][i]
+      const f32x4 dp = mma(vop, doop, f32x4{0.f, 0.f, 0.f, 0.f});                     // dP~^T [j][i]
+      const f32x4 st = stw[i];
+      f32x4 dsv, ptv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = BIAS ? fmaf(s[r], L2E, rb[16 * (tj - ti) + r]) : s[r] * L2E;
+        const float p = __builtin_amdgcn_exp2f(x - st[0]) * st[1];
+        float dpk = dp[r], pt = p;
+        if (DROP) {   // keep ? 1 / (1 - p) : 0, from the bit's sign-extension
+          const int pos = 16 * (ti & 1) + 4 * tj + r;
+          const float kf = __builtin_bit_cast(
+              float, (uint32_t)__builtin_amdgcn_sbfe((int)words[ti >> 1], pos, 1) & dsc_bits);
+          dpk *= kf;
+          pt *= kf;
+        }
+        const float ds = p * (dpk - st[2]);
+        if (BIAS) dg[tj - ti + NT - 1][r] += ds;
+        dsv[r] = ds;
+        ptv[r] = pt;
+      }
+      const u32x2 dsu = pk_bf4(dsv), ptu = pk_bf4(ptv);
+      dq[ti] = mma(ktop, __builtin_bit_cast(bf16x4, dsu), dq[ti]);                      // dq^T [d][i]
+      *(u32x2*)(ids + swz(i, g)) = dsu;
+      *(u32x2*)(ipt + swz(i, g)) = ptu;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // dk^T [d][j] = sum_i q^T [d][i] dS [i][j], dv^T [d][j] = sum_i do^T [d][i] p~ [i][j]
+    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = dk;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+      const int rw = 16 * ti + 4 * g + (c >> 2);
+      dk = mma(op_col<DH>(sq, 16 * ti, hs, g, c), tr4(ids + swz(rw, c & 3)), dk);      // B = dS [i][j]
+      dv = mma(op_col<DH>(sdo, 16 * ti, hs, g, c), tr4(ipt + swz(rw, c & 3)), dv);     // B = p~ [i][j]
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (4 * g < DH && j < K) {
+      float* dst = a.dqkv + ((long)b * K + j) * 3 * D + h * DH + 4 * g;
+      *(f32x4*)(dst + D) = dk;
+      *(f32x4*)(dst + 2 * D) = dv;
+    }
+  }
+  if (4 * g < DH) {
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+      const int i = 16 * ti + c;
+      if (i < K) *(f32x4*)(a.dqkv + ((long)b * K + i) * 3 * D + h * DH + 4 * g) = dq[ti] * a.scale;
+    }
+  }
+  if (BIAS) {
+    // diagonal sums of dS: register (dt, r) of lane (g, c) holds the sum over the tiles of diagonal dt of
+    // element (a = 4g + r, c) = diagonal 16 (dt - (NT-1)) + a - c.  Heads first (fixed order), then diagonals.
+    __syncthreads();                                    // staging / image space is reused
+    float* sd = (float*)smb;                            // [G][ND][16 a][16 c]
+#pragma unroll
+    for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sd[((w * ND + dt) * 16 + 4 * g + r) * 16 + c] = dg[dt][r];
+    __syncthreads();
+    float* sh = sd + G * ND * 256;                      // [ND][16][16] summed over heads
+    for (int e = threadIdx.x; e < ND * 256; e += blockDim.x) {
+      float s = 0.f;
+      for (int u = 0; u < G; ++u) s += sd[u * ND * 256 + e];
+      sh[e] = s;
+    }
+    __syncthreads();
+    // thread 2 x + half: diagonal d = x - (16 NT - 1); half 0 the tile diagonal with 0 <= d - 16 dt' <= 15,
+    // half 1 the one above it (-16 <= d - 16 dt' <= -1)
+    constexpr int NDG = 2 * 16 * NT - 1;
+    const int nrel = 2 * a.tk + 1;
+    float* out = a.drel_part + ((long)b * gridDim.y + blockIdx.y) * nrel;
+    for (int t0 = 0; t0 < 2 * NDG; t0 += blockDim.x) {
+      const int t = t0 + threadIdx.x;
+      const int x = t >> 1, half = t & 1;
+      const int d = x - (16 * NT - 1);
+      float s = 0.f;
+      if (x < NDG) {
+        const int dth = (d >= 0 ? d : d - 15) / 16;      // floor(d / 16)
+        const int dtp = dth + half;
+        const int e = d - 16 * dtp;
+        const int dtx = dtp + NT - 1;
+        if (dtx >= 0 && dtx < ND) {
+#pragma unroll 4
+          for (int aa = 0; aa < 16; ++aa) {
+            const int cc = aa - e;
+            if (cc >= 0 && cc < 16) s += sh[(dtx * 16 + aa) * 16 + cc];
+          }
+        }
+      }
+      // the pair (half 0, half 1) is lanes (2x, 2x+1): half 0 adds its neighbour's sum
+      const float o = __shfl_xor(s, 1);
+      if (half == 0 && x < NDG) {
+        const int ei = d + a.tk;
+        if (ei >= 0 && ei < nrel) out[ei] = (d > -K && d < K) ? s + o : 0.f;
+      }
+    }
+    // offsets outside [-(16 NT - 1), 16 NT - 1]: zero
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
+      const int d = e - a.tk;
+      if (d < -(16 * NT - 1) || d > 16 * NT - 1) out[e] = 0.f;
+    }
+  }
+}
+
+int pick_g(int H) {
+  int g = 1;
+  for (int c = 1; c <= 4; ++c)
+    if (H % c == 0) g = c;
+  return g;
+}
+
+template <int DH>
+size_t fwd_lds(int tk) { return ((size_t)3 * Stg<DH>::IM + Stg<DH>::PAD) * 2 + (size_t)rel_floats(tk) * 4; }
+
+template <int DH>
+size_t bwd_lds(int G, int NT, int tk) {
+  const size_t main = ((size_t)4 * Stg<DH>::IM + Stg<DH>::PAD) * 2 + (size_t)4 * 2 * IMG * 2 +
+                      (size_t)rel_floats(tk) * 4 + (size_t)4 * KT * 16;
+  const size_t ND = 2 * NT - 1, diag = ((size_t)G * ND * 256 + ND * 256) * 4;
+  return main > diag ? main : diag;
+}
+
+template <int NT, int DH, bool BIAS>
+void launch_fwd4(const AttnBfArgs& a, size_t sm, hipStream_t s) {
+  const dim3 grid(a.B, a.H / a.G), blk(64 * a.G);
+  if (a.drop.thresh == 0) attn_fwd_mf_kernel<NT, DH, BIAS, 0><<<grid, blk, sm, s>>>(a);
+  else if (a.K & 1) attn_fwd_mf_kernel<NT, DH, BIAS, 2><<<grid, blk, sm, s>>>(a);
+  else attn_fwd_mf_kernel<NT, DH, BIAS, 1><<<grid, blk, sm, s>>>(a);
+}
+
+template <int NT, int DH>
+void launch_fwd3(const AttnBfArgs& a, hipStream_t s) {
+  const size_t sm = fwd_lds<DH>(a.relmean ? a.tk : 0);
+  if (a.relmean) launch_fwd4<NT, DH, true>(a, sm, s);
+  else launch_fwd4<NT, DH, false>(a, sm, s);
+}
+
+template <int DH>
+void launch_fwd2(const AttnBfArgs& a, hipStream_t s) {
+  switch (a.nt) {
+    case 1: launch_fwd3<1, DH>(a, s); break;
+    case 2: launch_fwd3<2, DH>(a, s); break;
+    case 3: launch_fwd3<3, DH>(a, s); break;
+    default: launch_fwd3<4, DH>(a, s); break;
+  }
+}
+
+template <int NT, int DH>
+void launch_bwd3(const AttnBfArgs& a, hipStream_t s) {
+  const size_t sm = bwd_lds<DH>(a.G, NT, a.relmean ? a.tk : 0);
+  const dim3 grid(a.B, a.H / a.G), blk(64 * a.G);
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  if (bias && drop) attn_bwd_mf_kernel<NT, DH, true, true><<<grid, blk, sm, s>>>(a);
+  else if (bias) attn_bwd_mf_kernel<NT, DH, true, false><<<grid, blk, sm, s>>>(a);
+  else if (drop) attn_bwd_mf_kernel<NT, DH, false, true><<<grid, blk, sm, s>>>(a);
+  else attn_bwd_mf_kernel<NT, DH, false, false><<<grid, blk, sm, s>>>(a);
+}
+
+template <int DH>
+void launch_bwd2(const AttnBfArgs& a, hipStream_t s) {
+  switch (a.nt) {
+    case 1: launch_bwd3<1, DH>(a, s); break;
+    case 2: launch_bwd3<2, DH>(a, s); break;
+    case 3: launch_bwd3<3, DH>(a, s); break;
+    default: launch_bwd3<4, DH>(a, s); break;
+  }
+}
+
+bool bf_ok(int K, int H, int D) {
+  if (K < 1 || K > KT || H < 1 || D % H) return false;
+  const int dh = D / H;
+  return dh == 4 || dh == 8;
+}
+
+}  // namespace
+}  // namespace ctr
+
+using namespace ctr;
+
+extern "C" int ctr_attn_bf_ok(int K, int H, int D) { return bf_ok(K, H, D) ? 1 : 0; }
+
+extern "C" int ctr_attn_fwd_bf(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,
+                               uint32_t drop_key, uint32_t drop_thresh, float drop_scale, uint32_t* mask, float* o,
+                               float* mrow, float* lrow, void* stream) {
+  if (B == 0) return 0;
+  CTR_REQUIRE(bf_ok(K, H, D), "ctr_attn_fwd_bf: K <= 64 and head dim 4 or 8");
+  CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
+  CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
+  AttnBfArgs a{};
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.nt = (K + 15) / 16; a.tk = tk;
+  a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = mask; a.o = o; a.mrow = mrow; a.lrow = lrow;
+  hipStream_t s = (hipStream_t)stream;
+  if (D / H == 4) launch_fwd2<4>(a, s);
+  else launch_fwd2<8>(a, s);
+  return check_launch("attn_fwd_bf");
+}
+
+extern "C" int ctr_attn_bwd_bf_nparts(int H) { return H / pick_g(H); }
+
+extern "C" int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO, int B, int K, int H, int D,
+                               const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                               float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow,
+                               float* dqkv, float* drel_part, void* stream) {
+  if (B == 0) return 0;
+  CTR_REQUIRE(bf_ok(K, H, D), "ctr_attn_bwd_bf: K <= 64 and head dim 4 or 8");
+  CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
+  CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
+  AttnBfArgs a{};
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.nt = (K + 15) / 16; a.tk = tk;
+  a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = const_cast<uint32_t*>(mask); a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow);
+  a.lrow = const_cast<float*>(lrow); a.dO = dO; a.dqkv = dqkv; a.drel_part = drel_part;
+  hipStream_t s = (hipStream_t)stream;
+  if (D / H == 4) launch_bwd2<4>(a, s);
+  else launch_bwd2<8>(a, s);
+  return check_launch("attn_bwd_bf");
+}

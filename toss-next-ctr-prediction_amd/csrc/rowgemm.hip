@@ -169,7 +169,7 @@ __global__ __launch_bounds__(64) void rowgemm_wgrad_kernel(const float* __restri
                                                            int rows_per_wave, float* __restrict__ slab,
                                                            long ld_slab, int o_db) {
   constexpr int IO = NO / 16, JW = NIN / 16;
-  constexpr int U = 4;                                       // k-steps (4 rows each) loaded together
+  constexpr int U = 8;                                       // k-steps (4 rows each) loaded together
   const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
   const int m_begin = blockIdx.x * rows_per_wave, m_end = min(M, m_begin + rows_per_wave);
   f32x4 acc[IO][JW + 1];                                     // + the ones block (bias grad)
@@ -239,10 +239,13 @@ static bool wgrad_shape(int NO, int NIN) {
   return (NIN == 16 && (NO == 16 || NO == 48)) || (NIN == 32 && (NO == 32 || NO == 96));
 }
 
-// wave w of the weight-grad kernel owns rows [w*rpw, (w+1)*rpw): ~2048 waves, rpw a multiple of 16
+// wave w of the weight-grad kernel owns rows [w*rpw, (w+1)*rpw): ~1024 waves (one per SIMD: the fp32
+// 16x16x4 MFMAs, 32 cycles each, are spread over every SIMD), eight 4-row k-steps of loads in flight each,
+// rpw a multiple of 32 -- a 1024-row slab for the column sum (2048 waves of 4 k-steps wrote 2048 rows for
+// the same loads in flight)
 static void wgrad_split(int M, int* rpw, int* waves) {
-  const int target = std::max(1, std::min(2048, (M + 63) / 64));
-  *rpw = ((M + target - 1) / target + 15) / 16 * 16;
+  const int target = std::max(1, std::min(1024, (M + 63) / 64));
+  *rpw = ((M + target - 1) / target + 31) / 32 * 32;
   *waves = (M + *rpw - 1) / *rpw;
 }
 

@@ -356,6 +356,102 @@ __global__ __launch_bounds__(64) void colsum_final(const float* __restrict__ par
   if (threadIdx.x == 0) out[n] = div == 1.0f ? s : s / div;
 }
 
+// ---------------- several column sums in one launch pair (ctr_colsum_multi) ----------------
+// The backward's per-layer weight-grad slabs (fused FFN, encoder projections) are summed together once the
+// encoder layers are done: two launches instead of two per slab.  Per segment the partial pass is
+// colsum_partial_v4's (256-column tiles, row chunks of rpb rows, four row groups combined in order) and the
+// final pass sums the chunk partials in chunk order -- deterministic, one fixed order per segment.
+struct ColsumSegs {
+  int nseg;
+  int blk0[CTR_COLSUM_MAXSEG + 1];   // partial-pass block prefix over the segments
+  int q0[CTR_COLSUM_MAXSEG + 1];     // final-pass column-quad prefix
+  const float* X[CTR_COLSUM_MAXSEG];
+  float* out[CTR_COLSUM_MAXSEG];
+  long ld[CTR_COLSUM_MAXSEG];
+  long ws0[CTR_COLSUM_MAXSEG];       // float offset of the segment's partials in the workspace
+  int M[CTR_COLSUM_MAXSEG], N[CTR_COLSUM_MAXSEG], rpb[CTR_COLSUM_MAXSEG], np[CTR_COLSUM_MAXSEG];
+  int ctiles[CTR_COLSUM_MAXSEG];
+  float div[CTR_COLSUM_MAXSEG];
+};
+
+__device__ __forceinline__ int seg_of(const int* pre, int n, int x) {
+  int s = 0;
+  while (s + 1 < n && pre[s + 1] <= x) ++s;
+  return s;
+}
+
+__global__ __launch_bounds__(256) void colsum_multi_partial(ColsumSegs S, float* __restrict__ ws) {
+  __shared__ float4 red[4][64];
+  const int s = seg_of(S.blk0, S.nseg, blockIdx.x);
+  const int local = blockIdx.x - S.blk0[s];
+  const int tile = local % S.ctiles[s], part = local / S.ctiles[s];
+  const float* X = S.X[s];
+  const long ld = S.ld[s];
+  const int M = S.M[s], N = S.N[s];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = (tile * 64 + tx) * 4;
+  const int m0 = part * S.rpb[s], m1 = min(M, m0 + S.rpb[s]);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    int m = m0 + ty;
+    for (; m + 12 < m1; m += 16) {
+      const float4 a0 = *reinterpret_cast<const float4*>(X + (long)m * ld + n);
+      const float4 a1 = *reinterpret_cast<const float4*>(X + (long)(m + 4) * ld + n);
+      const float4 a2 = *reinterpret_cast<const float4*>(X + (long)(m + 8) * ld + n);
+      const float4 a3 = *reinterpret_cast<const float4*>(X + (long)(m + 12) * ld + n);
+      a.x += a0.x; a.y += a0.y; a.z += a0.z; a.w += a0.w;
+      a.x += a1.x; a.y += a1.y; a.z += a1.z; a.w += a1.w;
+      a.x += a2.x; a.y += a2.y; a.z += a2.z; a.w += a2.w;
+      a.x += a3.x; a.y += a3.y; a.z += a3.z; a.w += a3.w;
+    }
+    for (; m < m1; m += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(X + (long)m * ld + n);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[ty][tx] = a;
+  __syncthreads();
+  if (ty == 0 && n < N) {
+    const float4 r0 = red[0][tx], r1 = red[1][tx], r2 = red[2][tx], r3 = red[3][tx];
+    float4 o;
+    o.x = ((r0.x + r1.x) + r2.x) + r3.x;
+    o.y = ((r0.y + r1.y) + r2.y) + r3.y;
+    o.z = ((r0.z + r1.z) + r2.z) + r3.z;
+    o.w = ((r0.w + r1.w) + r2.w) + r3.w;
+    *reinterpret_cast<float4*>(ws + S.ws0[s] + (long)part * N + n) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_multi_final(ColsumSegs S, const float* __restrict__ ws) {
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= S.q0[S.nseg]) return;
+  const int s = seg_of(S.q0, S.nseg, q);
+  const int n = 4 * (q - S.q0[s]), N = S.N[s];
+  const float* p = ws + S.ws0[s] + n;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < S.np[s]; ++k) {
+    const float4 v = *reinterpret_cast<const float4*>(p + (long)k * N);
+    a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+  }
+  const float d = S.div[s];
+  if (d != 1.0f) {
+    a.x /= d; a.y /= d; a.z /= d; a.w /= d;
+  }
+  float* o = S.out[s] + n;
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;    // out need not be 16-byte aligned
+}
+
+// row chunk of a segment's partial pass: about 1024 blocks over the segment, at least 64 rows
+static int multi_rpb(int M, int N) {
+  const int ctiles = cdiv(N, 256);
+  return std::min(4096, std::max(64, cdiv((long)M * ctiles, 1024)));
+}
+
+static bool multi_seg_ok(const ctr_colsum_seg_t& g) {
+  return g.X && g.out && g.M > 0 && g.N > 0 && (g.N & 3) == 0 && (g.ld & 3) == 0 && (((uintptr_t)g.X) & 15) == 0 &&
+         g.ld >= g.N;
+}
+
 // ---------------- loss: bce_wll_style(logits) + aux_w * bce_wll_style(aux) and d/dz ----------------
 __global__ __launch_bounds__(1024) void loss_kernel(const float* __restrict__ z, const float* __restrict__ za,
                                                     const float* __restrict__ y, int B, float aux_w,
@@ -519,6 +615,40 @@ extern "C" int ctr_colsum(const float* X, long ld, int M, int N, float div, floa
   if (np <= 16) colsum_final_cols<<<cdiv(N, 256), 256, 0, s>>>(ws, np, N, div, out);
   else colsum_final<<<N, 64, 0, s>>>(ws, np, N, div, out);
   return check_launch("colsum");
+}
+
+extern "C" int ctr_colsum_multi_ok(const ctr_colsum_seg_t* seg) { return seg && multi_seg_ok(*seg) ? 1 : 0; }
+
+extern "C" size_t ctr_colsum_multi_ws_size(const ctr_colsum_seg_t* segs, int nseg) {
+  size_t n = 0;
+  for (int i = 0; i < nseg; ++i) n += (size_t)cdiv(segs[i].M, multi_rpb(segs[i].M, segs[i].N)) * segs[i].N;
+  return n * sizeof(float);
+}
+
+extern "C" int ctr_colsum_multi(const ctr_colsum_seg_t* segs, int nseg, float* ws, size_t ws_bytes, void* stream) {
+  CTR_REQUIRE(nseg >= 0 && nseg <= CTR_COLSUM_MAXSEG, "ctr_colsum_multi: 0 .. CTR_COLSUM_MAXSEG segments");
+  if (nseg == 0) return 0;
+  CTR_REQUIRE(ws_bytes >= ctr_colsum_multi_ws_size(segs, nseg), "ctr_colsum_multi: workspace too small");
+  ColsumSegs S = {};
+  S.nseg = nseg;
+  long wsoff = 0;
+  for (int i = 0; i < nseg; ++i) {
+    const ctr_colsum_seg_t& g = segs[i];
+    CTR_REQUIRE(multi_seg_ok(g), "ctr_colsum_multi: a segment needs M, N > 0, N and ld multiples of 4, 16-byte X");
+    S.X[i] = g.X; S.out[i] = g.out; S.ld[i] = g.ld; S.M[i] = g.M; S.N[i] = g.N;
+    S.div[i] = g.div == 0.0f ? 1.0f : g.div;
+    S.rpb[i] = multi_rpb(g.M, g.N);
+    S.np[i] = cdiv(g.M, S.rpb[i]);
+    S.ctiles[i] = cdiv(g.N, 256);
+    S.ws0[i] = wsoff;
+    wsoff += (long)S.np[i] * g.N;
+    S.blk0[i + 1] = S.blk0[i] + S.ctiles[i] * S.np[i];
+    S.q0[i + 1] = S.q0[i] + g.N / 4;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  colsum_multi_partial<<<S.blk0[nseg], 256, 0, s>>>(S, ws);
+  colsum_multi_final<<<cdiv(S.q0[nseg], 256), 256, 0, s>>>(S, ws);
+  return check_launch("colsum_multi");
 }
 
 extern "C" int ctr_loss(const float* z, const float* za, const float* y, int B, float aux_w, float* loss, float* dz,

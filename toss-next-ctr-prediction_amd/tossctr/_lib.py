@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CTR_LIB_PATH") or os.path.join(_HERE, "libctrhip.so")
 
 p, i, l, f, u, z = C.c_void_p, C.c_int, C.c_long, C.c_float, C.c_uint32, C.c_size_t
+COLSUM_MAXSEG = 16      # CTR_COLSUM_MAXSEG
 
 
 class GemmEpi(C.Structure):
@@ -35,6 +36,10 @@ class OptSeg(C.Structure):
 
 class OptChunk(C.Structure):
     _fields_ = [("seg", C.c_int32), ("pad", C.c_int32), ("e0", C.c_int64), ("e1", C.c_int64)]
+
+
+class ColsumSeg(C.Structure):
+    _fields_ = [("X", p), ("ld", C.c_long), ("M", i), ("N", i), ("out", p), ("div", f), ("pad", i)]
 
 
 class LazyTab(C.Structure):
@@ -76,6 +81,10 @@ SIGS = {
     "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
     "ctr_attn_bwd_nparts": (i, [i, i, i]),
     "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
+    "ctr_attn_bf_ok": (i, [i, i, i]),
+    "ctr_attn_fwd_bf": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
+    "ctr_attn_bwd_bf_nparts": (i, [i]),
+    "ctr_attn_bwd_bf": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_ffn_supported": (i, [i, i, i]),
     "ctr_ffn_slab_rows": (i, [i, i, i, i]),
     "ctr_ffn_mask_words": (i, [i, i]),
@@ -89,6 +98,9 @@ SIGS = {
     "ctr_rmsnorm_bwd": (i, [p, l, p, l, p, p, i, i, p, l, p, l, p, p]),
     "ctr_colsum_ws_size": (z, [i, i]),
     "ctr_colsum": (i, [p, l, i, i, f, p, p, p]),
+    "ctr_colsum_multi_ok": (i, [C.POINTER(ColsumSeg)]),
+    "ctr_colsum_multi_ws_size": (z, [C.POINTER(ColsumSeg), i]),
+    "ctr_colsum_multi": (i, [C.POINTER(ColsumSeg), i, p, z, p]),
     "ctr_loss": (i, [p, p, p, i, f, p, p, p, p]),
     "ctr_qnn_ucat": (i, [p, i, i, i, p, i, p]),
     "ctr_qnn_vfull": (i, [p, i, i, i, p, i, p]),

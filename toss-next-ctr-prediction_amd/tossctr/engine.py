@@ -9,6 +9,7 @@ Buffer names follow the reference's tensors (see the call-stack comments in each
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 import os
 
@@ -128,6 +129,7 @@ class Engine:
         self.G = arena.grad_views
         self.device = arena.device
         self._dev_index = torch.device(self.device).index or 0
+        self._pending_cs = None        # deferred column sums (colsum(defer=True)) while a backward collects them
         _lib.load()
         a = arch
         dev = self.device
@@ -182,6 +184,9 @@ class Engine:
         # FF % 32 == 0); other shapes keep the fp32 kernels (more precise than the reference's bf16)
         self.ffn_flags = 1 if (self.bf16 and self.ffn_fused and
                                _lib.query("ctr_ffn_supported", a.D, a.ffn_hidden, 1)) else 0   # CTR_FFN_BF16
+        # amp: bf16 -> the attention core on bf16 MFMA (attn_mf.hip: K <= 64, head dim 4 or 8), as the
+        # reference's autocast baddbmm / bmm; other shapes keep the fp32 kernels
+        self.attn_bf = bool(self.bf16 and a.n_layers > 0 and _lib.query("ctr_attn_bf_ok", a.top_k, a.H, a.D))
 
     def _tab_array(self, keys, bases):
         """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
@@ -340,7 +345,7 @@ class Engine:
         call("ctr_rowgemm", M, K, N, A, K, W, tb, C, N, bias, add, N if add else 0, resid, N if resid else 0, norm_w,
              norm_h, norm_r, 1e-6, self.s())
 
-    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey, tag=""):
+    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey, tag="", defer=False):
         """dW = dY^T X and db = colsum(dY) of one nn.Linear in one pass (rowgemm.hip): per-wave partial
         slab rows laid out like the grad arena from the weight on, reduced by one fixed-order colsum."""
         o0 = self.arena.offsets[wkey]
@@ -350,11 +355,30 @@ class Engine:
         rows = _lib.query("ctr_rowgemm_wgrad_rows", M)
         slab = W.get_zeroed(f"wg_slab_{n_out}x{n_in}_{tag}", (rows, ld))     # padding columns stay zero
         call("ctr_rowgemm_wgrad", dY, n_out, X, n_in, M, n_out, n_in, ptr(slab), ld, o_db, self.s())
-        self.colsum(ptr(slab), ld, rows, n_sl, ptr(self.arena.grad, o0))
+        self.colsum(ptr(slab), ld, rows, n_sl, ptr(self.arena.grad, o0), defer=defer)
 
-    def colsum(self, X, ld, M, N, out, div=1.0):
+    def colsum(self, X, ld, M, N, out, div=1.0, defer=False):
+        """out = colsum(X) / div.  ``defer``: X is a buffer nothing overwrites before the end of the encoder
+        backward (per-layer slabs) -- queue it for the one ctr_colsum_multi launch pair that sums all of them
+        (flush_colsums) instead of two launches of its own."""
+        if defer and self._pending_cs is not None:
+            seg = _lib.ColsumSeg(X, ld, M, N, out, float(div), 0)
+            if _lib.query("ctr_colsum_multi_ok", C.byref(seg)) and len(self._pending_cs) < _lib.COLSUM_MAXSEG:
+                self._pending_cs.append(seg)
+                return
         w = self.splitk_ws(_lib.query("ctr_colsum_ws_size", M, N) // 4 + 1)
         call("ctr_colsum", X, ld, M, N, float(div), out, ptr(w), self.s())
+
+    def flush_colsums(self):
+        """The deferred column sums, in one launch pair on the current stream (callers: the side stream, after
+        the last producer of the slabs was issued)."""
+        segs, self._pending_cs = self._pending_cs, None
+        if not segs:
+            return
+        arr = (_lib.ColsumSeg * len(segs))(*segs)
+        nb = _lib.query("ctr_colsum_multi_ws_size", arr, len(segs))
+        w = self.splitk_ws(nb // 4 + 1)
+        call("ctr_colsum_multi", arr, len(segs), ptr(w), w.numel() * 4, self.s())
 
     def wgrad(self, dY, ldy, X, ldx, M_rows, n_out, n_in, dW, lddw=None, bias_grad=None):
         """dW[n_out, n_in] = dY^T X over M_rows rows (+ db = colsum(dY))."""
@@ -432,8 +456,8 @@ class Engine:
             da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
             amask = W.get(f"amask{li}", (_lib.query("ctr_attn_mask_words", B, K, a.H),), torch.int32) \
                 if da[1] else None
-            call("ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean), a.top_k, scale, *da, ptr(amask), ptr(o),
-                 ptr(mrow), ptr(lrow), st)
+            call("ctr_attn_fwd_bf" if self.attn_bf else "ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean),
+                 a.top_k, scale, *da, ptr(amask), ptr(o), ptr(mrow), ptr(lrow), st)
             h1 = W.get(f"h1_{li}", (M, D))
             r1 = W.get(f"r1_{li}", (M,))
             x1 = W.get(f"x1_{li}", (M, D))
@@ -673,8 +697,11 @@ class Engine:
             self.colsum(ptr(daux), 1, B, 1, ptr(G["dare.aux_head.bias"]))
         # ---------------- encoder layers, last to first
         dx_other = W.get("dx_b", (B, K, D))
+        self._pending_cs = []          # the layers' slab column sums: one launch pair after the last layer
         for li in reversed(range(a.n_layers)):
             dx, dx_other = self._layer_backward(sv, li, dx, dx_other), dx
+        with self.side():
+            self.flush_colsums()
         # ---------------- top-K select -> dq, table row contributions
         tg = self.tg = {}
         dq = W.get("dq", (B, D))
@@ -783,7 +810,7 @@ class Engine:
             slab_sum = (ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
             if not _REORDER:
                 with self.side():
-                    self.colsum(*slab_sum)
+                    self.colsum(*slab_sum, defer=True)
                 slab_sum = None
         else:
             slab_sum = None
@@ -818,30 +845,32 @@ class Engine:
             if slab_sum is not None:     # main-stream product first, then the side stream's slab sums
                 self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
                 with self.side():
-                    self.colsum(*slab_sum)
+                    self.colsum(*slab_sum, defer=True)
                     self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
-                                    pre + "mha.out_proj.bias", tag=li)
+                                    pre + "mha.out_proj.bias", tag=li, defer=True)
             else:
                 with self.side():
                     self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
-                                    pre + "mha.out_proj.bias", tag=li)
+                                    pre + "mha.out_proj.bias", tag=li, defer=True)
                 self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
         else:
             if slab_sum is not None:
                 with self.side():
-                    self.colsum(*slab_sum)
+                    self.colsum(*slab_sum, defer=True)
             self.wgrad(ptr(dh1), D, ptr(Ls["o"]), D, M, D, D, ptr(G[pre + "mha.out_proj.weight"]),
                        bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
             self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
         # attention core
         dqkv = W.get(f"dqkv{li}", (M, 3 * D))
-        nparts = _lib.query("ctr_attn_bwd_nparts", a.H, K, D) * B
+        nparts = (_lib.query("ctr_attn_bwd_bf_nparts", a.H) if self.attn_bf else
+                  _lib.query("ctr_attn_bwd_nparts", a.H, K, D)) * B
         nrel = 2 * a.top_k + 1
         drp = W.get(f"drel_part{li}", (nparts, nrel))
         da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
         scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
-        call("ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale,
-             *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
+        call("ctr_attn_bwd_bf" if self.attn_bf else "ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H,
+             D, ptr(Ls["relmean"]), a.top_k, scale, *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]),
+             ptr(dqkv), ptr(drp), st)
         x_in = sv["xs"][li]
         # (here the side work goes first: queuing the in_proj input grad ahead of it measured 0.02 ms/step slower)
         with self.side():
@@ -849,7 +878,7 @@ class Engine:
                 call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), self.s())
             if self.rowgemm:
                 self.wgrad_rows(W, ptr(dqkv), ptr(x_in), M, 3 * D, D, pre + "mha.in_proj_weight",
-                                pre + "mha.in_proj_bias", tag=li)
+                                pre + "mha.in_proj_bias", tag=li, defer=True)
         # in_proj
         if self.rowgemm:
             self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
