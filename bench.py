@@ -384,7 +384,9 @@ def main():
         inp, y = data[i % nb]
         opt.param_groups[0]["lr"] = cosine_warmup_lr(0, gstep, steps_per_epoch, tr["lr"], tr["warmup_epochs"],
                                                      tr["epochs"])
-        return model.train_step(inp, y, opt, global_step=gstep + 1)
+        # row-sharded tables: the next batch's exchange is planned beside this step (tossctr/shard.py)
+        nxt = data[(i + 1) % nb][0] if shard else None
+        return model.train_step(inp, y, opt, global_step=gstep + 1, next_inputs=nxt)
 
     g = 0
     for _ in range(args.warmup):

@@ -437,6 +437,16 @@ int ctr_shard_offsets(const uint32_t* keys, const uint32_t* n_ptr, long n, long 
 /* rows (n, ld) -> packed[offsets[i], offsets[i+1]) ; packed -> rows (n, out_ld) zero-padded           */
 int ctr_shard_pack(const float* rows, int ld, long n, const uint32_t* offsets, float* packed, void* stream);
 int ctr_shard_unpack(const float* packed, const uint32_t* offsets, long n, float* out, int out_ld, void* stream);
+/* one exchange per phase: the per-peer pieces of several arrays (keys of both table groups; att rows, rep
+ * rows and packed categorical floats) copied into / out of ONE all-to-all buffer, whose per-peer segments
+ * are contiguous.  segs[0, nseg): n 4-byte words from src to dst (host array, passed by value; nseg <= 96
+ * per launch, more are issued in chunks)                                                             */
+typedef struct {
+  const void* src;
+  void* dst;
+  long long n;
+} ctr_seg_t;
+int ctr_copy_segments(const ctr_seg_t* segs, int nseg, void* stream);
 
 /* ---- fold-ensemble inference tail (src/infer.py:102-158)                                (infer.hip)
  * p = clip(iso(clip(sigmoid(clip(z/T, +-50))))) with the checkpoint's calibrator (has_T: temperature,

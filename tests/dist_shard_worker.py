@@ -3,7 +3,8 @@ ranks before anything in it touches the GPU).  World-2 runs put both ranks on cu
 (host-staged): the same collective sequence the RCCL run issues, on one card.
 
     python tests/dist_shard_worker.py --mode {single,replicated,sharded} --same-batch {0,1}
-                                      --lazy {0,1} [--steps N] [--config tiny|cfg5r] --out FILE
+                                      --lazy {0,1} [--steps N] [--config tiny|cfg5r] [--nccl 1]
+                                      [--prefetch 0|1] [--sync-check 1] --out FILE
 
 --config cfg5r: BASELINE config 5 at reduced scale (tossctr.configs.hb1e8_d64 with hash_buckets=4e6:
 D = 64, the yaml's d_c, 35 tables of 4M rows = 140M rows -> 28-bit owner-major keys at world 2; one
@@ -98,17 +99,26 @@ def run(rank, world, port, args):
     ema = ArenaEMA(model, base_decay=0.9)
     opt = FusedAdamW(model, lr=3e-3, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
                      lazy=bool(args.lazy))
-    losses, batches = [], []
+    losses, batches, staged = [], [], []
     for t in range(args.steps):
         bseed = 1000 + t + (0 if args.same_batch else 100 * rank)
         b = make_batch(Bs, Fn, Fm, list(cards.values()), L, vocab, seed=bseed)
         batches.append(b)
+        staged.append((model.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda()))
+    model.train()
+    for t in range(args.steps):
         opt.param_groups[0]["lr"] = 3e-3 * (1.0 - 0.2 * t)
-        inputs = model.stage(to_torch_batch(b))
-        y = torch.from_numpy(b["y"]).float().cuda()
-        model.train()
-        loss = model.train_step(inputs, y, opt, global_step=t + 1, seed=(9 << 32) | t)
-        losses.append(float(loss.item()))
+        inputs, y = staged[t]
+        # row-sharded: the next batch's exchange is planned beside this step (--prefetch 1, the default)
+        nxt = staged[t + 1][0] if args.prefetch and t + 1 < args.steps else None
+        # --sync-check: from the third step on (the first ones allocate and upload their tables) the step must
+        # not block the host on the device: torch raises on any synchronising call
+        if args.sync_check and t == 2:
+            torch.cuda.set_sync_debug_mode("error")
+        loss = model.train_step(inputs, y, opt, global_step=t + 1, seed=(9 << 32) | t, next_inputs=nxt)
+        losses.append(loss)
+    torch.cuda.set_sync_debug_mode("default")
+    losses = [float(x.item()) for x in losses]
     if args.config == "cfg5r":
         _dump_touched(model, opt, ema, batches, arch, rank, world, losses, args)
     else:
@@ -174,6 +184,10 @@ def main():
     ap.add_argument("--steps", type=int, default=STEPS)
     ap.add_argument("--config", choices=("tiny", "cfg5r"), default="tiny")
     ap.add_argument("--nccl", type=int, default=0, help="world 1 over RCCL instead of world 2 over gloo")
+    ap.add_argument("--prefetch", type=int, default=1, help="plan the next batch's exchange beside each step")
+    ap.add_argument("--sync-check", type=int, default=0,
+                    help="steps >= 2 under torch.cuda.set_sync_debug_mode('error') (needs --nccl 1: gloo stages "
+                         "through the host)")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     if args.mode == "single":

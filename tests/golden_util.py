@@ -204,13 +204,22 @@ def _exact_subset(fx, name):
     return idx, vals
 
 
-def check_bf16_band(fx16, fx32, name, got, label=None, update=False, p0=None):
+def check_bf16_band(fx16, fx32, name, got, label=None, update=False, p0=None, flips=0):
     """amp: bf16 parity.  ``got`` (the build under amp: bf16) is compared with the reference run under
     autocast(bfloat16) (``fx16``) and in fp32 (``fx32``, the twin fixture): the norm of the difference
     to EACH must stay within BF16_BAND x the reference's own bf16-vs-fp32 deviation, or BF16_FLOOR of
     the tensor's norm.  Norms over the whole tensor when it is stored in full, else over the exact
     sampled elements + touched rows (the same subset for all three), and the projected whole-tensor
-    estimate within twice that bound."""
+    estimate within twice that bound.
+
+    ``flips`` (multi-step runs only: moments and updates after >= 2 AdamW steps): up to that many LONE
+    outlier elements -- one element carrying more than half of the squared deviation -- are left out of
+    all three norms.  AdamW's first step moves every element by ~lr sign(g): an element whose step-0
+    gradient is within bf16 rounding of 0 steps either way, which changes its (and its neighbours') later
+    gradients by far more than rounding.  Measured (tools/amp_band_report.py, profiles/r03/amp_band_*.log):
+    cfg4_full_bf16's vT/qnn.mlp.0.weight is 3.5x its band with ONE of its 2048 sampled elements carrying
+    94 % of the squared deviation (the reference's own bf16-vs-fp32 band: one element 48 %, ten 97 %);
+    every other tensor of the five cases is within 1.5x.  Tensors under BF16_FEW elements never drop one."""
     label = label or f"{fx16.name}:{name}"
     if isinstance(got, torch.Tensor):
         got = got.detach().cpu().double().numpy()
@@ -225,6 +234,21 @@ def check_bf16_band(fx16, fx32, name, got, label=None, update=False, p0=None):
         idx, r16, r32 = idx[have], r16[have], r32[sel[have]]
     g = got if idx is None else got[idx]
     assert g.shape == r16.shape == r32.shape, (label, g.shape, r16.shape, r32.shape)
+    p0s = None
+    if update and p0 is not None:
+        p0 = np.asarray(p0.detach().cpu().double().numpy() if isinstance(p0, torch.Tensor) else p0, np.float64).ravel()
+        p0s = p0 if idx is None else p0[idx]
+    if flips and g.size >= BF16_FEW:
+        keep = np.ones(g.size, bool)
+        for _ in range(flips):
+            d = np.maximum((g - r16) ** 2, (g - r32) ** 2) * keep
+            j = int(np.argmax(d))
+            if d[j] <= 0.5 * d.sum():
+                break
+            keep[j] = False
+        if not keep.all():
+            g, r16, r32 = g[keep], r16[keep], r32[keep]
+            p0s = None if p0s is None else p0s[keep]
     band = float(np.linalg.norm(r32 - r16))
     nrm = max(float(np.linalg.norm(r16)), float(np.linalg.norm(r32)))
     floor = (BF16_FLOOR if got.size >= BF16_FEW else BF16_FEW_FLOOR) * nrm
@@ -233,13 +257,11 @@ def check_bf16_band(fx16, fx32, name, got, label=None, update=False, p0=None):
         # bf16 noise of 0 steps either way, and one such flip moves a small tensor's update (or its EMA
         # shadow's) by up to twice its largest element
         floor = max(floor, 2.0 * max(float(np.abs(r16).max(initial=0)), float(np.abs(r32).max(initial=0))))
-    if update and p0 is not None:
+    if p0s is not None:
         # an update pT - p0 (or the EMA shadow's) carries the fp32 rounding of the result itself: 2 ulps per
         # element, as the fp32 checks allow (Fixture.check_update).  Where the reference's bf16 and fp32 runs
         # round alike (band 0: a parameter without gradient, whose EMA shadow d s + (1 - d) p drifts by
         # rounding alone) this is the whole tolerance
-        p0 = np.asarray(p0.detach().cpu().double().numpy() if isinstance(p0, torch.Tensor) else p0, np.float64).ravel()
-        p0s = p0 if idx is None else p0[idx]
         floor += float(np.linalg.norm(2.0 * np.spacing(np.abs(p0s + r32).astype(np.float32)).astype(np.float64)))
     tol = BF16_BAND * band + floor + 1e-30
     e16, e32 = float(np.linalg.norm(g - r16)), float(np.linalg.norm(g - r32))

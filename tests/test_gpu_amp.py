@@ -82,16 +82,18 @@ def test_bf16_fused_steps_within_band(case):
         if tr["clip"] > 0:
             scalar_band(float(opt.norm_out[0].item()), float(f16.z[f"out{t}/gnorm"]), float(f32.z[f"out{t}/gnorm"]),
                         f"{case} gnorm {t}")
+    # after the first AdamW step a lone element may take the other sign step (golden_util.check_bf16_band)
+    fl = 1 if m["steps"] > 1 else 0
     sd = model.state_dict()
     for k, v in sd.items():
-        check_bf16_band(f16, f32, f"dT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k])
+        check_bf16_band(f16, f32, f"dT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k], flips=fl)
     ar = model.arena
     for k in m["grad_keys"]:
-        check_bf16_band(f16, f32, f"mT/{k}", ar._view(opt.m, k))
-        check_bf16_band(f16, f32, f"vT/{k}", ar._view(opt.v, k))
+        check_bf16_band(f16, f32, f"mT/{k}", ar._view(opt.m, k), flips=fl)
+        check_bf16_band(f16, f32, f"vT/{k}", ar._view(opt.v, k), flips=fl)
     if ema is not None:
         for k, v in ema.shadow_params().items():
-            check_bf16_band(f16, f32, f"demaT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k])
+            check_bf16_band(f16, f32, f"demaT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k], flips=fl)
 
 
 def test_bf16_differs_from_fp32_build():

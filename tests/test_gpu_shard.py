@@ -25,13 +25,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 _cache = {}
 
 
-def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0):
-    key = (mode, same, lazy, steps, config, nccl)
+def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0, prefetch=1, sync_check=0):
+    key = (mode, same, lazy, steps, config, nccl, prefetch, sync_check)
     if key not in _cache:
-        out = str(tmp_path_factory.mktemp("shard") / f"{mode}_{same}_{lazy}_{steps}_{config}_{nccl}.pt")
+        out = str(tmp_path_factory.mktemp("shard") / ("_".join(map(str, key)) + ".pt"))
         r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", mode,
                             "--same-batch", str(same), "--lazy", str(lazy), "--steps", str(steps), "--config", config,
-                            "--nccl", str(nccl), "--out", out], capture_output=True, text=True, timeout=250)
+                            "--nccl", str(nccl), "--prefetch", str(prefetch), "--sync-check", str(sync_check),
+                            "--out", out], capture_output=True, text=True, timeout=250)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         if config == "tiny":
             _cache[key] = torch.load(out, weights_only=True)
@@ -183,3 +184,23 @@ def test_rccl_world1_equals_single(tmp_path_factory, mode):
     for k in single["sd"]:
         assert torch.equal(got["sd"][k], single["sd"][k]), k
         assert torch.equal(got["ema"][k], single["ema"][k]), k
+
+
+def test_sharded_prefetch_equals_in_place_plan(tmp_path_factory):
+    """The next batch's exchange planned beside the step (a plan stream, two plan slots) = planned in place at
+    the step's fetch: bit for bit, world 2 with different batches per rank."""
+    pre = _run(tmp_path_factory, "sharded", 0)
+    inplace = _run(tmp_path_factory, "sharded", 0, prefetch=0)
+    assert pre["losses"] == inplace["losses"]
+    for k in pre["sd"]:
+        assert torch.equal(pre["sd"][k], inplace["sd"][k]), k
+        assert torch.equal(pre["ema"][k], inplace["ema"][k]), k
+
+
+def test_rccl_sharded_step_never_blocks_the_host(tmp_path_factory):
+    """The row-sharded step over RCCL issues without a host synchronisation: steps 2-5 of a world-1 run run
+    under torch.cuda.set_sync_debug_mode("error") (the exchange sizes come from counts planned beside the
+    previous step, read from pinned memory), and the run still equals the single-GPU one."""
+    single = _run(tmp_path_factory, "single", 1, steps=6)
+    got = _run(tmp_path_factory, "sharded", 1, steps=6, nccl=1, sync_check=1)
+    _compare(got, single, 1e-5, what="RCCL world-1 sharded (sync-checked) vs single: ")

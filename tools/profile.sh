@@ -9,6 +9,7 @@
 #     pmc       one rocprofv3 --pmc pass per counter group (FETCH_SIZE / WRITE_SIZE separately, as
 #               MI355X_MICROARCH.md prescribes), 3 timed steps with markers
 #     pmc4      the same counter groups at --config cfg4
+#     trace4    the kernel trace at --config cfg4 (6 timed steps)
 #     bench     the default bench line (100 timed steps + CPU baseline) and the driver's 20 + 5
 #     cfgs      cfg3 / cfg4 bench lines (parity configs, not the headline)
 #   default: trace pmc bench
@@ -40,6 +41,9 @@ for s in $steps; do
           python bench.py --steps 20 --warmup 10 --no-cpu-baseline --markers > "$out/trace.log" 2>&1 ;;
     pmc) pmc_groups "" cfg2 ;;
     pmc4) pmc_groups "_cfg4" cfg4 ;;
+    trace4)
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace4" -o trace4 -- \
+          python bench.py --config cfg4 --steps 6 --warmup 3 --no-cpu-baseline --markers > "$out/trace4.log" 2>&1 ;;
     bench)
       timeout -k 10 240 python bench.py > "$out/bench_n1.log" 2>&1
       timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$out/bench_n1_s20.log" 2>&1 ;;

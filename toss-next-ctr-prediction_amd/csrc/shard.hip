@@ -175,6 +175,31 @@ __global__ void shard_unpack_kernel(const float* __restrict__ packed, const uint
   }
 }
 
+// ctr_copy_segments: one workgroup row per segment (blockIdx.y), the segment table passed by value in the
+// kernel arguments (no upload).  16-byte moves when both ends are 16-byte aligned (att / rep rows of D floats
+// always are), 4-byte moves otherwise (the packed categorical runs start at arbitrary floats).
+constexpr int SEG_MAX = 96;
+struct SegArgs {
+  ctr_seg_t s[SEG_MAX];
+};
+
+__global__ __launch_bounds__(256) void copy_segments_kernel(const SegArgs a) {
+  const ctr_seg_t sg = a.s[blockIdx.y];
+  const long n = (long)sg.n;
+  const long t0 = blockIdx.x * 256L + threadIdx.x, step = gridDim.x * 256L;
+  if ((((uintptr_t)sg.src | (uintptr_t)sg.dst) & 15) == 0) {
+    const long n4 = n >> 2;
+    const uint4* s4 = (const uint4*)sg.src;
+    uint4* d4 = (uint4*)sg.dst;
+    for (long i = t0; i < n4; i += step) d4[i] = s4[i];
+    for (long i = (n4 << 2) + t0; i < n; i += step) ((uint32_t*)sg.dst)[i] = ((const uint32_t*)sg.src)[i];
+  } else {
+    const uint32_t* s = (const uint32_t*)sg.src;
+    uint32_t* d = (uint32_t*)sg.dst;
+    for (long i = t0; i < n; i += step) d[i] = s[i];
+  }
+}
+
 struct PlanWs {
   size_t temp_bytes, total;
   size_t off_okeys, off_iota, off_skeys, off_sidx, off_flags, off_seg;
@@ -307,4 +332,24 @@ extern "C" int ctr_shard_unpack(const float* packed, const uint32_t* offsets, lo
   if (n <= 0) return 0;
   shard_unpack_kernel<<<grid_for(n * out_ld), 256, 0, (hipStream_t)stream>>>(packed, offsets, n, out, out_ld);
   return check_launch("shard_unpack");
+}
+
+extern "C" int ctr_copy_segments(const ctr_seg_t* segs, int nseg, void* stream) {
+  CTR_REQUIRE(nseg >= 0 && (nseg == 0 || segs != nullptr), "ctr_copy_segments: bad segment table");
+  for (int s0 = 0; s0 < nseg; s0 += SEG_MAX) {
+    SegArgs a{};
+    int k = 0;
+    long maxn = 0;
+    for (int s = s0; s < nseg && s < s0 + SEG_MAX; ++s) {
+      if (segs[s].n <= 0) continue;
+      CTR_REQUIRE(segs[s].src != nullptr && segs[s].dst != nullptr, "ctr_copy_segments: null segment pointer");
+      a.s[k++] = segs[s];
+      maxn = std::max<long>(maxn, (long)segs[s].n);
+    }
+    if (k == 0) continue;
+    // ~4 KB per workgroup pass at 16-byte moves; at most 64 workgroups per segment
+    const int gx = (int)std::min<long>(std::max<long>((maxn + 4095) / 4096, 1), 64);
+    copy_segments_kernel<<<dim3(gx, k), 256, 0, (hipStream_t)stream>>>(a);
+  }
+  return check_launch("copy_segments");
 }

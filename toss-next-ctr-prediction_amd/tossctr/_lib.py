@@ -42,6 +42,10 @@ class ColsumSeg(C.Structure):
     _fields_ = [("X", p), ("ld", C.c_long), ("M", i), ("N", i), ("out", p), ("div", f), ("pad", i)]
 
 
+class Seg(C.Structure):
+    _fields_ = [("src", p), ("dst", p), ("n", C.c_longlong)]
+
+
 class LazyTab(C.Structure):
     _fields_ = [("p_off", C.c_int64), ("rows", C.c_int64), ("width", C.c_int32), ("key_base", C.c_uint32),
                 ("last", p)]
@@ -139,6 +143,7 @@ SIGS = {
     "ctr_shard_offsets": (i, [p, p, l, l, u, p, p, i, p, i, i, p, p, z, p]),
     "ctr_shard_pack": (i, [p, i, l, p, p, p]),
     "ctr_shard_unpack": (i, [p, p, l, p, i, p]),
+    "ctr_copy_segments": (i, [C.POINTER(Seg), i, p]),
     "ctr_calibrate": (i, [p, i, f, i, p, p, i, p, p]),
     "ctr_ensemble": (i, [p, i, i, i, p, i, p, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),

@@ -388,9 +388,10 @@ class Engine:
             self.colsum(dY, ldy, M_rows, n_out, bias_grad)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, X_num, X_mask, X_cat, seq, training: bool, seed: int, save: bool):
+    def forward(self, X_num, X_mask, X_cat, seq, training: bool, seed: int, save: bool, prefetch=None):
         """CTRModel.forward (src/models/wrapper.py:138-176). Inputs are device tensors:
         X_num f32 (B,Fn), X_mask f32 (B,Fm), X_cat int32 (B,Fc), seq int32 (B,L).
+        ``prefetch`` = the next batch's (X_cat, seq): row-sharded tables plan its exchange beside this step.
         Returns (logits, prob, aux) views into workspace buffers, and the saved context."""
         a, P = self.a, self.P
         B, L = int(X_cat.shape[0]), int(seq.shape[1])
@@ -414,6 +415,8 @@ class Engine:
         cat_e = W.get("cat_e", (B, a.Fc, D))
         tv = self._table_views(X_cat, seq)
         sv["tv"] = tv
+        if prefetch is not None and self.shards is not None:
+            self.shards.prefetch(*prefetch)
         dk = drop_args(seed, SITE_EMB, a.p_emb, training)
         call("ctr_cat_embed_fwd", ptr(tv["xcat"]), B, a.Fc, ptr(self.arena.buf), tv["cat_tab"], tv["cat_off"],
              ptr(self.cat_proj_off), ptr(self.cat_dims_t), tv["cat_ld"], D, ptr(cat_e), ptr(xF, cat_off), FD, *dk, st)

@@ -365,7 +365,9 @@ class FusedAdamW:
                 o.keys, o.G, o.n_uniq = s.get("keys"), s.get("G"), s.get("n_uniq")
                 o.g_ld, o.key_base = s.get("g_ld", 0), s.get("key_base", 0)
             raw = np.frombuffer(bytes(arr), dtype=np.uint8).copy()
-            self._segs_dev = torch.from_numpy(raw).to(self.arena.device)
+            # pinned + non-blocking: a rebuild (row-sharded exchange buffers that grew) must not stall the host
+            # on the device (the host allocator keeps the pinned block until the copy has run)
+            self._segs_dev = torch.from_numpy(raw).pin_memory().to(self.arena.device, non_blocking=True)
             self._seg_key = key
         return self._segs_dev
 

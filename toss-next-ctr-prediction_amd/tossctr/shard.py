@@ -14,9 +14,13 @@ are all 1/world per GPU), and a step exchanges only the rows a batch uses:
            ranks' contributions in rank order (deterministic) -> clip / AdamW / EMA on local rows.
 
 Per rank and step that is the batch's unique rows twice (rows out, grads back; categorical rows at their
-table's width d_c) instead of world x (all ranks' grads) for the replicated all-gather.  One host read of
-per-owner counts per step (forward) sizes every all-to-all of the step: the grads go back along the
-forward's request splits.
+table's width d_c) instead of world x (all ranks' grads) for the replicated all-gather.  Four all-to-alls per
+step: per-owner counts (3 numbers per peer), requested keys (both table groups in one buffer), rows back
+(att, rep and packed categorical rows in one buffer), grads to the owners (the same three in one buffer,
+along the forward's splits).  RCCL needs the splits on the host: the counts of batch t+1 are planned on a
+stream of their own while step t runs (``prefetch``, issued by ``CTRModel.train_step(next_inputs=...)``)
+and copied to pinned memory, so the host's read at step t+1 waits on nothing in flight.  Without a
+prefetch the plan runs in place and the read waits for it.
 
 The pad token's rows are never fetched: fetched row 0 is zero, which is what ``padding_idx`` keeps
 the pad rows at (zero init, zero grad, so AdamW/EMA leave them at zero).
@@ -76,6 +80,11 @@ class _Grow:
         return t[:n] if width is None else t[:n]
 
 
+class _Plan:
+    """One batch's exchange plan: its sorted owner-major unique keys, the batch remapped to fetched-row ids, the
+    categorical wire offsets, and the per-peer counts (device, then pinned host once ``event`` completes)."""
+
+
 class TableShards:
     """Owner map, fetch (forward) and grad routing (backward) for one CTRModel's tables."""
 
@@ -111,6 +120,10 @@ class TableShards:
         self.tabs_seq = None    # device ctr_lazy_tab_t arrays of the local shards (set by the engine)
         self.tabs_cat = None
         self.arena_buf = None   # the rank's parameter arena (local table shards)
+        self._slot = 0          # plan buffer slot of the next plan (alternates)
+        self._plan_stream = None
+        self._pending = None    # the plan prefetch() issued for the next fetch()
+        self._host = {}         # pinned count buffers per slot
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -127,7 +140,7 @@ class TableShards:
         remap = self.buf.get(f"{name}_remap", n, dtype=torch.int32)
         cnt = self.buf.get(f"{name}_cnt", self.world, dtype=torch.int64)
         wsz = _lib.query("ctr_shard_plan_ws_size", n)
-        ws = self.buf.get("plan_ws", wsz, dtype=torch.uint8)
+        ws = self.buf.get(f"{name}_ws", wsz, dtype=torch.uint8)
         if mode == 0:
             call("ctr_shard_plan", _ptr(X), n, 1, 0, self.a.pad_id, None, self.world, self.seq_lbits, self.seq_kbits,
                  _ptr(uniq), _ptr(nu), _ptr(remap), _ptr(cnt), _ptr(ws), wsz, self._stream())
@@ -140,43 +153,123 @@ class TableShards:
         """Offsets of categorical keys' rows at their table widths (and per-owner float counts)."""
         off = self.buf.get(f"{name}_off", cap + 1, dtype=torch.int32)
         wsz = _lib.query("ctr_shard_offsets_ws_size", cap)
-        ws = self.buf.get("off_ws", wsz, dtype=torch.uint8)
+        ws = self.buf.get(f"{name}_off_ws", wsz, dtype=torch.uint8)
         call("ctr_shard_offsets", _ptr(keys), _ptr(n_ptr), n, cap, self._mask(self.cat_lbits), _ptr(self.cat_lbase),
              _ptr(self.cat_dims), self.a.Fc, _ptr(off), self.world, self.cat_lbits, _ptr(counts), _ptr(ws), wsz,
              self._stream())
         return off
 
-    def _counts(self, name, *vecs):
-        """All-to-all of per-owner count vectors; ONE host read returns, per vector, (what this rank sends to
-        each owner, what it receives from each rank) -- the only host synchronisation of a step."""
-        W, k = self.world, len(vecs)
-        send = self.buf.get(f"{name}_csend", k * W, dtype=torch.int64).view(W, k)
-        for j, v in enumerate(vecs):
+    # ------------------------------------------------------------------ plan (ids -> owners; no host read)
+    def _issue_plan(self, X_cat, seq):
+        """Dedup + owner-major keys of one batch, the per-owner counts all-to-all, and an asynchronous copy of
+        the counts into pinned host memory, all on the current stream.  Plans alternate between two buffer
+        slots, so a prefetched plan never writes what the step in flight reads."""
+        W, slot = self.world, self._slot
+        self._slot ^= 1
+        pl = _Plan()
+        pl.X_cat, pl.seq = X_cat, seq
+        pl.uniq_s, _, pl.seq_c, cnt_s = self._plan(f"seq{slot}", seq, 1, 0)
+        pl.uniq_c, nu_c, pl.xcat_c, cnt_c = self._plan(f"cat{slot}", X_cat, X_cat.shape[1], 1)
+        fcnt = self.buf.get(f"fcnt{slot}", W, dtype=torch.int64)
+        pl.off_c = self._offsets(f"req{slot}", pl.uniq_c, nu_c, 0, X_cat.numel(), fcnt)
+        send = self.buf.get(f"csend{slot}", 3 * W, dtype=torch.int64).view(W, 3)
+        for j, v in enumerate((cnt_s, cnt_c, fcnt)):
             send[:, j].copy_(v)
-        recv = self.buf.get(f"{name}_crecv", k * W, dtype=torch.int64)
-        D.all_to_all_var(recv, send.view(-1), [k] * W, [k] * W, self.group)
-        h = torch.cat([send.view(-1), recv]).cpu().tolist()
-        return [h[j:k * W:k] for j in range(k)], [h[k * W + j::k] for j in range(k)]
+        recv = self.buf.get(f"crecv{slot}", 3 * W, dtype=torch.int64)
+        D.all_to_all_var(recv, send.view(-1), [3] * W, [3] * W, self.group)
+        host = self._host.get(slot)
+        if host is None:
+            host = self._host[slot] = torch.empty(6 * W, dtype=torch.int64, pin_memory=True)
+        host[:3 * W].copy_(send.view(-1), non_blocking=True)
+        host[3 * W:].copy_(recv, non_blocking=True)
+        pl.host = host
+        pl.event = torch.cuda.Event()
+        pl.event.record(torch.cuda.current_stream(self.device))
+        return pl
+
+    def prefetch(self, X_cat, seq):
+        """Plan the NEXT batch's exchange now, on a stream of its own: it runs beside the current step, so the
+        next fetch() finds its counts on the host without waiting.  Its buffers are written only after
+        everything queued so far on the current stream (the step in flight may still read the other slot)."""
+        cur = torch.cuda.current_stream(self.device)
+        if self._plan_stream is None:
+            self._plan_stream = torch.cuda.Stream(device=self.device)
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._plan_stream.wait_event(ev)
+        with torch.cuda.stream(self._plan_stream):
+            self._pending = self._issue_plan(X_cat, seq)
+
+    def _take_plan(self, X_cat, seq):
+        pl, self._pending = self._pending, None
+        if pl is not None and pl.X_cat is X_cat and pl.seq is seq:
+            torch.cuda.current_stream(self.device).wait_event(pl.event)
+        else:
+            pl = self._issue_plan(X_cat, seq)
+        # the host's only wait of the step: on counts computed beside the previous step when prefetched
+        pl.event.synchronize()
+        W = self.world
+        h = pl.host.tolist()
+        pl.send = [h[j:3 * W:3] for j in range(3)]
+        pl.recv = [h[3 * W + j::3] for j in range(3)]
+        return pl
+
+    # ------------------------------------------------------------------ one buffer per exchange
+    def _wire(self, counts, widths):
+        """Per-peer segments of several 4-byte arrays in one all-to-all buffer: peer w's segment holds, for
+        each array b, its counts[b][w] rows of widths[b] words (the arrays' rows are grouped by peer in rank
+        order).  Returns the pieces (array, word offset in the array, word offset in the wire, words), the
+        words per peer and the total."""
+        pieces, per_peer, off = [], [], 0
+        pref = [0] * len(counts)
+        for w in range(self.world):
+            start = off
+            for b, (c, wd) in enumerate(zip(counts, widths)):
+                n = int(c[w]) * wd
+                if n:
+                    pieces.append((b, pref[b] * wd, off, n))
+                off += n
+                pref[b] += int(c[w])
+            per_peer.append(off - start)
+        return pieces, per_peer, off
+
+    def _copy(self, pieces, arrays, wire, to_wire):
+        segs = (_lib.Seg * max(1, len(pieces)))()
+        wp = wire.data_ptr()
+        for i, (b, aoff, woff, n) in enumerate(pieces):
+            ap = arrays[b].data_ptr() + 4 * aoff
+            segs[i].src, segs[i].dst = (ap, wp + 4 * woff) if to_wire else (wp + 4 * woff, ap)
+            segs[i].n = n
+        call("ctr_copy_segments", segs, len(pieces), self._stream())
+
+    def _exchange(self, name, send_arrays, recv_arrays, send_counts, recv_counts, widths, dtype):
+        """ONE all-to-all for several arrays: gather their per-peer pieces into a wire buffer, exchange,
+        scatter the received pieces into the receive arrays."""
+        sp, s_peer, s_tot = self._wire(send_counts, widths)
+        rp, r_peer, r_tot = self._wire(recv_counts, widths)
+        ws = self.buf.get(f"{name}_wsend", s_tot, dtype=dtype)
+        wr = self.buf.get(f"{name}_wrecv", r_tot, dtype=dtype)
+        self._copy(sp, send_arrays, ws, True)
+        D.all_to_all_var(wr, ws, r_peer, s_peer, self.group)
+        self._copy(rp, recv_arrays, wr, False)
 
     # ------------------------------------------------------------------ forward
     def fetch(self, X_cat, seq):
         """Rows the batch reads, fetched from their owners.  Returns the remapped batch (fetched-row
         ids; 0 = pad) and the compact tables: att/rep (1 + n_uniq, D) with row 0 zero, cat (1 + n, 64).
-        Categorical rows travel at their table's width d_c (packed), not as 64-float rows."""
+        Categorical rows travel at their table's width d_c (packed), not as 64-float rows.  Two all-to-alls:
+        the requested keys of both table groups, then the att, rep and categorical rows in one buffer."""
         a, st = self.a, self._stream()
         Dm, LD = a.D, self.CAT_LD
-        uniq_s, _, seq_c, cnt_s = self._plan("seq", seq, 1, 0)
-        uniq_c, nu_c, xcat_c, cnt_c = self._plan("cat", X_cat, X_cat.shape[1], 1)
-        fcnt = self.buf.get("fcnt_c", self.world, dtype=torch.int64)
-        off_c = self._offsets("req", uniq_c, nu_c, 0, X_cat.numel(), fcnt)
-        (send_s, send_c, send_f), (recv_s, recv_c, recv_f) = self._counts("fwd", cnt_s, cnt_c, fcnt)
+        pl = self._take_plan(X_cat, seq)
+        (send_s, send_c, send_f), (recv_s, recv_c, recv_f) = pl.send, pl.recv
         ns, nc = sum(send_s), sum(send_c)
         rs, rc = sum(recv_s), sum(recv_c)
-        # requested keys -> owners
+        # requested keys -> owners (sequence and categorical keys in one exchange)
         req_s = self.buf.get("req_s", rs, dtype=torch.int32)
         req_c = self.buf.get("req_c", rc, dtype=torch.int32)
-        D.all_to_all_var(req_s, uniq_s[:ns], recv_s, send_s, self.group)
-        D.all_to_all_var(req_c, uniq_c[:nc], recv_c, send_c, self.group)
+        self._exchange("keys", (pl.uniq_s, pl.uniq_c), (req_s, req_c), (send_s, send_c), (recv_s, recv_c), (1, 1),
+                       torch.int32)
         # owner side: local keys, rows brought current, rows gathered (categorical ones packed at d_c)
         loc_s = self.buf.get("loc_s", rs, dtype=torch.int32)
         loc_c = self.buf.get("loc_c", rc, dtype=torch.int32)
@@ -195,18 +288,18 @@ class TableShards:
         off_o = self._offsets("own", req_c, None, rc, rc)
         pk_o = self.buf.get("cat_pk_o", sum(recv_f))
         call("ctr_shard_pack", _ptr(out_cat), LD, rc, _ptr(off_o), _ptr(pk_o), st)
-        # rows back, in the requester's unique-key order (fetched row u + 1 = unique key u)
+        # rows back, in the requester's unique-key order (fetched row u + 1 = unique key u).  Row 0 (pad) of
+        # att / rep / cat is zeroed once when the buffer is allocated and never written.
         att = self.buf.get("att", 1 + seq.numel(), Dm, zero=True)
         rep = self.buf.get("rep", 1 + seq.numel(), Dm, zero=True)
         cat = self.buf.get("cat", 1 + X_cat.numel(), LD, zero=True)
         pk_r = self.buf.get("cat_pk_r", sum(send_f))
-        D.all_to_all_var(att[1:1 + ns], out_att, send_s, recv_s, self.group)
-        D.all_to_all_var(rep[1:1 + ns], out_rep, send_s, recv_s, self.group)
-        D.all_to_all_var(pk_r, pk_o, send_f, recv_f, self.group)
-        call("ctr_shard_unpack", _ptr(pk_r), _ptr(off_c), nc, _ptr(cat, LD), LD, st)
-        return dict(seq=seq_c, xcat=xcat_c, att=att, rep=rep, cat=cat, n_seq=seq.numel(), n_cat=X_cat.numel(),
-                    splits=(send_s, recv_s, send_c, recv_c, send_f, recv_f), loc_s=loc_s, loc_c=loc_c, off_c=off_c,
-                    off_o=off_o)
+        self._exchange("rows", (out_att, out_rep, pk_o), (att[1:], rep[1:], pk_r), (recv_s, recv_s, recv_f),
+                       (send_s, send_s, send_f), (Dm, Dm, 1), torch.float32)
+        call("ctr_shard_unpack", _ptr(pk_r), _ptr(pl.off_c), nc, _ptr(cat, LD), LD, st)
+        return dict(seq=pl.seq_c, xcat=pl.xcat_c, att=att, rep=rep, cat=cat, n_seq=seq.numel(), n_cat=X_cat.numel(),
+                    splits=(send_s, recv_s, send_c, recv_c, send_f, recv_f), loc_s=loc_s, loc_c=loc_c,
+                    off_c=pl.off_c, off_o=off_o)
 
     # ------------------------------------------------------------------ backward
     def _rowgrad(self, name, keys, rows, n, width, bits):
@@ -256,9 +349,8 @@ class TableShards:
         rg_a = self.buf.get("ga_s", rs, Dm)
         rg_r = self.buf.get("gr_s", rs, Dm)
         rg_p = self.buf.get("gc_pk", sum(recv_f))
-        D.all_to_all_var(rg_a, ga, recv_s, send_s, self.group)
-        D.all_to_all_var(rg_r, gr, recv_s, send_s, self.group)
-        D.all_to_all_var(rg_p, pk, recv_f, send_f, self.group)
+        self._exchange("grads", (ga, gr, pk), (rg_a, rg_r, rg_p), (send_s, send_s, send_f), (recv_s, recv_s, recv_f),
+                       (Dm, Dm, 1), torch.float32)
         rg_c = self.buf.get("gc_c", rc, LD)
         call("ctr_shard_unpack", _ptr(rg_p), _ptr(fx["off_o"]), rc, _ptr(rg_c), LD, st)
         att, rep = self._rowgrad2("sh_seq", fx["loc_s"], rg_a, rg_r, rs, Dm, self.seq_lbits)

@@ -200,20 +200,28 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
         model.train()
         perm = idx_tr_dev[torch.randperm(len(idx_tr), generator=gen, device=device)]
         loss_sum = torch.zeros((), device=device)
-        for step in range(steps_per_epoch):
-            global_step += 1
+        def batch_at(step):
             lo, n_rows = rank_slice(len(idx_tr), bs, world, rank, step)
             # a rank left without rows on the last step still joins the step's collectives with one
             # row whose loss gradient is zeroed: it adds nothing to the averaged gradient
             idx = perm[lo:lo + n_rows] if n_rows else perm[:1]
-            inputs, y = store.batch(idx)
+            # row-sharded tables: batches alternate between two gather slots so the next one can be staged
+            # (and its exchange planned, tossctr/shard.py) while this step runs
+            return store.batch(idx, slot=step % 2 if shard else 0), n_rows
+
+        nxt = batch_at(0)
+        for step in range(steps_per_epoch):
+            global_step += 1
+            (inputs, y), n_rows = nxt
+            nxt = batch_at(step + 1) if shard and step + 1 < steps_per_epoch else None
             opt.param_groups[0]["lr"] = cosine_warmup_lr(epoch - 1, step, steps_per_epoch, cfg["train"]["lr"], warmup,
                                                          epochs)
             # DDP semantics per replica: the mean of the per-rank gradients over the ranks that
             # hold rows -- on the short last step a rank without rows does not dilute the average
             n_contrib = step_contributors(len(idx_tr), bs, world, step)
             loss_sum += model.train_step(inputs, y, opt, global_step=global_step, contribute=n_rows > 0,
-                                         contributors=n_contrib if n_contrib < world else None)[0]
+                                         contributors=n_contrib if n_contrib < world else None,
+                                         next_inputs=nxt[0][0] if nxt is not None else None)[0]
         tr_loss = float(loss_sum.item()) / max(1, steps_per_epoch)
         use_ema_eval = ema is not None and cfg["ema"].get("eval_with_ema", True)
         if use_ema_eval:

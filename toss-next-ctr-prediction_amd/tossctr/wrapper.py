@@ -218,17 +218,21 @@ class CTRModel(nn.Module):
         return logits.clone(), prob.clone(), aux.clone()
 
     # ------------------------------------------------------------------ fused training step
-    def train_step(self, inputs, y, opt, global_step, seed=None, contribute=True, contributors=None):
+    def train_step(self, inputs, y, opt, global_step, seed=None, contribute=True, contributors=None,
+                   next_inputs=None):
         """One reference step (src/train.py:152-199): forward -> bce_wll_style(+aux) -> backward ->
         clip -> AdamW -> EMA, all on device, no host sync.  ``inputs`` = staged (X_num, X_mask, X_cat,
         seq) device tensors (see ``stage``), ``y`` float labels on device.  Returns the loss (device).
         ``contribute=False`` (data parallel: a rank without rows on an epoch's last step) runs the step
         with a zero loss gradient, so the rank joins the collectives but adds nothing to the gradient;
         ``contributors`` = how many ranks hold rows this step (the all-reduced gradient is averaged over those,
-        not over the whole world; None: every rank)."""
+        not over the whole world; None: every rank).  ``next_inputs`` = the next step's staged inputs, if
+        known: row-sharded tables plan that batch's exchange beside this step (tossctr/shard.py), so the
+        next step's host read of the exchange sizes waits on nothing; they must stay unchanged until then."""
         seed = self.next_seed() if seed is None else seed
         eng = self.engine
-        _, _, _, sv = eng.forward(*inputs, training=True, seed=seed, save=True)
+        pf = (next_inputs[2], next_inputs[3]) if next_inputs is not None else None
+        _, _, _, sv = eng.forward(*inputs, training=True, seed=seed, save=True, prefetch=pf)
         loss, dz, daux = eng.loss(sv, y)
         if not contribute:
             loss.zero_()
