@@ -238,20 +238,27 @@ def test_attention_fwd_bwd_vs_torch(K, H, D, p, generic):
 
 
 def attn_bf_keep_bits(mask, B, H, K):
-    """(B*H, K, K) keep bits from ctr_attn_fwd_bf's lane-layout mask (attn_mf.hip): per head 2 x 64 words,
-    bit 16 (ti & 1) + 4 tj + r of word ti >> 1 in lane 16 g + c <-> (i = 16 ti + c, j = 16 tj + 4 g + r)."""
-    words = mask.cpu().numpy().view(np.uint32)[:B * H * 128].reshape(B * H, 2, 64)
+    """(B*H, K, K) keep bits from ctr_attn_fwd_bf's lane-layout mask (attn_mf.hip): per head NW x 64 words;
+    element (i = 16 ti + c, j = 16 tj + 4 g + r) is bit pos % 32 of word pos // 32 of lane 16 g + c, with
+    pos = 16 ti + 4 tj + r for nt = ceil(K / 16) <= 4 (NW 2), pos = 4 nt tj + 4 ti + r beyond (NW ceil(4 nt^2 / 32))."""
+    nt = (K + 15) // 16
+    nw = 2 if nt <= 4 else (4 * nt * nt + 31) // 32
+    words = mask.cpu().numpy().view(np.uint32)[:B * H * 64 * nw].reshape(B * H, nw, 64)
     i = np.arange(K)[:, None]
     j = np.arange(K)[None, :]
     ti, c, tj, g, r = i // 16, i % 16, j // 16, (j % 16) // 4, j % 4
-    bit = (16 * (ti & 1) + 4 * tj + r).astype(np.uint32)
-    w = words[:, ti >> 1, 16 * g + c]
-    return ((w >> bit[None]) & 1).astype(bool)
+    pos = (16 * ti + 4 * tj + r) if nt <= 4 else (4 * nt * tj + 4 * ti + r)
+    w = words[:, pos >> 5, 16 * g + c]
+    return ((w >> (pos & 31).astype(np.uint32)[None]) & 1).astype(bool)
 
 
 @pytest.mark.parametrize("K,H,D,p", [(60, 8, 32, 0.1), (16, 4, 16, 0.0), (37, 2, 8, 0.3), (64, 4, 16, 0.2),
                                      (61, 8, 32, 0.1), (50, 8, 64, 0.1), (64, 8, 64, 0.1), (40, 6, 24, 0.1),
-                                     (1, 8, 32, 0.1), (60, 8, 64, 0.0), (33, 3, 24, 0.1)])
+                                     (1, 8, 32, 0.1), (60, 8, 64, 0.0), (33, 3, 24, 0.1),
+                                     # K > 64 (attn_bwd_mfl_kernel, compact staging): cfg3 (K 100, dh 4), cfg4
+                                     # (K 148, dh 8), v3_k120, odd K, one key past a tile, the 160 maximum
+                                     (100, 8, 32, 0.1), (148, 8, 64, 0.1), (120, 8, 64, 0.15), (97, 4, 16, 0.2),
+                                     (65, 2, 16, 0.0), (160, 8, 64, 0.1), (129, 3, 24, 0.1)])
 @pytest.mark.parametrize("bias", [True, False])
 def test_attention_bf16_vs_torch(K, H, D, p, bias):
     """amp: the bf16-MFMA attention (ctr_attn_fwd_bf / ctr_attn_bwd_bf) against the fp32 torch reference of

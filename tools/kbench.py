@@ -160,7 +160,7 @@ def main():
                 t = timeit(fn, args.iters)
                 res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}({t * 1e3:.0f}us)")
             print(f"gemm_bf16 M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
-    if "attn" in which:
+    if "attn" in which or "attnbf" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1
         thr = int(round(args.p * (1 << 16)))
@@ -177,13 +177,25 @@ def main():
                            ptr(o), ptr(mrow), ptr(lrow), st)
         bwd = lambda: call("ctr_attn_bwd", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(rel), K, scale, 777, thr,
                            1.0 / 0.9, ptr(amask), ptr(mrow), ptr(lrow), ptr(dqkv), ptr(drp), st)
-        for generic in (0, 1):      # the packed kernels (where they apply), then the generic ones
+        for generic in ((0, 1) if "attn" in which else ()):   # packed (where it applies), then generic
             _lib.query("ctr_attn_set_generic", generic)
             tf = timeit(fwd, args.iters)
             tb = timeit(bwd, args.iters)
             print(f"attn_fwd{' generic' if generic else ''} B={B} K={K} H={H} D={D}: {tf * 1e3:.1f} us")
             print(f"attn_bwd{' generic' if generic else ''} B={B} K={K} H={H} D={D}: {tb * 1e3:.1f} us")
         _lib.query("ctr_attn_set_generic", 0)
+    if "attnbf" in which and _lib.query("ctr_attn_bf_ok", K, H, D):
+        # the amp bf16-MFMA attention (attn_mf.hip)
+        nparts = _lib.query("ctr_attn_bwd_bf_nparts", H) * B
+        drp = torch.empty(nparts, 2 * K + 1, device="cuda")
+        fwd = lambda: call("ctr_attn_fwd_bf", ptr(qkv), B, K, H, D, ptr(rel), K, scale, 777, thr, 1.0 / 0.9,
+                           ptr(amask), ptr(o), ptr(mrow), ptr(lrow), st)
+        bwd = lambda: call("ctr_attn_bwd_bf", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(rel), K, scale, 777, thr,
+                           1.0 / 0.9, ptr(amask), ptr(mrow), ptr(lrow), ptr(dqkv), ptr(drp), st)
+        tf = timeit(fwd, args.iters)
+        tb = timeit(bwd, args.iters)
+        print(f"attn_fwd_bf B={B} K={K} H={H} D={D}: {tf * 1e3:.1f} us")
+        print(f"attn_bwd_bf B={B} K={K} H={H} D={D}: {tb * 1e3:.1f} us")
 
 
 if __name__ == "__main__":

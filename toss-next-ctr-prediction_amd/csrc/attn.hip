@@ -883,8 +883,11 @@ extern "C" void ctr_attn_set_generic(int on) { ctr_attn_force_generic = on; }
 
 // row layout (this file) or the bf16-MFMA kernels' lane layout (attn_mf.hip: 128 words per head), whichever is larger
 extern "C" int ctr_attn_mask_words(int B, int K, int H) {
-  const int row = K * ((K + 31) / 32);
-  return B * H * (row > 128 ? row : 128);
+  // per head: the fp32 kernels' K rows of ceil(K / 32) words, or the bf16-MFMA kernels' lane layout
+  // (attn_mf.hip: 64 lanes x NW words, NW = 2 for nt = ceil(K / 16) <= 4, ceil(4 nt^2 / 32) beyond)
+  const int row = K * ((K + 31) / 32), nt = (K + 15) / 16;
+  const int lanes = 64 * (nt <= 4 ? 2 : (4 * nt * nt + 31) / 32);
+  return B * H * std::max(row, lanes);
 }
 
 extern "C" int ctr_attn_fwd(const float* qkv, int B, int K, int H, int D, const float* relmean, int tk, float scale,

@@ -7,8 +7,9 @@
 // and dS = p (dp - do.o) stay fp32 (the scores are not rounded to bf16 -- the reference rounds them; ours is
 // the more precise side of that difference).
 //
-// One wave per head, the whole K x K head in registers as 16 x 16 tiles (K padded to 64, nt = ceil(K/16)
-// tiles a side).  Every elementwise step works on the TRANSPOSED score tile S^T = K Q^T, whose MFMA
+// One wave per head, the whole K x K head in registers as 16 x 16 tiles (nt = ceil(K/16) tiles a side, K <= 160:
+// staged operands padded to KT = 64 rows for nt <= 4, 16 nt rows beyond; the forward holds one query tile's
+// row of score tiles at a time, the backward one key tile's column).  Every elementwise step works on the TRANSPOSED score tile S^T = K Q^T, whose MFMA
 // accumulator layout puts key j = 16 tj + 4g + r in register r of lane (g, c) and query i = 16 ti + c in the
 // lane: a softmax row (fixed i) is the lane's registers plus the four lane groups (two permlane swaps), and
 // the tile's registers ARE the B operand of the products that reduce over keys (o^T = v^T p~^T,
@@ -18,8 +19,9 @@
 // instead of the ~50 of the VALU kernels (which recompute p in a second pass for dq).
 //
 // Keep bits of p~ (the backward reads them instead of re-hashing) are stored in the lane layout: per head
-// 2 words x 64 lanes, bit 16 (ti & 1) + 4 tj + r of word ti >> 1 in lane (g, c) = element (i = 16 ti + c,
-// j = 16 tj + 4g + r).  The keep decision is the same counter hash as every other dropout site (common.h).
+// NW words x 64 lanes; element (i = 16 ti + c, j = 16 tj + 4g + r) is bit pos % 32 of word pos / 32 of lane (g, c),
+// pos = 16 ti + 4 tj + r for nt <= 4 (NW = 2: bit 16 (ti & 1) + 4 tj + r of word ti >> 1) and key-tile major
+// pos = 4 nt tj + 4 ti + r beyond (NW = ceil(4 nt^2 / 32)), where the backward walks key tiles in a loop.  The keep decision is the same counter hash as every other dropout site (common.h).
 // mrow holds the row max in log2 units (the forward's and backward's exp2 argument), lrow the row sum.
 #include "common.h"
 #include "ctr_hip.h"
@@ -32,8 +34,14 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-constexpr int KT = 64;                      // padded K (<= 4 16-key tiles a side)
+constexpr int NT_MAX = 10;                  // K <= 160
 constexpr float L2E = 1.4426950408889634f;
+// per tile count: staged rows, keep-bit stride per query tile, keep words per lane
+template <int NT>
+struct Kt {
+  static constexpr int KT = NT <= 4 ? 64 : 16 * NT;
+  static constexpr int NW = NT <= 4 ? 2 : (4 * NT * NT + 31) / 32;
+};
 
 struct AttnBfArgs {
   const float* qkv;      // (B*K, 3D)
@@ -114,22 +122,61 @@ __device__ __forceinline__ float grp_sum(float v) {
 // An MFMA operand read of lane group g takes slots 4g .. 4g+3 of the head -- groups with 4g >= HS read
 // zeros instead (registers, not LDS) -- so S^T = K Q^T carries -3e38 (-> -inf after the log2 scale) on every
 // padded key and an exact +-0 elsewhere: no per-element masking.
-template <int DH>
+// K > 64 (nt > 4) uses compact rows to halve the LDS per head: the four heads' dims back to back, then ONE mask
+// chunk (slot 4 dh) and one zero chunk (slot 4 dh + 4) shared by the heads of the row; a head's operand read
+// of lane group g takes dims 4g .. 4g+3 while 4g < dh, the row's mask chunk at 4g == dh, the zero chunk beyond.
+// Column (transposed) reads take 16 slots from the head's first dim: the slots past its dims land in output
+// rows d >= dh of the product, which are never stored.
+template <int DH, int NT>
 struct Stg {
-  static constexpr int HS = DH + 4;                 // slots per head
-  static constexpr int RS = 4 * HS + 4;             // row stride (bf16 elements), <= 4 heads
+  static constexpr bool CMP = NT > 4;
+  static constexpr int KT = Kt<NT>::KT;
+  static constexpr int HS = CMP ? DH : DH + 4;      // slots per head
+  static constexpr int RS = CMP ? 4 * DH + 8 : 4 * HS + 4;   // row stride (bf16 elements), <= 4 heads
   static constexpr int IM = KT * RS;                // elements per staged operand
   static constexpr int PAD = 16;                    // transposed reads past the last head of the last row
-  static constexpr int ZOFF = 4 * HS;               // a zero chunk: slots 4 HS .. 4 HS + 3 of row 0
+  static constexpr int MOFF = 4 * DH;               // compact: the row's mask chunk
+  static constexpr int ZOFF = CMP ? 4 * DH + 4 : 4 * HS;   // a zero chunk (compact: in every row; else row 0)
 };
 constexpr float NEG_BIG = -3.0e38f;
 
-template <int DH, bool WITH_DO>
+template <int DH, int NT, bool WITH_DO>
 __device__ __forceinline__ void stage(const AttnBfArgs& a, __bf16* sq, __bf16* sk, __bf16* sv, __bf16* sdo) {
-  using S = Stg<DH>;
+  using S = Stg<DH, NT>;
+  constexpr int KT = S::KT;
   const int K = a.K, D = a.D, G = a.G, b = blockIdx.x;
   const float* base = a.qkv + (long)b * K * 3 * D + blockIdx.y * G * DH;
   const float* dob = WITH_DO ? a.dO + (long)b * K * D + blockIdx.y * G * DH : nullptr;
+  if constexpr (S::CMP) {
+    constexpr int NCD = DH / 4, NCR = 4 * NCD + 2;  // chunks per row: 4 heads' dims, mask, zero
+    for (int e = threadIdx.x; e < KT * NCR; e += blockDim.x) {
+      const int j = e / NCR, ch = e - j * NCR;
+      f32x4 q = {0.f, 0.f, 0.f, 0.f}, k = q, v = q, d = q;
+      int o;
+      if (ch < 4 * NCD) {
+        const int u = ch / NCD, dc = ch - u * NCD;
+        o = j * S::RS + u * DH + 4 * dc;
+        if (u < G && j < K) {
+          const float* r = base + (long)j * 3 * D + u * DH + 4 * dc;
+          q = *(const f32x4*)r * a.scale;
+          k = *(const f32x4*)(r + D);
+          v = *(const f32x4*)(r + 2 * D);
+          if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * dc);
+        }
+      } else if (ch == 4 * NCD) {                   // the row's mask chunk
+        o = j * S::RS + S::MOFF;
+        q[0] = NEG_BIG;
+        k[0] = j >= K ? 1.f : 0.f;
+      } else {                                      // the row's zero chunk
+        o = j * S::RS + S::ZOFF;
+      }
+      *(bf16x4*)(sq + o) = to_bf4(q);
+      *(bf16x4*)(sk + o) = to_bf4(k);
+      *(bf16x4*)(sv + o) = to_bf4(v);
+      if (WITH_DO) *(bf16x4*)(sdo + o) = to_bf4(d);
+    }
+    return;
+  }
   constexpr int NCH = S::HS / 4;                    // 4-slot chunks per head
   for (int e = threadIdx.x; e < KT * 4 * NCH; e += blockDim.x) {
     const int ch = e % NCH, ju = e / NCH, u = ju & 3, j = ju >> 2;
@@ -166,65 +213,107 @@ __device__ __forceinline__ void stage(const AttnBfArgs& a, __bf16* sq, __bf16* s
 // (i = 16 ti + c, j = 16 tj + 4g + r) takes rel[j - i + tk] = srel[RPAD + 16 (tj - ti) + 4g + r - c + tk]; the
 // index stays inside the padded table for every padded row / key (whose values are discarded), so each
 // tile's four values are loads at one per-lane base + immediate offsets, no clamping
-constexpr int RPAD = KT;
+// (RPAD = the staged rows KT: 16 (nt - 1) + 15 < KT)
+template <int NT>
 __device__ __forceinline__ void stage_rel(const AttnBfArgs& a, float* srel) {
+  constexpr int RPAD = Kt<NT>::KT;
   const int nrel = 2 * a.tk + 1;
   for (int e = threadIdx.x; e < nrel + 2 * RPAD; e += blockDim.x) {
     const int x = e - RPAD;
     srel[e] = (x >= 0 && x < nrel) ? a.relmean[x] * L2E : 0.f;
   }
 }
-__host__ __device__ __forceinline__ int rel_floats(int tk) { return (2 * tk + 1 + 2 * RPAD + 3) & ~3; }   // 16-B multiple
+template <int NT>
+__host__ __device__ __forceinline__ int rel_floats(int tk) { return (2 * tk + 1 + 2 * Kt<NT>::KT + 3) & ~3; }   // 16-B multiple
 
 // dS / p~ image of one key tile: 64 query rows x 16 keys, bf16, row stride 16; the 4-key chunk ch of row rw
 // stored at chunk ch ^ ((rw >> 2) & 3): the ds_write_b64 of a score tile (16 lanes: rows 16 ti + 0..15, one
 // chunk) and the ds_read_b64_tr_b16 (32 lanes: rows 16 ti + 4g + q, chunks p) are both bank-conflict free
 __device__ __forceinline__ int swz(int rw, int ch) { return rw * 16 + 4 * (ch ^ ((rw >> 2) & 3)); }
-constexpr int IMG = KT * 16;                // bf16 elements per image
+template <int NT>
+__host__ __device__ constexpr int img_elems() { return Kt<NT>::KT * 16; }   // bf16 elements per image
 
 // operand reads: row access (lane (g, c) <- slots 4g .. 4g+3 of row `row`; zeros past the head's slots) and
 // transposed column access (lane (g, c) <- column c of rows row0 + 4g .. row0 + 4g + 3)
 // (the row read is unconditional: lanes past the head's slots read the zero chunk at ZOFF of the image)
-template <int DH>
+template <int DH, int NT>
 __device__ __forceinline__ bf16x4 op_row(const __bf16* img, int row, int hs, int g) {
-  return ld4(img + (4 * g < Stg<DH>::HS ? row * Stg<DH>::RS + hs + 4 * g : Stg<DH>::ZOFF));
+  using S = Stg<DH, NT>;
+  if constexpr (S::CMP)
+    return ld4(img + row * S::RS + (4 * g < DH ? hs + 4 * g : 4 * g == DH ? S::MOFF : S::ZOFF));
+  else
+    return ld4(img + (4 * g < S::HS ? row * S::RS + hs + 4 * g : S::ZOFF));
 }
-template <int DH>
+template <int DH, int NT>
 __device__ __forceinline__ bf16x4 op_col(const __bf16* img, int row0, int hs, int g, int c) {
-  return tr4(img + (row0 + 4 * g + (c >> 2)) * Stg<DH>::RS + hs + 4 * (c & 3));
+  return tr4(img + (row0 + 4 * g + (c >> 2)) * Stg<DH, NT>::RS + hs + 4 * (c & 3));
 }
 
 // ------------------------------------------------------------------------------------------------
 // forward.  NT = the tiles a side (ceil(K / 16)); DROPK: 0 none, 1 K even (pair hashes), 2 K odd
 template <int NT, int DH, bool BIAS, int DROPK>
 __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
-  using S = Stg<DH>;
+  using S = Stg<DH, NT>;
+  using KB = Kt<NT>;
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
   const int K = a.K, D = a.D, G = a.G;
   __bf16* sq = smb;
   __bf16* sk = sq + S::IM;
   __bf16* sv = sk + S::IM;
   float* srel = (float*)(sv + S::IM + S::PAD);
-  stage<DH, false>(a, sq, sk, sv, nullptr);
-  if (BIAS) stage_rel(a, srel);
+  stage<DH, NT, false>(a, sq, sk, sv, nullptr);
+  if (BIAS) stage_rel<NT>(a, srel);
   __syncthreads();
   const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int h = blockIdx.y * G + w, hs = w * S::HS;
   bf16x4 kop[NT], vtop[NT];
 #pragma unroll
   for (int tj = 0; tj < NT; ++tj) {
-    kop[tj] = op_row<DH>(sk, 16 * tj + c, hs, g);          // A = k [j][d]
-    vtop[tj] = op_col<DH>(sv, 16 * tj, hs, g, c);          // A = v^T [d][j]
+    kop[tj] = op_row<DH, NT>(sk, 16 * tj + c, hs, g);          // A = k [j][d]
+    vtop[tj] = op_col<DH, NT>(sv, 16 * tj, hs, g, c);          // A = v^T [d][j]
   }
-  const float* rb = srel + RPAD + a.tk + 4 * g - c;        // + 16 (tj - ti) + r
+  const float* rb = srel + KB::KT + a.tk + 4 * g - c;      // + 16 (tj - ti) + r
   const long hr = ((long)b * a.H + h) * K;                 // (head, row 0)
-  uint32_t words[2] = {0u, 0u};
+  uint32_t words[KB::NW];
+#pragma unroll
+  for (int q = 0; q < KB::NW; ++q) words[q] = 0u;
   const float dsc = DROPK ? a.drop.scale : 1.0f;
 #pragma unroll
   for (int ti = 0; ti < NT; ++ti) {
     __builtin_amdgcn_sched_barrier(0);
-    const bf16x4 qop = op_row<DH>(sq, 16 * ti + c, hs, g); // B = q^T [d][i]
+    const bf16x4 qop = op_row<DH, NT>(sq, 16 * ti + c, hs, g); // B = q^T [d][i]
     const int i = 16 * ti + c;
+    const uint32_t rowbase = (uint32_t)((hr + i) * K);
+    // nt > 4: this query tile's keep bits first (bit 4 tj + r of kbw), so the hash chains die before the exp
+    // pass instead of being interleaved with it (the interleaved form needed ~450 registers at nt = 10)
+    uint32_t kbw[2] = {0u, 0u};
+    if constexpr (DROPK != 0 && NT > 4) {
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) {
+        const uint32_t j0 = 16 * tj + 4 * g;
+        uint32_t half[4];
+        if (DROPK == 1) {
+          const uint32_t h0 = drop_pair_bits(a.drop, (rowbase + j0) >> 1);
+          const uint32_t h1 = drop_pair_bits(a.drop, (rowbase + j0 + 2) >> 1);
+          half[0] = h0 & 0xFFFFu;
+          half[1] = h0 >> 16;
+          half[2] = h1 & 0xFFFFu;
+          half[3] = h1 >> 16;
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t idx = rowbase + j0 + r;
+            const uint32_t hb = mix32((idx >> 1) ^ a.drop.key);
+            half[r] = (idx & 1u) ? hb >> 16 : hb & 0xFFFFu;
+          }
+        }
+        uint32_t nib = 0u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) nib |= (~sign_mask(half[r] - a.drop.thresh) & 1u) << r;
+        const int p = 4 * tj;
+        kbw[p >> 5] |= nib << (p & 31);
+      }
+    }
     f32x4 t[NT];
     float mx = -INFINITY;
 #pragma unroll
@@ -239,7 +328,6 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
     mx = grp_max(mx);
     float l = 0.f;
     uint32_t dropped = 0u;
-    const uint32_t rowbase = (uint32_t)((hr + i) * K);
     bf16x4 pb[NT];
 #pragma unroll
     for (int tj = 0; tj < NT; ++tj) {
@@ -249,7 +337,14 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
         pe[r] = __builtin_amdgcn_exp2f(t[tj][r] - mx);
         l += pe[r];
       }
-      if (DROPK) {
+      if (DROPK != 0 && NT > 4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {      // all ones where kept
+          const int p = 4 * tj + r;
+          const uint32_t km = (uint32_t)__builtin_amdgcn_sbfe((int)kbw[p >> 5], p & 31, 1);
+          pe[r] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, pe[r]) & km);
+        }
+      } else if (DROPK) {
         // keep iff the element's 16-bit hash half >= thresh; drop mask m = (half - thresh) >> 31 (arithmetic:
         // all ones = dropped), p~ = p & ~m, and the dropped-bit word collects m's bit (one v_and_or each) --
         // integer arithmetic throughout: compares would leave 64 lane masks in SGPRs (spilled).  The masked
@@ -293,12 +388,20 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
         a.lrow[hr + i] = l;
       }
     }
-    if (DROPK) words[ti >> 1] |= (~dropped & 0xFFFFu) << (16 * (ti & 1));
+    if (DROPK && NT <= 4) words[ti >> 1] |= (~dropped & 0xFFFFu) << (16 * (ti & 1));
+    if constexpr (DROPK != 0 && NT > 4) {     // stored layout: key-tile major (a nibble never straddles words)
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) {
+        const int p = 4 * tj, q = 4 * NT * tj + 4 * ti;
+        words[q >> 5] |= ((kbw[p >> 5] >> (p & 31)) & 0xFu) << (q & 31);
+      }
+    }
+
   }
   if (DROPK) {
-    uint32_t* mk = a.mask + ((long)b * a.H + h) * 128;
-    mk[lane] = words[0];
-    mk[64 + lane] = words[1];
+    uint32_t* mk = a.mask + ((long)b * a.H + h) * (64 * KB::NW);
+#pragma unroll
+    for (int q = 0; q < KB::NW; ++q) mk[64 * q + lane] = words[q];
   }
 }
 
@@ -307,8 +410,9 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
 // Key tiles outer (dk, dv of a key tile complete in its iteration), query tiles inner (dq accumulates).
 template <int NT, int DH, bool BIAS, bool DROP>
 __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
-  using S = Stg<DH>;
-  constexpr int ND = 2 * NT - 1;
+  using S = Stg<DH, NT>;
+  using KB = Kt<NT>;
+  constexpr int ND = 2 * NT - 1, IMG = img_elems<NT>(), KT = KB::KT;
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
   const int K = a.K, D = a.D, G = a.G;
   __bf16* sq = smb;
@@ -317,23 +421,23 @@ __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
   __bf16* sdo = sv + S::IM;
   __bf16* simg = sdo + S::IM + S::PAD;              // per wave: dS image, p~ image
   float* srel = (float*)(simg + 4 * 2 * IMG);
-  stage<DH, true>(a, sq, sk, sv, sdo);
-  if (BIAS) stage_rel(a, srel);
+  stage<DH, NT, true>(a, sq, sk, sv, sdo);
+  if (BIAS) stage_rel<NT>(a, srel);
   __syncthreads();
   const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int h = blockIdx.y * G + w, hs = w * S::HS;
   __bf16* ids = simg + w * 2 * IMG;
   __bf16* ipt = ids + IMG;
-  const float* rb = srel + RPAD + a.tk + 4 * g - c;
+  const float* rb = srel + KT + a.tk + 4 * g - c;
   const long hr = ((long)b * a.H + h) * K;
   // per query row i (lane): {max (log2), 1 / sum, D_i = do_i . o_i} in the wave's LDS row table, read back
   // per score tile (padded rows: p = 0, D = 0)
-  f32x4* stw = (f32x4*)(srel + rel_floats(BIAS ? a.tk : 0)) + w * KT;
-  {
+  f32x4* stw = (f32x4*)(srel + rel_floats<NT>(BIAS ? a.tk : 0)) + w * KT;
+  for (int row = lane; row < KT; row += 64) {
     f32x4 st = {0.f, 0.f, 0.f, 0.f};
-    if (lane < K) {
-      const float* dp = a.dO + ((long)b * K + lane) * D + h * DH;
-      const float* op = a.o + ((long)b * K + lane) * D + h * DH;
+    if (row < K) {
+      const float* dp = a.dO + ((long)b * K + row) * D + h * DH;
+      const float* op = a.o + ((long)b * K + row) * D + h * DH;
       float s = 0.f;
 #pragma unroll
       for (int q = 0; q < DH / 4; ++q) {
@@ -343,16 +447,18 @@ __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
         s = fmaf(x[2], y[2], s);
         s = fmaf(x[3], y[3], s);
       }
-      st = f32x4{a.mrow[hr + lane], 1.0f / a.lrow[hr + lane], s, 0.f};
+      st = f32x4{a.mrow[hr + row], 1.0f / a.lrow[hr + row], s, 0.f};
     }
-    stw[lane] = st;
+    stw[row] = st;
   }
   __builtin_amdgcn_wave_barrier();
-  uint32_t words[2] = {0u, 0u};
+  uint32_t words[KB::NW];
+#pragma unroll
+  for (int q = 0; q < KB::NW; ++q) words[q] = 0u;
   if (DROP) {
-    const uint32_t* mk = a.mask + ((long)b * a.H + h) * 128;
-    words[0] = mk[lane];
-    words[1] = mk[64 + lane];
+    const uint32_t* mk = a.mask + ((long)b * a.H + h) * (64 * KB::NW);
+#pragma unroll
+    for (int q = 0; q < KB::NW; ++q) words[q] = mk[64 * q + lane];
   }
   const uint32_t dsc_bits = __builtin_bit_cast(uint32_t, DROP ? a.drop.scale : 1.0f);
   f32x4 dq[NT];
@@ -367,14 +473,14 @@ __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
   for (int tj = 0; tj < NT; ++tj) {
     __builtin_amdgcn_sched_barrier(0);     // one key tile at a time: bounds the live registers
     const int j = 16 * tj + c;
-    const bf16x4 kop = op_row<DH>(sk, j, hs, g);                                       // A = k [j][d]
-    const bf16x4 vop = op_row<DH>(sv, j, hs, g);                                       // A = v [j][d]
-    const bf16x4 ktop = op_col<DH>(sk, 16 * tj, hs, g, c);                             // A = k^T [d][j]
+    const bf16x4 kop = op_row<DH, NT>(sk, j, hs, g);                                       // A = k [j][d]
+    const bf16x4 vop = op_row<DH, NT>(sv, j, hs, g);                                       // A = v [j][d]
+    const bf16x4 ktop = op_col<DH, NT>(sk, 16 * tj, hs, g, c);                             // A = k^T [d][j]
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int i = 16 * ti + c;
-      const bf16x4 qop = op_row<DH>(sq, i, hs, g);                                     // B = q^T [d][i]
-      const bf16x4 doop = op_row<DH>(sdo, i, hs, g);                                   // B = do^T [d][i]
+      const bf16x4 qop = op_row<DH, NT>(sq, i, hs, g);                                     // B = q^T [d][i]
+      const bf16x4 doop = op_row<DH, NT>(sdo, i, hs, g);                                   // B = do^T [d][i]
       const f32x4 s = mma(kop, qop, f32x4{0.f, 0.f, 0.f, 0.f});                       // S^T [j][i]
       const f32x4 dp = mma(vop, doop, f32x4{0.f, 0.f, 0.f, 0.f});                     // dP~^T [j][i]
       const f32x4 st = stw[i];
@@ -385,9 +491,9 @@ __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
         const float p = __builtin_amdgcn_exp2f(x - st[0]) * st[1];
         float dpk = dp[r], pt = p;
         if (DROP) {   // keep ? 1 / (1 - p) : 0, from the bit's sign-extension
-          const int pos = 16 * (ti & 1) + 4 * tj + r;
+          const int pos = 16 * ti + 4 * tj + r;
           const float kf = __builtin_bit_cast(
-              float, (uint32_t)__builtin_amdgcn_sbfe((int)words[ti >> 1], pos, 1) & dsc_bits);
+              float, (uint32_t)__builtin_amdgcn_sbfe((int)words[pos >> 5], pos & 31, 1) & dsc_bits);
           dpk *= kf;
           pt *= kf;
         }
@@ -407,8 +513,8 @@ __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int rw = 16 * ti + 4 * g + (c >> 2);
-      dk = mma(op_col<DH>(sq, 16 * ti, hs, g, c), tr4(ids + swz(rw, c & 3)), dk);      // B = dS [i][j]
-      dv = mma(op_col<DH>(sdo, 16 * ti, hs, g, c), tr4(ipt + swz(rw, c & 3)), dv);     // B = p~ [i][j]
+      dk = mma(op_col<DH, NT>(sq, 16 * ti, hs, g, c), tr4(ids + swz(rw, c & 3)), dk);      // B = dS [i][j]
+      dv = mma(op_col<DH, NT>(sdo, 16 * ti, hs, g, c), tr4(ipt + swz(rw, c & 3)), dv);     // B = p~ [i][j]
     }
     __builtin_amdgcn_wave_barrier();
     if (4 * g < DH && j < K) {
@@ -479,6 +585,202 @@ __global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// backward for K > 64 (nt > 4).  The nt <= 4 kernel's per-wave [KT][16] dS / p~ images and its (2 nt - 1) x 4
+// diagonal registers would take ~120 KB of LDS and ~500 registers per wave at nt = 10; here
+//   * dk, dv of the key tile accumulate per query tile through a 16 x 16 image pair (dS, p~ of tile (ti, tj)
+//     written, read back transposed, consumed) -- 1 KB per wave;
+//   * the positional-bias diagonal sums run in a window of nt tile diagonals: diagonal tile dt = tj - ti + nt - 1
+//     sits in window slot nt - 1 - ti while key tile tj runs, and slot 0 (dt = tj) is final after it (later
+//     key tiles only reach dt > tj), so it is folded into the wave's per-diagonal sums in LDS (a 16 x 16 scratch,
+//     31 lanes each summing one diagonal in a fixed order) and the window moves on -- with tj unrolled the move
+//     is register renaming.  The heads of the workgroup are summed in a fixed order at the end.
+#ifndef ATT_DB
+#define ATT_DB 1
+#endif
+#ifndef ATT_WPE
+#define ATT_WPE 0
+#endif
+#ifndef ATT_SB
+#define ATT_SB 0
+#endif
+template <int NT, int DH, bool BIAS, bool DROP>
+__global__ __launch_bounds__(256)
+#if ATT_WPE
+__attribute__((amdgpu_waves_per_eu(ATT_WPE)))
+#endif
+void attn_bwd_mfl_kernel(AttnBfArgs a) {
+  using S = Stg<DH, NT>;
+  using KB = Kt<NT>;
+  constexpr int KT = KB::KT, NDG = 32 * NT - 1, NDGP = (NDG + 3) & ~3;
+  extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
+  const int K = a.K, D = a.D, G = a.G;
+  __bf16* sq = smb;
+  __bf16* sk = sq + S::IM;
+  __bf16* sv = sk + S::IM;
+  __bf16* sdo = sv + S::IM;
+  __bf16* simg = sdo + S::IM + S::PAD;              // per wave: 16 x 16 dS image, 16 x 16 p~ image (x2)
+  float* srel = (float*)(simg + 4 * 4 * 256);
+  stage<DH, NT, true>(a, sq, sk, sv, sdo);
+  if (BIAS) stage_rel<NT>(a, srel);
+  const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = blockIdx.y * G + w, hs = w * S::HS;
+  __bf16* ids0 = simg + w * 4 * 256;
+  const float* rb = srel + KT + a.tk + 4 * g - c;
+  const long hr = ((long)b * a.H + h) * K;
+  f32x4* stw = (f32x4*)(srel + rel_floats<NT>(BIAS ? a.tk : 0)) + w * KT;
+  float* sdg = (float*)(stw + (4 - w) * KT) + w * (256 + NDGP);   // per wave: [16][16] scratch, NDG diagonal sums
+  float* dsum = sdg + 256;
+  for (int row = lane; row < KT; row += 64) {
+    f32x4 st = {0.f, 0.f, 0.f, 0.f};
+    if (row < K) {
+      const float* dp = a.dO + ((long)b * K + row) * D + h * DH;
+      const float* op = a.o + ((long)b * K + row) * D + h * DH;
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < DH / 4; ++q) {
+        const f32x4 x = *(const f32x4*)(dp + 4 * q), y = *(const f32x4*)(op + 4 * q);
+        s = fmaf(x[0], y[0], s);
+        s = fmaf(x[1], y[1], s);
+        s = fmaf(x[2], y[2], s);
+        s = fmaf(x[3], y[3], s);
+      }
+      st = f32x4{a.mrow[hr + row], 1.0f / a.lrow[hr + row], s, 0.f};
+    }
+    stw[row] = st;
+  }
+  if (BIAS)
+    for (int e = lane; e < NDGP; e += 64) dsum[e] = 0.f;
+  __syncthreads();
+  const uint32_t* mk = a.mask + ((long)b * a.H + h) * (64 * KB::NW) + lane;
+  const uint32_t dsc_bits = __builtin_bit_cast(uint32_t, DROP ? a.drop.scale : 1.0f);
+  // fold the finished tile diagonal dt (values v[r] of element (a = 4g + r, c): diagonal 16 (dt - nt + 1) + a - c)
+  // into dsum: lane e + 15 (e = a - c in [-15, 15]) sums its diagonal over a, ascending
+  auto fold = [&](int dt, const float (&v)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sdg[(4 * g + r) * 16 + c] = v[r];
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 31) {
+      const int e = lane - 15;
+      float sum = 0.f;
+      const int a0 = e > 0 ? e : 0, a1 = e < 0 ? 15 + e : 15;
+      for (int aa = a0; aa <= a1; ++aa) sum += sdg[aa * 16 + (aa - e)];
+      dsum[16 * dt + lane] += sum;          // diagonal 16 (dt - nt + 1) + e  ->  index 16 dt + e + 15
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  f32x4 dq[NT];
+  float win[NT][4];            // window slot k = tile diagonal tj + k
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti) dq[ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NT; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) win[k][r] = 0.f;
+  // key tiles in a loop (unrolled, the per-query-tile operands of every key tile were hoisted and kept live:
+  // ~340 registers at nt = 10); this tile's 4 nt keep bits (bit 4 ti + r) from the mask in global memory
+#pragma unroll 1
+  for (int tj = 0; tj < NT; ++tj) {
+    const int j = 16 * tj + c;
+    const bf16x4 kop = op_row<DH, NT>(sk, j, hs, g);                                   // A = k [j][d]
+    const bf16x4 vop = op_row<DH, NT>(sv, j, hs, g);                                   // A = v [j][d]
+    const bf16x4 ktop = op_col<DH, NT>(sk, 16 * tj, hs, g, c);                         // A = k^T [d][j]
+    uint64_t kb = 0;
+    if (DROP) {
+      const int p0 = 4 * NT * tj, w0 = p0 >> 5;
+      const uint64_t lo = mk[64 * w0], hi = w0 + 1 < KB::NW ? mk[64 * (w0 + 1)] : 0u;
+      kb = ((hi << 32) | lo) >> (p0 & 31);
+      if ((p0 & 31) + 4 * NT > 64) kb |= (uint64_t)mk[64 * (w0 + 2)] << (64 - (p0 & 31));
+    }
+    const float* rbt = rb + 16 * tj;
+    f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = dk;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+#if ATT_SB
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+      __bf16* ids = ids0 + (ATT_DB ? (ti & 1) * 512 : 0);
+      __bf16* ipt = ids + 256;
+      const int i = 16 * ti + c;
+      const bf16x4 qop = op_row<DH, NT>(sq, i, hs, g);                                 // B = q^T [d][i]
+      const bf16x4 doop = op_row<DH, NT>(sdo, i, hs, g);                               // B = do^T [d][i]
+      const f32x4 s = mma(kop, qop, f32x4{0.f, 0.f, 0.f, 0.f});                       // S^T [j][i]
+      const f32x4 dp = mma(vop, doop, f32x4{0.f, 0.f, 0.f, 0.f});                     // dP~^T [j][i]
+      const f32x4 st = stw[i];
+      f32x4 dsv, ptv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = BIAS ? fmaf(s[r], L2E, rbt[r - 16 * ti]) : s[r] * L2E;
+        const float p = __builtin_amdgcn_exp2f(x - st[0]) * st[1];
+        float dpk = dp[r], pt = p;
+        if (DROP) {
+          const int pos = 4 * ti + r;
+          const uint32_t wsel = pos < 32 ? (uint32_t)kb : (uint32_t)(kb >> 32);
+          const float kf = __builtin_bit_cast(float, (uint32_t)__builtin_amdgcn_sbfe((int)wsel, pos & 31, 1) & dsc_bits);
+          dpk *= kf;
+          pt *= kf;
+        }
+        const float ds = p * (dpk - st[2]);
+        if (BIAS) win[NT - 1 - ti][r] += ds;
+        dsv[r] = ds;
+        ptv[r] = pt;
+      }
+      const u32x2 dsu = pk_bf4(dsv), ptu = pk_bf4(ptv);
+      dq[ti] = mma(ktop, __builtin_bit_cast(bf16x4, dsu), dq[ti]);                      // dq^T [d][i]
+      // dk^T [d][j] += q^T [d][i] dS [i][j], dv^T [d][j] += do^T [d][i] p~ [i][j] over this tile's 16 queries
+      *(u32x2*)(ids + swz(c, g)) = dsu;
+      *(u32x2*)(ipt + swz(c, g)) = ptu;
+#if !ATT_DB
+      __builtin_amdgcn_wave_barrier();
+#endif
+      const int rw = 4 * g + (c >> 2);
+      dk = mma(op_col<DH, NT>(sq, 16 * ti, hs, g, c), tr4(ids + swz(rw, c & 3)), dk);   // B = dS [i][j]
+      dv = mma(op_col<DH, NT>(sdo, 16 * ti, hs, g, c), tr4(ipt + swz(rw, c & 3)), dv);  // B = p~ [i][j]
+#if !ATT_DB
+      __builtin_amdgcn_wave_barrier();
+#endif
+    }
+    if (4 * g < DH && j < K) {
+      float* dst = a.dqkv + ((long)b * K + j) * 3 * D + h * DH + 4 * g;
+      *(f32x4*)(dst + D) = dk;
+      *(f32x4*)(dst + 2 * D) = dv;
+    }
+    if (BIAS) {
+      fold(tj, win[0]);
+#pragma unroll
+      for (int k = 0; k + 1 < NT; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) win[k][r] = win[k + 1][r];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) win[NT - 1][r] = 0.f;
+    }
+  }
+  if (4 * g < DH) {
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+      const int i = 16 * ti + c;
+      if (i < K) *(f32x4*)(a.dqkv + ((long)b * K + i) * 3 * D + h * DH + 4 * g) = dq[ti] * a.scale;
+    }
+  }
+  if (BIAS) {
+#pragma unroll
+    for (int k = 0; k + 1 < NT; ++k) fold(NT + k, win[k]);     // tile diagonals nt .. 2 nt - 2
+    __syncthreads();
+    // heads of the group summed in a fixed order; diagonal d = x - (16 nt - 1) of the x-th sum
+    const int nrel = 2 * a.tk + 1;
+    float* out = a.drel_part + ((long)b * gridDim.y + blockIdx.y) * nrel;
+    const float* base = (const float*)(stw + (4 - w) * KT);     // wave 0's scratch
+    for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
+      const int d = e - a.tk, x = d + 16 * NT - 1;
+      float sum = 0.f;
+      if (d > -K && d < K) {
+        for (int u = 0; u < G; ++u) sum += base[u * (256 + NDGP) + 256 + x];
+      }
+      out[e] = sum;
+    }
+  }
+}
+
 int pick_g(int H) {
   int g = 1;
   for (int c = 1; c <= 4; ++c)
@@ -486,28 +788,47 @@ int pick_g(int H) {
   return g;
 }
 
-template <int DH>
-size_t fwd_lds(int tk) { return ((size_t)3 * Stg<DH>::IM + Stg<DH>::PAD) * 2 + (size_t)rel_floats(tk) * 4; }
+template <int DH, int NT>
+size_t fwd_lds(int tk) { return ((size_t)3 * Stg<DH, NT>::IM + Stg<DH, NT>::PAD) * 2 + (size_t)rel_floats<NT>(tk) * 4; }
 
-template <int DH>
-size_t bwd_lds(int G, int NT, int tk) {
-  const size_t main = ((size_t)4 * Stg<DH>::IM + Stg<DH>::PAD) * 2 + (size_t)4 * 2 * IMG * 2 +
-                      (size_t)rel_floats(tk) * 4 + (size_t)4 * KT * 16;
+template <int DH, int NT>
+size_t bwd_lds(int G, int tk) {
+  const size_t main = ((size_t)4 * Stg<DH, NT>::IM + Stg<DH, NT>::PAD) * 2 + (size_t)4 * 2 * img_elems<NT>() * 2 +
+                      (size_t)rel_floats<NT>(tk) * 4 + (size_t)4 * Kt<NT>::KT * 16;
   const size_t ND = 2 * NT - 1, diag = ((size_t)G * ND * 256 + ND * 256) * 4;
   return main > diag ? main : diag;
 }
 
+// nt > 4: operands, the four waves' 16 x 16 image pairs, bias table, stats rows, per-wave diagonal scratch + sums
+template <int DH, int NT>
+size_t bwdl_lds(int tk) {
+  constexpr int NDGP = (32 * NT - 1 + 3) & ~3;
+  return ((size_t)4 * Stg<DH, NT>::IM + Stg<DH, NT>::PAD) * 2 + (size_t)4 * 4 * 256 * 2 + (size_t)rel_floats<NT>(tk) * 4 +
+         (size_t)4 * Kt<NT>::KT * 16 + (size_t)4 * (256 + NDGP) * 4;
+}
+
+// more than 64 KB of dynamic LDS (nt > 4) has to be allowed per kernel
+template <class F>
+void allow_lds(F* kern, size_t sm) {
+  if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+}
+
+template <int NT, int DH, bool BIAS, int DROPK>
+void launch_fwd5(const AttnBfArgs& a, size_t sm, hipStream_t s) {
+  allow_lds(attn_fwd_mf_kernel<NT, DH, BIAS, DROPK>, sm);
+  attn_fwd_mf_kernel<NT, DH, BIAS, DROPK><<<dim3(a.B, a.H / a.G), dim3(64 * a.G), sm, s>>>(a);
+}
+
 template <int NT, int DH, bool BIAS>
 void launch_fwd4(const AttnBfArgs& a, size_t sm, hipStream_t s) {
-  const dim3 grid(a.B, a.H / a.G), blk(64 * a.G);
-  if (a.drop.thresh == 0) attn_fwd_mf_kernel<NT, DH, BIAS, 0><<<grid, blk, sm, s>>>(a);
-  else if (a.K & 1) attn_fwd_mf_kernel<NT, DH, BIAS, 2><<<grid, blk, sm, s>>>(a);
-  else attn_fwd_mf_kernel<NT, DH, BIAS, 1><<<grid, blk, sm, s>>>(a);
+  if (a.drop.thresh == 0) launch_fwd5<NT, DH, BIAS, 0>(a, sm, s);
+  else if (a.K & 1) launch_fwd5<NT, DH, BIAS, 2>(a, sm, s);
+  else launch_fwd5<NT, DH, BIAS, 1>(a, sm, s);
 }
 
 template <int NT, int DH>
 void launch_fwd3(const AttnBfArgs& a, hipStream_t s) {
-  const size_t sm = fwd_lds<DH>(a.relmean ? a.tk : 0);
+  const size_t sm = fwd_lds<DH, NT>(a.relmean ? a.tk : 0);
   if (a.relmean) launch_fwd4<NT, DH, true>(a, sm, s);
   else launch_fwd4<NT, DH, false>(a, sm, s);
 }
@@ -518,19 +839,35 @@ void launch_fwd2(const AttnBfArgs& a, hipStream_t s) {
     case 1: launch_fwd3<1, DH>(a, s); break;
     case 2: launch_fwd3<2, DH>(a, s); break;
     case 3: launch_fwd3<3, DH>(a, s); break;
-    default: launch_fwd3<4, DH>(a, s); break;
+    case 4: launch_fwd3<4, DH>(a, s); break;
+    case 5: launch_fwd3<5, DH>(a, s); break;
+    case 6: launch_fwd3<6, DH>(a, s); break;
+    case 7: launch_fwd3<7, DH>(a, s); break;
+    case 8: launch_fwd3<8, DH>(a, s); break;
+    case 9: launch_fwd3<9, DH>(a, s); break;
+    default: launch_fwd3<10, DH>(a, s); break;
+  }
+}
+
+template <int NT, int DH, bool BIAS, bool DROP>
+void launch_bwd4(const AttnBfArgs& a, size_t sm, hipStream_t s) {
+  if constexpr (NT > 4) {
+    allow_lds(attn_bwd_mfl_kernel<NT, DH, BIAS, DROP>, sm);
+    attn_bwd_mfl_kernel<NT, DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), dim3(64 * a.G), sm, s>>>(a);
+  } else {
+    allow_lds(attn_bwd_mf_kernel<NT, DH, BIAS, DROP>, sm);
+    attn_bwd_mf_kernel<NT, DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), dim3(64 * a.G), sm, s>>>(a);
   }
 }
 
 template <int NT, int DH>
 void launch_bwd3(const AttnBfArgs& a, hipStream_t s) {
-  const size_t sm = bwd_lds<DH>(a.G, NT, a.relmean ? a.tk : 0);
-  const dim3 grid(a.B, a.H / a.G), blk(64 * a.G);
+  const size_t sm = NT > 4 ? bwdl_lds<DH, NT>(a.relmean ? a.tk : 0) : bwd_lds<DH, NT>(a.G, a.relmean ? a.tk : 0);
   const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
-  if (bias && drop) attn_bwd_mf_kernel<NT, DH, true, true><<<grid, blk, sm, s>>>(a);
-  else if (bias) attn_bwd_mf_kernel<NT, DH, true, false><<<grid, blk, sm, s>>>(a);
-  else if (drop) attn_bwd_mf_kernel<NT, DH, false, true><<<grid, blk, sm, s>>>(a);
-  else attn_bwd_mf_kernel<NT, DH, false, false><<<grid, blk, sm, s>>>(a);
+  if (bias && drop) launch_bwd4<NT, DH, true, true>(a, sm, s);
+  else if (bias) launch_bwd4<NT, DH, true, false>(a, sm, s);
+  else if (drop) launch_bwd4<NT, DH, false, true>(a, sm, s);
+  else launch_bwd4<NT, DH, false, false>(a, sm, s);
 }
 
 template <int DH>
@@ -539,12 +876,18 @@ void launch_bwd2(const AttnBfArgs& a, hipStream_t s) {
     case 1: launch_bwd3<1, DH>(a, s); break;
     case 2: launch_bwd3<2, DH>(a, s); break;
     case 3: launch_bwd3<3, DH>(a, s); break;
-    default: launch_bwd3<4, DH>(a, s); break;
+    case 4: launch_bwd3<4, DH>(a, s); break;
+    case 5: launch_bwd3<5, DH>(a, s); break;
+    case 6: launch_bwd3<6, DH>(a, s); break;
+    case 7: launch_bwd3<7, DH>(a, s); break;
+    case 8: launch_bwd3<8, DH>(a, s); break;
+    case 9: launch_bwd3<9, DH>(a, s); break;
+    default: launch_bwd3<10, DH>(a, s); break;
   }
 }
 
 bool bf_ok(int K, int H, int D) {
-  if (K < 1 || K > KT || H < 1 || D % H) return false;
+  if (K < 1 || K > 16 * NT_MAX || H < 1 || D % H) return false;
   const int dh = D / H;
   return dh == 4 || dh == 8;
 }
@@ -560,7 +903,7 @@ extern "C" int ctr_attn_fwd_bf(const float* qkv, int B, int K, int H, int D, con
                                uint32_t drop_key, uint32_t drop_thresh, float drop_scale, uint32_t* mask, float* o,
                                float* mrow, float* lrow, void* stream) {
   if (B == 0) return 0;
-  CTR_REQUIRE(bf_ok(K, H, D), "ctr_attn_fwd_bf: K <= 64 and head dim 4 or 8");
+  CTR_REQUIRE(bf_ok(K, H, D), "ctr_attn_fwd_bf: K <= 160 and head dim 4 or 8");
   CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
   CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
   AttnBfArgs a{};
@@ -580,7 +923,7 @@ extern "C" int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO
                                float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow,
                                float* dqkv, float* drel_part, void* stream) {
   if (B == 0) return 0;
-  CTR_REQUIRE(bf_ok(K, H, D), "ctr_attn_bwd_bf: K <= 64 and head dim 4 or 8");
+  CTR_REQUIRE(bf_ok(K, H, D), "ctr_attn_bwd_bf: K <= 160 and head dim 4 or 8");
   CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
   CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
   AttnBfArgs a{};

@@ -209,10 +209,10 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
             # (and its exchange planned, tossctr/shard.py) while this step runs
             return store.batch(idx, slot=step % 2 if shard else 0), n_rows
 
-        nxt = batch_at(0)
+        nxt = batch_at(0) if shard else None
         for step in range(steps_per_epoch):
             global_step += 1
-            (inputs, y), n_rows = nxt
+            (inputs, y), n_rows = nxt if nxt is not None else batch_at(step)
             nxt = batch_at(step + 1) if shard and step + 1 < steps_per_epoch else None
             opt.param_groups[0]["lr"] = cosine_warmup_lr(epoch - 1, step, steps_per_epoch, cfg["train"]["lr"], warmup,
                                                          epochs)
