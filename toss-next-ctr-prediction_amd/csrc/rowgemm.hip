@@ -11,10 +11,11 @@
 //     holds whole 16-column strips of a row per lane group -> the RMSNorm row sum is a 16-lane
 //     reduction.
 //   ctr_rowgemm_wgrad dW = dY^T X over all rows, plus db = colsum(dY), for one nn.Linear
-//     Each wave owns a contiguous row range; a k-step of the MFMA is 4 rows (lane group g = row), the
-//     bias grad is one more 16-column block whose B operand is the ones column.  Each wave writes its
-//     partial [dW | db] slab row laid out like the gradient arena (weight, then the bias at o_db);
-//     ctr_colsum reduces the slab rows in a fixed order -- deterministic, no atomics.
+//     Each workgroup owns a contiguous row range (its four waves interleaved 32-row groups); a k-step of the
+//     MFMA is 4 rows (lane group g = row), the bias grad is one more 16-column block whose B operand is the
+//     ones column.  Each workgroup writes its partial [dW | db] slab row laid out like the gradient arena
+//     (weight, then the bias at o_db); ctr_colsum reduces the slab rows in a fixed order -- deterministic,
+//     no atomics.
 // f32-input MFMA = an exact fmaf chain per lane: results differ from torch's sgemm only in summation
 // order.
 #include "common.h"
@@ -162,23 +163,28 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
   }
 }
 
-// dW[NO x NIN] partial of one wave over rows [m_begin, m_end): C tile (I, J) = dY[:, 16I..]^T X[:, 16J..]
+// dW[NO x NIN] partial of one workgroup over rows [m_begin, m_end): C tile (I, J) = dY[:, 16I..]^T X[:, 16J..].
+// Four waves take interleaved 32-row groups of the range (eight 4-row k-steps of loads in flight each, four
+// waves per SIMD's worth of latency hiding: one wave per SIMD ran the streams at 2-2.5 TB/s); their partials
+// are summed in LDS in a fixed wave order and the workgroup writes one slab row -- deterministic.
 template <int NO, int NIN>
-__global__ __launch_bounds__(64) void rowgemm_wgrad_kernel(const float* __restrict__ dY, int ldy,
-                                                           const float* __restrict__ X, int ldx, int M,
-                                                           int rows_per_wave, float* __restrict__ slab,
-                                                           long ld_slab, int o_db) {
+__global__ __launch_bounds__(256) void rowgemm_wgrad_kernel(const float* __restrict__ dY, int ldy,
+                                                            const float* __restrict__ X, int ldx, int M,
+                                                            int rows_per_wg, float* __restrict__ slab,
+                                                            long ld_slab, int o_db) {
   constexpr int IO = NO / 16, JW = NIN / 16;
-  constexpr int U = 8;                                       // k-steps (4 rows each) loaded together
-  const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
-  const int m_begin = blockIdx.x * rows_per_wave, m_end = min(M, m_begin + rows_per_wave);
+  constexpr int U = NO >= 96 ? 4 : 8;                       // k-steps (4 rows each) loaded together
+  constexpr int NA = IO * (JW + 1) * 4;                      // accumulator floats per lane
+  __shared__ float red[3][NA][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int m_begin = blockIdx.x * rows_per_wg, m_end = min(M, m_begin + rows_per_wg);
   f32x4 acc[IO][JW + 1];                                     // + the ones block (bias grad)
 #pragma unroll
   for (int i = 0; i < IO; ++i)
 #pragma unroll
     for (int j = 0; j <= JW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float one = c == 0 ? 1.f : 0.f;
-  for (int m0 = m_begin; m0 < m_end; m0 += 4 * U) {
+  for (int m0 = m_begin + 4 * U * w; m0 < m_end; m0 += 4 * 4 * U) {
     float ay[U][IO], bx[U][JW];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -198,6 +204,24 @@ __global__ __launch_bounds__(64) void rowgemm_wgrad_kernel(const float* __restri
         acc[i][JW] = rg_mfma(ay[u][i], one, acc[i][JW]);
       }
   }
+  if (w > 0) {
+#pragma unroll
+    for (int i = 0; i < IO; ++i)
+#pragma unroll
+      for (int j = 0; j <= JW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w - 1][(i * (JW + 1) + j) * 4 + r][lane] = acc[i][j][r];
+  }
+  __syncthreads();
+  if (w != 0) return;
+#pragma unroll 1
+  for (int src = 0; src < 3; ++src)
+#pragma unroll
+    for (int i = 0; i < IO; ++i)
+#pragma unroll
+      for (int j = 0; j <= JW; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[src][(i * (JW + 1) + j) * 4 + r][lane];
   float* out = slab + (long)blockIdx.x * ld_slab;
 #pragma unroll
   for (int i = 0; i < IO; ++i)
@@ -239,13 +263,11 @@ static bool wgrad_shape(int NO, int NIN) {
   return (NIN == 16 && (NO == 16 || NO == 48)) || (NIN == 32 && (NO == 32 || NO == 96));
 }
 
-// wave w of the weight-grad kernel owns rows [w*rpw, (w+1)*rpw): ~1024 waves (one per SIMD: the fp32
-// 16x16x4 MFMAs, 32 cycles each, are spread over every SIMD), eight 4-row k-steps of loads in flight each,
-// rpw a multiple of 32 -- a 1024-row slab for the column sum (2048 waves of 4 k-steps wrote 2048 rows for
-// the same loads in flight)
+// workgroup b of the weight-grad kernel owns rows [b*rpw, (b+1)*rpw): ~512 workgroups of four waves (two per
+// CU), rpw a multiple of 128 (one 32-row group per wave per pass) -- a <= 512-row slab for the column sum
 static void wgrad_split(int M, int* rpw, int* waves) {
-  const int target = std::max(1, std::min(1024, (M + 63) / 64));
-  *rpw = ((M + target - 1) / target + 31) / 32 * 32;
+  const int target = std::max(1, std::min(512, (M + 255) / 256));
+  *rpw = ((M + target - 1) / target + 127) / 128 * 128;
   *waves = (M + *rpw - 1) / *rpw;
 }
 
@@ -287,9 +309,9 @@ extern "C" int ctr_rowgemm_wgrad(const float* dY, int ldy, const float* X, int l
   int rpw, grid;
   wgrad_split(M, &rpw, &grid);
   hipStream_t s = (hipStream_t)stream;
-  if (NIN == 16 && NO == 16) rowgemm_wgrad_kernel<16, 16><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
-  else if (NIN == 16) rowgemm_wgrad_kernel<48, 16><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
-  else if (NO == 32) rowgemm_wgrad_kernel<32, 32><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
-  else rowgemm_wgrad_kernel<96, 32><<<grid, 64, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  if (NIN == 16 && NO == 16) rowgemm_wgrad_kernel<16, 16><<<grid, 256, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  else if (NIN == 16) rowgemm_wgrad_kernel<48, 16><<<grid, 256, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  else if (NO == 32) rowgemm_wgrad_kernel<32, 32><<<grid, 256, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
+  else rowgemm_wgrad_kernel<96, 32><<<grid, 256, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
   return check_launch("rowgemm_wgrad");
 }
