@@ -101,24 +101,47 @@ __global__ __launch_bounds__(256) void topk_bwd_kernel(const int* __restrict__ t
   if (b >= B) return;
   const int* tb = tok + (long)b * K;
   const float* dv = dvals + (long)b * K;
+  // keys in chunks of TB_CH: the chunk's token / weight loads, then its row gathers, all independent (one memory
+  // round trip each per chunk instead of a token -> row dependency per key); summed in ascending k as before
+  constexpr int TB_CH = 16;
   if (D <= 32) {    // two half-waves take the even / odd k, combined in a fixed order
     const int d = lane & 31, h = lane >> 5;
     float acc = 0.f;
     if (d < D) {
-#pragma unroll 4
-      for (int k = h; k < K; k += 2) {
-        const int t = tb[k];
-        if (t != pad_id) acc = fmaf(dv[k], E_att[(long)t * D + d], acc);
+      for (int k0 = h; k0 < K; k0 += 2 * TB_CH) {
+        int t[TB_CH];
+        float w[TB_CH], e[TB_CH];
+#pragma unroll
+        for (int u = 0; u < TB_CH; ++u) {
+          const int k = k0 + 2 * u;
+          t[u] = k < K ? tb[k] : pad_id;
+          w[u] = k < K ? dv[k] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < TB_CH; ++u) e[u] = t[u] != pad_id ? E_att[(long)t[u] * D + d] : 0.f;
+#pragma unroll
+        for (int u = 0; u < TB_CH; ++u)
+          if (t[u] != pad_id) acc = fmaf(w[u], e[u], acc);
       }
     }
     const float other = __shfl_down(acc, 32);
     if (h == 0 && d < D) dq[(long)b * D + d] = acc + other;
   } else if (lane < D) {
     float acc = 0.f;
-#pragma unroll 4
-    for (int k = 0; k < K; ++k) {
-      const int t = tb[k];
-      if (t != pad_id) acc = fmaf(dv[k], E_att[(long)t * D + lane], acc);
+    for (int k0 = 0; k0 < K; k0 += TB_CH) {
+      int t[TB_CH];
+      float w[TB_CH], e[TB_CH];
+#pragma unroll
+      for (int u = 0; u < TB_CH; ++u) {
+        const int k = k0 + u;
+        t[u] = k < K ? tb[k] : pad_id;
+        w[u] = k < K ? dv[k] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < TB_CH; ++u) e[u] = t[u] != pad_id ? E_att[(long)t[u] * D + lane] : 0.f;
+#pragma unroll
+      for (int u = 0; u < TB_CH; ++u)
+        if (t[u] != pad_id) acc = fmaf(w[u], e[u], acc);
     }
     dq[(long)b * D + lane] = acc;
   }

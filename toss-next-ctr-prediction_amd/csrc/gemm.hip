@@ -13,6 +13,8 @@
 // fp32 from HBM, the staging store rounds to bf16 (v_cvt_pk_bf16_f32, round-to-nearest-even) into
 // [row][k] LDS tiles of BK = 32, and v_mfma_f32_16x16x32_bf16 accumulates in fp32 -- one MFMA per
 // 16x16 block and k-slice where the fp32 form issues eight.  Outputs and epilogues stay fp32.
+#include <cstdlib>
+
 #include "common.h"
 #include "ctr_hip.h"
 
@@ -571,6 +573,7 @@ struct GemmBfArgs {
   const __bf16* A;
   const __bf16* B;
   int mt, nt;            // tiles along M, N
+  int gm;                // grouped tile order: m-tiles per group (0: n fastest over all tiles)
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds) {
@@ -633,7 +636,21 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
   // bijective XCD remap: consecutive ids (same XCD: dispatch is round-robin over 8 XCDs)
   const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
   const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-  const int nt_i = id % p.nt, rest = id / p.nt, mt_i = rest % p.mt, z = rest / p.mt;
+  int nt_i, mt_i, z;
+  if (p.gm > 0) {
+    // grouped order: GM m-tiles fastest, then n, group by group -- the B slab of an n-tile is reused by the
+    // group's GM m-tiles while it is in the XCD's L2, and the group's A slabs stay there across n
+    const int per = p.mt * p.nt, t = id % per;
+    z = id / per;
+    const int gsz = p.gm * p.nt, grp = t / gsz, m0g = grp * p.gm, gm = min(p.mt - m0g, p.gm), u = t - grp * gsz;
+    mt_i = m0g + u % gm;
+    nt_i = u / gm;
+  } else {
+    nt_i = id % p.nt;
+    const int rest = id / p.nt;
+    mt_i = rest % p.mt;
+    z = rest / p.mt;
+  }
   const int m0 = mt_i * 128, n0 = nt_i * 128;
   const int kz0 = z * g.klen, kz1 = min(g.K, kz0 + g.klen);
   const int nkt = kz1 > kz0 ? (kz1 - kz0) / 64 : 0;
@@ -878,6 +895,11 @@ extern "C" int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta
   p.B = (const __bf16*)B;
   p.mt = cdiv(M, 128);
   p.nt = cdiv(N, 128);
+  static const int gm_env = [] {
+    const char* e = getenv("CTR_GEMM_BF_GM");
+    return e ? atoi(e) : -1;
+  }();
+  p.gm = gm_env >= 0 ? gm_env : 0;      // grouped order: level in the step (4.111 vs 4.117 ms), kept for A/B
   const int grid = p.mt * p.nt * splits;
   hipStream_t s = (hipStream_t)stream;
   if (!ta && tb) gemm_bf_kernel<false, true><<<grid, 256, 0, s>>>(p);
