@@ -116,27 +116,23 @@ __device__ __forceinline__ float grp_sum(float v) {
   return grp_reduce(v, [](float p, float q) { return p + q; });
 }
 
-// Workgroup staging: q * scale, k, v (and dO) of the group's G heads as bf16 [KT][RS] images.  Head u takes
-// HS = dh + 4 slots of a row: its dh dims, then a 4-slot chunk whose first slot carries the padded-key mask
-// through the score product (k: 1 on padded keys j >= K, q: -3e38), zeros elsewhere; rows >= K are zero.
-// An MFMA operand read of lane group g takes slots 4g .. 4g+3 of the head -- groups with 4g >= HS read
-// zeros instead (registers, not LDS) -- so S^T = K Q^T carries -3e38 (-> -inf after the log2 scale) on every
-// padded key and an exact +-0 elsewhere: no per-element masking.
-// K > 64 (nt > 4) uses compact rows to halve the LDS per head: the four heads' dims back to back, then ONE mask
-// chunk (slot 4 dh) and one zero chunk (slot 4 dh + 4) shared by the heads of the row; a head's operand read
-// of lane group g takes dims 4g .. 4g+3 while 4g < dh, the row's mask chunk at 4g == dh, the zero chunk beyond.
-// Column (transposed) reads take 16 slots from the head's first dim: the slots past its dims land in output
-// rows d >= dh of the product, which are never stored.
+// Workgroup staging: q * scale, k, v (and dO) of the group's G heads as bf16 [KT][RS] images; rows >= K are zero.
+// The mask chunk's first slot carries the padded-key mask through the score product (k: 1 on padded keys j >= K,
+// q: -3e38), so S^T = K Q^T carries -3e38 (-> -inf after the log2 scale) on every padded key and an exact +-0
+// elsewhere: no per-element masking.  Compact rows: the four heads' dims back to back, then ONE mask chunk (slot 4 dh) and one zero chunk (slot
+// 4 dh + 4) shared by the heads of the row; a head's operand read of lane group g takes dims 4g .. 4g+3 while
+// 4g < dh, the row's mask chunk at 4g == dh, the zero chunk beyond.  Column (transposed) reads take 16 slots from
+// the head's first dim: the slots past its dims land in output rows d >= dh of the product, which are never
+// stored.  (A mask chunk per head took 52 instead of 40 slots per row at dh = 8.)
 template <int DH, int NT>
 struct Stg {
-  static constexpr bool CMP = NT > 4;
   static constexpr int KT = Kt<NT>::KT;
-  static constexpr int HS = CMP ? DH : DH + 4;      // slots per head
-  static constexpr int RS = CMP ? 4 * DH + 8 : 4 * HS + 4;   // row stride (bf16 elements), <= 4 heads
+  static constexpr int HS = DH;                     // slots per head
+  static constexpr int RS = 4 * DH + 8;             // row stride (bf16 elements), <= 4 heads
   static constexpr int IM = KT * RS;                // elements per staged operand
   static constexpr int PAD = 16;                    // transposed reads past the last head of the last row
-  static constexpr int MOFF = 4 * DH;               // compact: the row's mask chunk
-  static constexpr int ZOFF = CMP ? 4 * DH + 4 : 4 * HS;   // a zero chunk (compact: in every row; else row 0)
+  static constexpr int MOFF = 4 * DH;               // the row's mask chunk
+  static constexpr int ZOFF = 4 * DH + 4;           // the row's zero chunk
 };
 constexpr float NEG_BIG = -3.0e38f;
 
@@ -147,60 +143,27 @@ __device__ __forceinline__ void stage(const AttnBfArgs& a, __bf16* sq, __bf16* s
   const int K = a.K, D = a.D, G = a.G, b = blockIdx.x;
   const float* base = a.qkv + (long)b * K * 3 * D + blockIdx.y * G * DH;
   const float* dob = WITH_DO ? a.dO + (long)b * K * D + blockIdx.y * G * DH : nullptr;
-  if constexpr (S::CMP) {
-    constexpr int NCD = DH / 4, NCR = 4 * NCD + 2;  // chunks per row: 4 heads' dims, mask, zero
-    for (int e = threadIdx.x; e < KT * NCR; e += blockDim.x) {
-      const int j = e / NCR, ch = e - j * NCR;
-      f32x4 q = {0.f, 0.f, 0.f, 0.f}, k = q, v = q, d = q;
-      int o;
-      if (ch < 4 * NCD) {
-        const int u = ch / NCD, dc = ch - u * NCD;
-        o = j * S::RS + u * DH + 4 * dc;
-        if (u < G && j < K) {
-          const float* r = base + (long)j * 3 * D + u * DH + 4 * dc;
-          q = *(const f32x4*)r * a.scale;
-          k = *(const f32x4*)(r + D);
-          v = *(const f32x4*)(r + 2 * D);
-          if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * dc);
-        }
-      } else if (ch == 4 * NCD) {                   // the row's mask chunk
-        o = j * S::RS + S::MOFF;
-        q[0] = NEG_BIG;
-        k[0] = j >= K ? 1.f : 0.f;
-      } else {                                      // the row's zero chunk
-        o = j * S::RS + S::ZOFF;
-      }
-      *(bf16x4*)(sq + o) = to_bf4(q);
-      *(bf16x4*)(sk + o) = to_bf4(k);
-      *(bf16x4*)(sv + o) = to_bf4(v);
-      if (WITH_DO) *(bf16x4*)(sdo + o) = to_bf4(d);
-    }
-    return;
-  }
-  constexpr int NCH = S::HS / 4;                    // 4-slot chunks per head
-  for (int e = threadIdx.x; e < KT * 4 * NCH; e += blockDim.x) {
-    const int ch = e % NCH, ju = e / NCH, u = ju & 3, j = ju >> 2;
-    if (u >= G) continue;
+  constexpr int NCD = DH / 4, NCR = 4 * NCD + 2;  // chunks per row: 4 heads' dims, mask, zero
+  for (int e = threadIdx.x; e < KT * NCR; e += blockDim.x) {
+    const int j = e / NCR, ch = e - j * NCR;
     f32x4 q = {0.f, 0.f, 0.f, 0.f}, k = q, v = q, d = q;
-    if (4 * ch < DH) {
-      if (j < K) {
-        const float* r = base + (long)j * 3 * D + u * DH + 4 * ch;
+    int o;
+    if (ch < 4 * NCD) {
+      const int u = ch / NCD, dc = ch - u * NCD;
+      o = j * S::RS + u * DH + 4 * dc;
+      if (u < G && j < K) {
+        const float* r = base + (long)j * 3 * D + u * DH + 4 * dc;
         q = *(const f32x4*)r * a.scale;
         k = *(const f32x4*)(r + D);
         v = *(const f32x4*)(r + 2 * D);
-        if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * ch);
+        if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * dc);
       }
-    } else {                                        // the mask chunk
+    } else if (ch == 4 * NCD) {                   // the row's mask chunk
+      o = j * S::RS + S::MOFF;
       q[0] = NEG_BIG;
       k[0] = j >= K ? 1.f : 0.f;
-    }
-    const int o = j * S::RS + u * S::HS + 4 * ch;
-    if (e < 1) {                                    // the zero chunk (row 0, past the 4th head)
-      const bf16x4 z4 = {};
-      *(bf16x4*)(sq + S::ZOFF) = z4;
-      *(bf16x4*)(sk + S::ZOFF) = z4;
-      *(bf16x4*)(sv + S::ZOFF) = z4;
-      if (WITH_DO) *(bf16x4*)(sdo + S::ZOFF) = z4;
+    } else {                                      // the row's zero chunk
+      o = j * S::RS + S::ZOFF;
     }
     *(bf16x4*)(sq + o) = to_bf4(q);
     *(bf16x4*)(sk + o) = to_bf4(k);
@@ -239,10 +202,7 @@ __host__ __device__ constexpr int img_elems() { return Kt<NT>::KT * 16; }   // b
 template <int DH, int NT>
 __device__ __forceinline__ bf16x4 op_row(const __bf16* img, int row, int hs, int g) {
   using S = Stg<DH, NT>;
-  if constexpr (S::CMP)
-    return ld4(img + row * S::RS + (4 * g < DH ? hs + 4 * g : 4 * g == DH ? S::MOFF : S::ZOFF));
-  else
-    return ld4(img + (4 * g < S::HS ? row * S::RS + hs + 4 * g : S::ZOFF));
+  return ld4(img + row * S::RS + (4 * g < DH ? hs + 4 * g : 4 * g == DH ? S::MOFF : S::ZOFF));
 }
 template <int DH, int NT>
 __device__ __forceinline__ bf16x4 op_col(const __bf16* img, int row0, int hs, int g, int c) {
@@ -408,8 +368,10 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
 // ------------------------------------------------------------------------------------------------
 // backward: dq, dk, dv into dqkv; positional-bias grad partials (diagonal sums of dS over the group's heads).
 // Key tiles outer (dk, dv of a key tile complete in its iteration), query tiles inner (dq accumulates).
+// four waves per SIMD (128 registers, no spill; with the compact rows four workgroups fit a CU's LDS): 141 -> 126 us
+// at cfg2 against three
 template <int NT, int DH, bool BIAS, bool DROP>
-__global__ __launch_bounds__(256) void attn_bwd_mf_kernel(AttnBfArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_mf_kernel(AttnBfArgs a) {
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   constexpr int ND = 2 * NT - 1, IMG = img_elems<NT>(), KT = KB::KT;

@@ -166,9 +166,11 @@ __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restric
   }
   const float* T = cm.tabs + cm.tab_off[c];
   const long tld = cm.row_ld ? cm.row_ld : dc;
-  for (int e = tid; e < nb * 64; e += 256) {
-    const int i = e >> 6, k = e & 63;
-    if (k < dc) sT[i * CE_LD + k] = T[(long)xcat[(long)(b0 + i) * Fc + c] * tld + k];
+  // (sample, element) items over the table's dc elements only (the 64-wide loop left most threads idle at the
+  // narrow tables and gave each busy thread 16 dependent index -> row round trips)
+  for (int e = tid; e < nb * dc; e += 256) {
+    const int i = e / dc, k = e - i * dc;
+    sT[i * CE_LD + k] = T[(long)xcat[(long)(b0 + i) * Fc + c] * tld + k];
   }
   __syncthreads();
   for (int e = tid; e < nb * D; e += 256) {
