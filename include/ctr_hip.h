@@ -199,6 +199,17 @@ int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO, int B, in
                     const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
                     float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow, float* dqkv,
                     float* drel_part, void* stream);
+/* amp: bf16 -- the first half of an encoder layer in one launch, src/models/dare.py:53-62
+ * (qkv = in_proj(x); o = attention(qkv); x1 = norm1(x + out_proj(o))): one workgroup per sample, K <= 64,
+ * D = 32, 4 or 8 heads, tk <= 64 (ctr_attn_layer_fwd_ok).  Writes exactly what ctr_rowgemm (in_proj),
+ * ctr_attn_fwd_bf and ctr_rowgemm (out_proj + residual + RMSNorm, eps) write -- qkv, o, mrow, lrow, mask, h1,
+ * r1, x1 -- with the same bits (same summation orders).                                                     */
+int ctr_attn_layer_fwd_ok(int K, int H, int D);
+int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
+                          const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                          float drop_scale, uint32_t* mask, const float* w_out, const float* b_out, const float* nw1,
+                          float eps, float* qkv, float* o, float* mrow, float* lrow, float* h1, float* r1, float* x1,
+                          void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused position-wise FFN + residual + RMSNorm of DAREEncoderLayer, src/models/dare.py:53-70

@@ -336,6 +336,58 @@ def test_attention_bf16_vs_torch(K, H, D, p, bias):
     assert torch.equal(dqkv, dqkv2) and (not bias or torch.equal(drp_first, drp2))
 
 
+@pytest.mark.parametrize("K,H,p", [(60, 8, 0.1), (64, 8, 0.1), (61, 8, 0.1), (48, 4, 0.2), (33, 8, 0.0),
+                                   (17, 4, 0.1), (1, 8, 0.1), (50, 4, 0.0)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_attn_layer_fwd_equals_three_launches(K, H, p, bias):
+    """amp: ctr_attn_layer_fwd_bf (in_proj -> attention -> out_proj + residual + RMSNorm in one launch) writes
+    bit for bit what ctr_rowgemm + ctr_attn_fwd_bf + ctr_rowgemm write: qkv, o, mrow, lrow, the keep bits, h1, r1,
+    x1 (the same summation orders; the three-launch path is covered against torch above)."""
+    L = _lib()
+    D = 32
+    assert L.query("ctr_attn_layer_fwd_ok", K, H, D) == 1
+    from tossctr.rng import drop_args
+    B, dh, tk = 37, D // H, K
+    g = torch.Generator(device="cuda").manual_seed(K * 17 + H)
+    x = torch.randn(B * K, D, device="cuda", generator=g)
+    w_in = torch.randn(3 * D, D, device="cuda", generator=g) * D ** -0.5
+    b_in = torch.randn(3 * D, device="cuda", generator=g) * 0.1
+    w_out = torch.randn(D, D, device="cuda", generator=g) * D ** -0.5
+    b_out = torch.randn(D, device="cuda", generator=g) * 0.1
+    nw = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
+    relmean = torch.randn(2 * tk + 1, device="cuda", generator=g)
+    rm = ptr(relmean) if bias else None
+    dk = drop_args(777, 3, p, True)
+    scale = float(np.float32(math.sqrt(1.0 / dh)))
+    st = stream()
+
+    def bufs():
+        return dict(qkv=torch.full((B * K, 3 * D), float("nan"), device="cuda"),
+                    o=torch.full((B * K, D), float("nan"), device="cuda"),
+                    mrow=torch.full((B * H * K,), float("nan"), device="cuda"),
+                    lrow=torch.full((B * H * K,), float("nan"), device="cuda"),
+                    mask=torch.zeros(L.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda"),
+                    h1=torch.full((B * K, D), float("nan"), device="cuda"),
+                    r1=torch.full((B * K,), float("nan"), device="cuda"),
+                    x1=torch.full((B * K, D), float("nan"), device="cuda"))
+    r, f = bufs(), bufs()
+    M = B * K
+    L.call("ctr_rowgemm", M, D, 3 * D, ptr(x), D, ptr(w_in), 1, ptr(r["qkv"]), 3 * D, ptr(b_in), None, 0, None, 0,
+           None, None, None, 1e-6, st)
+    L.call("ctr_attn_fwd_bf", ptr(r["qkv"]), B, K, H, D, rm, tk, scale, *dk, ptr(r["mask"]), ptr(r["o"]),
+           ptr(r["mrow"]), ptr(r["lrow"]), st)
+    L.call("ctr_rowgemm", M, D, D, ptr(r["o"]), D, ptr(w_out), 1, ptr(r["x1"]), D, ptr(b_out), None, 0, ptr(x), D,
+           ptr(nw), ptr(r["h1"]), ptr(r["r1"]), 1e-6, st)
+    L.call("ctr_attn_layer_fwd_bf", ptr(x), B, K, H, D, ptr(w_in), ptr(b_in), rm, tk, scale, *dk, ptr(f["mask"]),
+           ptr(w_out), ptr(b_out), ptr(nw), 1e-6, ptr(f["qkv"]), ptr(f["o"]), ptr(f["mrow"]), ptr(f["lrow"]),
+           ptr(f["h1"]), ptr(f["r1"]), ptr(f["x1"]), st)
+    torch.cuda.synchronize()
+    for name in r:
+        a, b = r[name], f[name]
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), \
+            (name, int((a.view(torch.int32) != b.view(torch.int32)).sum()), a.numel())
+
+
 @pytest.mark.parametrize("L_,K,D", [(100, 60, 32), (40, 40, 16), (400, 148, 64), (7, 3, 8)])
 def test_topk_select_vs_torch(L_, K, D):
     L = _lib()

@@ -23,6 +23,8 @@
 // pos = 16 ti + 4 tj + r for nt <= 4 (NW = 2: bit 16 (ti & 1) + 4 tj + r of word ti >> 1) and key-tile major
 // pos = 4 nt tj + 4 ti + r beyond (NW = ceil(4 nt^2 / 32)), where the backward walks key tiles in a loop.  The keep decision is the same counter hash as every other dropout site (common.h).
 // mrow holds the row max in log2 units (the forward's and backward's exp2 argument), lrow the row sum.
+#include <type_traits>
+
 #include "common.h"
 #include "ctr_hip.h"
 
@@ -743,6 +745,235 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fused first half of an encoder layer (amp: bf16, D = 32, every head of a sample in one workgroup, K <= 64):
+//   qkv = x W_in^T + b_in  ->  attention (the forward above, one wave per head)  ->
+//   x1 = norm1(x + o W_out^T + b_out)   (src/models/dare.py:53-62: MultiheadAttention + residual + RMSNorm)
+// One workgroup per sample.  The projections run on v_mfma_f32_16x16x4f32 (exact fp32 fmaf chains, as the row
+// kernels they replace): the x rows, the attention output o and the out-projection result pass through LDS, and
+// qkv / o / h1 / r1 / x1 are written for the backward and the next kernel -- two launches (in_proj, out_proj +
+// norm) and their boundaries fewer per layer, and qkv / o are not read back from HBM by the forward.
+namespace lf {
+constexpr int D = 32, RS = 40, MOFF = 32, ZOFF = 36;     // staged bf16 rows: 8 x 4 or 4 x 8 head dims, mask, zero
+constexpr int XS = D + 4;                                // fp32 x / o / y tile rows
+}  // namespace lf
+
+template <int DH>
+__device__ __forceinline__ bf16x4 lf_row(const __bf16* img, int row, int hs, int g) {
+  return ld4(img + row * lf::RS + (4 * g < DH ? hs + 4 * g : 4 * g == DH ? lf::MOFF : lf::ZOFF));
+}
+__device__ __forceinline__ bf16x4 lf_col(const __bf16* img, int row0, int hs, int g, int c) {
+  return tr4(img + (row0 + 4 * g + (c >> 2)) * lf::RS + hs + 4 * (c & 3));
+}
+
+struct LayerFwdArgs {
+  AttnBfArgs at;          // qkv (output), K, H, relmean, scale, drop, mask, o, mrow, lrow (B = samples)
+  const float* x;         // (B*K, 32) layer input
+  const float* w_in;      // (96, 32), b_in (96)
+  const float* b_in;
+  const float* w_out;     // (32, 32), b_out (32)
+  const float* b_out;
+  const float* nw1;       // (32) norm1 weight
+  float eps;
+  float* qkv;             // (B*K, 96) saved for the backward
+  float* h1;              // (B*K, 32) pre-norm sum, r1 (B*K) its rsqrt, x1 (B*K, 32) the layer's next input
+  float* r1;
+  float* x1;
+};
+
+template <int DH, bool BIAS, int DROPK>
+__global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
+  constexpr int NT = 4, KT = 64, G = lf::D / DH;     // all heads of the sample
+  const AttnBfArgs& a = L.at;
+  __shared__ __attribute__((aligned(16))) __bf16 sq[KT * lf::RS + 16];
+  __shared__ __attribute__((aligned(16))) __bf16 sk[KT * lf::RS + 16];
+  __shared__ __attribute__((aligned(16))) __bf16 sv[KT * lf::RS + 16];
+  __shared__ __attribute__((aligned(16))) float xt[KT * lf::XS];      // x rows, then the out-projection result
+  __shared__ __attribute__((aligned(16))) float ot[KT * lf::XS];      // attention output o
+  __shared__ float srel[2 * 64 + 2 * KT + 4];
+  const int K = a.K, b = blockIdx.x, tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const long row0 = (long)b * K;
+  // ---- x rows -> LDS (zero rows >= K); mask / zero chunks; positional bias (log2 units)
+  for (int e = tid; e < KT * lf::D / 4; e += 64 * G) {
+    const int i = e / (lf::D / 4), c4 = (e % (lf::D / 4)) * 4;
+    const f32x4 v = i < K ? *(const f32x4*)(L.x + (row0 + i) * lf::D + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(xt + i * lf::XS + c4) = v;
+  }
+  for (int j = tid; j < KT; j += 64 * G) {
+    const bf16x4 z4 = {};
+    bf16x4 mq = z4, mk = z4;
+    mq[0] = (__bf16)NEG_BIG;
+    mk[0] = (__bf16)(j >= K ? 1.f : 0.f);
+    *(bf16x4*)(sq + j * lf::RS + lf::MOFF) = mq;
+    *(bf16x4*)(sk + j * lf::RS + lf::MOFF) = mk;
+    *(bf16x4*)(sv + j * lf::RS + lf::MOFF) = z4;
+    *(bf16x4*)(sq + j * lf::RS + lf::ZOFF) = z4;
+    *(bf16x4*)(sk + j * lf::RS + lf::ZOFF) = z4;
+    *(bf16x4*)(sv + j * lf::RS + lf::ZOFF) = z4;
+  }
+  if (BIAS) stage_rel<NT>(a, srel);
+  __syncthreads();
+  // ---- in-projection: 4 row blocks x 6 column blocks of 16, K = 32 (8 MFMA k-steps of 4); tile t -> (rb, cb)
+  for (int t = w; t < 24; t += G) {
+    const int rb = t / 6, cb = t % 6;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {       // lane group g takes k = 8g + kk: rowgemm.hip's order, the same bits
+      const float av = xt[(16 * rb + c) * lf::XS + 8 * g + kk];                 // A[i = c][k]
+      const float bv = L.w_in[(16 * cb + c) * lf::D + 8 * g + kk];              // B[k][n = c] = W_in[n][k]
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+    }
+    const int n = 16 * cb + c, sec = n >> 5, col = n & 31;                      // q | k | v section, column
+    const float bias = L.b_in[n];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * rb + 4 * g + r;
+      const float v = acc[r] + bias;
+      if (i < K) L.qkv[(row0 + i) * (3 * lf::D) + n] = v;
+      __bf16* dst = sec == 0 ? sq : sec == 1 ? sk : sv;
+      dst[i * lf::RS + col] = (__bf16)(i < K ? (sec == 0 ? v * a.scale : v) : 0.f);
+    }
+  }
+  __syncthreads();
+  // ---- attention, wave w = head h (attn_fwd_mf_kernel's per-head body at nt = 4)
+  {
+    const int h = w, hs = h * DH;
+    bf16x4 kop[NT], vtop[NT];
+#pragma unroll
+    for (int tj = 0; tj < NT; ++tj) {
+      kop[tj] = lf_row<DH>(sk, 16 * tj + c, hs, g);
+      vtop[tj] = lf_col(sv, 16 * tj, hs, g, c);
+    }
+    const float* rb = srel + KT + a.tk + 4 * g - c;
+    const long hr = ((long)b * a.H + h) * K;
+    uint32_t words[2] = {0u, 0u};
+    const float dsc = DROPK ? a.drop.scale : 1.0f;
+    const int nt = (K + 15) >> 4;
+    const uint32_t dmask = nt >= 4 ? 0xFFFFu : (1u << (4 * nt)) - 1u;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x4 qop = lf_row<DH>(sq, 16 * ti + c, hs, g);
+      const int i = 16 * ti + c;
+      const uint32_t rowbase = (uint32_t)((hr + i) * K);
+      f32x4 t[NT];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) {
+        const f32x4 sc = mma(kop[tj], qop, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          t[tj][r] = BIAS ? fmaf(sc[r], L2E, rb[16 * (tj - ti) + r]) : sc[r] * L2E;
+          mx = fmaxf(mx, t[tj][r]);
+        }
+      }
+      mx = grp_max(mx);
+      float l = 0.f;
+      uint32_t dropped = 0u;
+      bf16x4 pb[NT];
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) {
+        float pe[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pe[r] = __builtin_amdgcn_exp2f(t[tj][r] - mx);
+          l += pe[r];
+        }
+        if (DROPK) {
+          const uint32_t j0 = 16 * tj + 4 * g;
+          uint32_t half[4];
+          if (DROPK == 1) {
+            const uint32_t h0 = drop_pair_bits(a.drop, (rowbase + j0) >> 1);
+            const uint32_t h1v = drop_pair_bits(a.drop, (rowbase + j0 + 2) >> 1);
+            half[0] = h0 & 0xFFFFu;
+            half[1] = h0 >> 16;
+            half[2] = h1v & 0xFFFFu;
+            half[3] = h1v >> 16;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const uint32_t idx = rowbase + j0 + r;
+              const uint32_t hb = mix32((idx >> 1) ^ a.drop.key);
+              half[r] = (idx & 1u) ? hb >> 16 : hb & 0xFFFFu;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const uint32_t m = sign_mask(half[r] - a.drop.thresh);
+            pe[r] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, pe[r]) & ~m);
+            dropped |= m & (1u << (4 * tj + r));
+          }
+        }
+        pb[tj] = __builtin_bit_cast(bf16x4, pk_bf4(f32x4{pe[0], pe[1], pe[2], pe[3]}));
+      }
+      l = grp_sum(l);
+      f32x4 oacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) oacc = mma(vtop[tj], pb[tj], oacc);
+      const float inv = dsc / l;
+      if (4 * g < DH) {
+        const f32x4 ov = oacc * inv;
+        *(f32x4*)(ot + i * lf::XS + h * DH + 4 * g) = i < K ? ov : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (i < K) *(f32x4*)(a.o + (row0 + i) * lf::D + h * DH + 4 * g) = ov;
+      }
+      if (i < K && g == 0) {
+        a.mrow[hr + i] = mx;
+        a.lrow[hr + i] = l;
+      }
+      // the words attn_fwd_mf_kernel writes at nt = ceil(K / 16): key tiles >= nt kept, query tiles >= nt none
+      if (DROPK && ti < nt) words[ti >> 1] |= (~(dropped & dmask) & 0xFFFFu) << (16 * (ti & 1));
+    }
+    if (DROPK) {
+      uint32_t* mk = a.mask + ((long)b * a.H + h) * 128;
+      mk[lane] = words[0];
+      mk[64 + lane] = words[1];
+    }
+  }
+  __syncthreads();
+  // ---- out-projection + bias + residual + RMSNorm: wave w < 4 takes row block w, both 16-column blocks, and
+  // finishes it as rowgemm.hip's epilogue does (same k order, same per-row sum and 16-lane reduction: same bits)
+  if (w < 4) {
+    const int rb = w;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const float av = ot[(16 * rb + c) * lf::XS + 8 * g + kk];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, L.w_out[(16 * j + c) * lf::D + 8 * g + kk], acc[j], 0, 0, 0);
+    }
+    float bj[2], nw[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bj[j] = L.b_out[16 * j + c];
+      nw[j] = L.nw1[16 * j + c];
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int i = 16 * rb + 4 * g + rr;
+      float v[2], ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        v[j] = acc[j][rr] + bj[j];
+        v[j] = xt[i * lf::XS + 16 * j + c] + v[j];
+        ss += v[j] * v[j];
+      }
+      ss = group_sum<16>(ss);
+      const float r = 1.0f / sqrtf(ss / (float)lf::D + L.eps);
+      if (i < K) {
+        const long row = row0 + i;
+        if (c == 0) L.r1[row] = r;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          L.h1[row * lf::D + 16 * j + c] = v[j];
+          L.x1[row * lf::D + 16 * j + c] = nw[j] * v[j] * r;
+        }
+      }
+    }
+  }
+}
+
 int pick_g(int H) {
   int g = 1;
   for (int c = 1; c <= 4; ++c)
@@ -897,4 +1128,46 @@ extern "C" int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO
   if (D / H == 4) launch_bwd2<4>(a, s);
   else launch_bwd2<8>(a, s);
   return check_launch("attn_bwd_bf");
+}
+
+extern "C" int ctr_attn_layer_fwd_ok(int K, int H, int D) {
+  return (K >= 1 && K <= 64 && D == 32 && (H == 8 || H == 4)) ? 1 : 0;
+}
+
+extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
+                                     const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                                     float drop_scale, uint32_t* mask, const float* w_out, const float* b_out,
+                                     const float* nw1, float eps, float* qkv, float* o, float* mrow, float* lrow,
+                                     float* h1, float* r1, float* x1, void* stream) {
+  if (B == 0) return 0;
+  CTR_REQUIRE(ctr_attn_layer_fwd_ok(K, H, D), "ctr_attn_layer_fwd_bf: K <= 64, D = 32, 4 or 8 heads");
+  CTR_REQUIRE(!relmean || (tk >= K - 1 && tk <= 64), "positional-bias table shorter than K or longer than 2*64+1");
+  CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
+  LayerFwdArgs L{};
+  AttnBfArgs& a = L.at;
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = H; a.nt = (K + 15) / 16; a.tk = tk;
+  a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = mask; a.o = o; a.mrow = mrow; a.lrow = lrow;
+  L.x = x; L.w_in = w_in; L.b_in = b_in; L.w_out = w_out; L.b_out = b_out; L.nw1 = nw1; L.eps = eps;
+  L.qkv = qkv; L.h1 = h1; L.r1 = r1; L.x1 = x1;
+  hipStream_t s = (hipStream_t)stream;
+  const int nth = 64 * H;
+  const int dk = drop_thresh == 0 ? 0 : (K & 1) ? 2 : 1;
+  auto go = [&](auto dh_tag, auto bias_tag) {
+    constexpr int DH = decltype(dh_tag)::value;
+    constexpr bool BS = decltype(bias_tag)::value;
+    if (dk == 0) attn_layer_fwd_kernel<DH, BS, 0><<<B, nth, 0, s>>>(L);
+    else if (dk == 1) attn_layer_fwd_kernel<DH, BS, 1><<<B, nth, 0, s>>>(L);
+    else attn_layer_fwd_kernel<DH, BS, 2><<<B, nth, 0, s>>>(L);
+  };
+  using I4 = std::integral_constant<int, 4>;
+  using I8 = std::integral_constant<int, 8>;
+  using BT = std::true_type;
+  using BF = std::false_type;
+  if (H == 8) {
+    if (relmean) go(I4{}, BT{}); else go(I4{}, BF{});
+  } else {
+    if (relmean) go(I8{}, BT{}); else go(I8{}, BF{});
+  }
+  return check_launch("attn_layer_fwd_bf");
 }

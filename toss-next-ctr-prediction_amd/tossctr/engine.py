@@ -187,6 +187,10 @@ class Engine:
         # amp: bf16 -> the attention core on bf16 MFMA (attn_mf.hip: K <= 64, head dim 4 or 8), as the
         # reference's autocast baddbmm / bmm; other shapes keep the fp32 kernels
         self.attn_bf = bool(self.bf16 and a.n_layers > 0 and _lib.query("ctr_attn_bf_ok", a.top_k, a.H, a.D))
+        # ... and the layer's in_proj -> attention -> out_proj + residual + RMSNorm in one launch where it fits
+        # (attn_mf.hip: K <= 64, D = 32; the same bits as the three launches; CTR_ATTN_LAYER=0 for A/B)
+        self.attn_layer = bool(self.attn_bf and self.rowgemm and os.environ.get("CTR_ATTN_LAYER", "1") != "0" and
+                               _lib.query("ctr_attn_layer_fwd_ok", a.top_k, a.H, a.D))
 
     def _tab_array(self, keys, bases):
         """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
@@ -443,12 +447,6 @@ class Engine:
             Ls = {}
             x = xs[-1]
             qkv = W.get(f"qkv{li}", (M, 3 * D))
-            if self.rowgemm:
-                self.rowgemm_call(M, D, 3 * D, ptr(x), ptr(P[pre + "mha.in_proj_weight"]), 1, ptr(qkv),
-                                  bias=ptr(P[pre + "mha.in_proj_bias"]))
-            else:
-                self.gemm(M, 3 * D, D, ptr(x), D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 1, ptr(qkv), 3 * D,
-                          GemmEpi(bias=ptr(P[pre + "mha.in_proj_bias"])))
             relmean = None
             if a.add_pos:
                 relmean = W.get(f"relmean{li}", (2 * a.top_k + 1,))
@@ -459,19 +457,32 @@ class Engine:
             da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
             amask = W.get(f"amask{li}", (_lib.query("ctr_attn_mask_words", B, K, a.H),), torch.int32) \
                 if da[1] else None
-            call("ctr_attn_fwd_bf" if self.attn_bf else "ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean),
-                 a.top_k, scale, *da, ptr(amask), ptr(o), ptr(mrow), ptr(lrow), st)
             h1 = W.get(f"h1_{li}", (M, D))
             r1 = W.get(f"r1_{li}", (M,))
             x1 = W.get(f"x1_{li}", (M, D))
-            if self.rowgemm:
-                self.rowgemm_call(M, D, D, ptr(o), ptr(P[pre + "mha.out_proj.weight"]), 1, ptr(x1),
-                                  bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), norm_w=ptr(P[pre + "norm1.w"]),
-                                  norm_h=ptr(h1), norm_r=ptr(r1))
+            if self.attn_layer:
+                # in_proj -> attention -> out_proj + residual + RMSNorm in one launch (attn_mf.hip)
+                call("ctr_attn_layer_fwd_bf", ptr(x), B, K, a.H, D, ptr(P[pre + "mha.in_proj_weight"]),
+                     ptr(P[pre + "mha.in_proj_bias"]), ptr(relmean), a.top_k, scale, *da, ptr(amask),
+                     ptr(P[pre + "mha.out_proj.weight"]), ptr(P[pre + "mha.out_proj.bias"]), ptr(P[pre + "norm1.w"]),
+                     1e-6, ptr(qkv), ptr(o), ptr(mrow), ptr(lrow), ptr(h1), ptr(r1), ptr(x1), st)
             else:
-                self.gemm(M, D, D, ptr(o), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 1, ptr(x1), D,
-                          GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), ld_resid=D,
-                                  norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1), norm_eps=1e-6))
+                if self.rowgemm:
+                    self.rowgemm_call(M, D, 3 * D, ptr(x), ptr(P[pre + "mha.in_proj_weight"]), 1, ptr(qkv),
+                                      bias=ptr(P[pre + "mha.in_proj_bias"]))
+                else:
+                    self.gemm(M, 3 * D, D, ptr(x), D, 0, ptr(P[pre + "mha.in_proj_weight"]), D, 1, ptr(qkv), 3 * D,
+                              GemmEpi(bias=ptr(P[pre + "mha.in_proj_bias"])))
+                call("ctr_attn_fwd_bf" if self.attn_bf else "ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean),
+                     a.top_k, scale, *da, ptr(amask), ptr(o), ptr(mrow), ptr(lrow), st)
+                if self.rowgemm:
+                    self.rowgemm_call(M, D, D, ptr(o), ptr(P[pre + "mha.out_proj.weight"]), 1, ptr(x1),
+                                      bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x),
+                                      norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1))
+                else:
+                    self.gemm(M, D, D, ptr(o), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 1, ptr(x1), D,
+                              GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x), ld_resid=D,
+                                      norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1), norm_eps=1e-6))
             FF = a.ffn_hidden
             dfk = drop_args(seed, SITE_FFN0 + 2 * li, a.ffn_p, training)
             h2 = W.get(f"h2_{li}", (M, D))
