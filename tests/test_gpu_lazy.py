@@ -126,3 +126,62 @@ def test_touch_first_chunk_full_class_plus_hot_row():
     ml.sync()
     assert torch.equal(md.arena.buf, ml.arena.buf)
     assert torch.equal(od.m, ol.m) and torch.equal(od.v, ol.v)
+
+
+@pytest.mark.parametrize("ema", [True, False])
+def test_cat_flush_classified_equals_row_group_kernel(ema, monkeypatch):
+    """ctr_lazy_flush (lazy_flush_cls_kernel: classified row lists, four elements per lane) against the
+    per-row-group kernel it replaced (CTR_FLUSH_LEGACY=1, checked bitwise against the dense stream above), on a
+    synthetic state over every lane layout: widths 1..64 with rows that are and are not 16-byte aligned, rows
+    current / never stepped / stepped at random ticks, ticks without the AdamW step or without the EMA."""
+    from tossctr import _lib
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    g = torch.Generator(device=dev).manual_seed(11)
+    T = 23
+    hist = torch.zeros((T + 2) * _lib.query("ctr_opt_hist_entry_bytes"), dtype=torch.uint8, device=dev)
+    for t in range(1, T + 1):
+        _lib.call("ctr_opt_hist_record", hist.data_ptr(), t, 3e-3 * min(1.0, t / 7), 0.05, 0.9, 0.999, 1e-8, t,
+                  0.99, 0 if t == 9 else 1, 1 if (ema and t != 14) else 0, st)
+    widths = [1, 3, 4, 5, 7, 8, 9, 12, 16, 17, 22, 30, 33, 43, 51, 57, 64]
+    rows = [2500 + 97 * i for i in range(len(widths))]
+    n = sum(r * w for r, w in zip(rows, widths))
+    nrows = sum(rows)
+    u = torch.rand(nrows, generator=g, device=dev)
+    last0 = torch.zeros(nrows, dtype=torch.int32, device=dev)
+    nz = u < 0.3
+    last0[nz] = torch.randint(1, T, (int(nz.sum()),), generator=g, device=dev, dtype=torch.int32) | -2 ** 31
+    mid = (u >= 0.3) & (u < 0.6)
+    last0[mid] = torch.randint(1, T, (int(mid.sum()),), generator=g, device=dev, dtype=torch.int32)
+    last0[(u >= 0.6) & (u < 0.65)] = T
+    row_nz = torch.cat([(last0[o:o + r] < 0).float().repeat_interleave(w)
+                        for o, r, w in zip(np.cumsum([0] + rows[:-1]).tolist(), rows, widths)])
+    P0 = torch.randn(n, generator=g, device=dev)
+    M0 = torch.randn(n, generator=g, device=dev) * 1e-3 * row_nz
+    V0 = torch.rand(n, generator=g, device=dev) * 1e-6 * row_nz
+    E0 = P0 + 0.01 * torch.randn(n, generator=g, device=dev)
+    last = torch.empty_like(last0)
+    arr = (_lib.LazyTab * len(widths))()
+    po = ro = 0
+    for i, (r, w) in enumerate(zip(rows, widths)):
+        arr[i].p_off, arr[i].rows, arr[i].width, arr[i].key_base, arr[i].last = po, r, w, ro, last.data_ptr() + 4 * ro
+        po += r * w
+        ro += r
+    tabs = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+
+    def flush(legacy):
+        monkeypatch.setenv("CTR_FLUSH_LEGACY", "1" if legacy else "0")
+        last.copy_(last0)
+        P, M, V, E = P0.clone(), M0.clone(), V0.clone(), E0.clone() if ema else None
+        _lib.call("ctr_lazy_flush", tabs.data_ptr(), len(widths), max(rows), P.data_ptr(), M.data_ptr(),
+                  V.data_ptr(), E.data_ptr() if ema else None, hist.data_ptr(), T, st)
+        torch.cuda.synchronize()
+        return P, M, V, E, last.clone()
+
+    ref = flush(True)
+    got = flush(False)
+    for name, a, b in zip("PMVE", ref[:4], got[:4]):
+        if a is not None:
+            assert torch.equal(a.view(torch.int32), b.view(torch.int32)), (name, int((a != b).sum()))
+    assert torch.equal(ref[4], got[4])
+    assert bool(((ref[4] & 0x7FFFFFFF) == T).all())

@@ -323,7 +323,12 @@ __device__ __forceinline__ int flush_lg(int width) {
 // dead lanes), whose tick loop is wave-uniform.  The chunk's rows are first ordered zero-moment rows
 // first, stepped rows last (LDS), so a wave's rows are of one kind and take the short or the full replay
 // -- in table order a wave almost always held a stepped row and ran the full replay for all of them.
-__global__ __launch_bounds__(256) void lazy_flush_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+#ifdef LZ_WPE
+#define LZ_OCC __attribute__((amdgpu_waves_per_eu(LZ_WPE)))
+#else
+#define LZ_OCC
+#endif
+__global__ __launch_bounds__(256) LZ_OCC void lazy_flush_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
                                                          float* P, float* M, float* V, float* E,
                                                          const OptScalars* __restrict__ hist, int tick) {
   __shared__ long chunk0[FLUSH_MAXTABS + 1];
@@ -631,7 +636,13 @@ __device__ __forceinline__ void replay_pair_list(const ctr_lazy_tab_t& ta, const
   constexpr int LPT = W / 4;               // lanes per table row
   constexpr int LPP = 2 * LPT;             // lanes per row pair
   constexpr int PPS = 64 / LPP;            // row pairs per slot
-  constexpr int NS = 2;                    // slots per lane
+#ifndef PAIR_NS0
+#define PAIR_NS0 2
+#endif
+#ifndef PAIR_NS1
+#define PAIR_NS1 2
+#endif
+  constexpr int NS = CL ? PAIR_NS1 : PAIR_NS0;   // slots per lane
   constexpr int GRP = PPS * NS;            // row pairs per wave group
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int u = lane / LPP, c = lane % LPP;
@@ -713,37 +724,274 @@ constexpr int CLS_CH = 1024;     // rows per workgroup iteration of the flush
 // workgroup: 400 workgroups at cfg2, 141 us; 256: 1600 workgroups)
 constexpr int TOUCH_CH = 256;
 
-// flush of the DARE table pair: a workgroup sorts CLS_CH consecutive row pairs behind `tick` into the lists
-template <int W>
+// flush of the DARE table pair: a workgroup sorts CLS_CH consecutive row pairs behind `tick` into a zero-moment
+// and a stepped list (CL < 0) and replays both, or lists only class CL (one kernel per class, as
+// lazy_flush_cls_kernel: the zero-moment pass at the short replay's register count)
+template <int W, int CL>
 __global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs, float* P,
                                                                   float* M, float* V, float* E,
                                                                   const OptScalars* __restrict__ hist, int tick) {
-  __shared__ int lrow[2][CLS_CH];
-  __shared__ int ls[2][CLS_CH];
-  __shared__ int cnt[2];
+  constexpr int NL = CL < 0 ? 2 : 1;
+  __shared__ int lrow[NL][CLS_CH];
+  __shared__ int ls[NL][CLS_CH];
+  __shared__ int cnt[NL];
   const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
   const int tid = threadIdx.x;
   const long rows = ta.rows;
   for (long r0 = (long)blockIdx.x * CLS_CH; r0 < rows; r0 += (long)gridDim.x * CLS_CH) {
-    if (tid < 2) cnt[tid] = 0;
+    if (tid < NL) cnt[tid] = 0;
     __syncthreads();
-    for (int i = tid; i < CLS_CH; i += 256) {
-      const long r = r0 + i;
-      if (r < rows) {
-        const int w = ta.last[r];
-        const int st = ltick(w);
-        if (st < tick) {
-          const int cl = (w & LAST_NZ) ? 1 : 0;
-          const int pos = atomicAdd(&cnt[cl], 1);
-          lrow[cl][pos] = (int)r;
-          ls[cl][pos] = st;
-        }
+    int wv[CLS_CH / 256];
+#pragma unroll
+    for (int q = 0; q < CLS_CH / 256; ++q) {
+      const long r = r0 + tid + 256 * q;
+      wv[q] = r < rows ? ta.last[r] : tick;
+    }
+#pragma unroll
+    for (int q = 0; q < CLS_CH / 256; ++q) {
+      const int st = ltick(wv[q]);
+      const int cl = (wv[q] & LAST_NZ) ? 1 : 0;
+      if (st < tick && (CL < 0 || cl == CL)) {
+        const int li = CL < 0 ? cl : 0;
+        const int pos = atomicAdd(&cnt[li], 1);
+        lrow[li][pos] = (int)(r0 + tid + 256 * q);
+        ls[li][pos] = st;
       }
     }
     __syncthreads();
-    replay_pair_list<W, 0>(ta, tb, lrow[0], ls[0], cnt[0], P, M, V, E, hist, tick, true);
-    replay_pair_list<W, 1>(ta, tb, lrow[1], ls[1], cnt[1], P, M, V, E, hist, tick, true);
+    if (CL <= 0) replay_pair_list<W, 0>(ta, tb, lrow[0], ls[0], cnt[0], P, M, V, E, hist, tick, true);
+    if (CL != 0) replay_pair_list<W, 1>(ta, tb, lrow[NL - 1], ls[NL - 1], cnt[NL - 1], P, M, V, E, hist, tick, true);
     __syncthreads();      // the lists are refilled by the next iteration
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Classified flush of the categorical tables (any width <= 64): the pair kernel's scheme for one table
+// at a time.  A workgroup iteration takes CLS_CH consecutive rows of one table (the chunk grid is
+// table-major), lists those behind `tick` of its class in LDS (one state-word load per row, four in flight
+// per thread), and the waves replay the list in groups: LPR lanes hold a row, four elements each (float4
+// when the table's rows are 16-byte aligned, else elements c + LPR t), NS rows per lane -- 64 / LPR x NS
+// rows per group, one wave-uniform tick loop, a lane applying tick k only past its row's own tick.  (The
+// per-row-group kernel before it, lazy_flush_kernel, sorted 256 / lg rows per iteration and replayed one row
+// per lane group: two barriers and two memory round trips per 64 rows.)  Same adam.h arithmetic per element
+// as every other replay: bit-identical to the dense stream.
+template <int LPR, bool VEC, int CL, int NS>
+__device__ __forceinline__ void replay_tab_list(const ctr_lazy_tab_t& tb, const int* lrow, const int* ls, int n,
+                                                float* P, float* M, float* V, float* E,
+                                                const OptScalars* __restrict__ hist, int tick) {
+  constexpr int RPS = 64 / LPR;            // rows per slot
+  constexpr int GRP = RPS * NS;            // rows per wave group
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int u = lane / LPR, c = lane % LPR;
+  const int W = tb.width;
+  for (int g0 = wv * GRP; g0 < n; g0 += nw * GRP) {
+    long base[NS];
+    int row[NS], s[NS];
+    bool live[NS];
+    f32x2 p[NS][2], m[NS][2], v[NS][2], e[NS][2];
+    int smin = tick;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      const int idx = g0 + q * RPS + u;
+      live[q] = idx < n;
+      row[q] = live[q] ? lrow[idx] : 0;
+      s[q] = live[q] ? ls[idx] : tick;
+      base[q] = tb.p_off + (long)row[q] * W;
+      float pv[4] = {0.f, 0.f, 0.f, 0.f}, mv[4] = {0.f, 0.f, 0.f, 0.f}, vv[4] = {0.f, 0.f, 0.f, 0.f},
+            ev[4] = {0.f, 0.f, 0.f, 0.f};
+      if (VEC) {
+        if (live[q] && 4 * c < W) {
+          const long o = base[q] + 4 * c;
+          const f32x4 a = *(const f32x4*)(P + o);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) pv[t] = a[t];
+          if (CL) {
+            const f32x4 b = *(const f32x4*)(M + o), d = *(const f32x4*)(V + o);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              mv[t] = b[t];
+              vv[t] = d[t];
+            }
+          }
+          if (E) {
+            const f32x4 b = *(const f32x4*)(E + o);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) ev[t] = b[t];
+          }
+        }
+      } else if (live[q]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = c + LPR * t;
+          if (j < W) {
+            const long o = base[q] + j;
+            pv[t] = P[o];
+            if (CL) {
+              mv[t] = M[o];
+              vv[t] = V[o];
+            }
+            if (E) ev[t] = E[o];
+          }
+        }
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        p[q][h] = f32x2{pv[2 * h], pv[2 * h + 1]};
+        m[q][h] = f32x2{mv[2 * h], mv[2 * h + 1]};
+        v[q][h] = f32x2{vv[2 * h], vv[2 * h + 1]};
+        e[q][h] = f32x2{ev[2 * h], ev[2 * h + 1]};
+      }
+      smin = min(smin, s[q]);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
+    smin = __builtin_amdgcn_readfirstlane(smin);
+    for_ticks(hist, smin + 1, tick, [&](const OptScalars& sc, int k) {
+#pragma unroll
+      for (int q = 0; q < NS; ++q) {
+        if (k > s[q]) {
+          if (sc.do_adam) {
+            if (CL) {
+              idle_adam_pk(sc, p[q][0], m[q][0], v[q][0]);
+              idle_adam_pk(sc, p[q][1], m[q][1], v[q][1]);
+            } else {
+              p[q][0] = p[q][0] * splat2(sc.decay_mul);
+              p[q][1] = p[q][1] * splat2(sc.decay_mul);
+            }
+          }
+          if (sc.do_ema) {
+            ema_pk(sc, p[q][0], e[q][0]);
+            ema_pk(sc, p[q][1], e[q][1]);
+          }
+        }
+      }
+    });
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      if (!live[q]) continue;
+      const float pv[4] = {p[q][0].x, p[q][0].y, p[q][1].x, p[q][1].y};
+      const float mv[4] = {m[q][0].x, m[q][0].y, m[q][1].x, m[q][1].y};
+      const float vv[4] = {v[q][0].x, v[q][0].y, v[q][1].x, v[q][1].y};
+      const float ev[4] = {e[q][0].x, e[q][0].y, e[q][1].x, e[q][1].y};
+      if (VEC) {
+        if (4 * c < W) {
+          const long o = base[q] + 4 * c;
+          *(f32x4*)(P + o) = f32x4{pv[0], pv[1], pv[2], pv[3]};
+          if (CL) {
+            *(f32x4*)(M + o) = f32x4{mv[0], mv[1], mv[2], mv[3]};
+            *(f32x4*)(V + o) = f32x4{vv[0], vv[1], vv[2], vv[3]};
+          }
+          if (E) *(f32x4*)(E + o) = f32x4{ev[0], ev[1], ev[2], ev[3]};
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = c + LPR * t;
+          if (j < W) {
+            const long o = base[q] + j;
+            P[o] = pv[t];
+            if (CL) {
+              M[o] = mv[t];
+              V[o] = vv[t];
+            }
+            if (E) E[o] = ev[t];
+          }
+        }
+      }
+      if (c == 0) tb.last[row[q]] = tick | (CL ? LAST_NZ : 0);
+    }
+  }
+}
+
+// lanes per row of the classified flush: four elements per lane
+__device__ __forceinline__ int cls_lpr(int width) {
+  const int need = (width + 3) / 4;
+  return need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : need <= 8 ? 8 : 16;
+}
+
+#ifndef FLUSH_NS0
+#define FLUSH_NS0 2
+#endif
+#ifndef FLUSH_NS1
+#define FLUSH_NS1 2
+#endif
+// One kernel per class (zero-moment rows first, then the stepped rows): the short replay alone needs far fewer
+// registers than the full one (one kernel holding both ran at the full replay's 112 VGPRs, four waves per SIMD),
+// so the zero-moment pass runs at a higher occupancy.  Each pass reads the
+// state words of every row (140 MB at cfg2, a few percent of the row bytes) and lists its own class.
+template <int CL>
+__global__ __launch_bounds__(256) void lazy_flush_cls_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+                                                             float* P, float* M, float* V, float* E,
+                                                             const OptScalars* __restrict__ hist, int tick) {
+  __shared__ long chunk0[FLUSH_MAXTABS + 1];
+  __shared__ int lrow[CLS_CH];
+  __shared__ int ls[CLS_CH];
+  __shared__ int cnt;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    long c = 0;
+    for (int t = 0; t < ntabs; ++t) {
+      chunk0[t] = c;
+      c += cdiv(tabs[t].rows, (long)CLS_CH);
+    }
+    chunk0[ntabs] = c;
+  }
+  __syncthreads();
+  const long nchunks = chunk0[ntabs];
+  for (long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    int a = 0, b = ntabs;
+    while (b - a > 1) {
+      const int mid = (a + b) >> 1;
+      if (chunk0[mid] <= ch) a = mid; else b = mid;
+    }
+    const ctr_lazy_tab_t tb = tabs[a];
+    const long r0 = (ch - chunk0[a]) * CLS_CH;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    int wv[CLS_CH / 256];
+#pragma unroll
+    for (int q = 0; q < CLS_CH / 256; ++q) {
+      const long r = r0 + tid + 256 * q;
+      wv[q] = r < tb.rows ? tb.last[r] : tick;
+    }
+#pragma unroll
+    for (int q = 0; q < CLS_CH / 256; ++q) {
+      const int st = ltick(wv[q]);
+      if (st < tick && ((wv[q] & LAST_NZ) ? 1 : 0) == CL) {
+        const int pos = atomicAdd(&cnt, 1);
+        lrow[pos] = (int)(r0 + tid + 256 * q);
+        ls[pos] = st;
+      }
+    }
+    __syncthreads();
+    const int n = cnt;
+    if (n > 0) {
+      constexpr int NS = CL ? FLUSH_NS1 : FLUSH_NS0;
+      const bool vec = (tb.width & 3) == 0 && (tb.p_off & 3) == 0;    // block-uniform
+      switch (cls_lpr(tb.width)) {
+        case 1:
+          if (vec) replay_tab_list<1, true, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          else replay_tab_list<1, false, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          break;
+        case 2:
+          if (vec) replay_tab_list<2, true, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          else replay_tab_list<2, false, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          break;
+        case 4:
+          if (vec) replay_tab_list<4, true, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          else replay_tab_list<4, false, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          break;
+        case 8:
+          if (vec) replay_tab_list<8, true, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          else replay_tab_list<8, false, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          break;
+        default:
+          if (vec) replay_tab_list<16, true, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          else replay_tab_list<16, false, CL, NS>(tb, lrow, ls, n, P, M, V, E, hist, tick);
+          break;
+      }
+    }
+    __syncthreads();      // the list is refilled by the next iteration
   }
 }
 
@@ -841,7 +1089,16 @@ extern "C" int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_ro
                               float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(ntabs <= FLUSH_MAXTABS, "ctr_lazy_flush: too many tables");
   if (ntabs <= 0 || tick <= 0 || max_rows <= 0) return 0;
-  lazy_flush_kernel<<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist, tick);
+  const char* lg = getenv("CTR_FLUSH_LEGACY");   // read per call (one flush per sync): tests compare both kernels
+  if (lg && atoi(lg) != 0)   // the per-row-group kernel, kept for A/B
+    lazy_flush_kernel<<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist, tick);
+  else
+  {
+    lazy_flush_cls_kernel<0><<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist,
+                                                                    tick);
+    lazy_flush_cls_kernel<1><<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist,
+                                                                    tick);
+  }
   return check_launch("lazy_flush");
 }
 
@@ -897,6 +1154,9 @@ extern "C" int ctr_lazy_update_pair(const ctr_lazy_tab_t* tabs, int width, const
   return check_launch("lazy_update_pair");
 }
 
+#ifndef PAIR_SPLIT
+#define PAIR_SPLIT 0
+#endif
 extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long rows, float* P, float* M, float* V,
                                    float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_flush_pair: two tables of width <= 64");
@@ -905,11 +1165,46 @@ extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long r
   const OptScalars* h = (const OptScalars*)hist;
   hipStream_t s = (hipStream_t)stream;
   switch (width) {      // the classified flush for the widths whose rows split into float4 lanes
-    case 4: lazy_flush_pair_cls_kernel<4><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
-    case 8: lazy_flush_pair_cls_kernel<8><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
-    case 16: lazy_flush_pair_cls_kernel<16><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
-    case 32: lazy_flush_pair_cls_kernel<32><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
-    case 64: lazy_flush_pair_cls_kernel<64><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 4:
+      if (PAIR_SPLIT) {
+        lazy_flush_pair_cls_kernel<4, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+        lazy_flush_pair_cls_kernel<4, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      } else {
+        lazy_flush_pair_cls_kernel<4, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      }
+      return check_launch("lazy_flush_pair");
+    case 8:
+      if (PAIR_SPLIT) {
+        lazy_flush_pair_cls_kernel<8, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+        lazy_flush_pair_cls_kernel<8, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      } else {
+        lazy_flush_pair_cls_kernel<8, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      }
+      return check_launch("lazy_flush_pair");
+    case 16:
+      if (PAIR_SPLIT) {
+        lazy_flush_pair_cls_kernel<16, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+        lazy_flush_pair_cls_kernel<16, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      } else {
+        lazy_flush_pair_cls_kernel<16, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      }
+      return check_launch("lazy_flush_pair");
+    case 32:
+      if (PAIR_SPLIT) {
+        lazy_flush_pair_cls_kernel<32, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+        lazy_flush_pair_cls_kernel<32, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      } else {
+        lazy_flush_pair_cls_kernel<32, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      }
+      return check_launch("lazy_flush_pair");
+    case 64:
+      if (PAIR_SPLIT) {
+        lazy_flush_pair_cls_kernel<64, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+        lazy_flush_pair_cls_kernel<64, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      } else {
+        lazy_flush_pair_cls_kernel<64, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
+      }
+      return check_launch("lazy_flush_pair");
     default: break;
   }
   if (width <= 32)
