@@ -57,6 +57,7 @@ def trace_durations(md):
 
 
 def short(n, width=70):
+    n = n.replace("(anonymous namespace)::", "")
     n = re.sub(r"\(.*", "", n).replace("ctr::", "").replace("void ", "")
     return n[:width]
 

@@ -58,7 +58,20 @@ struct AttnBfArgs {
   const float* dO;       // (B*K, D)
   float* dqkv;           // (B*K, 3D)
   float* drel_part;      // (B * H/G, 2tk+1)
+  int ngrp;              // head groups per sample (H / G)
 };
+
+// workgroup -> (sample, head group), 1-D grid: with ngrp > 1 head groups a sample's workgroups are 8 apart in
+// dispatch order -- on the same XCD (workgroups are dealt round-robin to the 8 XCDs) and close in time -- so the
+// second one finds the sample's qkv / o / dO lines in that XCD's L2.  (As a (B, ngrp) grid the head groups of a
+// sample ran B workgroups apart on different XCDs and each fetched whole 128-byte lines for its half rows.)
+__device__ __forceinline__ int wg_sample(const AttnBfArgs& a) {
+  if (a.ngrp == 1) return blockIdx.x;
+  const int span = 8 * a.ngrp, q = blockIdx.x / span;
+  return 8 * q + (blockIdx.x - q * span) % 8;
+}
+__device__ __forceinline__ int wg_group(const AttnBfArgs& a) { return a.ngrp == 1 ? 0 : (blockIdx.x % (8 * a.ngrp)) / 8; }
+__host__ __forceinline__ int wg_grid(const AttnBfArgs& a) { return a.ngrp == 1 ? a.B : (a.B + 7) / 8 * 8 * a.ngrp; }
 
 __device__ __forceinline__ f32x4 mma(bf16x4 a, bf16x4 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c,
@@ -142,9 +155,9 @@ template <int DH, int NT, bool WITH_DO>
 __device__ __forceinline__ void stage(const AttnBfArgs& a, __bf16* sq, __bf16* sk, __bf16* sv, __bf16* sdo) {
   using S = Stg<DH, NT>;
   constexpr int KT = S::KT;
-  const int K = a.K, D = a.D, G = a.G, b = blockIdx.x;
-  const float* base = a.qkv + (long)b * K * 3 * D + blockIdx.y * G * DH;
-  const float* dob = WITH_DO ? a.dO + (long)b * K * D + blockIdx.y * G * DH : nullptr;
+  const int K = a.K, D = a.D, G = a.G, b = wg_sample(a), hg = wg_group(a);
+  const float* base = a.qkv + (long)b * K * 3 * D + hg * G * DH;
+  const float* dob = WITH_DO ? a.dO + (long)b * K * D + hg * G * DH : nullptr;
   constexpr int NCD = DH / 4, NCR = 4 * NCD + 2;  // chunks per row: 4 heads' dims, mask, zero
   for (int e = threadIdx.x; e < KT * NCR; e += blockDim.x) {
     const int j = e / NCR, ch = e - j * NCR;
@@ -215,6 +228,7 @@ __device__ __forceinline__ bf16x4 op_col(const __bf16* img, int row0, int hs, in
 // forward.  NT = the tiles a side (ceil(K / 16)); DROPK: 0 none, 1 K even (pair hashes), 2 K odd
 template <int NT, int DH, bool BIAS, int DROPK>
 __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
+  if (wg_sample(a) >= a.B) return;      // the grid's tail past the last sample
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
@@ -226,8 +240,8 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
   stage<DH, NT, false>(a, sq, sk, sv, nullptr);
   if (BIAS) stage_rel<NT>(a, srel);
   __syncthreads();
-  const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int h = blockIdx.y * G + w, hs = w * S::HS;
+  const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = wg_group(a) * G + w, hs = w * S::HS;
   bf16x4 kop[NT], vtop[NT];
 #pragma unroll
   for (int tj = 0; tj < NT; ++tj) {
@@ -374,6 +388,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
 // at cfg2 against three
 template <int NT, int DH, bool BIAS, bool DROP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_mf_kernel(AttnBfArgs a) {
+  if (wg_sample(a) >= a.B) return;      // the grid's tail past the last sample
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   constexpr int ND = 2 * NT - 1, IMG = img_elems<NT>(), KT = KB::KT;
@@ -388,8 +403,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   stage<DH, NT, true>(a, sq, sk, sv, sdo);
   if (BIAS) stage_rel<NT>(a, srel);
   __syncthreads();
-  const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int h = blockIdx.y * G + w, hs = w * S::HS;
+  const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = wg_group(a) * G + w, hs = w * S::HS;
   __bf16* ids = simg + w * 2 * IMG;
   __bf16* ipt = ids + IMG;
   const float* rb = srel + KT + a.tk + 4 * g - c;
@@ -515,7 +530,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     // half 1 the one above it (-16 <= d - 16 dt' <= -1)
     constexpr int NDG = 2 * 16 * NT - 1;
     const int nrel = 2 * a.tk + 1;
-    float* out = a.drel_part + ((long)b * gridDim.y + blockIdx.y) * nrel;
+    float* out = a.drel_part + ((long)b * a.ngrp + wg_group(a)) * nrel;
     for (int t0 = 0; t0 < 2 * NDG; t0 += blockDim.x) {
       const int t = t0 + threadIdx.x;
       const int x = t >> 1, half = t & 1;
@@ -574,6 +589,7 @@ __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(ATT_WPE)))
 #endif
 void attn_bwd_mfl_kernel(AttnBfArgs a) {
+  if (wg_sample(a) >= a.B) return;      // the grid's tail past the last sample
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   constexpr int KT = KB::KT, NDG = 32 * NT - 1, NDGP = (NDG + 3) & ~3;
@@ -587,8 +603,8 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
   float* srel = (float*)(simg + 4 * 4 * 256);
   stage<DH, NT, true>(a, sq, sk, sv, sdo);
   if (BIAS) stage_rel<NT>(a, srel);
-  const int b = blockIdx.x, w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int h = blockIdx.y * G + w, hs = w * S::HS;
+  const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = wg_group(a) * G + w, hs = w * S::HS;
   __bf16* ids0 = simg + w * 4 * 256;
   const float* rb = srel + KT + a.tk + 4 * g - c;
   const long hr = ((long)b * a.H + h) * K;
@@ -732,7 +748,7 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
     __syncthreads();
     // heads of the group summed in a fixed order; diagonal d = x - (16 nt - 1) of the x-th sum
     const int nrel = 2 * a.tk + 1;
-    float* out = a.drel_part + ((long)b * gridDim.y + blockIdx.y) * nrel;
+    float* out = a.drel_part + ((long)b * a.ngrp + wg_group(a)) * nrel;
     const float* base = (const float*)(stw + (4 - w) * KT);     // wave 0's scratch
     for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
       const int d = e - a.tk, x = d + 16 * NT - 1;
@@ -1009,7 +1025,7 @@ void allow_lds(F* kern, size_t sm) {
 template <int NT, int DH, bool BIAS, int DROPK>
 void launch_fwd5(const AttnBfArgs& a, size_t sm, hipStream_t s) {
   allow_lds(attn_fwd_mf_kernel<NT, DH, BIAS, DROPK>, sm);
-  attn_fwd_mf_kernel<NT, DH, BIAS, DROPK><<<dim3(a.B, a.H / a.G), dim3(64 * a.G), sm, s>>>(a);
+  attn_fwd_mf_kernel<NT, DH, BIAS, DROPK><<<wg_grid(a), dim3(64 * a.G), sm, s>>>(a);
 }
 
 template <int NT, int DH, bool BIAS>
@@ -1046,10 +1062,10 @@ template <int NT, int DH, bool BIAS, bool DROP>
 void launch_bwd4(const AttnBfArgs& a, size_t sm, hipStream_t s) {
   if constexpr (NT > 4) {
     allow_lds(attn_bwd_mfl_kernel<NT, DH, BIAS, DROP>, sm);
-    attn_bwd_mfl_kernel<NT, DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), dim3(64 * a.G), sm, s>>>(a);
+    attn_bwd_mfl_kernel<NT, DH, BIAS, DROP><<<wg_grid(a), dim3(64 * a.G), sm, s>>>(a);
   } else {
     allow_lds(attn_bwd_mf_kernel<NT, DH, BIAS, DROP>, sm);
-    attn_bwd_mf_kernel<NT, DH, BIAS, DROP><<<dim3(a.B, a.H / a.G), dim3(64 * a.G), sm, s>>>(a);
+    attn_bwd_mf_kernel<NT, DH, BIAS, DROP><<<wg_grid(a), dim3(64 * a.G), sm, s>>>(a);
   }
 }
 
@@ -1100,7 +1116,7 @@ extern "C" int ctr_attn_fwd_bf(const float* qkv, int B, int K, int H, int D, con
   CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
   CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
   AttnBfArgs a{};
-  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.nt = (K + 15) / 16; a.tk = tk;
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.ngrp = H / a.G; a.nt = (K + 15) / 16; a.tk = tk;
   a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = mask; a.o = o; a.mrow = mrow; a.lrow = lrow;
   hipStream_t s = (hipStream_t)stream;
@@ -1120,7 +1136,7 @@ extern "C" int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO
   CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
   CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
   AttnBfArgs a{};
-  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.nt = (K + 15) / 16; a.tk = tk;
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.ngrp = H / a.G; a.nt = (K + 15) / 16; a.tk = tk;
   a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = const_cast<uint32_t*>(mask); a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow);
   a.lrow = const_cast<float*>(lrow); a.dO = dO; a.dqkv = dqkv; a.drel_part = drel_part;
@@ -1145,7 +1161,7 @@ extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D,
   CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
   LayerFwdArgs L{};
   AttnBfArgs& a = L.at;
-  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = H; a.nt = (K + 15) / 16; a.tk = tk;
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = H; a.ngrp = 1; a.nt = (K + 15) / 16; a.tk = tk;
   a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = mask; a.o = o; a.mrow = mrow; a.lrow = lrow;
   L.x = x; L.w_in = w_in; L.b_in = b_in; L.w_out = w_out; L.b_out = b_out; L.nw1 = nw1; L.eps = eps;
