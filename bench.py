@@ -96,7 +96,7 @@ def kernel_work(name, a, B, ffn_M):
     H = a.H
     if name == "ctr_attn_fwd_bf":
         return "hbm", float(B * K * (16 * D + 8 * H) + B * H * 512), "B"
-    if name == "ctr_attn_bwd_bf":
+    if name in ("ctr_attn_bwd_bf", "ctr_attn_bwd_bf_oproj"):     # _oproj reads dh1 rows in place of dO
         return "hbm", float(B * K * (32 * D + 8 * H) + B * H * 512), "B"
     # the fused layer forward (in_proj -> attention -> out_proj + residual + RMSNorm, attn_mf.hip): reads x (4 D)
     # and writes qkv (12 D), o (4 D), h1 and x1 (8 D), r1 (4), the row stats (8 H) and the keep bits per row
@@ -240,7 +240,7 @@ def pmc_traffic(name):
              "ctr_attn_bwd": ("attn_bwd_wave_kernel", "attn_bwd_kernel"),
              "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel"),
              "ctr_attn_bwd_bf": ("attn_bwd_mf_kernel",), "ctr_attn_fwd_bf": ("attn_fwd_mf_kernel",),
-             "ctr_attn_layer_fwd_bf": ("attn_layer_fwd_kernel",)}.get(name)
+             "ctr_attn_layer_fwd_bf": ("attn_layer_fwd_kernel",), "ctr_attn_bwd_bf_oproj": ("attn_bwd_mf_kernel",)}.get(name)
     if kerns is None:
         return None
     base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS
@@ -407,7 +407,7 @@ def main():
     # host-issue sensitive), so the timed steps bracket only the roofline candidates (the kernels with an
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd",
-                  "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf")
+                  "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
                           "ctr_adamw_ema", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")

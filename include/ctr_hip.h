@@ -199,6 +199,15 @@ int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO, int B, in
                     const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
                     float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow, float* dqkv,
                     float* drel_part, void* stream);
+/* amp: bf16 -- ctr_attn_bwd_bf with the out-projection's input grad fused in front (K <= 64, D = 32, 4 or 8 heads:
+ * ctr_attn_bwd_bf_oproj_ok): dO = dh1 W_out (src/models/dare.py:53-62, MHA out_proj backward) is formed per workgroup
+ * from the (B*K, 32) rows dh1 and out_proj.weight (32, 32) with the same bits as ctr_rowgemm(dh1, W_out, tb = 0), and
+ * never written; the other arguments and outputs as ctr_attn_bwd_bf.                                          */
+int ctr_attn_bwd_bf_oproj_ok(int K, int H, int D);
+int ctr_attn_bwd_bf_oproj(const float* qkv, const float* o, const float* dh1, const float* w_out, int B, int K, int H,
+                          int D, const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                          float drop_scale, const uint32_t* mask, const float* mrow, const float* lrow, float* dqkv,
+                          float* drel_part, void* stream);
 /* amp: bf16 -- the first half of an encoder layer in one launch, src/models/dare.py:53-62
  * (qkv = in_proj(x); o = attention(qkv); x1 = norm1(x + out_proj(o))): one workgroup per sample, K <= 64,
  * D = 32, 4 or 8 heads, tk <= 64 (ctr_attn_layer_fwd_ok).  Writes exactly what ctr_rowgemm (in_proj),

@@ -388,6 +388,49 @@ def test_attn_layer_fwd_equals_three_launches(K, H, p, bias):
             (name, int((a.view(torch.int32) != b.view(torch.int32)).sum()), a.numel())
 
 
+@pytest.mark.parametrize("K,H,p", [(60, 8, 0.1), (64, 8, 0.1), (61, 8, 0.1), (48, 4, 0.2), (33, 8, 0.0),
+                                   (17, 4, 0.1), (1, 8, 0.1), (50, 4, 0.0)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_attn_bwd_oproj_equals_two_launches(K, H, p, bias):
+    """amp: ctr_attn_bwd_bf_oproj (dO = dh1 W_out formed inside the attention backward) writes bit for bit what
+    ctr_rowgemm(dh1, W_out) + ctr_attn_bwd_bf write: dqkv and the positional-bias partials."""
+    L = _lib()
+    D = 32
+    assert L.query("ctr_attn_bwd_bf_oproj_ok", K, H, D) == 1
+    from tossctr.rng import drop_args
+    B, dh, tk = 37, D // H, K
+    g = torch.Generator(device="cuda").manual_seed(K * 29 + H)
+    qkv = torch.randn(B * K, 3 * D, device="cuda", generator=g)
+    dh1 = torch.randn(B * K, D, device="cuda", generator=g)
+    w_out = torch.randn(D, D, device="cuda", generator=g) * D ** -0.5
+    relmean = torch.randn(2 * tk + 1, device="cuda", generator=g)
+    rm = ptr(relmean) if bias else None
+    dk = drop_args(555, 5, p, True)
+    scale = float(np.float32(math.sqrt(1.0 / dh)))
+    st = stream()
+    o = torch.empty(B * K, D, device="cuda")
+    mrow = torch.empty(B * H * K, device="cuda")
+    lrow = torch.empty(B * H * K, device="cuda")
+    mask = torch.zeros(L.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
+    L.call("ctr_attn_fwd_bf", ptr(qkv), B, K, H, D, rm, tk, scale, *dk, ptr(mask), ptr(o), ptr(mrow), ptr(lrow), st)
+    nparts = L.query("ctr_attn_bwd_bf_nparts", H) * B
+    do = torch.empty(B * K, D, device="cuda")
+    L.call("ctr_rowgemm", B * K, D, D, ptr(dh1), D, ptr(w_out), 0, ptr(do), D, None, None, 0, None, 0, None, None, None,
+           1e-6, st)
+    r_dqkv = torch.full((B * K, 3 * D), float("nan"), device="cuda")
+    r_drp = torch.full((nparts, 2 * tk + 1), float("nan"), device="cuda")
+    L.call("ctr_attn_bwd_bf", ptr(qkv), ptr(o), ptr(do), B, K, H, D, rm, tk, scale, *dk, ptr(mask), ptr(mrow),
+           ptr(lrow), ptr(r_dqkv), ptr(r_drp), st)
+    f_dqkv = torch.full_like(r_dqkv, float("nan"))
+    f_drp = torch.full_like(r_drp, float("nan"))
+    L.call("ctr_attn_bwd_bf_oproj", ptr(qkv), ptr(o), ptr(dh1), ptr(w_out), B, K, H, D, rm, tk, scale, *dk, ptr(mask),
+           ptr(mrow), ptr(lrow), ptr(f_dqkv), ptr(f_drp), st)
+    torch.cuda.synchronize()
+    assert torch.equal(r_dqkv.view(torch.int32), f_dqkv.view(torch.int32)), int((r_dqkv != f_dqkv).sum())
+    if bias:
+        assert torch.equal(r_drp.view(torch.int32), f_drp.view(torch.int32))
+
+
 @pytest.mark.parametrize("L_,K,D", [(100, 60, 32), (40, 40, 16), (400, 148, 64), (7, 3, 8)])
 def test_topk_select_vs_torch(L_, K, D):
     L = _lib()

@@ -59,6 +59,8 @@ struct AttnBfArgs {
   float* dqkv;           // (B*K, 3D)
   float* drel_part;      // (B * H/G, 2tk+1)
   int ngrp;              // head groups per sample (H / G)
+  const float* dh1;      // backward with the out-projection fused (nt <= 4, D = 32): dO = dh1 W_out computed in
+  const float* w_out;    // the kernel from the (B*K, 32) rows dh1 and W_out (32, 32); dO is then unused
 };
 
 // workgroup -> (sample, head group), 1-D grid: with ngrp > 1 head groups a sample's workgroups are 8 apart in
@@ -400,8 +402,58 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   __bf16* sdo = sv + S::IM;
   __bf16* simg = sdo + S::IM + S::PAD;              // per wave: dS image, p~ image
   float* srel = (float*)(simg + 4 * 2 * IMG);
-  stage<DH, NT, true>(a, sq, sk, sv, sdo);
-  if (BIAS) stage_rel<NT>(a, srel);
+  const bool opj = a.dh1 != nullptr;      // block-uniform
+  const int GD = G * DH;                    // the workgroup's columns of dO
+  float* dot = (float*)simg;                // opj: the dO tile [KT][GD] (fp32), in the image space until the loop
+  if (opj) {
+    // dO = dh1 W_out on v_mfma_f32_16x16x4f32 in rowgemm.hip's k order (lane group g: k = 8g + kk; + 0.f as its
+    // bias-less epilogue): the same bits as the ctr_rowgemm launch it replaces.  Tiles: 4 row blocks x ncb column
+    // blocks of the workgroup's GD columns, at most two per wave; operands straight from global (a lane's dh1
+    // row segment is two 16-byte loads), issued before the q / k / v staging so the round trips overlap.
+    const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63, g0 = l0 >> 4, c0 = l0 & 15;
+    const int ncb = (GD + 15) >> 4, cbase = wg_group(a) * GD;
+    const long r0 = (long)wg_sample(a) * K;
+    f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    int tiles[2] = {-1, -1};
+    for (int t = w0, q = 0; t < 4 * ncb && q < 2; t += G, ++q) {
+      tiles[q] = t;
+      const int rb = t / ncb, i = 16 * rb + c0, n = cbase + 16 * (t % ncb) + c0;
+      const bool nin = 16 * (t % ncb) + c0 < GD;
+      f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
+      if (i < K) {
+        x0 = *(const f32x4*)(a.dh1 + (r0 + i) * 32 + 8 * g0);
+        x1 = *(const f32x4*)(a.dh1 + (r0 + i) * 32 + 8 * g0 + 4);
+      }
+      float wv[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) wv[kk] = nin ? a.w_out[(8 * g0 + kk) * 32 + n] : 0.f;
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk < 4 ? x0[kk] : x1[kk - 4], wv[kk], acc[q], 0, 0, 0);
+    }
+    stage<DH, NT, false>(a, sq, sk, sv, nullptr);
+    for (int j = threadIdx.x; j < KT; j += blockDim.x) {   // sdo's mask / zero chunks
+      *(bf16x4*)(sdo + j * S::RS + S::MOFF) = bf16x4{};
+      *(bf16x4*)(sdo + j * S::RS + S::ZOFF) = bf16x4{};
+    }
+    if (BIAS) stage_rel<NT>(a, srel);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (tiles[q] < 0) continue;
+      const int rb = tiles[q] / ncb, col = 16 * (tiles[q] % ncb) + c0;
+      if (col >= GD) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * rb + 4 * g0 + r;
+        const float v = i < K ? acc[q][r] + 0.f : 0.f;
+        dot[i * GD + col] = v;
+        sdo[i * S::RS + col] = (__bf16)v;
+      }
+    }
+  } else {
+    stage<DH, NT, true>(a, sq, sk, sv, sdo);
+    if (BIAS) stage_rel<NT>(a, srel);
+  }
   __syncthreads();
   const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int h = wg_group(a) * G + w, hs = w * S::HS;
@@ -415,7 +467,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   for (int row = lane; row < KT; row += 64) {
     f32x4 st = {0.f, 0.f, 0.f, 0.f};
     if (row < K) {
-      const float* dp = a.dO + ((long)b * K + row) * D + h * DH;
+      const float* dp = opj ? dot + row * GD + w * DH : a.dO + ((long)b * K + row) * D + h * DH;
       const float* op = a.o + ((long)b * K + row) * D + h * DH;
       float s = 0.f;
 #pragma unroll
@@ -431,6 +483,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     stw[row] = st;
   }
   __builtin_amdgcn_wave_barrier();
+  if (opj) __syncthreads();                 // every wave's dO-tile reads before the images overwrite it
   uint32_t words[KB::NW];
 #pragma unroll
   for (int q = 0; q < KB::NW; ++q) words[q] = 0u;
@@ -1144,6 +1197,30 @@ extern "C" int ctr_attn_bwd_bf(const float* qkv, const float* o, const float* dO
   if (D / H == 4) launch_bwd2<4>(a, s);
   else launch_bwd2<8>(a, s);
   return check_launch("attn_bwd_bf");
+}
+
+extern "C" int ctr_attn_bwd_bf_oproj_ok(int K, int H, int D) {
+  return (bf_ok(K, H, D) && K <= 64 && D == 32 && pick_g(H) == 4 && (4 * (D / H)) % 16 == 0) ? 1 : 0;
+}
+
+extern "C" int ctr_attn_bwd_bf_oproj(const float* qkv, const float* o, const float* dh1, const float* w_out, int B, int K,
+                                     int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
+                                     uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
+                                     const float* lrow, float* dqkv, float* drel_part, void* stream) {
+  if (B == 0) return 0;
+  CTR_REQUIRE(ctr_attn_bwd_bf_oproj_ok(K, H, D), "ctr_attn_bwd_bf_oproj: K <= 64, D = 32, 4 or 8 heads");
+  CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
+  CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
+  AttnBfArgs a{};
+  a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = pick_g(H); a.ngrp = H / a.G; a.nt = (K + 15) / 16; a.tk = tk;
+  a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = const_cast<uint32_t*>(mask); a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow);
+  a.lrow = const_cast<float*>(lrow); a.dO = nullptr; a.dqkv = dqkv; a.drel_part = drel_part;
+  a.dh1 = dh1; a.w_out = w_out;
+  hipStream_t s = (hipStream_t)stream;
+  if (D / H == 4) launch_bwd2<4>(a, s);
+  else launch_bwd2<8>(a, s);
+  return check_launch("attn_bwd_bf_oproj");
 }
 
 extern "C" int ctr_attn_layer_fwd_ok(int K, int H, int D) {

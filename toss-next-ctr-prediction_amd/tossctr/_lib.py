@@ -87,6 +87,8 @@ SIGS = {
     "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_attn_bf_ok": (i, [i, i, i]),
     "ctr_attn_fwd_bf": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
+    "ctr_attn_bwd_bf_oproj_ok": (i, [i, i, i]),
+    "ctr_attn_bwd_bf_oproj": (i, [p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_attn_layer_fwd_ok": (i, [i, i, i]),
     "ctr_attn_layer_fwd_bf": (i, [p, i, i, i, i, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),
     "ctr_attn_bwd_bf_nparts": (i, [i]),

@@ -191,6 +191,10 @@ class Engine:
         # (attn_mf.hip: K <= 64, D = 32; the same bits as the three launches; CTR_ATTN_LAYER=0 for A/B)
         self.attn_layer = bool(self.attn_bf and self.rowgemm and os.environ.get("CTR_ATTN_LAYER", "1") != "0" and
                                _lib.query("ctr_attn_layer_fwd_ok", a.top_k, a.H, a.D))
+        # ... and in the backward the out-projection's input grad dO = dh1 W_out inside the attention backward
+        # (ctr_attn_bwd_bf_oproj: same bits, dO never written; CTR_ATTN_OPROJ=0 for A/B)
+        self.attn_oproj = bool(self.attn_bf and self.rowgemm and os.environ.get("CTR_ATTN_OPROJ", "1") != "0" and
+                               _lib.query("ctr_attn_bwd_bf_oproj_ok", a.top_k, a.H, a.D))
 
     def _tab_array(self, keys, bases):
         """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
@@ -855,7 +859,13 @@ class Engine:
             self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
         # out_proj
         do = W.get("do", (M, D))
-        if self.rowgemm:
+        if self.attn_oproj:              # dO is formed inside the attention backward below
+            with self.side():
+                if slab_sum is not None:
+                    self.colsum(*slab_sum, defer=True)
+                self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
+                                pre + "mha.out_proj.bias", tag=li, defer=True)
+        elif self.rowgemm:
             if slab_sum is not None:     # main-stream product first, then the side stream's slab sums
                 self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
                 with self.side():
@@ -882,9 +892,14 @@ class Engine:
         drp = W.get(f"drel_part{li}", (nparts, nrel))
         da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
         scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
-        call("ctr_attn_bwd_bf" if self.attn_bf else "ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K, a.H,
-             D, ptr(Ls["relmean"]), a.top_k, scale, *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]),
-             ptr(dqkv), ptr(drp), st)
+        if self.attn_oproj:
+            call("ctr_attn_bwd_bf_oproj", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]),
+                 B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale, *da, ptr(Ls["amask"]), ptr(Ls["mrow"]),
+                 ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
+        else:
+            call("ctr_attn_bwd_bf" if self.attn_bf else "ctr_attn_bwd", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(do), B, K,
+                 a.H, D, ptr(Ls["relmean"]), a.top_k, scale, *da, ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]),
+                 ptr(dqkv), ptr(drp), st)
         x_in = sv["xs"][li]
         # (here the side work goes first: queuing the in_proj input grad ahead of it measured 0.02 ms/step slower)
         with self.side():
