@@ -212,10 +212,11 @@ int ctr_attn_bwd_bf_oproj(const float* qkv, const float* o, const float* dh1, co
  * (qkv = in_proj(x); o = attention(qkv); x1 = norm1(x + out_proj(o))): one workgroup per sample, K <= 64,
  * D = 32, 4 or 8 heads, tk <= 64 (ctr_attn_layer_fwd_ok).  Writes exactly what ctr_rowgemm (in_proj),
  * ctr_attn_fwd_bf and ctr_rowgemm (out_proj + residual + RMSNorm, eps) write -- qkv, o, mrow, lrow, mask, h1,
- * r1, x1 -- with the same bits (same summation orders).                                                     */
+ * r1, x1 -- with the same bits (same summation orders).  rel_w = pbias.rel.weight ((2tk+1) x H) or null: the
+ * head-mean bias is formed in the kernel and written to relmean (ctr_pos_bias_mean's bits) for the backward.   */
 int ctr_attn_layer_fwd_ok(int K, int H, int D);
 int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
-                          const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                          const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
                           float drop_scale, uint32_t* mask, const float* w_out, const float* b_out, const float* nw1,
                           float eps, float* qkv, float* o, float* mrow, float* lrow, float* h1, float* r1, float* x1,
                           void* stream);

@@ -355,8 +355,11 @@ def test_attn_layer_fwd_equals_three_launches(K, H, p, bias):
     w_out = torch.randn(D, D, device="cuda", generator=g) * D ** -0.5
     b_out = torch.randn(D, device="cuda", generator=g) * 0.1
     nw = 1 + 0.1 * torch.randn(D, device="cuda", generator=g)
-    relmean = torch.randn(2 * tk + 1, device="cuda", generator=g)
+    rel_w = torch.randn(2 * tk + 1, H, device="cuda", generator=g)
+    relmean = torch.empty(2 * tk + 1, device="cuda")
+    L.call("ctr_pos_bias_mean", ptr(rel_w), H, 2 * tk + 1, ptr(relmean), stream())
     rm = ptr(relmean) if bias else None
+    f_relmean = torch.full_like(relmean, float("nan"))
     dk = drop_args(777, 3, p, True)
     scale = float(np.float32(math.sqrt(1.0 / dh)))
     st = stream()
@@ -378,7 +381,8 @@ def test_attn_layer_fwd_equals_three_launches(K, H, p, bias):
            ptr(r["mrow"]), ptr(r["lrow"]), st)
     L.call("ctr_rowgemm", M, D, D, ptr(r["o"]), D, ptr(w_out), 1, ptr(r["x1"]), D, ptr(b_out), None, 0, ptr(x), D,
            ptr(nw), ptr(r["h1"]), ptr(r["r1"]), 1e-6, st)
-    L.call("ctr_attn_layer_fwd_bf", ptr(x), B, K, H, D, ptr(w_in), ptr(b_in), rm, tk, scale, *dk, ptr(f["mask"]),
+    L.call("ctr_attn_layer_fwd_bf", ptr(x), B, K, H, D, ptr(w_in), ptr(b_in), ptr(rel_w) if bias else None,
+           ptr(f_relmean) if bias else None, tk, scale, *dk, ptr(f["mask"]),
            ptr(w_out), ptr(b_out), ptr(nw), 1e-6, ptr(f["qkv"]), ptr(f["o"]), ptr(f["mrow"]), ptr(f["lrow"]),
            ptr(f["h1"]), ptr(f["r1"]), ptr(f["x1"]), st)
     torch.cuda.synchronize()
@@ -386,6 +390,8 @@ def test_attn_layer_fwd_equals_three_launches(K, H, p, bias):
         a, b = r[name], f[name]
         assert torch.equal(a.view(torch.int32), b.view(torch.int32)), \
             (name, int((a.view(torch.int32) != b.view(torch.int32)).sum()), a.numel())
+    if bias:     # the head-mean table the kernel formed and wrote for the backward
+        assert torch.equal(relmean.view(torch.int32), f_relmean.view(torch.int32))
 
 
 @pytest.mark.parametrize("K,H,p", [(60, 8, 0.1), (64, 8, 0.1), (61, 8, 0.1), (48, 4, 0.2), (33, 8, 0.0),

@@ -843,6 +843,8 @@ struct LayerFwdArgs {
   const float* w_out;     // (32, 32), b_out (32)
   const float* b_out;
   const float* nw1;       // (32) norm1 weight
+  const float* rel_w;     // pbias.rel.weight (2tk+1, H): the head-mean bias formed here (null: no bias) ...
+  float* relmean;         // ... and written by workgroup 0 for the backward (ctr_pos_bias_mean's bits)
   float eps;
   float* qkv;             // (B*K, 96) saved for the backward
   float* h1;              // (B*K, 32) pre-norm sum, r1 (B*K) its rsqrt, x1 (B*K, 32) the layer's next input
@@ -881,7 +883,21 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
     *(bf16x4*)(sk + j * lf::RS + lf::ZOFF) = z4;
     *(bf16x4*)(sv + j * lf::RS + lf::ZOFF) = z4;
   }
-  if (BIAS) stage_rel<NT>(a, srel);
+  if (BIAS) {   // stage_rel of the head-mean table, each entry summed over the heads as pos_bias_mean_kernel does
+    const int nrel = 2 * a.tk + 1;
+    for (int e = tid; e < nrel + 2 * KT; e += 64 * G) {
+      const int x = e - KT;
+      float v = 0.f;
+      if (x >= 0 && x < nrel) {
+        float sm = 0.f;
+        for (int hh = 0; hh < a.H; ++hh) sm += L.rel_w[(long)x * a.H + hh];
+        const float mean = sm / (float)a.H;
+        if (b == 0) L.relmean[x] = mean;
+        v = mean * L2E;
+      }
+      srel[e] = v;
+    }
+  }
   __syncthreads();
   // ---- in-projection: 4 row blocks x 6 column blocks of 16, K = 32 (8 MFMA k-steps of 4); tile t -> (rb, cb)
   for (int t = w; t < 24; t += G) {
@@ -1228,19 +1244,21 @@ extern "C" int ctr_attn_layer_fwd_ok(int K, int H, int D) {
 }
 
 extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
-                                     const float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                                     const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
                                      float drop_scale, uint32_t* mask, const float* w_out, const float* b_out,
                                      const float* nw1, float eps, float* qkv, float* o, float* mrow, float* lrow,
                                      float* h1, float* r1, float* x1, void* stream) {
   if (B == 0) return 0;
   CTR_REQUIRE(ctr_attn_layer_fwd_ok(K, H, D), "ctr_attn_layer_fwd_bf: K <= 64, D = 32, 4 or 8 heads");
-  CTR_REQUIRE(!relmean || (tk >= K - 1 && tk <= 64), "positional-bias table shorter than K or longer than 2*64+1");
+  CTR_REQUIRE(!rel_w || (relmean && tk >= K - 1 && tk <= 64),
+              "positional bias: needs the relmean output, tk >= K - 1 and tk <= 64");
   CTR_REQUIRE(!drop_thresh || mask, "attention forward with dropout needs a keep-bit buffer");
   LayerFwdArgs L{};
   AttnBfArgs& a = L.at;
   a.qkv = qkv; a.B = B; a.K = K; a.H = H; a.D = D; a.G = H; a.ngrp = 1; a.nt = (K + 15) / 16; a.tk = tk;
   a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = mask; a.o = o; a.mrow = mrow; a.lrow = lrow;
+  L.rel_w = rel_w; L.relmean = relmean;
   L.x = x; L.w_in = w_in; L.b_in = b_in; L.w_out = w_out; L.b_out = b_out; L.nw1 = nw1; L.eps = eps;
   L.qkv = qkv; L.h1 = h1; L.r1 = r1; L.x1 = x1;
   hipStream_t s = (hipStream_t)stream;
@@ -1258,9 +1276,9 @@ extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D,
   using BT = std::true_type;
   using BF = std::false_type;
   if (H == 8) {
-    if (relmean) go(I4{}, BT{}); else go(I4{}, BF{});
+    if (rel_w) go(I4{}, BT{}); else go(I4{}, BF{});
   } else {
-    if (relmean) go(I8{}, BT{}); else go(I8{}, BF{});
+    if (rel_w) go(I8{}, BT{}); else go(I8{}, BF{});
   }
   return check_launch("attn_layer_fwd_bf");
 }

@@ -90,7 +90,7 @@ SIGS = {
     "ctr_attn_bwd_bf_oproj_ok": (i, [i, i, i]),
     "ctr_attn_bwd_bf_oproj": (i, [p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_attn_layer_fwd_ok": (i, [i, i, i]),
-    "ctr_attn_layer_fwd_bf": (i, [p, i, i, i, i, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),
+    "ctr_attn_layer_fwd_bf": (i, [p, i, i, i, i, p, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),
     "ctr_attn_bwd_bf_nparts": (i, [i]),
     "ctr_attn_bwd_bf": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_ffn_supported": (i, [i, i, i]),

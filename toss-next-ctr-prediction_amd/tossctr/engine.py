@@ -454,7 +454,8 @@ class Engine:
             relmean = None
             if a.add_pos:
                 relmean = W.get(f"relmean{li}", (2 * a.top_k + 1,))
-                call("ctr_pos_bias_mean", ptr(P[pre + "pbias.rel.weight"]), a.H, 2 * a.top_k + 1, ptr(relmean), st)
+                if not self.attn_layer:      # (the fused layer forward forms the head mean itself)
+                    call("ctr_pos_bias_mean", ptr(P[pre + "pbias.rel.weight"]), a.H, 2 * a.top_k + 1, ptr(relmean), st)
             o = W.get(f"o{li}", (M, D))
             mrow = W.get(f"mrow{li}", (B * a.H * K,))
             lrow = W.get(f"lrow{li}", (B * a.H * K,))
@@ -467,7 +468,8 @@ class Engine:
             if self.attn_layer:
                 # in_proj -> attention -> out_proj + residual + RMSNorm in one launch (attn_mf.hip)
                 call("ctr_attn_layer_fwd_bf", ptr(x), B, K, a.H, D, ptr(P[pre + "mha.in_proj_weight"]),
-                     ptr(P[pre + "mha.in_proj_bias"]), ptr(relmean), a.top_k, scale, *da, ptr(amask),
+                     ptr(P[pre + "mha.in_proj_bias"]), ptr(P[pre + "pbias.rel.weight"]) if a.add_pos else None,
+                     ptr(relmean), a.top_k, scale, *da, ptr(amask),
                      ptr(P[pre + "mha.out_proj.weight"]), ptr(P[pre + "mha.out_proj.bias"]), ptr(P[pre + "norm1.w"]),
                      1e-6, ptr(qkv), ptr(o), ptr(mrow), ptr(lrow), ptr(h1), ptr(r1), ptr(x1), st)
             else:
