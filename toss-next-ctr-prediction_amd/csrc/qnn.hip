@@ -168,6 +168,34 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
   float* sM = dqs + QRp;                         // [NT*NT tiles][4][64] M (C layout)
   float* sW = sM + NT * NT * 4 * 64;             // [4 waves][D] w partials
   const int b = blockIdx.x;
+  // the first PF row blocks of this wave's z / dz_add rows are loaded before anything else: their round trips
+  // overlap the U staging and the M / w products instead of following them (wait-mem 0.75 with the loads issued
+  // per block after the barriers).  cfg2 (F = 200: 3-4 blocks per wave): 104 -> 80 us (4.0 TB/s) at PF = 1 or 2,
+  // 96 / 100 us at PF = 3 / 4 (the registers held cost occupancy)
+#ifndef QNN_PF
+#define QNN_PF 2
+#endif
+  constexpr int PF = QNN_PF;
+  const float* zb = z + (long)b * F * D;
+  const float* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
+  f32x4 zpre[PF][NT];
+  float apre[PF][4][NT];
+  {
+    const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63, g0 = l0 >> 4, c0 = l0 & 15;
+#pragma unroll
+    for (int it = 0; it < PF; ++it) {
+      const int f0 = 16 * w0 + 64 * it, fa = f0 + c0;
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+        zpre[it][i] = fa < F ? *(const f32x4*)(zb + (long)fa * D + 16 * i + 4 * g0) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = f0 + 4 * g0 + r;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) apre[it][r][j] = (ab && f < F) ? ab[(long)f * D + 16 * j + c0] : 0.f;
+      }
+    }
+  }
   stage_ucat<D>(ucat, QR, QRp, sU);
   for (int q = threadIdx.x; q < QRp; q += 256) {
     const float d = q < QR ? dquad[(long)b * QR + q] : 0.f;
@@ -218,19 +246,38 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
     const int e = 16 * j + c;
     wv[j] = 2.f * (((sW[e] + sW[D + e]) + sW[2 * D + e]) + sW[3 * D + e]);
   }
-  const float* zb = z + (long)b * F * D;
-  const float* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
   float* ob = dz + (long)b * F * D;
-  for (int f0 = 16 * w; f0 < F; f0 += 64) {
+  int it = 0;
+  for (int f0 = 16 * w; f0 < F; f0 += 64, ++it) {
     const int fa = f0 + c;                       // A-operand row of this lane
     f32x4 acc[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the lane's four A values of a 16-column block are contiguous: one 16-byte load per block
     f32x4 zq[NT];
+    float aq[4][NT];
+    if (it < PF) {
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
-      zq[i] = fa < F ? *(const f32x4*)(zb + (long)fa * D + 16 * i + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < PF; ++q)
+        if (q == it) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) zq[i] = zpre[q][i];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < NT; ++j) aq[r][j] = apre[q][r][j];
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+        zq[i] = fa < F ? *(const f32x4*)(zb + (long)fa * D + 16 * i + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = f0 + 4 * g + r;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) aq[r][j] = (ab && f < F) ? ab[(long)f * D + 16 * j + c] : 0.f;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NT; ++i)
 #pragma unroll
@@ -246,7 +293,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
         for (int j = 0; j < NT; ++j) {
           const int e = 16 * j + c;
           float v = wv[j] - 2.f * acc[j][r];
-          if (ab) v += ab[(long)f * D + e];
+          if (ab) v += aq[r][j];
           ob[(long)f * D + e] = v;
         }
       }
