@@ -86,18 +86,30 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
   float zs[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) zs[i] = 0.f;
-  for (int f0 = 0; f0 < F; f0 += 4) {
-    const int f = f0 + g;
-    float v[NT];
+  // FU row quads per step: their loads go out together (one quad's loads per round trip left the wave
+  // latency-bound: 50 dependent round trips per sample at F = 200); sums and products in the same order
+#ifndef QNN_FU
+#define QNN_FU 8
+#endif
+  constexpr int FU = QNN_FU;
+  for (int f00 = 0; f00 < F; f00 += 4 * FU) {
+    float v[FU][NT];
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      v[i] = f < F ? zb[(long)f * D + 16 * i + c] : 0.f;
-      zs[i] += v[i];
+    for (int u = 0; u < FU; ++u) {
+      const int f = f00 + 4 * u + g;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) v[u][i] = f < F ? zb[(long)f * D + 16 * i + c] : 0.f;
     }
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+    for (int u = 0; u < FU; ++u) {
+      if (f00 + 4 * u >= F) break;
 #pragma unroll
-      for (int j = 0; j < NT; ++j) acc[i][j] = mfma4q(v[i], v[j], acc[i][j]);
+      for (int i = 0; i < NT; ++i) zs[i] += v[u][i];
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma4q(v[u][i], v[u][j], acc[i][j]);
+    }
   }
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
