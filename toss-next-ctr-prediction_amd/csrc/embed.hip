@@ -253,19 +253,32 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_proj_partial(const int* __r
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  __shared__ int sidx[CP_SUB];
   for (int s0 = b0; s0 < b1; s0 += CP_SUB) {
     const int ns = min(CP_SUB, b1 - s0);
     __syncthreads();
-    for (int e = threadIdx.x; e < CP_SUB * 64; e += 256) {
-      const int i = e >> 6, k = e & 63;
-      float tv = 0.f, gv = 0.f;
+    // the sub-chunk's row ids first (one load each), then every thread's 16 gathers in flight at once: the
+    // per-element id -> row load chain left the staging latency-bound (wait-mem 0.81)
+    if (threadIdx.x < CP_SUB) sidx[threadIdx.x] = threadIdx.x < ns ? xcat[(long)(s0 + threadIdx.x) * Fc + c] : 0;
+    __syncthreads();
+    constexpr int EPT = CP_SUB * 64 / 256;
+    float tv[EPT], gv[EPT];
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = threadIdx.x + 256 * u, i = e >> 6, k = e & 63;
+      tv[u] = 0.f;
+      gv[u] = 0.f;
       if (i < ns) {
         const long b = s0 + i;
-        if (k < dc) tv = T[(long)xcat[b * Fc + c] * tld + k];
-        if (k < D) gv = dcat[(b * Fc + c) * D + k];
+        if (k < dc) tv[u] = T[(long)sidx[i] * tld + k];
+        if (k < D) gv[u] = dcat[(b * Fc + c) * D + k];
       }
-      sT[i * CP_LD + k] = tv;
-      sG[i * CP_LD + k] = gv;
+    }
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = threadIdx.x + 256 * u, i = e >> 6, k = e & 63;
+      sT[i * CP_LD + k] = tv[u];
+      sG[i * CP_LD + k] = gv[u];
     }
     __syncthreads();
     if (active) {
