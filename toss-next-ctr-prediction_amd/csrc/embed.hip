@@ -166,11 +166,30 @@ __global__ __launch_bounds__(256) void cat_embed_fwd_kernel(const int* __restric
   }
   const float* T = cm.tabs + cm.tab_off[c];
   const long tld = cm.row_ld ? cm.row_ld : dc;
-  // (sample, element) items over the table's dc elements only (the 64-wide loop left most threads idle at the
-  // narrow tables and gave each busy thread 16 dependent index -> row round trips)
-  for (int e = tid; e < nb * dc; e += 256) {
-    const int i = e / dc, k = e - i * dc;
-    sT[i * CE_LD + k] = T[(long)xcat[(long)(b0 + i) * Fc + c] * tld + k];
+  __shared__ int sidx[CE_SPB];
+  if (tid < nb) sidx[tid] = xcat[(long)(b0 + tid) * Fc + c];
+  __syncthreads();
+  // (sample, element) items over the table's dc elements only, the row ids from LDS and a thread's (up to 16)
+  // gathers issued together (an id -> row load chain per item left the staging latency-bound)
+  {
+    constexpr int EPT = CE_SPB * 64 / 256;
+    float tv[EPT];
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = tid + 256 * u;
+      if (e < nb * dc) {
+        const int i = e / dc, k = e - i * dc;
+        tv[u] = T[(long)sidx[i] * tld + k];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = tid + 256 * u;
+      if (e < nb * dc) {
+        const int i = e / dc, k = e - i * dc;
+        sT[i * CE_LD + k] = tv[u];
+      }
+    }
   }
   __syncthreads();
   for (int e = tid; e < nb * D; e += 256) {
