@@ -74,16 +74,30 @@ __global__ __launch_bounds__(NT) void topk_fwd_kernel(const int* __restrict__ se
       __syncthreads();
     }
   }
+  int* stok = si;        // (in place: entry k is read and rewritten by the same thread)
   for (int k = t; k < K; k += NT) {
     const int l = si[k];
+    const int tk = srow[l];
     idx_out[(long)b * K + k] = l;
-    tok_out[(long)b * K + k] = srow[l];
+    tok_out[(long)b * K + k] = tk;
     vals[(long)b * K + k] = ss[k];
+    stok[k] = tk;
   }
-  for (int e = t; e < K * D; e += NT) {
-    const int k = e / D, d = e % D;
-    const int tok = srow[si[k]];
-    sel[((long)b * K + k) * D + d] = E_rep[(long)tok * D + d];
+  __syncthreads();
+  // the selected rep rows: tokens from LDS (a token -> row load chain per element before), 16-byte copies
+  if ((D & 3) == 0 && ((((uintptr_t)E_rep) | ((uintptr_t)sel)) & 15) == 0) {
+    const int D4 = D >> 2;
+#pragma unroll 4
+    for (int e = t; e < K * D4; e += NT) {
+      const int k = e / D4, d4 = e - k * D4;
+      *(float4*)(sel + ((long)b * K + k) * D + 4 * d4) = *(const float4*)(E_rep + (long)stok[k] * D + 4 * d4);
+    }
+  } else {
+#pragma unroll 4
+    for (int e = t; e < K * D; e += NT) {
+      const int k = e / D, d = e % D;
+      sel[((long)b * K + k) * D + d] = E_rep[(long)stok[k] * D + d];
+    }
   }
 }
 
