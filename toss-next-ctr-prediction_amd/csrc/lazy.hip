@@ -227,10 +227,19 @@ __device__ __forceinline__ RowPtrs row_ptrs(const ctr_lazy_tab_t& tb, long row, 
 
 // One 8-lane group per (id, table) item.  The group leader claims the row with a CAS on last[row]
 // (s -> tick); only the winner replays, so a row read many times in a batch is caught up once.
-__global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+// STAGED (ntabs <= FLUSH_MAXTABS): the table descriptors are copied to LDS first -- the key -> table binary search
+// and the descriptor reads were a chain of dependent global loads ahead of every row's own loads
+template <bool STAGED>
+__global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* __restrict__ gtabs, int ntabs,
                                                          const int32_t* __restrict__ X, long nitems, int ncols,
                                                          int per_column, float* P, float* M, float* V, float* E,
                                                          const OptScalars* __restrict__ hist, int tick) {
+  __shared__ ctr_lazy_tab_t stabs[STAGED ? FLUSH_MAXTABS : 1];
+  if (STAGED) {
+    for (int i = threadIdx.x; i < ntabs; i += 256) stabs[i] = gtabs[i];
+    __syncthreads();
+  }
+  const ctr_lazy_tab_t* tabs = STAGED ? stabs : gtabs;
   const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
   const int l8 = threadIdx.x & (LG - 1);
   int s = tick, win = 0, ti = 0, nz = 0;
@@ -275,19 +284,27 @@ __global__ __launch_bounds__(256) void lazy_touch_kernel(const ctr_lazy_tab_t* _
 }
 
 // One 8-lane group per compact grad slot: keys are unique, so no claim is needed.
-__global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
+template <bool STAGED>
+__global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* __restrict__ gtabs, int ntabs,
                                                           const uint32_t* __restrict__ keys,
                                                           const float* __restrict__ G, int g_ld,
                                                           const uint32_t* __restrict__ n_uniq, long cap,
                                                           const float* __restrict__ coef_ptr, float* P, float* M,
                                                           float* V, float* E, const OptScalars* __restrict__ hist,
                                                           int tick) {
+  __shared__ ctr_lazy_tab_t stabs[STAGED ? FLUSH_MAXTABS : 1];
   const long item = (blockIdx.x * 256L + threadIdx.x) / LG;
   const int l8 = threadIdx.x & (LG - 1);
+  // the slot's key and the unique count load side by side (the key was loaded after the count)
+  uint32_t key = item < cap ? keys[item] : LAZY_INVALID;
   const long nu = min(cap, (long)*n_uniq);
-  bool live = item < nu;
-  uint32_t key = live ? keys[item] : LAZY_INVALID;
-  live = live && key != LAZY_INVALID;
+  if (STAGED) {
+    for (int i = threadIdx.x; i < ntabs; i += 256) stabs[i] = gtabs[i];
+    __syncthreads();
+  }
+  const ctr_lazy_tab_t* tabs = STAGED ? stabs : gtabs;
+  bool live = item < nu && key != LAZY_INVALID;
+  if (!live) key = LAZY_INVALID;
   int a = 0;
   long row = 0;
   int s = tick - 1, w = 0;
@@ -1070,8 +1087,13 @@ extern "C" int ctr_lazy_touch(const ctr_lazy_tab_t* tabs, int ntabs, const int32
   CTR_REQUIRE(ntabs > 0 && (per_column != 1 || ntabs == ncols), "ctr_lazy_touch: per_column needs ntabs == ncols");
   if (tick <= 0 || nx <= 0 || ncols <= 0) return 0;
   const long nitems = per_column ? nx * ncols : nx * ncols * ntabs;
-  lazy_touch_kernel<<<(unsigned)cdiv(nitems * LG, 256L), 256, 0, (hipStream_t)stream>>>(
-      tabs, ntabs, X, nitems, ncols, per_column, P, M, V, E, (const OptScalars*)hist, tick);
+  const unsigned grid = (unsigned)cdiv(nitems * LG, 256L);
+  if (ntabs <= FLUSH_MAXTABS)
+    lazy_touch_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, X, nitems, ncols, per_column, P, M, V,
+                                                                   E, (const OptScalars*)hist, tick);
+  else
+    lazy_touch_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, X, nitems, ncols, per_column, P, M,
+                                                                    V, E, (const OptScalars*)hist, tick);
   return check_launch("lazy_touch");
 }
 
@@ -1080,8 +1102,13 @@ extern "C" int ctr_lazy_update(const ctr_lazy_tab_t* tabs, int ntabs, const uint
                                float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(ntabs > 0 && tick > 0, "ctr_lazy_update: bad tables / tick");
   if (cap <= 0) return 0;
-  lazy_update_kernel<<<(unsigned)cdiv(cap * LG, 256L), 256, 0, (hipStream_t)stream>>>(
-      tabs, ntabs, keys, G, g_ld, n_uniq, cap, coef, P, M, V, E, (const OptScalars*)hist, tick);
+  const unsigned grid = (unsigned)cdiv(cap * LG, 256L);
+  if (ntabs <= FLUSH_MAXTABS)
+    lazy_update_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, keys, G, g_ld, n_uniq, cap, coef, P,
+                                                                    M, V, E, (const OptScalars*)hist, tick);
+  else
+    lazy_update_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, keys, G, g_ld, n_uniq, cap, coef,
+                                                                     P, M, V, E, (const OptScalars*)hist, tick);
   return check_launch("lazy_update");
 }
 
