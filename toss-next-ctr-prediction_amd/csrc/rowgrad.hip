@@ -31,16 +31,18 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ c
                                                      const uint32_t* __restrict__ sorted_idx,
                                                      const uint32_t* __restrict__ counts,
                                                      const uint32_t* __restrict__ offsets,
-                                                     const uint32_t* __restrict__ n_uniq,
+                                                     const uint32_t* __restrict__ n_uniq, uint32_t n,
                                                      float* __restrict__ out) {
   const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  if (u >= n) return;
+  // the slot's key / offset / count load beside the unique count (they followed it: one more round trip)
+  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = counts[u];
   if (u >= *n_uniq) return;
-  if (uniq_keys[u] == 0xFFFFFFFFu) {
+  if (key == 0xFFFFFFFFu) {
     if (lane < width) out[(long)u * width + lane] = 0.f;
     return;
   }
-  const uint32_t off = offsets[u], cnt = counts[u];
   if (lane < width) {
     float acc = 0.f;
     uint32_t i = 0;
@@ -67,19 +69,20 @@ __global__ __launch_bounds__(256) void segsum2_kernel(const float* __restrict__ 
                                                       const uint32_t* __restrict__ sorted_idx,
                                                       const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ offsets,
-                                                      const uint32_t* __restrict__ n_uniq, float* __restrict__ oa,
-                                                      float* __restrict__ ob) {
+                                                      const uint32_t* __restrict__ n_uniq, uint32_t n,
+                                                      float* __restrict__ oa, float* __restrict__ ob) {
   const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, c = lane & 31;
+  if (u >= n) return;
+  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = counts[u];   // beside the unique count
   if (u >= *n_uniq) return;
   const float* __restrict__ src = lane < 32 ? ca : cb;
   float* __restrict__ dst = lane < 32 ? oa : ob;
   if (c >= width) return;
-  if (uniq_keys[u] == 0xFFFFFFFFu) {
+  if (key == 0xFFFFFFFFu) {
     dst[(long)u * width + c] = 0.f;
     return;
   }
-  const uint32_t off = offsets[u], cnt = counts[u];
   float acc = 0.f;
   uint32_t i = 0;
   for (; i + 4 <= cnt; i += 4) {   // issue 4 independent row loads, add in order
@@ -161,11 +164,11 @@ static int rowgrad_core(const uint32_t* keys, const float* const* contrib, float
   CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
   if (ncontrib == 2 && width <= 32)
     segsum2_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, counts, offsets,
-                                              n_uniq, uniq_grad[0], uniq_grad[1]);
+                                              n_uniq, (uint32_t)n, uniq_grad[0], uniq_grad[1]);
   else
     for (int q = 0; q < ncontrib; ++q)
       segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
-                                               uniq_grad[q]);
+                                               (uint32_t)n, uniq_grad[q]);
   return check_launch("rowgrad");
 }
 
