@@ -410,7 +410,7 @@ def main():
                   "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
-                          "ctr_adamw_ema", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
+                          "ctr_adamw_ema", "ctr_adamw_ema_hist", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
     if args.kernel_events == "all":
         _lib.time_calls(roof_timed)
     if args.markers:

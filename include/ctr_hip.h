@@ -366,6 +366,12 @@ int ctr_opt_chunk_elems(void);
 int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, uint32_t* krange, float* P,
                   float* M, float* V, float* E, const float* dgrad, const float* coef, float lr, float wd, float beta1,
                   float beta2, float eps, int step, float ema_decay, int do_adam, int do_ema, void* stream);
+/* ctr_adamw_ema (do_adam = 1) with hist[tick] = the same tick's scalars recorded in the same launches
+ * (ctr_opt_hist_record + ctr_adamw_ema of a lazy FusedAdamW step, one dispatch fewer)                        */
+int ctr_adamw_ema_hist(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, uint32_t* krange,
+                       float* P, float* M, float* V, float* E, const float* dgrad, const float* coef, float lr, float wd,
+                       float beta1, float beta2, float eps, int step, float ema_decay, int do_ema, void* hist, int tick,
+                       void* stream);
 int ctr_norm_nparts_per_call(void);
 int ctr_sqnorm_dense(const float* x, long n, float* part, void* stream);
 int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int width, int ld,

@@ -21,10 +21,15 @@ constexpr int OPT_MAXROWS = OPT_CHUNK / 4 + 2;  // sparse segments need width >=
 // For every sparse-segment chunk: [lo, hi) = index range of the sorted unique keys that fall in the
 // chunk's rows.  One thread per chunk (binary searches run in parallel, not as a serial prologue of
 // every streaming workgroup).
+// (hist != null: thread 0 also records the tick's scalars in the lazy tables' history -- the separate one-thread
+// launch before it cost a dispatch and its boundary every step)
 __global__ __launch_bounds__(256) void chunk_key_range_kernel(const ctr_opt_chunk_t* __restrict__ chunks, int nchunks,
                                                               const ctr_opt_seg_t* __restrict__ segs,
-                                                              uint32_t* __restrict__ range) {
+                                                              uint32_t* __restrict__ range,
+                                                              OptScalars* __restrict__ hist = nullptr, int tick = 0,
+                                                              OptScalars hs = OptScalars{}) {
   const int c = blockIdx.x * 256 + threadIdx.x;
+  if (hist && c == 0) hist[tick] = hs;
   if (c >= nchunks) return;
   const ctr_opt_chunk_t ch = chunks[c];
   const ctr_opt_seg_t sg = segs[ch.seg];
@@ -216,6 +221,19 @@ extern "C" int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const c
   if (do_adam) chunk_key_range_kernel<<<cdiv(nchunks, 256), 256, 0, st>>>(chunks, nchunks, segs, krange);
   adamw_ema_kernel<<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);
   return check_launch("adamw_ema");
+}
+
+extern "C" int ctr_adamw_ema_hist(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs,
+                                  uint32_t* krange, float* P, float* M, float* V, float* E, const float* dgrad,
+                                  const float* coef, float lr, float wd, float beta1, float beta2, float eps, int step,
+                                  float ema_decay, int do_ema, void* hist, int tick, void* stream) {
+  CTR_REQUIRE(hist != nullptr && tick > 0, "ctr_adamw_ema_hist: bad history / tick");
+  const OptScalars s = make_opt_scalars(lr, wd, beta1, beta2, eps, step, ema_decay, 1, do_ema);
+  hipStream_t st = (hipStream_t)stream;
+  chunk_key_range_kernel<<<std::max(1, cdiv(nchunks, 256)), 256, 0, st>>>(chunks, nchunks, segs, krange,
+                                                                        (OptScalars*)hist, tick, s);
+  if (nchunks > 0) adamw_ema_kernel<<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);
+  return check_launch("adamw_ema_hist");
 }
 
 extern "C" int ctr_norm_nparts_per_call(void) { return NORM_BLOCKS; }

@@ -125,6 +125,7 @@ SIGS = {
     "ctr_rowgrad2": (i, [p, p, p, i, i, i, i, p, p, p, p, p, z, p]),
     "ctr_opt_chunk_elems": (i, []),
     "ctr_adamw_ema": (i, [p, i, p, p, p, p, p, p, p, p, f, f, f, f, f, i, f, i, i, p]),
+    "ctr_adamw_ema_hist": (i, [p, i, p, p, p, p, p, p, p, p, f, f, f, f, f, i, f, i, p, i, p]),
     "ctr_norm_nparts_per_call": (i, []),
     "ctr_sqnorm_dense": (i, [p, l, p, p]),
     "ctr_sqnorm_rows": (i, [p, p, p, i, i, u, p, p]),

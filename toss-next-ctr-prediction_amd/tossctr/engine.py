@@ -164,7 +164,7 @@ class Engine:
         # backward side stream: weight / bias grads whose inputs are final run beside the input-grad chain
         # (one stream per engine; joined before the optimizer and before a data-parallel bucket hand-off)
         self._side = None
-        self.side_stream = True
+        self.side_stream = os.environ.get("CTR_SIDE_STREAM", "1") != "0"   # (0: one stream, for A/B)
         self.stream = None
         self.last = None
         self.grad_ready = None   # data parallel: called once the head's dense grads are final (bucket 1)

@@ -462,15 +462,19 @@ class FusedAdamW:
         if self._timing:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        shadow = ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf)
         if self.lazy:
+            # the tick's scalars go to the lazy tables' history in the same launches as the dense update
             self.tick += 1
-            call("ctr_opt_hist_record", ptr(self._hist_for(self.tick)), self.tick, float(g["lr"]),
+            call("ctr_adamw_ema_hist", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
+                 ptr(self.v), shadow, ptr(self.arena.grad), ptr(self.norm_out, 1), float(g["lr"]),
+                 float(g["weight_decay"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(decay),
+                 do_ema, ptr(self._hist_for(self.tick)), self.tick, st)
+        else:
+            call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
+                 ptr(self.v), shadow, ptr(self.arena.grad), ptr(self.norm_out, 1), float(g["lr"]),
                  float(g["weight_decay"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1,
                  do_ema, st)
-        call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
-             ptr(self.v), ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf), ptr(self.arena.grad),
-             ptr(self.norm_out, 1), float(g["lr"]), float(g["weight_decay"]),
-             float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1, do_ema, st)
         if self.lazy:
             ta, tr, tc = tg["att"], tg["rep"], tg["cat"]
             if ta["keys"] is tr["keys"] and ta["G"].shape[1] == tr["G"].shape[1]:
