@@ -42,6 +42,87 @@ def make_params(shapes, seed: int, pad_id: int = 0):
     return out
 
 
+def reference_init(A, seed: int):
+    """The reference's own initial parameters: ``torch.manual_seed(seed); CTRModel(...)``, restated as the
+    torch.nn default initialisers the reference's constructors run, drawn from torch's CPU generator in the
+    reference's construction order (src/models/wrapper.py:24-100; feature_embed.py:15-17,38-40; dare.py:43-51,
+    89-90,106-114; qnn_alpha.py:64-84).  ``A``: oracle.model.Arch.  Returns {state_dict key: float32 ndarray}.
+    Pinned bitwise against the reference's model by tests/golden/gen_golden.py (``init: reference`` cases)."""
+    import math
+
+    import torch
+    from torch.nn import init
+
+    out = {}
+    torch.manual_seed(seed)
+
+    def linear(key, n_out, n_in, bias=True):      # nn.Linear.reset_parameters
+        w = torch.empty(n_out, n_in)
+        init.kaiming_uniform_(w, a=math.sqrt(5))
+        out[key + ".weight"] = w
+        if bias:
+            b = torch.empty(n_out)
+            bound = 1 / math.sqrt(n_in) if n_in > 0 else 0
+            init.uniform_(b, -bound, bound)
+            out[key + ".bias"] = b
+
+    def embedding(key, rows, width, pad=None):    # nn.Embedding.reset_parameters
+        w = torch.empty(rows, width)
+        init.normal_(w)
+        if pad is not None:
+            w[pad].zero_()
+        out[key] = w
+
+    D, fe = A.D, A.f_embed
+    if A.Fn > 0:
+        out["num_embed.weight"] = torch.randn(A.Fn, fe) * 0.02
+        out["num_embed.bias"] = torch.zeros(A.Fn, fe)
+        linear("num_embed.out_proj", D, fe, bias=False)
+    if A.Fm > 0:
+        out["mask_embed.weight"] = torch.randn(A.Fm, fe) * 0.02
+        linear("mask_embed.out_proj", D, fe, bias=False)
+    for c, card, d in zip(A.cat_names, A.cat_cards, A.cat_dims):
+        embedding(f"cat_embs.{c}.weight", card, d)
+        linear(f"cat_proj.{c}", D, d, bias=False)
+    linear("ctx_mlp.0", D, D * ((A.Fn > 0) + (A.Fm > 0) + 1))
+    embedding("dare.emb_att.weight", A.seq_vocab, D, A.pad_id)
+    embedding("dare.emb_rep.weight", A.seq_vocab, D, A.pad_id)
+    for i in range(A.n_layers):
+        p = f"dare.layers.{i}."
+        # nn.MultiheadAttention: out_proj (an nn.Linear) is built first, then _reset_parameters draws
+        # xavier_uniform_ for in_proj_weight and zeroes both biases
+        linear(p + "mha.out_proj", D, D)
+        w = torch.empty(3 * D, D)
+        init.xavier_uniform_(w)
+        out[p + "mha.in_proj_weight"] = w
+        out[p + "mha.in_proj_bias"] = torch.zeros(3 * D)
+        out[p + "mha.out_proj.bias"].zero_()
+        out[p + "norm1.w"] = torch.ones(D)
+        linear(p + "ffn.0", A.ffn_hidden, D)
+        linear(p + "ffn.3", D, A.ffn_hidden)
+        out[p + "norm2.w"] = torch.ones(D)
+        if A.add_pos:
+            embedding(p + "pbias.rel.weight", 2 * A.top_k + 1, A.H)
+    linear("dare.aux_head", 1, D)
+    if A.use_qnn:
+        FD, C = A.F * D, A.qh * A.qP
+        out["qnn.pre_norm.w"] = torch.ones(FD)
+        out["qnn.U"] = torch.randn(A.qh, D, A.qr) * 0.02
+        out["qnn.V"] = torch.randn(A.qh, A.qr, A.qP) * 0.02
+        if A.use_se:
+            linear("qnn.se.fc.0", C // A.se_r, C)
+            linear("qnn.se.fc.2", C, C // A.se_r)
+        din = C + FD
+        for j, h in enumerate(A.mlp_hidden):
+            linear(f"qnn.mlp.{3 * j}", h, din)
+            din = h
+        linear(f"qnn.mlp.{3 * len(A.mlp_hidden)}", 1, din)
+    else:
+        linear("fc.0", 512, D * (1 + (A.Fn > 0) + (A.Fm > 0) + A.Fc))
+        linear("fc.3", 1, 512)
+    return {k: out[k].numpy() for k, _ in A.param_shapes()}
+
+
 def make_batch(B, Fn, Fm, cards, L, vocab, seed, pad_id=0, edge_rows=True, lognormal=False, pos_rate=0.3):
     r = np.random.default_rng(seed)
     X_num = r.standard_normal((B, Fn)).astype(np.float32)

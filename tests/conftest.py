@@ -17,12 +17,14 @@ def pytest_configure(config):
 # BASELINE configs first: under `pytest -x` a late failure must not leave a config's parity unreached.
 # cfg1 = the dare_base plumbing run, cfg2/cfg3 = cfg2_dims/cfg3_dims, cfg4 = cfg4_full (+ the k148 / k120
 # reduced cases), cfg5 = the reduced row-sharded run; each in fp32 and (test_gpu_amp) amp bf16.
-_CONFIG_CASES = ("cfg2_dims", "cfg3_dims", "cfg4_full", "k148", "k120")
+_CONFIG_CASES = ("cfg2_dims", "cfg2_ref", "cfg3_dims", "cfg4_full", "k148", "k120")
 _EARLY = (
+    lambda n: "test_gpu_fullshape.py::" in n,
     lambda n: "test_gpu_parity.py::test_autograd_path_step0" in n and any(f"[{c}]" in n for c in _CONFIG_CASES),
     lambda n: "test_gpu_amp.py::" in n,
     lambda n: "test_gpu_plumbing.py::" in n,
-    lambda n: "test_gpu_shard.py::test_cfg5_reduced" in n,
+    lambda n: "test_gpu_shard.py::test_cfg5_reduced" in n or "cfg5w" in n,
+    lambda n: "test_gpu_lazy.py::test_lazy_matches_dense_bitwise_at_cfg_widths" in n,
     lambda n: "test_gpu_parity.py::test_fused_train_steps" in n and any(f"[{c}-" in n for c in _CONFIG_CASES),
 )
 

@@ -6,6 +6,11 @@ ranks before anything in it touches the GPU).  World-2 runs put both ranks on cu
                                       --lazy {0,1} [--steps N] [--config tiny|cfg5r] [--nccl 1]
                                       [--prefetch 0|1] [--sync-check 1] --out FILE
 
+--config cfg5w: BASELINE config 5's WIDTHS (tossctr.configs.hb1e8_d64: D = 64, the yaml's 35 d_c, K = 100, S1,
+three encoder layers, 82 + 82 numeric / mask features, MLP 13952-512-256) with small tables (997 hashed rows,
+20,000 DARE rows), B = 16 per rank, the reference's own init (oracle.synth.reference_init) and the yaml's
+lr 3e-4: checked against the oracle by tests/test_gpu_shard.py.  Dumps like --config tiny.
+
 --config cfg5r: BASELINE config 5 at reduced scale (tossctr.configs.hb1e8_d64 with hash_buckets=4e6:
 D = 64, the yaml's d_c, 35 tables of 4M rows = 140M rows -> 28-bit owner-major keys at world 2; one
 encoder layer, B = 32).  Tables are filled by a function of (global row, column) so that the sharded
@@ -68,6 +73,7 @@ def run(rank, world, port, args):
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         pg = dist.group.WORLD
+    lr0 = 3e-3
     if args.config == "tiny":
         fx = Fixture(CASE)
         m = fx.meta
@@ -75,6 +81,12 @@ def run(rank, world, port, args):
         clip = m["train"]["clip"] or 1.0
         vocab = int(m["vocab"]) * 8                 # sparse tables: most rows skip most ticks
         cards = {k: v * 4 + 1 for k, v in fx.cat_cards.items()}
+    elif args.config == "cfg5w":
+        from tossctr.configs import N_NUM_NEXT, cat_cardinals, hb1e8_d64
+        cfg = hb1e8_d64(hash_buckets=997)
+        Fn = Fm = N_NUM_NEXT
+        L, Bs, clip, vocab, lr0 = 100, 16, 0.5, 20_000, 3e-4
+        cards = cat_cardinals(cfg)
     else:
         from tossctr.configs import N_NUM_NEXT, cat_cardinals, hb1e8_d64
         cfg = hb1e8_d64(hash_buckets=4_000_000)
@@ -90,6 +102,9 @@ def run(rank, world, port, args):
     if args.config == "tiny":
         model.load_state_dict({k: torch.from_numpy(v) for k, v in make_params(arch.param_shapes(), 5,
                                                                               arch.pad_id).items()})
+    elif args.config == "cfg5w":
+        from oracle.synth import reference_init
+        model.load_state_dict({k: torch.from_numpy(v) for k, v in reference_init(arch, 5).items()})
     else:
         dense = [(k, s) for k, s in arch.param_shapes() if not (k.startswith("cat_embs.") or ".emb_" in k)]
         with torch.no_grad():
@@ -97,7 +112,7 @@ def run(rank, world, port, args):
                 model.arena.views[k].copy_(torch.from_numpy(v))
             _fill_tables_by_index(model, rank, world)
     ema = ArenaEMA(model, base_decay=0.9)
-    opt = FusedAdamW(model, lr=3e-3, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
+    opt = FusedAdamW(model, lr=lr0, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
                      lazy=bool(args.lazy))
     losses, batches, staged = [], [], []
     for t in range(args.steps):
@@ -107,18 +122,36 @@ def run(rank, world, port, args):
         staged.append((model.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda()))
     model.train()
     for t in range(args.steps):
-        opt.param_groups[0]["lr"] = 3e-3 * (1.0 - 0.2 * t)
+        opt.param_groups[0]["lr"] = lr0 * (1.0 - 0.2 * t)
         inputs, y = staged[t]
+        if args.interleave_eval and t == 2:
+            # an evaluation forward between step 1 (which planned batch 2's exchange) and step 2: the
+            # prefetched plan does not match it and is dropped, step 2 plans in place
+            model.eval()
+            with torch.no_grad():
+                model(to_torch_batch(make_batch(Bs, Fn, Fm, list(cards.values()), L, vocab, seed=99 + rank)), seed=3)
+            model.train()
+        # --short-last: on the last step rank 1 holds no rows (tossctr.train.rank_slice's short last step): it
+        # joins the collectives with a zero gradient and the gradient is averaged over the one contributor
+        short = args.short_last and t == args.steps - 1
+        kw = dict(contribute=not (short and rank == 1), contributors=1 if short else None)
         # row-sharded: the next batch's exchange is planned beside this step (--prefetch 1, the default)
         nxt = staged[t + 1][0] if args.prefetch and t + 1 < args.steps else None
         # --sync-check: from the third step on (the first ones allocate and upload their tables) the step must
         # not block the host on the device: torch raises on any synchronising call
         if args.sync_check and t == 2:
             torch.cuda.set_sync_debug_mode("error")
-        loss = model.train_step(inputs, y, opt, global_step=t + 1, seed=(9 << 32) | t, next_inputs=nxt)
+        loss = model.train_step(inputs, y, opt, global_step=t + 1, seed=(9 << 32) | t, next_inputs=nxt, **kw)
         losses.append(loss)
     torch.cuda.set_sync_debug_mode("default")
     losses = [float(x.item()) for x in losses]
+    if model.shards is not None and args.prefetch:
+        # every step after the first consumed the plan made beside the step before it, except the one an
+        # evaluation forward came in front of (--interleave-eval)
+        sh = model.shards
+        want_miss = 1 if args.interleave_eval and args.steps > 2 else 0
+        assert (sh.prefetch_hits, sh.prefetch_misses) == (args.steps - 1 - want_miss, want_miss), \
+            (sh.prefetch_hits, sh.prefetch_misses)
     if args.config == "cfg5r":
         _dump_touched(model, opt, ema, batches, arch, rank, world, losses, args)
     else:
@@ -133,7 +166,9 @@ def run(rank, world, port, args):
         local_rows = int(model.arena.shapes["dare.emb_att.weight"][0])
         if rank == 0:
             torch.save({"sd": sd, "ema": shadow, "m": mom, "v": vel, "losses": losses, "logits": logits,
-                        "gnorm": float(opt.norm_out[0]), "local_rows": local_rows, "vocab": vocab, "cards": cards},
+                        "gnorm": float(opt.norm_out[0]), "local_rows": local_rows, "vocab": vocab, "cards": cards,
+                        "cfg": cfg, "Fn": Fn, "Fm": Fm, "L": L, "B": Bs, "lr0": lr0, "clip": clip,
+                        "init": "reference" if args.config == "cfg5w" else "synthetic"},
                        args.out)
     if pg is not None:
         dist.barrier()
@@ -182,12 +217,14 @@ def main():
     ap.add_argument("--same-batch", type=int, default=0)
     ap.add_argument("--lazy", type=int, default=1)
     ap.add_argument("--steps", type=int, default=STEPS)
-    ap.add_argument("--config", choices=("tiny", "cfg5r"), default="tiny")
+    ap.add_argument("--config", choices=("tiny", "cfg5w", "cfg5r"), default="tiny")
     ap.add_argument("--nccl", type=int, default=0, help="world 1 over RCCL instead of world 2 over gloo")
     ap.add_argument("--prefetch", type=int, default=1, help="plan the next batch's exchange beside each step")
     ap.add_argument("--sync-check", type=int, default=0,
                     help="steps >= 2 under torch.cuda.set_sync_debug_mode('error') (needs --nccl 1: gloo stages "
                          "through the host)")
+    ap.add_argument("--interleave-eval", type=int, default=0, help="an eval forward between steps 1 and 2")
+    ap.add_argument("--short-last", type=int, default=0, help="rank 1 contributes nothing on the last step")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     if args.mode == "single":

@@ -191,23 +191,32 @@ def put_allow(store, name, allow, rows, shape):
 
 
 def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, store_params, train_cfg,
-             y_override=None, lognormal=False, amp_twin=None, allow_replays=ALLOW_REPLAYS):
+             y_override=None, lognormal=False, amp_twin=None, allow_replays=ALLOW_REPLAYS, init="synthetic"):
     """One fixture.  ``amp_twin``: the name of the fp32 fixture this case repeats (same inputs, seeds and
     parameters) under ``amp: bf16`` -- the forward and the loss run inside
     ``torch.autocast("cpu", dtype=torch.bfloat16)`` as src/train.py:158-164 wraps them in
     ``torch.cuda.amp.autocast(dtype=bfloat16)`` (CPU autocast here: no GPU in the generating container);
-    backward, clip, AdamW and EMA outside it, on the fp32 master parameters."""
+    backward, clip, AdamW and EMA outside it, on the fp32 master parameters.
+
+    ``init="reference"``: the parameters are the reference's OWN initialisation (``torch.manual_seed(pseed)``
+    before ``CTRModel(...)``), which ``oracle.synth.reference_init`` restates -- asserted bitwise here, so the
+    GPU box (no reference there) rebuilds P0 from the seed; ``"synthetic"``: ``oracle.synth.make_params``."""
     CTRModel, ref_dare, build_ema, cosine_warmup_lr, bce_wll_style = load_ref()
     if amp_twin is not None:
         cfg = dict(cfg, amp="bf16")
     amp_ctx = (lambda: torch.autocast("cpu", dtype=torch.bfloat16)) if amp_twin else contextlib.nullcontext
     cat_cols = list(cat_cards)
     A = make_arch(cfg, vocab, Fn, Fm, cat_cards, cat_cols)
-    torch.manual_seed(0)
+    torch.manual_seed(pseed if init == "reference" else 0)
     model = CTRModel(cfg, vocab, Fn, Fm, dict(cat_cards), cat_cols)
-    P0 = synth.make_params(A.param_shapes(), pseed, pad_id=A.pad_id)
     sd = model.state_dict()
     assert list(sd.keys()) == [k for k, _ in A.param_shapes()], "state_dict order/keys mismatch"
+    if init == "reference":
+        P0 = synth.reference_init(A, pseed)
+        for k, v in sd.items():
+            assert np.array_equal(v.numpy(), P0[k]), f"reference_init differs from the reference's init on {k}"
+    else:
+        P0 = synth.make_params(A.param_shapes(), pseed, pad_id=A.pad_id)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in P0.items()}, strict=True)
     ema = build_ema(model, cfg)
     opt = torch.optim.AdamW(model.parameters(), lr=train_cfg["lr"], weight_decay=train_cfg["wd"])
@@ -215,7 +224,7 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
     store = {}
     meta = dict(name=name, cfg=cfg, B=B, L=L, vocab=vocab, Fn=Fn, Fm=Fm, cat_cards=cat_cards,
                 steps=steps, pseed=pseed, bseed=bseed, store_params=store_params, train=train_cfg,
-                lrs=[], seeds=[], amp="bf16" if amp_twin else "none", twin=amp_twin)
+                lrs=[], seeds=[], amp="bf16" if amp_twin else "none", twin=amp_twin, init=init)
     if store_params:
         for k, v in P0.items():
             store[f"p0/{k}"] = v
@@ -496,6 +505,9 @@ def main():
     if "--cfg4" in sys.argv:
         gen_r3(only_cfg4=True)
         return
+    if "--r4" in sys.argv:
+        gen_r4()
+        return
     tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
     cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
     run_case("tiny_concat", tiny_cfg(), B=64, L=32, vocab=5000, Fn=6, Fm=6, cat_cards=cards, steps=3,
@@ -526,6 +538,7 @@ def main():
     gen_infer()
     gen_bf16()
     gen_r3()
+    gen_r4()
 
 
 def gen_r3(only_cfg4=False):
@@ -554,6 +567,20 @@ def gen_r3(only_cfg4=False):
     cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
     run_case("tiny_ffn40", tiny_cfg(D=32, H=4, ffn_hidden=40), B=40, L=28, vocab=3000, Fn=5, Fm=5,
              cat_cards=cards, steps=2, pseed=15, bseed=1000, store_params=True, train_cfg=tr)
+
+
+def gen_r4():
+    """Round-4 case: BASELINE config 2's widths in the regime the reference trains in -- its OWN
+    initialisation (oracle.synth.reference_init, checked bitwise in run_case) and the yaml's lr 3e-4
+    (cfgs/dare_qnn_next.yaml:254), no warm-up -- so the logits stay near 0 (loss ~0.7) and the clip at 0.5
+    is mild, unlike cfg2_dims (synthetic init, lr 3e-3: saturated logits, every step clipped ~1000x).
+    fp32 and its amp bf16 twin, three steps."""
+    tr = dict(lr=3e-4, wd=1e-4, clip=0.5, steps_per_epoch=10, warmup_epochs=0, epochs=8)
+    cfg2, cols = cfg2_cfg()
+    kw = dict(B=16, L=100, vocab=3000, Fn=82, Fm=82, cat_cards={c: 200 for c in cols}, steps=3, pseed=71,
+              bseed=1100, store_params=False, train_cfg=tr, init="reference")
+    run_case("cfg2_ref", cfg2, **kw)
+    run_case("cfg2_ref_bf16", cfg2, **kw, amp_twin="cfg2_ref")
 
 
 def gen_bf16():

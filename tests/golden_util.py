@@ -12,10 +12,10 @@ from oracle.model import make_arch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["tiny_concat", "tiny_s1_relu", "tiny_s2", "base_fc", "cfg2_dims", "cfg3_dims", "k148", "k120", "cfg4_full",
-         "tiny_ffn40"]
+         "tiny_ffn40", "cfg2_ref"]
 # amp: bf16 twins (gen_golden.gen_bf16): the reference under torch.autocast(bfloat16) on the inputs,
 # seeds and parameters of the fp32 fixture named in meta["twin"]
-BF16_CASES = ["tiny_concat_bf16", "cfg2_dims_bf16", "cfg3_dims_bf16", "k148_bf16", "cfg4_full_bf16"]
+BF16_CASES = ["tiny_concat_bf16", "cfg2_dims_bf16", "cfg3_dims_bf16", "k148_bf16", "cfg4_full_bf16", "cfg2_ref_bf16"]
 # AdamW updates elementwise (Fixture.check_update): |d| <= 2 ulp + the replayed-conditioning allowance +
 # ELEM_RTOL_UPDATE (10 |ref| + max |ref|); ill-conditioned elements (sqrt(v_hat) < 100 eps) only norm-wise
 ELEM_RTOL_UPDATE = 1e-3
@@ -56,6 +56,8 @@ class Fixture:
         self.arch = make_arch(m["cfg"], m["vocab"], m["Fn"], m["Fm"], self.cat_cards, self.cat_cols)
 
     def params0(self):
+        if self.meta.get("init") == "reference":     # the reference's own init, restated (gen_golden.run_case)
+            return synth.reference_init(self.arch, self.meta["pseed"])
         if self.meta["store_params"]:
             return {k: self.z[f"p0/{k}"] for k, _ in self.arch.param_shapes()}
         return synth.make_params(self.arch.param_shapes(), self.meta["pseed"], pad_id=self.arch.pad_id)

@@ -82,8 +82,10 @@ def test_bf16_fused_steps_within_band(case):
         if tr["clip"] > 0:
             scalar_band(float(opt.norm_out[0].item()), float(f16.z[f"out{t}/gnorm"]), float(f32.z[f"out{t}/gnorm"]),
                         f"{case} gnorm {t}")
-    # after the first AdamW step a lone element may take the other sign step (golden_util.check_bf16_band)
-    fl = 1 if m["steps"] > 1 else 0
+    # after the first AdamW step a lone element may take the other sign step (golden_util.check_bf16_band):
+    # measured only on cfg4_full_bf16 (vT/qnn.mlp.0.weight, profiles/r03/amp_band_start.log), so only that
+    # case may leave one such element out; every other case is held to the full band
+    fl = 1 if case == "cfg4_full_bf16" and m["steps"] > 1 else 0
     sd = model.state_dict()
     for k, v in sd.items():
         check_bf16_band(f16, f32, f"dT/{k}", v.double().cpu() - p0[k], update=True, p0=p0[k], flips=fl)

@@ -75,6 +75,73 @@ def test_lazy_matches_dense_bitwise(case):
     assert 0 < int(touched.sum()) < ta.shape[0] // 2
 
 
+def _pooled_batch(B, m, cards, L, vocab, seed, pool_seq, pool_cat):
+    """make_batch with half of the history tokens and of the categorical ids drawn from small pools spread
+    over the tables, so rows recur after gaps of every length (a token of the 4000-row pool returns every
+    few ticks, a uniform one almost never): the replay of 1 .. T missed ticks is exercised row by row."""
+    b = make_batch(B, m["Fn"], m["Fm"], list(cards.values()), L, vocab, seed=seed)
+    r = np.random.default_rng(seed + 17)
+    seq = b["seq"]
+    sel = (seq != 0) & (r.random(seq.shape) < 0.5)
+    seq[sel] = pool_seq[r.integers(0, pool_seq.size, int(sel.sum()))]
+    xc = b["X_cat"]
+    for c in range(xc.shape[1]):
+        s = r.random(B) < 0.5
+        xc[s, c] = pool_cat[c][r.integers(0, pool_cat[c].size, int(s.sum()))]
+    return b
+
+
+@pytest.mark.parametrize("case,vocab,card", [("cfg2_dims", 2_000_000, 60_000), ("cfg4_full", 5_000_000, 60_000)],
+                         ids=["D32_cfg2", "D64_cfg4"])
+def test_lazy_matches_dense_bitwise_at_cfg_widths(case, vocab, card):
+    """Lazy = dense, bit for bit, at the widths the bench runs: cfg2 (D = 32: lazy_*_pair*<32>, 35 tables of
+    the yaml's d_c) and cfg4 (D = 64, L = 400, K = 148, 4 layers: lazy_*_pair*<64>), over 32 ticks with a
+    changing lr, an EMA-only tick, an evaluation read and two mid-run flushes; tables >= 40x the rows the run
+    touches, and pooled ids (_pooled_batch), so rows replay gaps of every length up to the whole run."""
+    from tossctr import ArenaEMA, FusedAdamW
+    fx = Fixture(case)
+    m, tr = fx.meta, fx.meta["train"]
+    cards = {k: card for k in fx.cat_cards}
+    md, ml = _models(fx, vocab, cards)
+    ema_d = ArenaEMA(md, base_decay=0.99, warmup_steps=5, warmup_type="cosine")
+    ema_l = ArenaEMA(ml, base_decay=0.99, warmup_steps=5, warmup_type="cosine")
+    od = FusedAdamW(md, lr=1e-3, weight_decay=1e-4, max_grad_norm=0.5, ema=ema_d, lazy=False)
+    ol = FusedAdamW(ml, lr=1e-3, weight_decay=1e-4, max_grad_norm=0.5, ema=ema_l, lazy=True)
+    B, L = (48, int(m["L"])) if case == "cfg2_dims" else (24, int(m["L"]))
+    steps = 32
+    r = np.random.default_rng(9)
+    pool_seq = r.choice(np.arange(1, vocab), 4000, replace=False).astype(np.int32)
+    pool_cat = [r.choice(card, 200, replace=False).astype(np.int32) for _ in cards]
+    seen_seq, seen_cat = set(), [set() for _ in cards]
+    for t in range(steps):
+        b = _pooled_batch(B, m, cards, L, vocab, 2000 + t, pool_seq, pool_cat)
+        seen_seq.update(np.unique(b["seq"]).tolist())
+        for c, s in enumerate(seen_cat):
+            s.update(np.unique(b["X_cat"][:, c]).tolist())
+        lr = 1e-3 * 0.5 * (1 + math.cos(math.pi * t / steps)) + 1e-5
+        for model, opt in ((md, od), (ml, ol)):
+            opt.param_groups[0]["lr"] = lr
+            model.train()
+            model.train_step(model.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda(), opt,
+                             global_step=t + 1, seed=(5 << 32) | t)
+            if t == 4:
+                opt.ema.update(model, global_step=t + 1)
+            if t == 6:
+                model.eval()
+                with torch.no_grad():
+                    model(to_torch_batch(_pooled_batch(B, m, cards, L, vocab, 77, pool_seq, pool_cat)))
+        if t in (11, 23):
+            ml.sync()
+        assert torch.equal(od.norm_out, ol.norm_out), t
+    assert vocab >= 40 * len(seen_seq) and all(card >= 40 * len(s) for s in seen_cat)
+    ml.sync()
+    assert ol.tick == steps + 1
+    assert torch.equal(md.arena.buf, ml.arena.buf)
+    assert torch.equal(od.m, ol.m)
+    assert torch.equal(od.v, ol.v)
+    assert torch.equal(ema_d.shadow, ema_l.shadow)
+
+
 def test_lazy_state_dict_flushes():
     from tossctr import FusedAdamW
     fx = Fixture("tiny_concat")

@@ -25,16 +25,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 _cache = {}
 
 
-def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0, prefetch=1, sync_check=0):
-    key = (mode, same, lazy, steps, config, nccl, prefetch, sync_check)
+def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0, prefetch=1, sync_check=0,
+         interleave=0, short_last=0):
+    key = (mode, same, lazy, steps, config, nccl, prefetch, sync_check, interleave, short_last)
     if key not in _cache:
         out = str(tmp_path_factory.mktemp("shard") / ("_".join(map(str, key)) + ".pt"))
         r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", mode,
                             "--same-batch", str(same), "--lazy", str(lazy), "--steps", str(steps), "--config", config,
                             "--nccl", str(nccl), "--prefetch", str(prefetch), "--sync-check", str(sync_check),
-                            "--out", out], capture_output=True, text=True, timeout=250)
+                            "--interleave-eval", str(interleave), "--short-last", str(short_last), "--out", out], capture_output=True, text=True, timeout=250)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-        if config == "tiny":
+        if config in ("tiny", "cfg5w"):
             _cache[key] = torch.load(out, weights_only=True)
         else:
             ranks = 1 if mode == "single" else 2
@@ -81,8 +82,8 @@ def test_sharded_lazy_equals_dense_stream(tmp_path_factory):
         assert torch.equal(lazy["ema"][k], dense["ema"][k]), k
 
 
-@pytest.mark.parametrize("mode", ["replicated", "sharded"])
-def test_data_parallel_step_matches_oracle(tmp_path_factory, mode):
+@pytest.mark.parametrize("mode,config", [("replicated", "tiny"), ("sharded", "tiny"), ("sharded", "cfg5w")])
+def test_data_parallel_step_matches_oracle(tmp_path_factory, mode, config):
     """world 2 with a different batch per rank against the CPU restatement applied per
     replica (oracle.model.TrainState.step_data_parallel: each rank's grads on its own batch -- its own SE
     batch mean and loss class counts -- averaged as DDP does, then one clip -> AdamW -> EMA).  After one
@@ -91,21 +92,24 @@ def test_data_parallel_step_matches_oracle(tmp_path_factory, mode):
     merged on their owners when sharded); checked norm-wise at 2e-4 / 4e-4 (moment tolerances,
     golden_util.Fixture.check_moment).  The update pT - p0 is checked norm-wise at 1e-4 (+ 2 fp32 ulps)
     on the elements whose AdamW step is well conditioned (sqrt(v_hat) >= 100 eps), and everywhere
-    elementwise within one lr."""
-    from golden_util import Fixture, to_torch_batch
+    elementwise within one lr.
+
+    config "cfg5w": BASELINE config 5's widths through the row-sharded exchange (D = 64, the yaml's 35 d_c,
+    K = 100, S1, 3 layers, 82 + 82 features; small tables), from the reference's own init at the yaml's lr 3e-4
+    (tests/dist_shard_worker.py)."""
+    from golden_util import to_torch_batch
     from oracle.model import TrainState, make_arch
-    from oracle.synth import make_batch, make_params
-    res = _run(tmp_path_factory, mode, 0, steps=1)
-    fx = Fixture("tiny_concat")
-    m = fx.meta
+    from oracle.synth import make_batch, make_params, reference_init
+    res = _run(tmp_path_factory, mode, 0, steps=1, config=config)
     cards = res["cards"]
     cols = list(cards)
     vocab = res["vocab"]
-    A = make_arch(m["cfg"], vocab, m["Fn"], m["Fm"], cards, cols)
-    P0 = {k: torch.from_numpy(v) for k, v in make_params(A.param_shapes(), 5, A.pad_id).items()}
-    lr = 3e-3
-    st = TrainState(P0, A, lr, 0.05, m["train"]["clip"] or 1.0, ema_cfg={"enabled": True, "decay": 0.9})
-    bs = [make_batch(40, m["Fn"], m["Fm"], list(cards.values()), int(m["L"]), vocab, seed=1000 + 100 * r)
+    A = make_arch(res["cfg"], vocab, res["Fn"], res["Fm"], cards, cols)
+    P0 = reference_init(A, 5) if res["init"] == "reference" else make_params(A.param_shapes(), 5, A.pad_id)
+    P0 = {k: torch.from_numpy(v) for k, v in P0.items()}
+    lr = res["lr0"]
+    st = TrainState(P0, A, lr, 0.05, res["clip"], ema_cfg={"enabled": True, "decay": 0.9})
+    bs = [make_batch(res["B"], res["Fn"], res["Fm"], list(cards.values()), res["L"], vocab, seed=1000 + 100 * r)
           for r in range(2)]
     losses, _, gnorm = st.step_data_parallel([to_torch_batch(b) for b in bs],
                                              [torch.from_numpy(b["y"]).float() for b in bs], lr, [(9 << 32)] * 2)
@@ -186,15 +190,30 @@ def test_rccl_world1_equals_single(tmp_path_factory, mode):
         assert torch.equal(got["ema"][k], single["ema"][k]), k
 
 
-def test_sharded_prefetch_equals_in_place_plan(tmp_path_factory):
+@pytest.mark.parametrize("interleave", [0, 1], ids=["prefetched", "eval_in_between"])
+def test_sharded_prefetch_equals_in_place_plan(tmp_path_factory, interleave):
     """The next batch's exchange planned beside the step (a plan stream, two plan slots) = planned in place at
-    the step's fetch: bit for bit, world 2 with different batches per rank."""
-    pre = _run(tmp_path_factory, "sharded", 0)
+    the step's fetch: bit for bit, world 2 with different batches per rank.  The worker asserts that every
+    step after the first consumed its prefetched plan (TableShards.prefetch_hits), so the overlap is really
+    exercised.  ``eval_in_between``: an evaluation forward between step 1 and step 2 fetches another batch, so
+    the plan made for step 2 is dropped (ordered behind on the fetching stream) and step 2 plans in place --
+    still the same bits, and exactly one miss."""
+    pre = _run(tmp_path_factory, "sharded", 0, interleave=interleave)
     inplace = _run(tmp_path_factory, "sharded", 0, prefetch=0)
     assert pre["losses"] == inplace["losses"]
     for k in pre["sd"]:
         assert torch.equal(pre["sd"][k], inplace["sd"][k]), k
         assert torch.equal(pre["ema"][k], inplace["ema"][k]), k
+
+
+@pytest.mark.parametrize("mode", ["replicated", "sharded"])
+def test_short_last_step_matches_single(tmp_path_factory, mode):
+    """An epoch's short last step (tossctr.train.rank_slice: a rank without rows): world 2 on the same batches,
+    where on the last step rank 1 runs train_step(contribute=False) and both ranks average over
+    contributors=1 -- equal to the single-GPU run of the same batches (1e-5: the clip norm's cross-rank sum)."""
+    single = _run(tmp_path_factory, "single", 1)
+    got = _run(tmp_path_factory, mode, 1, short_last=1)
+    _compare(got, single, 1e-5, what=f"{mode} short last step vs single: ")
 
 
 def test_rccl_sharded_step_never_blocks_the_host(tmp_path_factory):

@@ -48,10 +48,12 @@ def test_oracle_matches_reference(case):
             fx.check_update("demaT", k, v.double() - P[k].double(), P[k])
     with torch.no_grad():
         z, p, a = forward(st.P, to_torch_batch(fx.batch(m["steps"] - 1)), A, Dropper(0, training=False))
-    # after the optimizer steps the parameters themselves agree only within the update allowances above, so
-    # the eval forward is held to the north star's 1e-4 (cfg4_full: 4 layers at D = 64 give 1.4e-5)
-    fx.check("eval/logits", z, 1e-4, 1e-6)
-    fx.check("eval/aux", a, 1e-4, 1e-6)
+    # after the optimizer steps the parameters themselves agree only within the update allowances above;
+    # cfg4_full (4 layers at D = 64) carries that to 1.4e-5 on its eval logits, so it alone is held to the
+    # north star's 1e-4 and every other case to 1e-5
+    ev = 1e-4 if case == "cfg4_full" else 1e-5
+    fx.check("eval/logits", z, ev, 1e-6)
+    fx.check("eval/aux", a, ev, 1e-6)
 
 
 def test_rng_mask_rate_and_determinism():

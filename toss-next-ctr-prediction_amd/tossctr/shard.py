@@ -124,6 +124,8 @@ class TableShards:
         self._plan_stream = None
         self._pending = None    # the plan prefetch() issued for the next fetch()
         self._host = {}         # pinned count buffers per slot
+        self.prefetch_hits = 0      # fetches that consumed the plan prefetch() made for them
+        self.prefetch_misses = 0    # prefetched plans dropped because another batch was fetched first
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -202,9 +204,18 @@ class TableShards:
 
     def _take_plan(self, X_cat, seq):
         pl, self._pending = self._pending, None
+        cur = torch.cuda.current_stream(self.device)
         if pl is not None and pl.X_cat is X_cat and pl.seq is seq:
-            torch.cuda.current_stream(self.device).wait_event(pl.event)
+            cur.wait_event(pl.event)
+            self.prefetch_hits += 1
         else:
+            if pl is not None:
+                # a prefetched plan for another batch (e.g. an evaluation forward came in between): it is
+                # dropped, but its device writes and its copy into the pinned counts of its slot may still be
+                # running on the plan stream -- order everything after it, or the next in-place plan that reuses
+                # that slot on this stream could race with it
+                cur.wait_event(pl.event)
+                self.prefetch_misses += 1
             pl = self._issue_plan(X_cat, seq)
         # the host's only wait of the step: on counts computed beside the previous step when prefetched
         pl.event.synchronize()
