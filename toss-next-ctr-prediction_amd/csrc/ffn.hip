@@ -66,7 +66,6 @@ struct FfnArgs {
   const float* nw1;
   float* dh1;          // (M, D) output: grad wrt h1
   __bf16* wbf;         // amp bf16: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF) in bf16, written by the forward
-  int dbg;             // column-owner backward debug dumps (CTR_FFN_DEBUG), 0 = off
 };
 
 template <int D>
@@ -1797,27 +1796,6 @@ __global__ __launch_bounds__(512) void ffn_bwd_own_kernel(FfnArgs a, int steps_p
     prepare(s0, rc, dh2c);
   }
   __syncthreads();
-  if (a.dbg && blockIdx.x == 0) {      // debug: dump step s0's images / wave 0's first products into dx
-    const char* img = lds + (s0 % 3) * T::IMG;
-    if (a.dbg <= 2) {
-      for (int q = tid; q < 32 * D; q += 512) {
-        const int r = q / D, d = q % D;
-        a.dx[q] = (float)*(const __bf16*)(img + (a.dbg == 1 ? T::O_XB : T::O_HB) + r * T::XRS + d * 2);
-      }
-    } else if (w == 0) {
-      bf16x8 xa = *(const bf16x8*)(img + T::O_XB + c * T::XRS + 8 * g * 2);
-      bf16x8 ha = *(const bf16x8*)(img + T::O_HB + c * T::XRS + 8 * g * 2);
-      f32x4 pre = mfma_bf(xa, w1b[0][0], f32x4{0.f, 0.f, 0.f, 0.f});
-      f32x4 dfo = mfma_bf(ha, w2b[0][0], f32x4{0.f, 0.f, 0.f, 0.f});
-      for (int r = 0; r < 4; ++r) {
-        a.dx[(4 * g + r) * D + c] = pre[r];
-        a.dx[(4 * g + r) * D + 16 + c] = dfo[r];
-        a.dx[(16 + 4 * g + r) * D + c] = (float)w1b[0][0][r];
-        a.dx[(16 + 4 * g + r) * D + 16 + c] = (float)xa[r];
-      }
-    }
-    return;
-  }
   for (int s = s0; s < s1; ++s) {
     const bool more = s + 1 < s1;
     if (more) issue(s + 1, rn);
@@ -1870,17 +1848,351 @@ __global__ __launch_bounds__(512) void ffn_bwd_own_kernel(FfnArgs a, int steps_p
   }
 }
 
-// the owner-form shapes: D = 32 (D = 64 needs more registers than two waves per SIMD hold), FF = 128 NT,
-// NT <= 3
+// ---------------------------------------------------------------- amp: bf16, D = 64 column-owner backward, two passes
+// D = 64 (cfgs/v3_k148_s1.yaml) in the owner form above: a wave's dW1 AND dW2 slices (2 x 16 NT x 64 floats) plus its
+// resident weights need more registers than two waves per SIMD hold, so the weight grads are split over two passes
+// over the rows, each with its own accumulators in registers and ONE slab write per workgroup at the end:
+//   PASS 1: pre / dfo -> dact -> dW1, db1 (owner registers) and dx = dact W1 + dh2 -> norm1 backward, the norm
+//           weights' / db2 column sums.  The dx contraction over FF is NOT split over the waves (an 8-way fp32
+//           partial exchange of 32 x 64 rows per wave would need 140 KB of LDS): every wave writes its dact columns
+//           into a shared [FF][32 rows] bf16 image, and after one barrier wave w computes the whole 16 x 16 dx tile
+//           (row block w / 4, column block w % 4) over all FF from that image and W1^T (LDS-resident, bf16), so
+//           each dx element is one fixed-order MFMA chain (deterministic).  Two barriers per 32-row step.
+//   PASS 2: pre -> fo -> dW2 = dh2^T fo (owner registers).  Recomputes pre and the norm2 backward of dy.
+// The pass-2 re-read of x / dy / h2 (3 x 4 B x M x 64) replaces the per-tile slab read-modify-writes of the
+// rows-per-wave kernel (ffn_bwd_bf_kernel<64>: 2 GB written per launch at cfg4).
+template <int NT>
+struct FfnOwn64 {
+  static constexpr int D = 64, NW = 8, SR = 32, KH = 2, NJ = 4, VPL = 4;
+  static constexpr int FF = 128 * NT, NCH = FF / 32, NP = FF / 32;
+  static constexpr int XRS = 160;                                  // bytes per bf16 image row (as FfnOwn<64>)
+  static constexpr int O_XB = 0, O_HB = SR * XRS, O_KB = 2 * SR * XRS;
+  static constexpr int IMG = 2 * SR * XRS + NCH * SR * 4;          // one step's images; two of them
+  static constexpr int O_DA = 2 * IMG;                             // pass 1: dact [FF][32 rows] bf16 (own_stg)
+  static constexpr int DA = FF * 24 * 4;
+  static constexpr int XCS = D + 4;                                // pass 1: dx tiles [32 rows][XCS] fp32
+  static constexpr int O_DX = O_DA + DA, DXB = SR * XCS * 4;
+  static constexpr int W1S = FF * 2 + 16;                          // pass 1: W1^T [64 d][FF] bf16, row bytes
+  static constexpr int O_W1T = O_DX + DXB;
+  static constexpr int LDS1 = O_W1T + D * W1S;
+  static constexpr int LDS2 = 2 * IMG;
+  static_assert(NCH <= 16 && LDS1 <= 160 * 1024, "FfnOwn64: shape");
+};
+
+template <int NT, int PASS, bool NORMS, bool DROP>
+__global__ __launch_bounds__(512) void ffn_bwd_own64_kernel(FfnArgs a, int steps_per_wg) {
+  using T = FfnOwn64<NT>;
+  constexpr int D = 64, VPL = T::VPL, KH = T::KH, NJ = T::NJ, FF = T::FF;
+  __shared__ __attribute__((aligned(16))) char lds[PASS == 1 ? T::LDS1 : T::LDS2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  const int M = a.M;
+  const int nsteps = (M + T::SR - 1) / T::SR;
+  const int s0 = blockIdx.x * steps_per_wg, s1 = min(nsteps, s0 + steps_per_wg);
+  const int nb16 = (M + 15) / 16;
+  const int fw = 16 * NT * w;                   // this wave's first FF column
+  const float dsc = a.drop.scale;
+
+  // ---- resident weights: W1 slice (pre) in registers; W2^T slice (dfo) and W1^T (dx, LDS) in pass 1
+  const auto rw = buf_rsrc(a.wbf, (uint32_t)(3 * FF * D) * 2);
+  bf16x8 w1b[NT][KH], w2b[PASS == 1 ? NT : 1][KH];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      const uint32_t o = (uint32_t)((fw + 16 * t + c) * D + 32 * kh + 8 * g) * 2;
+      w1b[t][kh] = buf_ld_bf8(rw, o, 0);
+      if constexpr (PASS == 1) w2b[t][kh] = buf_ld_bf8(rw, o + (uint32_t)(FF * D) * 2, 0);
+    }
+  if constexpr (PASS == 1) {
+    for (int q = tid; q < D * FF / 8; q += 512) {      // W1^T rows d, 8 ff per 16-byte chunk
+      const int d = q / (FF / 8), f8 = (q % (FF / 8)) * 8;
+      *(bf16x8*)(lds + T::O_W1T + d * T::W1S + f8 * 2) = buf_ld_bf8(rw, (uint32_t)(2 * FF * D + d * FF + f8) * 2, 0);
+    }
+  }
+  float b1v[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) b1v[t] = a.b1[fw + 16 * t + c];
+
+  // ---- accumulators over the whole launch: dW1 + db1 (pass 1) or dW2 (pass 2)
+  f32x4 dwa[NT][NJ];
+  float db1[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    db1[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dwa[t][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float cb2[VPL], cn2[VPL], cn1[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) cb2[v] = cn2[v] = cn1[v] = 0.f;
+
+  // ---- loader / epilogue lane map: row 4w + g of the step, columns c0 .. c0 + 3
+  const int rl = 4 * w + g, c0 = VPL * c;
+  const uint32_t mbytes = (uint32_t)M * D * 4;
+  const auto rr2 = buf_rsrc(a.r2, NORMS ? (uint32_t)M * 4 : 0u);
+  const auto rr1 = buf_rsrc(a.r1, NORMS && PASS == 1 ? (uint32_t)M * 4 : 0u);
+  const auto rout = buf_rsrc(NORMS ? a.dh1 : a.dx, PASS == 1 ? mbytes : 0u);
+  const auto rmask = buf_rsrc(a.mask, DROP ? (uint32_t)nb16 * 16 * (FF / 32) * 4 : 0u);
+  float nw2[VPL], nw1[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    nw2[v] = NORMS ? a.nw2[c0 + v] : 0.f;
+    nw1[v] = NORMS && PASS == 1 ? a.nw1[c0 + v] : 0.f;
+  }
+  struct Raw {
+    fvec<VPL> x, dy, h2;
+    float r2;
+    uint32_t kw;
+  };
+  struct Nr1 {        // the norm1 backward's operands of the step's epilogue row (pass 1)
+    fvec<VPL> h1;
+    float r1;
+  };
+  auto issue = [&](int s, Raw& R) {
+    const int m = T::SR * s + rl;
+    const bool ok = m < M;
+    const long e = (long)m * D + c0;
+    R.x = ld_row<VPL>(a.x + e, ok);
+    R.dy = ld_row<VPL>((NORMS ? a.dy : a.dh) + e, ok);
+    if (NORMS) {
+      R.h2 = ld_row<VPL>(a.h2 + e, ok);
+      R.r2 = buf_ld(rr2, ok ? (uint32_t)m * 4 : BUF_OOB);
+    }
+    if (DROP) {      // keep word of chunk lane / 4, row 4w + lane % 4 (lanes >= 4 NCH idle)
+      const int row = T::SR * s + 4 * w + (lane & 3), ch = lane >> 2;
+      const bool okk = lane < 4 * T::NCH && row < M;
+      R.kw = __builtin_bit_cast(uint32_t, buf_ld(rmask, okk ? rw_word(ch, nb16, row >> 4, row & 15) * 4 : BUF_OOB));
+    }
+  };
+  auto issue_n1 = [&](int s, Nr1& N) {
+    const int m = T::SR * s + rl;
+    const bool ok = m < M;
+    N.h1 = ld_row<VPL>(a.h1 + (long)m * D + c0, ok);
+    N.r1 = buf_ld(rr1, ok ? (uint32_t)m * 4 : BUF_OOB);
+  };
+  // norm2 backward of the loaded rows -> dh2 (pass 1 keeps it for the row's epilogue) + the images of step s
+  auto prepare = [&](int s, const Raw& R, float (&dh2)[VPL]) {
+    char* img = lds + (s & 1) * T::IMG;
+    if (NORMS) {
+      float dot = 0.f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dot = fmaf(nw2[v] * R.dy.v[v], R.h2.v[v], dot);
+      dot = group_sum<16>(dot);
+      const float rm = R.r2;
+      const float coef = rm * rm * rm / (float)D * dot;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        dh2[v] = nw2[v] * R.dy.v[v] * rm - R.h2.v[v] * coef;
+        if constexpr (PASS == 1) {
+          cb2[v] += dh2[v];
+          cn2[v] = fmaf(R.dy.v[v] * R.h2.v[v], rm, cn2[v]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dh2[v] = R.dy.v[v];
+    }
+    *(bf16x4*)(img + T::O_XB + rl * T::XRS + c0 * 2) =
+        bf16x4{(__bf16)R.x.v[0], (__bf16)R.x.v[1], (__bf16)R.x.v[2], (__bf16)R.x.v[3]};
+    *(bf16x4*)(img + T::O_HB + rl * T::XRS + c0 * 2) = bf16x4{(__bf16)dh2[0], (__bf16)dh2[1], (__bf16)dh2[2], (__bf16)dh2[3]};
+    if (DROP && lane < 4 * T::NCH) *(uint32_t*)(img + T::O_KB + ((lane >> 2) * T::SR + 4 * w + (lane & 3)) * 4) = R.kw;
+  };
+
+  // transposed image reads: lane 4q + p of group g -> row 16b + 4g + q, columns 16j + 4p .. +3, so lane c gets
+  // column 16j + c at the rows {4g .. 4g + 3} of both 16-row blocks (the k-set of the row contractions)
+  auto tr_cols = [&](const char* base, int j) {
+    const int o0 = (4 * g + (c >> 2)) * T::XRS + (16 * j + 4 * (c & 3)) * 2, o1 = o0 + 16 * T::XRS;
+    return cat8(lds_tr4((const __bf16*)(base + o0)), lds_tr4((const __bf16*)(base + o1)));
+  };
+
+  // the step's products: pass 1 -> dW1 / db1 and the dact image; pass 2 -> dW2
+  auto compute = [&](int s) {
+    const char* img = lds + (s & 1) * T::IMG;
+    bf16x8 xa[2][KH], ha[PASS == 1 ? 2 : 1][KH];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) {
+        const int o = (16 * b + c) * T::XRS + (32 * kh + 8 * g) * 2;
+        xa[b][kh] = *(const bf16x8*)(img + T::O_XB + o);
+        if constexpr (PASS == 1) ha[b][kh] = *(const bf16x8*)(img + T::O_HB + o);
+      }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int f0 = fw + 16 * t;
+      f32x4 pre[2], dfo[2];
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        pre[b] = dfo[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh) {
+          pre[b] = mfma_bf(xa[b][kh], w1b[t][kh], pre[b]);
+          if constexpr (PASS == 1) dfo[b] = mfma_bf(ha[b][kh], w2b[t][kh], dfo[b]);
+        }
+      }
+      f32x4 out[2];       // pass 1: dact; pass 2: fo
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        u32x4 kw = {0u, 0u, 0u, 0u};
+        if (DROP) kw = *(const u32x4*)(img + T::O_KB + ((f0 >> 5) * T::SR + 16 * b + 4 * g) * 4);
+        const int bit = (f0 & 31) + c;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          // pre[b][r]: row 16b + 4g + r, column f0 + c
+          const f32x2 z = f32x2{pre[b][2 * q], pre[b][2 * q + 1]} + b1v[t];
+          f32x2 e;
+          const f32x2 cdf = cdf_as2(z, e);
+          f32x2 sc = {1.f, 1.f};
+          if (DROP) sc = f32x2{((kw[2 * q] >> bit) & 1u) ? dsc : 0.f, ((kw[2 * q + 1] >> bit) & 1u) ? dsc : 0.f};
+          f32x2 v;
+          if constexpr (PASS == 1) {
+            const f32x2 gg = z * e * 0.39894228040143268f + cdf;
+            v = f32x2{dfo[b][2 * q], dfo[b][2 * q + 1]} * sc * gg;
+          } else {
+            v = z * cdf * sc;
+          }
+          out[b][2 * q] = v.x;
+          out[b][2 * q + 1] = v.y;
+        }
+        if constexpr (PASS == 1) db1[t] += (out[b][0] + out[b][1]) + (out[b][2] + out[b][3]);
+      }
+      const bf16x8 ao = pack8(out[0], out[1]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (PASS == 1) dwa[t][j] = mfma_bf(ao, tr_cols(img + T::O_XB, j), dwa[t][j]);   // C[ff f0+4g+r][d 16j+c]
+        else dwa[t][j] = mfma_bf(tr_cols(img + T::O_HB, j), ao, dwa[t][j]);                     // C[d 16j+4g+r][ff f0+c]
+      }
+      if constexpr (PASS == 1) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          *(bf16x4*)(lds + T::O_DA + own_stg(f0 + c, 16 * b + 4 * g)) = __builtin_convertvector(out[b], bf16x4);
+      }
+    }
+  };
+
+  // pass 1: wave w's dx tile (rows 16 (w / 4) .., columns 16 (w % 4) ..) over all FF from the dact image
+  auto dx_tile = [&]() {
+    const int rb = w >> 2, dj = w & 3;
+    const int rm = 16 * rb + 4 * (c & 3);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < T::NP; ++p) {
+      const int fl = 32 * p + 8 * g + (c >> 2);
+      const bf16x8 av = cat8(lds_tr4((const __bf16*)(lds + T::O_DA + own_stg(fl, rm))),
+                             lds_tr4((const __bf16*)(lds + T::O_DA + own_stg(fl + 4, rm))));
+      const bf16x8 bv = *(const bf16x8*)(lds + T::O_W1T + (16 * dj + c) * T::W1S + (32 * p + 8 * g) * 2);
+      acc = mfma_bf(av, bv, acc);
+    }
+    float* xs = (float*)(lds + T::O_DX);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) xs[(16 * rb + 4 * g + r) * T::XCS + 16 * dj + c] = acc[r];
+  };
+
+  // pass 1: dx1 = dact W1 + dh2 of this lane's row -> norm1 backward (or dx)
+  auto epilogue = [&](int s, const float (&dh2)[VPL], const Nr1& N) {
+    const fvec<VPL> pv = *(const fvec<VPL>*)((const float*)(lds + T::O_DX) + rl * T::XCS + c0);
+    float dx1[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dx1[v] = pv.v[v] + dh2[v];
+    const int m = T::SR * s + rl;
+    const uint32_t off = m < M ? (uint32_t)(m * D + c0) * 4 : BUF_OOB;
+    if (!NORMS) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) buf_st(dx1[v], rout, off + 4 * v);
+      return;
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dot = fmaf(nw1[v] * dx1[v], N.h1.v[v], dot);
+    dot = group_sum<16>(dot);
+    const float rm = N.r1;
+    const float coef = rm * rm * rm / (float)D * dot;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      buf_st(nw1[v] * dx1[v] * rm - N.h1.v[v] * coef, rout, off + 4 * v);
+      cn1[v] = fmaf(dx1[v] * N.h1.v[v], rm, cn1[v]);
+    }
+  };
+
+  // ---- the step pipeline (images double-buffered; pass 1: dact image and dx tiles single, two barriers a step)
+  Raw rn;
+  Nr1 n1;
+  float dh2c[VPL], dh2n[VPL];
+  if (s0 < s1) {
+    Raw r0;
+    issue(s0, r0);
+    prepare(s0, r0, dh2c);
+  }
+  __syncthreads();       // W1^T and the first images
+  for (int s = s0; s < s1; ++s) {
+    const bool more = s + 1 < s1;
+    if (more) issue(s + 1, rn);
+    if constexpr (PASS == 1) {
+      if (NORMS) issue_n1(s, n1);
+      compute(s);
+      lds_sync();        // every wave's dact columns are in the image
+      dx_tile();
+      if (more) prepare(s + 1, rn, dh2n);
+      lds_sync();        // the dx tiles and the next images are complete
+      epilogue(s, dh2c, n1);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dh2c[v] = dh2n[v];
+    } else {
+      compute(s);
+      if (more) prepare(s + 1, rn, dh2n);
+      lds_sync();        // the next images are complete; this step's are free
+    }
+  }
+
+  // ---- the workgroup's slab row, written once
+  float* slab = a.slab + (long)blockIdx.x * a.ld_slab;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int f0 = fw + 16 * t;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (PASS == 1) slab[a.o_w1 + (long)(f0 + 4 * g + r) * D + 16 * j + c] = dwa[t][j][r];
+        else slab[a.o_w2 + (long)(16 * j + 4 * g + r) * FF + f0 + c] = dwa[t][j][r];
+      }
+    if constexpr (PASS == 1) {
+      float v = db1[t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      if (g == 0) slab[a.o_b1 + f0 + c] = v;
+    }
+  }
+  if constexpr (PASS == 1 && NORMS) {
+    // column sums of the norm weights / db2: lanes of one column (4 per wave, 8 waves), fixed order
+    __syncthreads();
+    float* red = (float*)(lds + T::O_DA);   // [wave][3][D]
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      float q[3] = {cb2[v], cn2[v], cn1[v]};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        q[k] += __shfl_xor(q[k], 16, 64);
+        q[k] += __shfl_xor(q[k], 32, 64);
+        if (g == 0) red[(w * 3 + k) * D + c0 + v] = q[k];
+      }
+    }
+    __syncthreads();
+    if (tid < 3 * D) {
+      const int k = tid / D, col = tid % D;
+      float sum = 0.f;
+#pragma unroll
+      for (int src = 0; src < T::NW; ++src) sum += red[(src * 3 + k) * D + col];
+      slab[(k == 0 ? a.o_b2 : k == 1 ? a.o_n2 : a.o_n1) + col] = sum;
+    }
+  }
+}
+
+// the owner-form shapes: D = 32 (one pass) and D = 64 (two passes, ffn_bwd_own64_kernel), FF = 128 NT, NT <= 3
 static int ffn_own_nt(int D, int FF) {
-  if (D != 32 || FF % 128 != 0) return 0;
+  if ((D != 32 && D != 64) || FF % 128 != 0) return 0;
   const int nt = FF / 128;
-  if (nt < 1 || nt > 3) return 0;      // NT = 4 spills at 256 VGPRs
-  static const bool off = [] {
-    const char* e = getenv("CTR_FFN_BWD_LEGACY");
-    return e && *e && *e != '0';
-  }();
-  return off ? 0 : nt;
+  return nt >= 1 && nt <= 3 ? nt : 0;     // NT = 4 spills at 256 VGPRs
 }
 static int ffn_own_steps_per_wg(long M) {
   const long ns = (M + 31) / 32;
@@ -1894,21 +2206,35 @@ static int ffn_own_grid(long M) {
 }
 
 template <int D, int NT>
-static void launch_ffn_own(const FfnArgs& a0, hipStream_t s) {
-  FfnArgs a = a0;
-  static const int dbg = [] {
-    const char* e = getenv("CTR_FFN_DEBUG");
-    return e ? atoi(e) : 0;
-  }();
-  a.dbg = dbg;
+static void launch_ffn_own(const FfnArgs& a, hipStream_t s) {
   const int per = ffn_own_steps_per_wg(a.M), grid = ffn_own_grid(a.M);
   const bool drop = a.drop.thresh != 0;
-  if (a.dy) {
-    if (drop) ffn_bwd_own_kernel<D, NT, true, true><<<grid, 512, 0, s>>>(a, per);
-    else ffn_bwd_own_kernel<D, NT, true, false><<<grid, 512, 0, s>>>(a, per);
-  } else {
-    if (drop) ffn_bwd_own_kernel<D, NT, false, true><<<grid, 512, 0, s>>>(a, per);
-    else ffn_bwd_own_kernel<D, NT, false, false><<<grid, 512, 0, s>>>(a, per);
+  if constexpr (D == 32) {
+    if (a.dy) {
+      if (drop) ffn_bwd_own_kernel<D, NT, true, true><<<grid, 512, 0, s>>>(a, per);
+      else ffn_bwd_own_kernel<D, NT, true, false><<<grid, 512, 0, s>>>(a, per);
+    } else {
+      if (drop) ffn_bwd_own_kernel<D, NT, false, true><<<grid, 512, 0, s>>>(a, per);
+      else ffn_bwd_own_kernel<D, NT, false, false><<<grid, 512, 0, s>>>(a, per);
+    }
+  } else {      // D = 64: pass 1 (dW1, db1, dx / dh1, norm columns), then pass 2 (dW2) into the same slab rows
+    if (a.dy) {
+      if (drop) {
+        ffn_bwd_own64_kernel<NT, 1, true, true><<<grid, 512, 0, s>>>(a, per);
+        ffn_bwd_own64_kernel<NT, 2, true, true><<<grid, 512, 0, s>>>(a, per);
+      } else {
+        ffn_bwd_own64_kernel<NT, 1, true, false><<<grid, 512, 0, s>>>(a, per);
+        ffn_bwd_own64_kernel<NT, 2, true, false><<<grid, 512, 0, s>>>(a, per);
+      }
+    } else {
+      if (drop) {
+        ffn_bwd_own64_kernel<NT, 1, false, true><<<grid, 512, 0, s>>>(a, per);
+        ffn_bwd_own64_kernel<NT, 2, false, true><<<grid, 512, 0, s>>>(a, per);
+      } else {
+        ffn_bwd_own64_kernel<NT, 1, false, false><<<grid, 512, 0, s>>>(a, per);
+        ffn_bwd_own64_kernel<NT, 2, false, false><<<grid, 512, 0, s>>>(a, per);
+      }
+    }
   }
 }
 
@@ -1978,9 +2304,9 @@ static void launch_ffn_bf(const FfnArgs& a, bool bwd, hipStream_t s) {
   }
   if (const int nt = ffn_own_nt(D, a.FF)) {
     switch (nt) {
-      case 1: launch_ffn_own<32, 1>(a, s); return;
-      case 2: launch_ffn_own<32, 2>(a, s); return;
-      default: launch_ffn_own<32, 3>(a, s); return;
+      case 1: launch_ffn_own<D, 1>(a, s); return;
+      case 2: launch_ffn_own<D, 2>(a, s); return;
+      default: launch_ffn_own<D, 3>(a, s); return;
     }
   }
   const int grid = ffn_bf_grid(a.M, D);
