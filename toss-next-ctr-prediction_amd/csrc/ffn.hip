@@ -2008,18 +2008,19 @@ __global__ __launch_bounds__(512) void ffn_bwd_own64_kernel(FfnArgs a, int steps
   // the step's products: pass 1 -> dW1 / db1 and the dact image; pass 2 -> dW2
   auto compute = [&](int s) {
     const char* img = lds + (s & 1) * T::IMG;
-    bf16x8 xa[2][KH], ha[PASS == 1 ? 2 : 1][KH];
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int kh = 0; kh < KH; ++kh) {
-        const int o = (16 * b + c) * T::XRS + (32 * kh + 8 * g) * 2;
-        xa[b][kh] = *(const bf16x8*)(img + T::O_XB + o);
-        if constexpr (PASS == 1) ha[b][kh] = *(const bf16x8*)(img + T::O_HB + o);
-      }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int f0 = fw + 16 * t;
+      // the A rows are re-read per column tile (registers: a wave holds its W1 / W2^T slices and dW1)
+      bf16x8 xa[2][KH], ha[PASS == 1 ? 2 : 1][KH];
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh) {
+          const int o = (16 * b + c) * T::XRS + (32 * kh + 8 * g) * 2;
+          xa[b][kh] = *(const bf16x8*)(img + T::O_XB + o);
+          if constexpr (PASS == 1) ha[b][kh] = *(const bf16x8*)(img + T::O_HB + o);
+        }
       f32x4 pre[2], dfo[2];
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
