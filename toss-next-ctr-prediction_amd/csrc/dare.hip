@@ -294,28 +294,34 @@ __global__ void pos_bias_mean_kernel(const float* __restrict__ rel, int H, int n
   }
 }
 
-// drel[d, h] = (sum_p part[p, d]) / H ; one workgroup per distance d, fixed-order block reduction
 // drel[d, h] = (sum_p part[p, d]) / H for every head h (the head-mean bias), in two passes over the
-// (nparts, n) partials: pass 1, block (column d, row split s) sums rows [s*PB_ROWS, ...) of column d in a
-// fixed order and writes the sum over the split's first row, column d (that block is the only reader /
-// writer of that column in those rows: the partials are scratch); pass 2 sums the splits in order.
-constexpr int PB_ROWS = 512;
-__global__ __launch_bounds__(256) void pos_bias_grad_part(float* __restrict__ part, int nparts, int n) {
-  __shared__ float red[4];
-  const int d = blockIdx.x, p0 = blockIdx.y * PB_ROWS, p1 = min(nparts, p0 + PB_ROWS);
-  float s = 0.f;
-  for (int p = p0 + threadIdx.x; p < p1; p += 256) s += part[(long)p * n + d];
-  s = block_sum(s, red);
-  if (threadIdx.x == 0) part[(long)p0 * n + d] = s;
+// (nparts, n) partials: pass 1, block s sums its PB_ROWS consecutive rows, a thread per column (coalesced row
+// reads, the rows' loads issued together, summed in row order) and writes the sums over the block's first row
+// (that block is the only reader / writer of those rows: the partials are scratch); pass 2, a block per column d
+// sums the blocks' rows in a fixed-order block reduction.  (A block per column over all rows read the column
+// at a 4n-byte stride: 25 us per call at cfg2.)
+constexpr int PB_ROWS = 32;
+__global__ __launch_bounds__(128) void pos_bias_grad_part(float* __restrict__ part, int nparts, int n) {
+  const int p0 = blockIdx.x * PB_ROWS, np = min(nparts - p0, PB_ROWS);
+  for (int d = threadIdx.x; d < n; d += 128) {
+    float v[PB_ROWS];
+#pragma unroll
+    for (int k = 0; k < PB_ROWS; ++k) v[k] = k < np ? part[(long)(p0 + k) * n + d] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < PB_ROWS; ++k) s += v[k];
+    part[(long)p0 * n + d] = s;
+  }
 }
 
 __global__ __launch_bounds__(256) void pos_bias_grad_kernel(const float* __restrict__ part, int nsplit, int H, int n,
                                                             float* __restrict__ drel) {
-  const int d = blockIdx.x * 256 + threadIdx.x;
-  if (d >= n) return;
+  __shared__ float red[4];
+  const int d = blockIdx.x;
   float s = 0.f;
-  for (int k = 0; k < nsplit; ++k) s += part[(long)k * PB_ROWS * n + d];
-  for (int h = 0; h < H; ++h) drel[(long)d * H + h] = s / (float)H;
+  for (int k = threadIdx.x; k < nsplit; k += 256) s += part[(long)k * PB_ROWS * n + d];
+  s = block_sum(s, red);
+  if (threadIdx.x < H) drel[(long)d * H + threadIdx.x] = s / (float)H;
 }
 
 }  // namespace ctr
@@ -388,7 +394,7 @@ extern "C" int ctr_pos_bias_grad(float* part, int nparts, int H, int n, float* d
   if (n <= 0) return 0;
   const int nsplit = std::max(1, cdiv(nparts, PB_ROWS));
   // the partials are the attention backward's per-(sample, head group) scratch: reduced in place
-  if (nparts > 0) pos_bias_grad_part<<<dim3(n, nsplit), 256, 0, (hipStream_t)stream>>>(part, nparts, n);
-  pos_bias_grad_kernel<<<cdiv(n, 256), 256, 0, (hipStream_t)stream>>>(part, nparts > 0 ? nsplit : 0, H, n, drel);
+  if (nparts > 0) pos_bias_grad_part<<<nsplit, 128, 0, (hipStream_t)stream>>>(part, nparts, n);
+  pos_bias_grad_kernel<<<n, 256, 0, (hipStream_t)stream>>>(part, nparts > 0 ? nsplit : 0, H, n, drel);
   return check_launch("pos_bias_grad");
 }
