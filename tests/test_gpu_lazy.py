@@ -196,11 +196,13 @@ def test_touch_first_chunk_full_class_plus_hot_row():
 
 
 @pytest.mark.parametrize("ema", [True, False])
-def test_cat_flush_classified_equals_row_group_kernel(ema, monkeypatch):
-    """ctr_lazy_flush (lazy_flush_cls_kernel: classified row lists, four elements per lane) against the
-    per-row-group kernel it replaced (CTR_FLUSH_LEGACY=1, checked bitwise against the dense stream above), on a
-    synthetic state over every lane layout: widths 1..64 with rows that are and are not 16-byte aligned, rows
-    current / never stepped / stepped at random ticks, ticks without the AdamW step or without the EMA."""
+def test_cat_flush_classified_equals_touch_replay(ema):
+    """ctr_lazy_flush (lazy_flush_cls_kernel: classified row lists, four elements per lane, the next chunk's state
+    words loaded during the current chunk's replay) against an independent replay of the same rows: ctr_lazy_touch
+    over EVERY key (lazy_touch_kernel: an 8-lane group per row, replay_rows_wave; itself checked bitwise against
+    the dense stream through the model tests above), on a synthetic state over every lane layout: widths 1..64
+    with rows that are and are not 16-byte aligned, rows current / never stepped / stepped at random ticks, ticks
+    without the AdamW step or without the EMA.  Bitwise."""
     from tossctr import _lib
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev).cuda_stream
@@ -235,18 +237,21 @@ def test_cat_flush_classified_equals_row_group_kernel(ema, monkeypatch):
         po += r * w
         ro += r
     tabs = torch.from_numpy(np.frombuffer(bytes(arr), dtype=np.uint8).copy()).to(dev)
+    keys = torch.arange(nrows, dtype=torch.int32, device=dev)
 
-    def flush(legacy):
-        monkeypatch.setenv("CTR_FLUSH_LEGACY", "1" if legacy else "0")
+    def run(flush):
         last.copy_(last0)
         P, M, V, E = P0.clone(), M0.clone(), V0.clone(), E0.clone() if ema else None
-        _lib.call("ctr_lazy_flush", tabs.data_ptr(), len(widths), max(rows), P.data_ptr(), M.data_ptr(),
-                  V.data_ptr(), E.data_ptr() if ema else None, hist.data_ptr(), T, st)
+        args = (P.data_ptr(), M.data_ptr(), V.data_ptr(), E.data_ptr() if ema else None, hist.data_ptr(), T, st)
+        if flush:
+            _lib.call("ctr_lazy_flush", tabs.data_ptr(), len(widths), max(rows), *args)
+        else:
+            _lib.call("ctr_lazy_touch", tabs.data_ptr(), len(widths), keys.data_ptr(), nrows, 1, 2, *args)
         torch.cuda.synchronize()
         return P, M, V, E, last.clone()
 
-    ref = flush(True)
-    got = flush(False)
+    ref = run(False)
+    got = run(True)
     for name, a, b in zip("PMVE", ref[:4], got[:4]):
         if a is not None:
             assert torch.equal(a.view(torch.int32), b.view(torch.int32)), (name, int((a != b).sum()))

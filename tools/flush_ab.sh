@@ -1,5 +1,5 @@
 #!/bin/bash
-# flush A/B inside the 20-step bench: rounds of (default, CTR_FLUSH_LEGACY=1, exp libs...), flush_ms per run
+# flush A/B inside the 20-step bench: rounds of (default, exp libs...), flush_ms per run
 # usage: tools/flush_ab.sh rounds name...
 set -e
 rounds=$1; shift
@@ -9,7 +9,6 @@ run() {  # label env...
   echo "$label $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/fab.log) $(grep -o '"flush_ms": [0-9.]*' gpurun_out/fab.log)"
 }
 for i in $(seq 1 "$rounds"); do
-  run base CTR_FLUSH_LEGACY=0
-  run legacy CTR_FLUSH_LEGACY=1
+  run base X=0
   for v in "$@"; do run "$v" CTR_LIB_PATH=exp/lib_$v.so; done
 done

@@ -329,75 +329,6 @@ __global__ __launch_bounds__(256) void lazy_update_kernel(const ctr_lazy_tab_t* 
   if (live && l8 == 0) tb.last[row] = tick | LAST_NZ;
 }
 
-// lanes per row for a table in the flush: enough that a lane holds <= LQ elements, as few as possible
-__device__ __forceinline__ int flush_lg(int width) {
-  const int need = (width + LQ - 1) / LQ;
-  return need <= 1 ? 1 : need <= 2 ? 2 : need <= 4 ? 4 : 8;
-}
-
-// Persistent grid over (table, chunk of 256/lg rows) work items.  Per chunk everything (table, lg, nq)
-// is workgroup-uniform; every lane enters the wave replay (rows past the table or already current are
-// dead lanes), whose tick loop is wave-uniform.  The chunk's rows are first ordered zero-moment rows
-// first, stepped rows last (LDS), so a wave's rows are of one kind and take the short or the full replay
-// -- in table order a wave almost always held a stepped row and ran the full replay for all of them.
-#ifdef LZ_WPE
-#define LZ_OCC __attribute__((amdgpu_waves_per_eu(LZ_WPE)))
-#else
-#define LZ_OCC
-#endif
-__global__ __launch_bounds__(256) LZ_OCC void lazy_flush_kernel(const ctr_lazy_tab_t* __restrict__ tabs, int ntabs,
-                                                         float* P, float* M, float* V, float* E,
-                                                         const OptScalars* __restrict__ hist, int tick) {
-  __shared__ long chunk0[FLUSH_MAXTABS + 1];
-  __shared__ int ord_row[256], ord_w[256], n_lo, n_hi;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    long c = 0;
-    for (int t = 0; t < ntabs; ++t) {
-      chunk0[t] = c;
-      c += cdiv(tabs[t].rows, 256 / flush_lg(tabs[t].width));
-    }
-    chunk0[ntabs] = c;
-  }
-  __syncthreads();
-  const long nchunks = chunk0[ntabs];
-  for (long c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    int a = 0, b = ntabs;
-    while (b - a > 1) {
-      const int mid = (a + b) >> 1;
-      if (chunk0[mid] <= c) a = mid; else b = mid;
-    }
-    const ctr_lazy_tab_t tb = tabs[a];
-    const int lg = flush_lg(tb.width);
-    const int nrow = 256 / lg;
-    const long row0 = (c - chunk0[a]) * nrow;
-    if (tid == 0) n_lo = n_hi = 0;
-    __syncthreads();
-    if (tid < nrow) {
-      const long rr = row0 + tid;
-      const int wr = rr < tb.rows ? tb.last[rr] : tick;
-      const int pos = (wr & LAST_NZ) ? nrow - 1 - atomicAdd(&n_hi, 1) : atomicAdd(&n_lo, 1);
-      ord_row[pos] = tid;
-      ord_w[pos] = wr;
-    }
-    __syncthreads();
-    const long row = row0 + ord_row[tid / lg];
-    const bool in = row < tb.rows;
-    const int w = in ? ord_w[tid / lg] : tick;
-    const int s = ltick(w);
-    const bool nzr = (w & LAST_NZ) != 0;
-    const bool live = in && s < tick;
-    const int l = tid & (lg - 1);
-    const RowPtrs r = row_ptrs(tb, in ? row : 0, P, M, V, E);
-    if ((tb.width & 7) == 0 && (tb.p_off & 3) == 0)     // block-uniform
-      replay_rows_wave<true>(r.p, r.m, r.v, r.e, tb.width, l, lg, LQ, live, s, nzr, hist, tick);
-    else
-      replay_rows_wave<false>(r.p, r.m, r.v, r.e, tb.width, l, lg, cdiv(tb.width, lg), live, s, nzr, hist, tick);
-    if (live && l == 0) tb.last[row] = tick | (w & LAST_NZ);
-    __syncthreads();      // the order arrays are refilled by the next chunk
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 // DARE table pair (emb_att, emb_rep): both are read for the same tokens and get gradients for the
 // same keys, so a token's att row and rep row always share their last-applied tick.  One WAVE per
@@ -654,7 +585,7 @@ __device__ __forceinline__ void replay_pair_list(const ctr_lazy_tab_t& ta, const
   constexpr int LPP = 2 * LPT;             // lanes per row pair
   constexpr int PPS = 64 / LPP;            // row pairs per slot
 #ifndef PAIR_NS0
-#define PAIR_NS0 2
+#define PAIR_NS0 4
 #endif
 #ifndef PAIR_NS1
 #define PAIR_NS1 2
@@ -755,15 +686,21 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy
   const ctr_lazy_tab_t ta = tabs[0], tb = tabs[1];
   const int tid = threadIdx.x;
   const long rows = ta.rows;
-  for (long r0 = (long)blockIdx.x * CLS_CH; r0 < rows; r0 += (long)gridDim.x * CLS_CH) {
-    if (tid < NL) cnt[tid] = 0;
-    __syncthreads();
-    int wv[CLS_CH / 256];
+  const long step = (long)gridDim.x * CLS_CH;
+  // the state words of a chunk are loaded while the previous chunk replays (a memory round trip per chunk
+  // otherwise sat between the list barriers with nothing else in flight)
+  int wv[CLS_CH / 256];
+  auto load_words = [&](long r0) {
 #pragma unroll
     for (int q = 0; q < CLS_CH / 256; ++q) {
       const long r = r0 + tid + 256 * q;
       wv[q] = r < rows ? ta.last[r] : tick;
     }
+  };
+  load_words((long)blockIdx.x * CLS_CH);
+  for (long r0 = (long)blockIdx.x * CLS_CH; r0 < rows; r0 += step) {
+    if (tid < NL) cnt[tid] = 0;
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < CLS_CH / 256; ++q) {
       const int st = ltick(wv[q]);
@@ -776,6 +713,7 @@ __global__ __launch_bounds__(256) void lazy_flush_pair_cls_kernel(const ctr_lazy
       }
     }
     __syncthreads();
+    if (r0 + step < rows) load_words(r0 + step);
     if (CL <= 0) replay_pair_list<W, 0>(ta, tb, lrow[0], ls[0], cnt[0], P, M, V, E, hist, tick, true);
     if (CL != 0) replay_pair_list<W, 1>(ta, tb, lrow[NL - 1], ls[NL - 1], cnt[NL - 1], P, M, V, E, hist, tick, true);
     __syncthreads();      // the lists are refilled by the next iteration
@@ -927,7 +865,7 @@ __device__ __forceinline__ int cls_lpr(int width) {
 }
 
 #ifndef FLUSH_NS0
-#define FLUSH_NS0 2
+#define FLUSH_NS0 4
 #endif
 #ifndef FLUSH_NS1
 #define FLUSH_NS1 2
@@ -955,22 +893,37 @@ __global__ __launch_bounds__(256) void lazy_flush_cls_kernel(const ctr_lazy_tab_
   }
   __syncthreads();
   const long nchunks = chunk0[ntabs];
-  for (long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  // chunk -> (table, first row); the state words of a chunk are loaded while the previous chunk replays
+  auto locate = [&](long ch, int& ti, long& r0) {
     int a = 0, b = ntabs;
     while (b - a > 1) {
       const int mid = (a + b) >> 1;
       if (chunk0[mid] <= ch) a = mid; else b = mid;
     }
-    const ctr_lazy_tab_t tb = tabs[a];
-    const long r0 = (ch - chunk0[a]) * CLS_CH;
-    if (tid == 0) cnt = 0;
-    __syncthreads();
-    int wv[CLS_CH / 256];
+    ti = a;
+    r0 = (ch - chunk0[a]) * CLS_CH;
+  };
+  int wv[CLS_CH / 256];
+  auto load_words = [&](long ch) {
+    int ti;
+    long r0;
+    locate(ch, ti, r0);
+    const long trows = tabs[ti].rows;
+    const int* last = tabs[ti].last;
 #pragma unroll
     for (int q = 0; q < CLS_CH / 256; ++q) {
       const long r = r0 + tid + 256 * q;
-      wv[q] = r < tb.rows ? tb.last[r] : tick;
+      wv[q] = r < trows ? last[r] : tick;
     }
+  };
+  if (blockIdx.x < nchunks) load_words(blockIdx.x);
+  for (long ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    int ti;
+    long r0;
+    locate(ch, ti, r0);
+    const ctr_lazy_tab_t tb = tabs[ti];
+    if (tid == 0) cnt = 0;
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < CLS_CH / 256; ++q) {
       const int st = ltick(wv[q]);
@@ -982,6 +935,7 @@ __global__ __launch_bounds__(256) void lazy_flush_cls_kernel(const ctr_lazy_tab_
     }
     __syncthreads();
     const int n = cnt;
+    if (ch + gridDim.x < nchunks) load_words(ch + gridDim.x);
     if (n > 0) {
       constexpr int NS = CL ? FLUSH_NS1 : FLUSH_NS0;
       const bool vec = (tb.width & 3) == 0 && (tb.p_off & 3) == 0;    // block-uniform
@@ -1116,16 +1070,10 @@ extern "C" int ctr_lazy_flush(const ctr_lazy_tab_t* tabs, int ntabs, long max_ro
                               float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(ntabs <= FLUSH_MAXTABS, "ctr_lazy_flush: too many tables");
   if (ntabs <= 0 || tick <= 0 || max_rows <= 0) return 0;
-  const char* lg = getenv("CTR_FLUSH_LEGACY");   // read per call (one flush per sync): tests compare both kernels
-  if (lg && atoi(lg) != 0)   // the per-row-group kernel, kept for A/B
-    lazy_flush_kernel<<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist, tick);
-  else
-  {
-    lazy_flush_cls_kernel<0><<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist,
-                                                                    tick);
-    lazy_flush_cls_kernel<1><<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist,
-                                                                    tick);
-  }
+  lazy_flush_cls_kernel<0><<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist,
+                                                                  tick);
+  lazy_flush_cls_kernel<1><<<2048, 256, 0, (hipStream_t)stream>>>(tabs, ntabs, P, M, V, E, (const OptScalars*)hist,
+                                                                  tick);
   return check_launch("lazy_flush");
 }
 
@@ -1181,9 +1129,6 @@ extern "C" int ctr_lazy_update_pair(const ctr_lazy_tab_t* tabs, int width, const
   return check_launch("lazy_update_pair");
 }
 
-#ifndef PAIR_SPLIT
-#define PAIR_SPLIT 0
-#endif
 extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long rows, float* P, float* M, float* V,
                                    float* E, const void* hist, int tick, void* stream) {
   CTR_REQUIRE(pair_ok(tabs) && width >= 1 && width <= 64, "ctr_lazy_flush_pair: two tables of width <= 64");
@@ -1192,46 +1137,11 @@ extern "C" int ctr_lazy_flush_pair(const ctr_lazy_tab_t* tabs, int width, long r
   const OptScalars* h = (const OptScalars*)hist;
   hipStream_t s = (hipStream_t)stream;
   switch (width) {      // the classified flush for the widths whose rows split into float4 lanes
-    case 4:
-      if (PAIR_SPLIT) {
-        lazy_flush_pair_cls_kernel<4, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-        lazy_flush_pair_cls_kernel<4, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      } else {
-        lazy_flush_pair_cls_kernel<4, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      }
-      return check_launch("lazy_flush_pair");
-    case 8:
-      if (PAIR_SPLIT) {
-        lazy_flush_pair_cls_kernel<8, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-        lazy_flush_pair_cls_kernel<8, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      } else {
-        lazy_flush_pair_cls_kernel<8, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      }
-      return check_launch("lazy_flush_pair");
-    case 16:
-      if (PAIR_SPLIT) {
-        lazy_flush_pair_cls_kernel<16, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-        lazy_flush_pair_cls_kernel<16, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      } else {
-        lazy_flush_pair_cls_kernel<16, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      }
-      return check_launch("lazy_flush_pair");
-    case 32:
-      if (PAIR_SPLIT) {
-        lazy_flush_pair_cls_kernel<32, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-        lazy_flush_pair_cls_kernel<32, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      } else {
-        lazy_flush_pair_cls_kernel<32, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      }
-      return check_launch("lazy_flush_pair");
-    case 64:
-      if (PAIR_SPLIT) {
-        lazy_flush_pair_cls_kernel<64, 0><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-        lazy_flush_pair_cls_kernel<64, 1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      } else {
-        lazy_flush_pair_cls_kernel<64, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick);
-      }
-      return check_launch("lazy_flush_pair");
+    case 4: lazy_flush_pair_cls_kernel<4, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 8: lazy_flush_pair_cls_kernel<8, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 16: lazy_flush_pair_cls_kernel<16, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 32: lazy_flush_pair_cls_kernel<32, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
+    case 64: lazy_flush_pair_cls_kernel<64, -1><<<cgrid, 256, 0, s>>>(tabs, P, M, V, E, h, tick); return check_launch("lazy_flush_pair");
     default: break;
   }
   if (width <= 32)
