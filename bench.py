@@ -76,9 +76,10 @@ def kernel_work(name, a, B, ffn_M):
     figures x the units one launch processes ("Roofline accounting").
     FFN: the four products (8 FF D flop per row backward, 4 forward; the backward's pre-activation
     recompute not counted).  Attention core (src/models/dare.py:39-70, MHA over K candidates, dh = D / H):
-    per (sample, head) QK^T and PV = 4 K^2 dh flop forward; dP = dO V^T, dV = P^T dO, dQ = dS K,
-    dK = dS^T Q = 8 K^2 dh backward (the score recompute not counted), on the fp32 vector units (dh = 4 / 8
-    is too thin for MFMA tiles) -> priced against the fp32 vector peak."""
+    amp none -- the fp32 VALU kernels (attn.hip): per (sample, head) QK^T and PV = 4 K^2 dh flop forward, dP, dV,
+    dQ, dK = 8 K^2 dh backward (the score recompute not counted), priced against the fp32 vector peak; amp bf16
+    -- the bf16-MFMA kernels (attn_mf.hip), whose products are a few % of the bf16 peak: priced against HBM by
+    the bytes each launch must move (below)."""
     D, FF = a.D, a.ffn_hidden
     if name in ("ctr_ffn_bwd", "ctr_ffn_bwd_norms"):     # dfo = dh W2, dW2 = dh^T fo, dW1 = dact^T x, dx = dact W1 (pre recompute excluded)
         return "mfma", 8.0 * ffn_M * FF * D, "flop"
@@ -91,17 +92,20 @@ def kernel_work(name, a, B, ffn_M):
         return "valu", 8.0 * B * K * K * D, "flop"
     # amp: the bf16-MFMA attention (attn_mf.hip) -- its products take a few % of the bf16 MFMA peak, so its
     # roofline is HBM: per (sample, candidate) row the fp32 qkv read (12 D B), o write (4 D), row max / sum
-    # (8 H) and keep bits (8 H: 2 words per head per 64-row tile, 128 per head over <= 64 rows); the backward
+    # (8 H); per (sample, head) the keep bits in the kernels' lane layout, 64 lanes x NW words (NW = 2 for
+    # nt = ceil(K / 16) <= 4 tiles a side: 512 B; ceil(4 nt^2 / 32) beyond: 3.3 KB at K = 148); the backward
     # reads qkv, o, dO (20 D), the row stats and bits, and writes dqkv (12 D)
     H = a.H
+    nt = (K + 15) // 16
+    mask = B * H * 64 * 4 * (2 if nt <= 4 else (4 * nt * nt + 31) // 32)
     if name == "ctr_attn_fwd_bf":
-        return "hbm", float(B * K * (16 * D + 8 * H) + B * H * 512), "B"
+        return "hbm", float(B * K * (16 * D + 8 * H) + mask), "B"
     if name in ("ctr_attn_bwd_bf", "ctr_attn_bwd_bf_oproj"):     # _oproj reads dh1 rows in place of dO
-        return "hbm", float(B * K * (32 * D + 8 * H) + B * H * 512), "B"
+        return "hbm", float(B * K * (32 * D + 8 * H) + mask), "B"
     # the fused layer forward (in_proj -> attention -> out_proj + residual + RMSNorm, attn_mf.hip): reads x (4 D)
     # and writes qkv (12 D), o (4 D), h1 and x1 (8 D), r1 (4), the row stats (8 H) and the keep bits per row
     if name == "ctr_attn_layer_fwd_bf":
-        return "hbm", float(B * K * (28 * D + 4 + 8 * H) + B * H * 512), "B"
+        return "hbm", float(B * K * (28 * D + 4 + 8 * H) + mask), "B"
     return None
 
 
@@ -143,23 +147,47 @@ def per_sample_bytes(a, L):
     return inp + 12 * (L * a.D + a.K_eff(L) * a.D + sum(a.cat_dims))
 
 
-def step_bytes_lazy(a, B, L, opt, U, timed_steps, with_ema):
+def lazy_row_classes(opt):
+    """Per table (key, rows, width, rows that have taken a gradient tick): bit 31 of a row's lazy state word
+    (csrc/lazy.hip LAST_NZ) -- such a row's replay moves p, m, v (, e); a row without it has zero moments and
+    moves p (, e) only.  Read after the run's flush (the flush leaves the bit alone)."""
+    ar = opt.arena
+    keys = ["dare.emb_att.weight", "dare.emb_rep.weight"] + [f"cat_embs.{c}.weight" for c in opt.engine.a.cat_names]
+    out, r0 = [], 0
+    for k in keys:
+        rows, width = ar.shapes[k]
+        nz = int((opt.last[r0:r0 + rows] < 0).sum().item())
+        out.append((k, rows, width, nz))
+        r0 += rows
+    return out
+
+
+def step_bytes_lazy(a, B, L, opt, U, timed_steps, with_ema, classes):
     """Algorithmic HBM bytes of one step of THIS build (exact-lazy tables, SURVEY §8(d) row-lazy form,
-    with U measured in the run): B x per-sample term; the dense-parameter stream (read p, m, v, (e), grad,
-    write p, m, v, (e)); the forward's touch of the rows the batch reads (a row is brought current once:
-    read + write p, m, v, (e)); the real tick on the rows that get a gradient (same + the compact grad
-    row); and the run's final flush of every table row (same per element) spread over the timed steps.
+    with U measured in the run), at what each kind of row must move (fp32; with EMA):
+      * stepped rows (a gradient tick taken: non-zero moments) read + write p, m, v, e = 32 B per element;
+      * zero-moment rows (never stepped) read + write p and e only = 16 B (idle ticks keep m, v at +0);
+    B x per-sample term; the dense-parameter stream (read p, m, v, (e), grad, write p, m, v, (e)); the forward's
+    touch of the rows the batch reads (each brought current once); the real tick on the rows that get a gradient
+    (read the row's class, write p, m, v, e, read the compact grad row); and the run's final flush of every
+    table row by its class (``classes``, lazy_row_classes) plus its state word (read + write), spread over the
+    timed steps.  The touch / update rows are split by the fraction of stepped rows of their table group.
     U = {"seq_fwd": unique tokens read, "seq_bwd": unique top-K tokens (both DARE tables),
     "cat_fwd"/"cat_bwd": unique (table, row) floats} -- rows, or floats for cat (sum of d_c)."""
     ar = opt.arena
-    st = 32 if with_ema else 24          # p, m, v (, e) read + written, fp32
+    full = 32 if with_ema else 24        # p, m, v (, e) read + written, fp32
+    zero = 16 if with_ema else 8         # p (, e) read + written
     lo, hi = ar.nograd_range
-    dense = ar.n_dense_grad * (st + 4) + ((hi - lo) * 12 if with_ema else 0)
+    dense = ar.n_dense_grad * (full + 4) + ((hi - lo) * 12 if with_ema else 0)
     D = a.D
-    touch = (2 * U["seq_fwd"] * D + U["cat_fwd"]) * st
-    update = (2 * U["seq_bwd"] * D + U["cat_bwd"]) * (st + 4)
-    t0, t1 = ar.table_range
-    flush = (t1 - t0) * st / max(1, timed_steps)
+    seq = [c for c in classes if ".emb_" in c[0]]
+    cat = [c for c in classes if c[0].startswith("cat_embs.")]
+    f_seq = sum(c[3] for c in seq) / max(1, sum(c[1] for c in seq))
+    f_cat = sum(c[3] * c[2] for c in cat) / max(1, sum(c[1] * c[2] for c in cat))
+    mix = lambda f: f * full + (1 - f) * zero                                                 # noqa: E731
+    touch = 2 * U["seq_fwd"] * D * mix(f_seq) + U["cat_fwd"] * mix(f_cat)
+    update = (2 * U["seq_bwd"] * D * (mix(f_seq) / 2 + full / 2 + 4) + U["cat_bwd"] * (mix(f_cat) / 2 + full / 2 + 4))
+    flush = sum(nz * w * full + (rows - nz) * w * zero + 8 * rows for _, rows, w, nz in classes) / max(1, timed_steps)
     return {"per_sample": B * per_sample_bytes(a, L), "dense_opt": dense, "touch": touch, "update": update,
             "flush": flush}
 
@@ -446,8 +474,10 @@ def main():
         opt.time_kernels(False)
         kstats = _lib.timed_ms()
         _lib.time_calls(())
-    # U of the exact-lazy byte count: the unique rows of the last timed step's batch and gradients
+    # U of the exact-lazy byte count: the unique rows of the last timed step's batch and gradients; the tables'
+    # row classes (stepped / zero-moment) for the flush bytes
     U = measure_unique(model, data[(g - 1) % nb][0], model.engine.tg) if world == 1 else None
+    classes = lazy_row_classes(opt) if world == 1 and not args.dense_opt else None
     if pg is not None:
         t = torch.tensor([elapsed], device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -511,17 +541,18 @@ def main():
             "table_update": "dense stream" if args.dense_opt else "exact lazy (replay on read/grad; final flush timed)",
             "flush_ms": round(flush_ms, 3),
         }
-        # whole-step figures: FLOPs of the matrix products against the fp32 MFMA peak; HBM bytes of this
-        # build's exact-lazy step (U measured above) against 8 TB/s; the dense-equivalent bytes of the
-        # reference semantics only for comparison with a dense implementation's ceiling
+        # whole-step figures: FLOPs of the matrix products against the MFMA peak of the run's dtype (bf16 under
+        # amp: bf16; the fp32 figure beside it); HBM bytes of this build's exact-lazy step (U measured above)
+        # against 8 TB/s; the dense-equivalent bytes of the reference semantics only for comparison with a dense
+        # implementation's ceiling
         flops = 3.0 * fwd_flops_per_sample(a, args.seq_len) * args.batch
+        fpeak = MFMA_BF16_PEAK_TFS if args.amp == "bf16" else MFMA_F32_PEAK_TFS
         rec["step_flops"] = {"flop_per_step": flops, "achieved": round(flops / (ms * 1e-3) / 1e12, 2),
-                             "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                             "frac": round(flops / (ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, 4)}
-        if args.amp == "bf16":     # against the bf16 peak too (attention / projections stay fp32 VALU)
-            rec["step_flops"]["frac_of_bf16_peak"] = round(flops / (ms * 1e-3) / 1e12 / MFMA_BF16_PEAK_TFS, 4)
+                             "peak": fpeak, "unit": "TFLOP/s", "peak_dtype": "bf16" if args.amp == "bf16" else "f32",
+                             "frac": round(flops / (ms * 1e-3) / 1e12 / fpeak, 4),
+                             "frac_of_fp32_peak": round(flops / (ms * 1e-3) / 1e12 / MFMA_F32_PEAK_TFS, 4)}
         if U is not None and not args.dense_opt:
-            parts = step_bytes_lazy(a, args.batch, args.seq_len, opt, U, args.steps, ema is not None)
+            parts = step_bytes_lazy(a, args.batch, args.seq_len, opt, U, args.steps, ema is not None, classes)
             tb = sum(parts.values())
             rec["step_hbm"] = {"mode": "exact-lazy row bytes (SURVEY 8(d) row-lazy form, U measured)",
                                "unique": U, "bytes": {k: int(v) for k, v in parts.items()},

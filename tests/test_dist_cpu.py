@@ -144,3 +144,14 @@ def test_shard_layout_helpers_and_cfg5_key_widths():
         assert top < (1 << sh.cat_kbits) - 1
         top = ((world - 1) << sh.seq_lbits) | (sh.seq_rows - 1)
         assert top < (1 << sh.seq_kbits) - 1
+
+
+def test_fold_parallel_assignment():
+    """dist: {mode: folds}: every fold of the K-fold split is trained by exactly one rank, round-robin."""
+    from tossctr.train import fold_owner
+    for world in (2, 3, 5, 8):
+        for n in (5, 7, 10):
+            owners = [fold_owner(f, world) for f in range(n)]
+            assert all(0 <= o < world for o in owners)
+            counts = [owners.count(r) for r in range(world)]
+            assert max(counts) - min(counts) <= 1 and sum(counts) == n

@@ -99,6 +99,45 @@ def test_kfold_loop_world2_sharded_tables(tmp_path):
     assert abs(ref - score) < 1e-6 * max(1.0, abs(ref)), (ref, score)
 
 
+def test_kfold_fold_parallel_world2_equals_single(tmp_path):
+    """dist: {mode: folds} (src/train.py:334-346): two ranks (gloo on one card) train the five
+    folds round-robin (rank 0: folds 0, 2, 4; rank 1: folds 1, 3) with no collective while training, each
+    writing its folds' checkpoints -- every fold's score and weights equal a single-process run of main(), bit
+    for bit (fold-local seeds, deterministic kernels)."""
+    import json
+    import subprocess
+    import sys
+    from tossctr.data import synth_rows, write_shard_cache
+    from tossctr.train import main
+    cols = ["c0", "c1", "c2", "c3"]
+    arr = synth_rows(2000, 6, 6, [203] * 4, 24, 3000, seed=8, pos_rate=0.2)
+    man = write_shard_cache(str(tmp_path / "cache"), arr, shard_rows=700, num_cols=[f"n{i}" for i in range(6)],
+                            cat_cols=cols, group_key="c0")
+    cfg = tiny_run_cfg(str(tmp_path / "folds"), man)
+    cfg["cv"]["n_splits"] = 5
+    cfg["train"]["epochs"] = 1
+    cfg["dist"] = {"mode": "folds"}
+    cfg_path, out = str(tmp_path / "cfg.json"), str(tmp_path / "res.json")
+    with open(cfg_path, "w") as f:
+        json.dump(cfg, f)
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "dist_train_worker.py"), cfg_path, out],
+                       capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    with open(out) as f:
+        got = {int(k): v for k, v in json.load(f).items()}
+    single = dict(cfg, logging=dict(cfg["logging"], log_dir=str(tmp_path / "single" / "runs")))
+    ref = main(single)
+    assert sorted(got) == sorted(ref) == [0, 1, 2, 3, 4]
+    for fold in ref:
+        assert got[fold] == ref[fold], (fold, got[fold], ref[fold])
+        a = torch.load(os.path.join(cfg["logging"]["log_dir"], "tiny", f"ckpt_folds_{fold}.pt"), weights_only=True)
+        b = torch.load(os.path.join(single["logging"]["log_dir"], "tiny", f"ckpt_folds_{fold}.pt"), weights_only=True)
+        for k, v in b["state"]["model"].items():
+            assert torch.equal(a["state"]["model"][k], v), (fold, k)
+    assert os.path.exists(os.path.join(cfg["logging"]["log_dir"], "tiny", "train_log_rank1.csv"))
+
+
 def test_fold_teardown_frees_device_memory(tmp_path):
     """train_one_fold releases its arena, moments, EMA shadow and workspaces before returning (the
     model <-> optimizer cycle is broken and collected, src/train.py:280-316): two folds in a row end at

@@ -2278,13 +2278,9 @@ template <int D>
 static void launch_ffn_bf(const FfnArgs& a, bool bwd, hipStream_t s) {
   const bool drop = a.drop.thresh != 0;
   if (!bwd) {
-    static const bool legacy = [] {
-      const char* e = getenv("CTR_FFN_FWD_LEGACY");
-      return e && *e && *e != '0';
-    }();
     if constexpr (D == 32) {
       const size_t sm = ffn_fwdp_lds<D>(a.FF);
-      if (!legacy && sm <= 80 * 1024) {      // two workgroups per CU
+      if (sm <= 80 * 1024) {      // two workgroups per CU
         static bool attr = false;
         if (!attr) {
           (void)hipFuncSetAttribute((const void*)ffn_fwd_bfp_kernel<D, true>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -573,7 +573,7 @@ struct GemmBfArgs {
   const __bf16* A;
   const __bf16* B;
   int mt, nt;            // tiles along M, N
-  int gm;                // grouped tile order: m-tiles per group (0: n fastest over all tiles)
+  int gm;                // tile order: -1 XCD column partition, 0 n fastest over all tiles, > 0 m-groups
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds) {
@@ -633,23 +633,38 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 128 * 64];     // [stage][A | B][128 x 64]
   const GemmArgs& g = p.g;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  // bijective XCD remap: consecutive ids (same XCD: dispatch is round-robin over 8 XCDs)
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
-  const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
   int nt_i, mt_i, z;
-  if (p.gm > 0) {
-    // grouped order: GM m-tiles fastest, then n, group by group -- the B slab of an n-tile is reused by the
-    // group's GM m-tiles while it is in the XCD's L2, and the group's A slabs stay there across n
-    const int per = p.mt * p.nt, t = id % per;
-    z = id / per;
-    const int gsz = p.gm * p.nt, grp = t / gsz, m0g = grp * p.gm, gm = min(p.mt - m0g, p.gm), u = t - grp * gsz;
-    mt_i = m0g + u % gm;
-    nt_i = u / gm;
+  if (p.gm < 0) {
+    // XCD column partition (nt >= 8): workgroups are dealt round-robin to the 8 XCDs, so XCD x runs ids x, x + 8,
+    // ... in order; it takes the n-tiles [nt x / 8, nt (x + 1) / 8) -- a B column group that stays in its L2 --
+    // for every m-tile, m slow / n fast so that consecutive tiles also share the A slab.  (n fastest over all
+    // tiles made every XCD stream all of B once per m-tile from the MALL: 241 MB of L2 fills for the QNN MLP
+    // input grad's 12 MB of operands.)
+    const int x = blockIdx.x & 7, l = blockIdx.x >> 3;
+    const int nlo = p.nt * x / 8, nw = p.nt * (x + 1) / 8 - nlo;
+    const int per = p.mt * nw;
+    z = l / per;
+    const int t = l - z * per;
+    if (z >= (int)((g.K + g.klen - 1) / g.klen)) return;    // the grid is sized for the widest XCD
+    mt_i = t / nw;
+    nt_i = nlo + t % nw;
   } else {
-    nt_i = id % p.nt;
-    const int rest = id / p.nt;
-    mt_i = rest % p.mt;
-    z = rest / p.mt;
+    // bijective XCD remap: consecutive ids (same XCD: dispatch is round-robin over 8 XCDs)
+    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+    const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+    if (p.gm > 0) {
+      // grouped order: GM m-tiles fastest, then n, group by group
+      const int per = p.mt * p.nt, t = id % per;
+      z = id / per;
+      const int gsz = p.gm * p.nt, grp = t / gsz, m0g = grp * p.gm, gm = min(p.mt - m0g, p.gm), u = t - grp * gsz;
+      mt_i = m0g + u % gm;
+      nt_i = u / gm;
+    } else {
+      nt_i = id % p.nt;
+      const int rest = id / p.nt;
+      mt_i = rest % p.mt;
+      z = rest / p.mt;
+    }
   }
   const int m0 = mt_i * 128, n0 = nt_i * 128;
   const int kz0 = z * g.klen, kz1 = min(g.K, kz0 + g.klen);
@@ -658,6 +673,9 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
   const long lda = g.lda, ldb = g.ldb;
 
   auto stage = [&](int buf, int k0) {
+#ifdef GBF_NOLOAD
+    if (k0 > 0) return;
+#endif
     __bf16* ta = smem + buf * 2 * 8192;
     __bf16* tb = ta + 8192;
     if (TA) stage_km(p.A, lda, m0, g.M, k0, ta, w, lane);
@@ -698,6 +716,9 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
     __syncthreads();
   }
 
+#ifdef GBF_NOSTORE
+  if (acc[0][0][0] != 12345.f) return;
+#endif
   const ctr_gemm_epi_t& e = g.epi;
   const int lrow = wm + (lane >> 4) * 4, lcol = wn + (lane & 15);
   if (g.ws) {   // split-K partial: raw slab, the reduce kernel applies the epilogue
@@ -895,12 +916,9 @@ extern "C" int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta
   p.B = (const __bf16*)B;
   p.mt = cdiv(M, 128);
   p.nt = cdiv(N, 128);
-  static const int gm_env = [] {
-    const char* e = getenv("CTR_GEMM_BF_GM");
-    return e ? atoi(e) : -1;
-  }();
-  p.gm = gm_env >= 0 ? gm_env : 0;      // grouped order: level in the step (4.111 vs 4.117 ms), kept for A/B
-  const int grid = p.mt * p.nt * splits;
+  // XCD column partition where there are n-tiles for every XCD (grid: the widest XCD's tiles x 8)
+  p.gm = p.nt >= 8 ? -1 : 0;
+  const int grid = p.gm < 0 ? 8 * p.mt * cdiv(p.nt, 8) * splits : p.mt * p.nt * splits;
   hipStream_t s = (hipStream_t)stream;
   if (!ta && tb) gemm_bf_kernel<false, true><<<grid, 256, 0, s>>>(p);
   else if (!ta && !tb) gemm_bf_kernel<false, false><<<grid, 256, 0, s>>>(p);

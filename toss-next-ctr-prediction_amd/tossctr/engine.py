@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import ctypes as C
 import math
-import os
 
 import numpy as np
 import torch
@@ -20,9 +19,7 @@ from . import _lib
 from ._lib import GemmEpi, call
 from .arch import QUERY_MODES, Arch
 # Side-stream issue order: the main stream's next product is queued before the side stream's grads (its
-# event wait then resolves behind queued main-stream work; 4.82 -> 4.79 ms/step).  CTR_SIDE_ORDER=legacy
-# restores the side-first order for A/B runs.
-_REORDER = os.environ.get("CTR_SIDE_ORDER", "main-first") != "legacy"
+# event wait then resolves behind queued main-stream work; 4.82 -> 4.79 ms/step).
 
 from .rng import (SITE_DARE, SITE_EMB, SITE_FC, SITE_FFN0, SITE_MLP0, SITE_QNN, SITE_ATTN0, drop_args)
 
@@ -164,7 +161,7 @@ class Engine:
         # backward side stream: weight / bias grads whose inputs are final run beside the input-grad chain
         # (one stream per engine; joined before the optimizer and before a data-parallel bucket hand-off)
         self._side = None
-        self.side_stream = os.environ.get("CTR_SIDE_STREAM", "1") != "0"   # (0: one stream, for A/B)
+        self.side_stream = True      # False: everything on the current stream (A/B experiments)
         self.stream = None
         self.last = None
         self.grad_ready = None   # data parallel: called once the head's dense grads are final (bucket 1)
@@ -188,12 +185,12 @@ class Engine:
         # reference's autocast baddbmm / bmm; other shapes keep the fp32 kernels
         self.attn_bf = bool(self.bf16 and a.n_layers > 0 and _lib.query("ctr_attn_bf_ok", a.top_k, a.H, a.D))
         # ... and the layer's in_proj -> attention -> out_proj + residual + RMSNorm in one launch where it fits
-        # (attn_mf.hip: K <= 64, D = 32; the same bits as the three launches; CTR_ATTN_LAYER=0 for A/B)
-        self.attn_layer = bool(self.attn_bf and self.rowgemm and os.environ.get("CTR_ATTN_LAYER", "1") != "0" and
+        # (attn_mf.hip: K <= 64, D = 32; the same bits as the three launches)
+        self.attn_layer = bool(self.attn_bf and self.rowgemm and
                                _lib.query("ctr_attn_layer_fwd_ok", a.top_k, a.H, a.D))
         # ... and in the backward the out-projection's input grad dO = dh1 W_out inside the attention backward
-        # (ctr_attn_bwd_bf_oproj: same bits, dO never written; CTR_ATTN_OPROJ=0 for A/B)
-        self.attn_oproj = bool(self.attn_bf and self.rowgemm and os.environ.get("CTR_ATTN_OPROJ", "1") != "0" and
+        # (ctr_attn_bwd_bf_oproj: same bits, dO never written)
+        self.attn_oproj = bool(self.attn_bf and self.rowgemm and
                                _lib.query("ctr_attn_bwd_bf_oproj_ok", a.top_k, a.H, a.D))
 
     def _tab_array(self, keys, bases):
@@ -734,9 +731,6 @@ class Engine:
              ptr(att_c), ptr(att_k), ptr(rep_k), st)
         # att and rep contributions share their keys (the top-K tokens): one sort for both, on the side
         # stream beside the context / embedding backward (its inputs are final; its own sort workspace)
-        if not _REORDER:
-            with self.side():
-                tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
         # ---------------- context / query
         mode = QUERY_MODES[a.query_mode]
         dcat = W.get("dcat", (B, a.Fc, D))
@@ -746,9 +740,8 @@ class Engine:
              B, mode, self.qi, ptr(P["ctx_mlp.0.weight"]), ptr(sv["hq"]), ptr(dq),
              ptr(dxF, cat_off) if a.use_qnn else None, FD, *dk, ptr(dfc), dfc.shape[1] if dfc is not None else 0,
              ptr(dxF, num_off), ptr(dxF, mask_off), ptr(dcat), ptr(dpre), st)
-        if _REORDER:     # the side-stream sort after the main stream's next product is queued
-            with self.side():
-                tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
+        with self.side():     # the side-stream sort after the main stream's next product is queued
+            tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
         if mode != 0:
             self.wgrad(ptr(dpre), D, ptr(sv["ctx"]), a.nctx * D, B, D, a.nctx * D, ptr(G["ctx_mlp.0.weight"]),
                        bias_grad=ptr(G["ctx_mlp.0.bias"]))
@@ -828,10 +821,6 @@ class Engine:
                  ptr(P[pre + "ffn.0.bias"]), ptr(P[pre + "ffn.3.weight"]), *dfk, ptr(Ls["fmask"]), ptr(dh1),
                  ptr(slab), ld_sl, *o, ptr(Ls["fwbf"]), self.ffn_flags, st)
             slab_sum = (ptr(slab), ld_sl, nb, n_sl, ptr(self.arena.grad, o0))
-            if not _REORDER:
-                with self.side():
-                    self.colsum(*slab_sum, defer=True)
-                slab_sum = None
         else:
             slab_sum = None
             # x2 = norm2(x1 + ffn(x1))

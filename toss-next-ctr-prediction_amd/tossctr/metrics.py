@@ -200,7 +200,7 @@ class Logger:
 
     COLS = ["fold", "epoch", "split", "loss", "AP", "WLL", "Score", "lr", "bs", "K", "tau"]
 
-    def __init__(self, log_dir, tb=True, csv_log=True, quiet=False):
+    def __init__(self, log_dir, tb=True, csv_log=True, quiet=False, csv_name="train_log.csv"):
         self.tb = None
         if tb:
             try:
@@ -209,7 +209,7 @@ class Logger:
             except Exception:
                 self.tb = None
         self.quiet = quiet
-        self.csv_path = os.path.join(log_dir, "train_log.csv") if csv_log else None
+        self.csv_path = os.path.join(log_dir, csv_name) if csv_log else None
         if self.csv_path:
             os.makedirs(log_dir, exist_ok=True)
             if not os.path.exists(self.csv_path):

@@ -11,9 +11,7 @@ ever written.
 """
 from __future__ import annotations
 
-import contextlib
 import math
-import os
 
 import numpy as np
 import torch
@@ -343,9 +341,7 @@ class FusedAdamW:
             return
         # the DARE pair and the categorical tables are disjoint rows: their flushes run side by side (both
         # are bound by memory latency and replay issue, neither fills the chip alone)
-        # (CTR_FLUSH_SERIAL=1: one after the other on the current stream, for per-kernel timing)
-        serial = os.environ.get("CTR_FLUSH_SERIAL", "0") != "0"
-        with (contextlib.nullcontext() if serial else self.engine.side()):
+        with self.engine.side():
             call("ctr_lazy_flush_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, self._seq_rows,
                  ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick,
                  self.engine.s())

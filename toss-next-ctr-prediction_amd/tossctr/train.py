@@ -15,7 +15,10 @@ MI355X differences (same results, different mechanics):
   * optional data parallelism: run under torchrun, every rank takes its own stride of each epoch's
     permutation; dense grads are all-reduced and the embedding tables row-sharded over the ranks
     (tossctr/shard.py; ``dist: {shard_tables: false}`` in the yaml keeps them replicated); validation
-    batches are spread over the ranks and their logits all-gathered.
+    batches are spread over the ranks and their logits all-gathered;
+  * or fold parallelism (``dist: {mode: folds}``): rank r trains folds r, r + W, ... of the
+    same StratifiedGroupKFold split, each exactly as a single-GPU run would (no collective while training),
+    and writes those folds' checkpoints; the scores are gathered once at the end.
 """
 from __future__ import annotations
 
@@ -62,9 +65,19 @@ def check_supported(cfg):
         raise NotImplementedError("sampler.type: balanced is not supported (no reference config enables it)")
 
 
+_FOLD_LOCAL = False      # set by main() in fold-parallel mode: training runs with no process group
+
+
 def _dist():
     import torch.distributed as dist
+    if _FOLD_LOCAL:
+        return None
     return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def fold_owner(fold: int, world: int) -> int:
+    """Fold-parallel mode: the rank that trains ``fold`` (folds dealt round-robin over the ranks)."""
+    return fold % world
 
 
 def _cardinals(cfg, cat_cols):
@@ -279,7 +292,9 @@ def train_one_fold(cfg, fold, idx_tr, idx_va, manifest_path, logger, store=None,
 
 
 def main(cfg_path_or_dict):
-    """src/train.py:319-352."""
+    """src/train.py:319-352.  Under torchrun: data parallel within each fold (default), or fold parallel with
+    ``dist: {mode: folds}`` (every rank trains its own folds, fold_owner)."""
+    global _FOLD_LOCAL
     from sklearn.model_selection import StratifiedGroupKFold
     from .data import DeviceShards, load_labels_groups_for_split
     from .metrics import Logger
@@ -293,27 +308,45 @@ def main(cfg_path_or_dict):
     set_seed(cfg["seed"], deterministic=cfg.get("deterministic", True))
     dist = _dist()
     rank = dist.get_rank() if dist else 0
+    world = dist.get_world_size() if dist else 1
+    mode = str((cfg.get("dist", {}) or {}).get("mode", "data")).lower()
+    if mode not in ("data", "folds"):
+        raise ValueError(f"dist.mode must be 'data' or 'folds', got {mode!r}")
+    folds_mode = mode == "folds" and world > 1
     device = torch.device("cuda", torch.cuda.current_device())
     out_dir = os.path.join(cfg["logging"]["log_dir"], cfg["exp_name"])
+    # fold parallel: every rank logs the folds it trains (rank > 0 to a CSV of its own: no shared appends)
     logger = Logger(out_dir, tb=cfg["logging"].get("tb", False), csv_log=cfg["logging"].get("csv_log", True),
-                    quiet=rank != 0)
+                    quiet=rank != 0 and not folds_mode,
+                    csv_name="train_log.csv" if rank == 0 or not folds_mode else f"train_log_rank{rank}.csv")
     manifest_path = cfg["data"]["manifest_train"]
     y, groups = load_labels_groups_for_split(manifest_path)
     n_splits = int(cfg["cv"]["n_splits"])
     sgkf = StratifiedGroupKFold(n_splits=max(5, n_splits), shuffle=True, random_state=cfg["seed"])
     store = DeviceShards(manifest_path, device)
     results = {}
-    for fold, (tr, va) in enumerate(sgkf.split(np.zeros_like(y), y, groups)):
-        if n_splits == 1 and fold > 0:
-            break
-        ckpt = os.path.join(out_dir, f"ckpt_folds_{fold}.pt")
-        if os.path.exists(ckpt):
-            continue
-        state, score = train_one_fold(cfg, fold, tr, va, manifest_path, logger, store=store, device=device)
-        if rank == 0:
-            os.makedirs(out_dir, exist_ok=True)
-            torch.save({"state": state, "score": float(score)}, ckpt)
-        results[fold] = score
+    _FOLD_LOCAL = folds_mode
+    try:
+        for fold, (tr, va) in enumerate(sgkf.split(np.zeros_like(y), y, groups)):
+            if n_splits == 1 and fold > 0:
+                break
+            if folds_mode and fold_owner(fold, world) != rank:
+                continue
+            ckpt = os.path.join(out_dir, f"ckpt_folds_{fold}.pt")
+            if os.path.exists(ckpt):
+                continue
+            state, score = train_one_fold(cfg, fold, tr, va, manifest_path, logger, store=store, device=device)
+            if rank == 0 or folds_mode:
+                os.makedirs(out_dir, exist_ok=True)
+                torch.save({"state": state, "score": float(score)}, ckpt)
+            results[fold] = score
+    finally:
+        _FOLD_LOCAL = False
+    if folds_mode:       # every rank returns every fold's score (the run's only collective)
+        parts = [None] * world
+        dist.all_gather_object(parts, {int(k): float(v) for k, v in results.items()})
+        results = {k: v for p in parts for k, v in p.items()}
+        results = dict(sorted(results.items()))
     return results
 
 
