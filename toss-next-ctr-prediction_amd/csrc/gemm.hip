@@ -573,7 +573,7 @@ struct GemmBfArgs {
   const __bf16* A;
   const __bf16* B;
   int mt, nt;            // tiles along M, N
-  int gm;                // tile order: -1 XCD column partition, 0 n fastest over all tiles, > 0 m-groups
+  int gm;                // tile order: -1 XCD column partition, 0 n fastest (bf_tile)
 };
 
 __device__ __forceinline__ void glds16(const void* src, void* lds) {
@@ -628,54 +628,52 @@ __device__ __forceinline__ bf16x8 frag_km(const __bf16* tile, int cb16, int ks, 
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// tile t of a workgroup's sequence -> (split z, m-tile, n-tile); false past the end.
+//   gm < 0, XCD column partition (nt >= 8): workgroups are dealt round-robin to the 8 XCDs, so XCD x runs ids
+//     x, x + 8, ...; it takes the n-tiles [nt x / 8, nt (x + 1) / 8) -- a B column group that stays in its L2 --
+//     for every m-tile, m slow / n fast, so the workgroups running at once also share a few A slabs.  (n fastest
+//     over all tiles made every XCD stream all of B once per m-tile from the MALL: 241 MB of L2 fills for the
+//     QNN MLP input grad's 12 MB of operands.)
+//   gm = 0: n fastest, then m, then z, after a bijective XCD remap, strided by the grid.
+__device__ __forceinline__ bool bf_tile(const GemmBfArgs& p, int nsplit, int t, int& z, int& mt_i, int& nt_i) {
+  if (p.gm < 0) {
+    const int x = blockIdx.x & 7, gx = gridDim.x >> 3;
+    const int nlo = p.nt * x / 8, nw = p.nt * (x + 1) / 8 - nlo;
+    const int idx = (blockIdx.x >> 3) + t * gx, per = p.mt * nw;
+    if (nw == 0 || idx >= per * nsplit) return false;
+    z = idx / per;
+    const int r = idx - z * per;
+    mt_i = r / nw;
+    nt_i = nlo + r % nw;
+    return true;
+  }
+  // bijective XCD remap: consecutive ids on one XCD (dispatch is round-robin over the 8 XCDs), so the tiles of
+  // one split's k range share that XCD's L2
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
+  const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
+  const int idx = id + t * nwg, per = p.mt * p.nt;
+  if (idx >= per * nsplit) return false;
+  z = idx / per;
+  const int r = idx - z * per;
+  mt_i = r / p.nt;
+  nt_i = r % p.nt;
+  return true;
+}
+
+// Persistent: a workgroup walks its tiles (bf_tile), and the first k-slice of its NEXT tile is staged while the
+// current tile's epilogue stores go out, so a tile's store drain overlaps the next tile's first DMA (one
+// workgroup per tile left the next workgroup on that CU waiting for both in turn: the 124 MB fp32 output of
+// the QNN MLP's input grad took more time to store than to compute).
 template <bool TA, bool TB>
 __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * 2 * 128 * 64];     // [stage][A | B][128 x 64]
   const GemmArgs& g = p.g;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  int nt_i, mt_i, z;
-  if (p.gm < 0) {
-    // XCD column partition (nt >= 8): workgroups are dealt round-robin to the 8 XCDs, so XCD x runs ids x, x + 8,
-    // ... in order; it takes the n-tiles [nt x / 8, nt (x + 1) / 8) -- a B column group that stays in its L2 --
-    // for every m-tile, m slow / n fast so that consecutive tiles also share the A slab.  (n fastest over all
-    // tiles made every XCD stream all of B once per m-tile from the MALL: 241 MB of L2 fills for the QNN MLP
-    // input grad's 12 MB of operands.)
-    const int x = blockIdx.x & 7, l = blockIdx.x >> 3;
-    const int nlo = p.nt * x / 8, nw = p.nt * (x + 1) / 8 - nlo;
-    const int per = p.mt * nw;
-    z = l / per;
-    const int t = l - z * per;
-    if (z >= (int)((g.K + g.klen - 1) / g.klen)) return;    // the grid is sized for the widest XCD
-    mt_i = t / nw;
-    nt_i = nlo + t % nw;
-  } else {
-    // bijective XCD remap: consecutive ids (same XCD: dispatch is round-robin over 8 XCDs)
-    const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, qq = nwg / 8, rr = nwg % 8;
-    const int id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + orig / 8;
-    if (p.gm > 0) {
-      // grouped order: GM m-tiles fastest, then n, group by group
-      const int per = p.mt * p.nt, t = id % per;
-      z = id / per;
-      const int gsz = p.gm * p.nt, grp = t / gsz, m0g = grp * p.gm, gm = min(p.mt - m0g, p.gm), u = t - grp * gsz;
-      mt_i = m0g + u % gm;
-      nt_i = u / gm;
-    } else {
-      nt_i = id % p.nt;
-      const int rest = id / p.nt;
-      mt_i = rest % p.mt;
-      z = rest / p.mt;
-    }
-  }
-  const int m0 = mt_i * 128, n0 = nt_i * 128;
-  const int kz0 = z * g.klen, kz1 = min(g.K, kz0 + g.klen);
-  const int nkt = kz1 > kz0 ? (kz1 - kz0) / 64 : 0;
+  const int nsplit = (g.K + g.klen - 1) / g.klen;
   const int wm = (w >> 1) * 64, wn = (w & 1) * 64;
   const long lda = g.lda, ldb = g.ldb;
 
-  auto stage = [&](int buf, int k0) {
-#ifdef GBF_NOLOAD
-    if (k0 > 0) return;
-#endif
+  auto stage = [&](int buf, int m0, int n0, int k0) {
     __bf16* ta = smem + buf * 2 * 8192;
     __bf16* tb = ta + 8192;
     if (TA) stage_km(p.A, lda, m0, g.M, k0, ta, w, lane);
@@ -684,69 +682,83 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
     else stage_km(p.B, ldb, n0, g.N, k0, tb, w, lane);
   };
 
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (nkt > 0) {
-    stage(0, kz0);
-    __builtin_amdgcn_s_waitcnt(0);       // vmcnt(0) lgkmcnt(0)...: the DMA has landed
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) stage(cur ^ 1, kz0 + (kt + 1) * 64);
-    const __bf16* ta = smem + cur * 2 * 8192;
-    const __bf16* tb = ta + 8192;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = TA ? frag_km(ta, (wm >> 4) + i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = TB ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_km(tb, (wn >> 4) + j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_waitcnt(0);       // the next slice's DMA (and this slice's reads) complete
-    __syncthreads();
-  }
-
-#ifdef GBF_NOSTORE
-  if (acc[0][0][0] != 12345.f) return;
-#endif
-  const ctr_gemm_epi_t& e = g.epi;
-  const int lrow = wm + (lane >> 4) * 4, lcol = wn + (lane & 15);
-  if (g.ws) {   // split-K partial: raw slab, the reduce kernel applies the epilogue
-    float* slab = g.ws + (long)z * g.M * g.N;
+  int z, mt_i, nt_i;
+  if (!bf_tile(p, nsplit, 0, z, mt_i, nt_i)) return;
+  int bi = 0;                                // LDS buffer holding the current k-slice
+  stage(0, mt_i * 128, nt_i * 128, z * g.klen);
+  __builtin_amdgcn_s_waitcnt(0);             // vmcnt(0) lgkmcnt(0)...: the DMA has landed
+  __syncthreads();
+  for (int t = 0;; ++t) {
+    const int m0 = mt_i * 128, n0 = nt_i * 128;
+    const int kz0 = z * g.klen, kz1 = min(g.K, kz0 + g.klen);
+    const int nkt = kz1 > kz0 ? (kz1 - kz0) / 64 : 0;
+    int zn, mn, nn;
+    const bool more = bf_tile(p, nsplit, t + 1, zn, mn, nn);
+    f32x4 acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = n0 + lcol + j * 16;
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = bi;
+      if (kt + 1 < nkt) stage(cur ^ 1, m0, n0, kz0 + (kt + 1) * 64);
+      else if (more) stage(cur ^ 1, mn * 128, nn * 128, zn * g.klen);   // the next tile's first slice
+      const __bf16* ta = smem + cur * 2 * 8192;
+      const __bf16* tb = ta + 8192;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + lrow + i * 16 + r;
-          if (m < g.M && n < g.N) slab[(long)m * g.N + n] = acc[i][j][r];
-        }
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = TA ? frag_km(ta, (wm >> 4) + i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = TB ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_km(tb, (wn >> 4) + j, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + lcol + j * 16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + lrow + i * 16 + r;
-        if (m < g.M && n < g.N) *cptr(g, m, n) = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
+      bi ^= 1;
+      if (kt + 1 < nkt) {
+        __builtin_amdgcn_s_waitcnt(0);       // the next slice's DMA (and this slice's reads) complete
+        __syncthreads();
       }
     }
+
+    const ctr_gemm_epi_t& e = g.epi;
+    const int lrow = wm + (lane >> 4) * 4, lcol = wn + (lane & 15);
+    if (g.ws) {   // split-K partial: raw slab, the reduce kernel applies the epilogue
+      float* slab = g.ws + (long)z * g.M * g.N;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + lcol + j * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + lrow + i * 16 + r;
+            if (m < g.M && n < g.N) slab[(long)m * g.N + n] = acc[i][j][r];
+          }
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n0 + lcol + j * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + lrow + i * 16 + r;
+            if (m < g.M && n < g.N) *cptr(g, m, n) = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
+          }
+        }
+    }
+    if (!more) break;
+    __builtin_amdgcn_s_waitcnt(0);           // the next tile's first slice (and this tile's stores)
+    __syncthreads();
+    z = zn;
+    mt_i = mn;
+    nt_i = nn;
+  }
 }
 
 // fp32 (rows, cols) with row stride lds -> bf16 with row stride ldd (RNE); 4 elements per thread
@@ -916,9 +928,11 @@ extern "C" int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta
   p.B = (const __bf16*)B;
   p.mt = cdiv(M, 128);
   p.nt = cdiv(N, 128);
-  // XCD column partition where there are n-tiles for every XCD (grid: the widest XCD's tiles x 8)
+  // XCD column partition where there are n-tiles for every XCD; persistent grid: two workgroups per CU (64 KB
+  // of LDS each) at most, a multiple of 8 for the partition
   p.gm = p.nt >= 8 ? -1 : 0;
-  const int grid = p.gm < 0 ? 8 * p.mt * cdiv(p.nt, 8) * splits : p.mt * p.nt * splits;
+  const int tiles = p.gm < 0 ? 8 * p.mt * cdiv(p.nt, 8) * splits : p.mt * p.nt * splits;
+  const int grid = std::min(tiles, 512);
   hipStream_t s = (hipStream_t)stream;
   if (!ta && tb) gemm_bf_kernel<false, true><<<grid, 256, 0, s>>>(p);
   else if (!ta && !tb) gemm_bf_kernel<false, false><<<grid, 256, 0, s>>>(p);
