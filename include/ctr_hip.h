@@ -90,6 +90,13 @@ int ctr_gemm_bf16_ok(int M, int N, int K, int lda, int ta, int ldb, int tb, int 
 int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta, const void* B, int ldb, int tb,
                   float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
                   void* stream);
+/* ctr_gemm_bf16 with flags.  CTR_GEMM_OUT_BF16: C (and the C2 segment) are bf16, the RNE of the fp32
+ * accumulation (splits = 1) -- the dtype autocast gives the reference's matmul output, e.g. the QNN MLP's
+ * input grad [dz | dinter] (src/models/qnn_alpha.py:120-124 under src/train.py:158-164).               */
+#define CTR_GEMM_OUT_BF16 1
+int ctr_gemm_bf16_ex(int M, int N, int K, const void* A, int lda, int ta, const void* B, int ldb, int tb,
+                     void* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
+                     int flags, void* stream);
 int ctr_to_bf16(const float* src, long lds, int rows, int cols, void* dst, long ldd, void* stream);
 
 
@@ -305,10 +312,10 @@ int ctr_qnn_vfull(const float* V, int H, int R, int P, float* vfull, int inverse
  * zsum = sum_f z_f, G = z^T z (D x D), S = zsum @ Ucat, quad = S*S - diag(Ucat^T G Ucat) (QR wide) */
 int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int QR, float* zsum, float* G,
                      float* S, float* quad, void* stream);
-/* backward to z: dz_f = 2 Ucat (dquad o S) - 2 (Ucat diag(dquad) Ucat^T) z_f (+ dz_add, nullable);
- * DS = dquad o S (for dUcat)                                                                       */
+/* backward to z: dz_f = 2 Ucat (dquad o S) - 2 (Ucat diag(dquad) Ucat^T) z_f (+ dz_add, nullable; fp32, or
+ * bf16 when add_bf16 -- the MLP's input grad under amp: bf16); DS = dquad o S (for dUcat)           */
 int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
-                     const float* dquad, const float* dz_add, float* dz, float* DS, void* stream);
+                     const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS, void* stream);
 /* dUcat = 2 (T1 - sum_e Ucat[e,c] T[d*D+e, c]) with T1 = zsum^T DS (D x QR), T = G^T dquad (D*D x QR) */
 int ctr_qnn_du_combine(const float* T1, const float* T, const float* ucat, int D, int QR, float* ducat,
                        void* stream);
@@ -320,7 +327,8 @@ int ctr_scale_drop(const float* x, int B, int C, const float* gate, uint32_t dro
 int ctr_scale_drop_bf(const float* x, int B, int C, const float* gate, uint32_t drop_key, uint32_t drop_thresh,
                       float drop_scale, float* out, long out_ld, void* obf, long obf_ld, void* stream);
 size_t ctr_se_bwd_ws(int B, int C);
-int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, int Cr, const float* gate,
+/* dout fp32, or bf16 when dout_bf16 (the MLP's input grad under amp: bf16)                          */
+int ctr_se_bwd(const void* dout, long dout_ld, int dout_bf16, const float* x, int B, int C, int Cr, const float* gate,
                const float* g1, const float* mean, const float* W1, const float* W2, uint32_t drop_key,
                uint32_t drop_thresh, float drop_scale, float* dx, float* dW1, float* db1, float* dW2, float* db2,
                float* ws, void* stream);

@@ -64,3 +64,51 @@ def test_gemm_bf16_epilogue_and_c2():
     full = Ab.double() @ Wk.double()
     assert rel(C1.double(), full[:, :nc]) < 1e-5
     assert rel(C2.double(), full[:, nc:]) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K,nc", [(4096, 7552, 512, 6400), (520, 384, 256, 256), (257, 88, 128, 0)])
+def test_gemm_bf16_out_bf16_is_rounded_fp32(M, N, K, nc):
+    """CTR_GEMM_OUT_BF16 (the QNN MLP's input grad [dz | dinter] under amp): every element is the RNE bf16 of
+    the fp32 result the same call writes without the flag -- same accumulation, only the store differs --
+    including the C2 segment and a row tail (M % 128 != 0)."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    Wk = torch.randn(K, N, device="cuda", generator=g)
+    Ab, Wb = bf16_image(L, A), bf16_image(L, Wk)
+    n2 = N - nc
+    seg = L.GemmSeg(C2=None, ldc2=0, nc=N)
+    C32 = torch.empty(M, N, device="cuda")
+    L.call("ctr_gemm_bf16_ex", M, N, K, ptr(Ab), K, 0, ptr(Wb), N, 0, ptr(C32), N, None, 1, None, None, 0, stream())
+    C1 = torch.empty(M, nc if nc else N, dtype=torch.bfloat16, device="cuda")
+    C2 = torch.empty(M, max(n2, 1), dtype=torch.bfloat16, device="cuda")
+    if nc:
+        seg = L.GemmSeg(C2=ptr(C2), ldc2=n2, nc=nc)
+    L.call("ctr_gemm_bf16_ex", M, N, K, ptr(Ab), K, 0, ptr(Wb), N, 0, ptr(C1), C1.shape[1], None, 1, None,
+           seg if nc else None, 1, stream())
+    ref = C32.bfloat16()
+    if nc:
+        assert torch.equal(C1, ref[:, :nc]) and torch.equal(C2, ref[:, nc:])
+    else:
+        assert torch.equal(C1, ref)
+    assert rel(C32.double(), Ab.double() @ Wb.double()) < 1e-5
+
+
+def test_gemm_bf16_epilogue_stays_inside_n():
+    """N far below the 128-column tile (the tiny configs' MLP: N = 32 / 40): the epilogue's pre-activation
+    stores and aux / add reads stop at column N -- a guard region past the last row stays untouched."""
+    L = _lib()
+    M, N, K = 300, 40, 128
+    g = torch.Generator(device="cuda").manual_seed(7)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    Ab, Wb = bf16_image(L, A), bf16_image(L, W)
+    C = torch.full((M + 8, N), 7.0, device="cuda")
+    pre = torch.full((M + 8, N), 7.0, device="cuda")
+    epi = L.GemmEpi(bias=ptr(bias), act=1, pre=ptr(pre))
+    L.call("ctr_gemm_bf16", M, N, K, ptr(Ab), K, 0, ptr(Wb), K, 1, ptr(C), N, epi, 1, None, None, stream())
+    z = Ab.double() @ Wb.double().t() + bias.double()
+    assert rel(pre[:M].double(), z) < 1e-5
+    assert rel(C[:M].double(), z.clamp_min(0)) < 1e-5
+    assert (pre[M:] == 7.0).all() and (C[M:] == 7.0).all()

@@ -823,9 +823,15 @@ def test_qnn_gram_vs_torch(B, F, D, QR):
     dz_add = torch.randn(B, F, D, device="cuda", generator=g)
     q_ref.backward(dquad.double())
     dz, DS = torch.empty(B, F, D, device="cuda"), torch.empty(B, QR, device="cuda")
-    L.call("ctr_qnn_gram_bwd", ptr(z), B, F, D, ptr(U), QR, ptr(S), ptr(dquad), ptr(dz_add), ptr(dz), ptr(DS),
+    L.call("ctr_qnn_gram_bwd", ptr(z), B, F, D, ptr(U), QR, ptr(S), ptr(dquad), ptr(dz_add), 0, ptr(dz), ptr(DS),
            stream())
     assert rel(dz.double(), zr.grad + dz_add.double()) < 1e-5
+    # amp: the addend (the QNN MLP's input grad) arrives as bf16; the same sums with its values widened
+    dz_add_bf = dz_add.bfloat16()
+    dz2 = torch.empty_like(dz)
+    L.call("ctr_qnn_gram_bwd", ptr(z), B, F, D, ptr(U), QR, ptr(S), ptr(dquad), ptr(dz_add_bf), 1, ptr(dz2), ptr(DS),
+           stream())
+    assert rel(dz2.double(), zr.grad + dz_add_bf.double()) < 1e-5
     T1 = (zsum.t() @ DS).contiguous()
     T = (G.t() @ dquad).contiguous()
     du = torch.empty(D, QR, device="cuda")

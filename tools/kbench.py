@@ -160,6 +160,17 @@ def main():
                 t = timeit(fn, args.iters)
                 res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}({t * 1e3:.0f}us)")
             print(f"gemm_bf16 M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
+        # the input grad as the step runs it: bf16 [dz | dinter] output split at column 6400
+        Mg, Ng, Kg, nc = 4096, 7552, 512, 6400
+        Ag = torch.randn(Mg, Kg, device="cuda").bfloat16()
+        Bg = torch.randn(Kg, Ng, device="cuda").bfloat16()
+        C1 = torch.empty(Mg, nc, device="cuda", dtype=torch.bfloat16)
+        C2 = torch.empty(Mg, Ng - nc, device="cuda", dtype=torch.bfloat16)
+        seg = _lib.GemmSeg(C2=ptr(C2), ldc2=Ng - nc, nc=nc)
+        fn = lambda: call("ctr_gemm_bf16_ex", Mg, Ng, Kg, ptr(Ag), Kg, 0, ptr(Bg), Ng, 0, ptr(C1), nc, None, 1, None,
+                          seg, 1, st)
+        t = timeit(fn, args.iters)
+        print(f"gemm_bf16 out bf16 + C2 M={Mg} N={Ng} K={Kg}: {2.0 * Mg * Ng * Kg / t / 1e9:.0f} TF/s ({t * 1e3:.0f}us)")
     if "attn" in which or "attnbf" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1

@@ -97,6 +97,13 @@ __device__ __forceinline__ uint32_t sign_mask(uint32_t x) {
   asm("v_ashrrev_i32 %0, 31, %1" : "=v"(m) : "v"(x));
   return m;
 }
+// all ones where bit B of x is set, one v_bfe_i32 (as C, sbfe & constant became and + compare + select: three
+// VALU per keep bit instead of one)
+__device__ __forceinline__ uint32_t bit_mask(uint32_t x, int b) {
+  uint32_t m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(x), "i"(b));
+  return m;
+}
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 // RNE bf16 pairs (v_cvt_pk_bf16_f32 each), as two dwords: one conversion for both the MFMA operand and the
 // LDS image (through to_bf4 the compiler converted twice, differently packed)
@@ -133,6 +140,15 @@ __device__ __forceinline__ float grp_sum(float v) {
   return grp_reduce(v, [](float p, float q) { return p + q; });
 }
 
+// Workgroup barrier ordering LDS only.  __syncthreads() also waits for every outstanding global load and store
+// (its release fence is for all address spaces): the prologue's early loads and the dqkv stores of the backward
+// would be waited for at each barrier instead of draining behind the following work.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Workgroup staging: q * scale, k, v (and dO) of the group's G heads as bf16 [KT][RS] images; rows >= K are zero.
 // The mask chunk's first slot carries the padded-key mask through the score product (k: 1 on padded keys j >= K,
 // q: -3e38), so S^T = K Q^T carries -3e38 (-> -inf after the log2 scale) on every padded key and an exact +-0
@@ -154,10 +170,10 @@ struct Stg {
 constexpr float NEG_BIG = -3.0e38f;
 
 template <int DH, int NT, bool WITH_DO>
-__device__ __forceinline__ void stage(const AttnBfArgs& a, __bf16* sq, __bf16* sk, __bf16* sv, __bf16* sdo) {
+__device__ __forceinline__ void stage(const AttnBfArgs& a, int b, int hg, __bf16* sq, __bf16* sk, __bf16* sv, __bf16* sdo) {
   using S = Stg<DH, NT>;
   constexpr int KT = S::KT;
-  const int K = a.K, D = a.D, G = a.G, b = wg_sample(a), hg = wg_group(a);
+  const int K = a.K, D = a.D, G = a.G;
   const float* base = a.qkv + (long)b * K * 3 * D + hg * G * DH;
   const float* dob = WITH_DO ? a.dO + (long)b * K * D + hg * G * DH : nullptr;
   constexpr int NCD = DH / 4, NCR = 4 * NCD + 2;  // chunks per row: 4 heads' dims, mask, zero
@@ -230,7 +246,8 @@ __device__ __forceinline__ bf16x4 op_col(const __bf16* img, int row0, int hs, in
 // forward.  NT = the tiles a side (ceil(K / 16)); DROPK: 0 none, 1 K even (pair hashes), 2 K odd
 template <int NT, int DH, bool BIAS, int DROPK>
 __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
-  if (wg_sample(a) >= a.B) return;      // the grid's tail past the last sample
+  const int b = wg_sample(a), hgrp = wg_group(a);
+  if (b >= a.B) return;      // the grid's tail past the last sample
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
@@ -239,11 +256,11 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
   __bf16* sk = sq + S::IM;
   __bf16* sv = sk + S::IM;
   float* srel = (float*)(sv + S::IM + S::PAD);
-  stage<DH, NT, false>(a, sq, sk, sv, nullptr);
+  stage<DH, NT, false>(a, b, hgrp, sq, sk, sv, nullptr);
   if (BIAS) stage_rel<NT>(a, srel);
   __syncthreads();
-  const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int h = wg_group(a) * G + w, hs = w * S::HS;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = hgrp * G + w, hs = w * S::HS;
   bf16x4 kop[NT], vtop[NT];
 #pragma unroll
   for (int tj = 0; tj < NT; ++tj) {
@@ -388,9 +405,16 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
 // Key tiles outer (dk, dv of a key tile complete in its iteration), query tiles inner (dq accumulates).
 // four waves per SIMD (128 registers, no spill; with the compact rows four workgroups fit a CU's LDS): 141 -> 126 us
 // at cfg2 against three
+// start of tile diagonal ee = a - c (-15 .. 15) in a 16 x 16 tile stored diagonal-major, rows of 16 - |ee| floats
+__device__ __forceinline__ int diag_off(int ee) {
+  const int n = ee + 15;
+  return n <= 16 ? n * (n + 1) / 2 : 256 - (31 - n) * (32 - n) / 2;
+}
+
 template <int NT, int DH, bool BIAS, bool DROP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_mf_kernel(AttnBfArgs a) {
-  if (wg_sample(a) >= a.B) return;      // the grid's tail past the last sample
+  const int b = wg_sample(a), hgrp = wg_group(a);
+  if (b >= a.B) return;      // the grid's tail past the last sample
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   constexpr int ND = 2 * NT - 1, IMG = img_elems<NT>(), KT = KB::KT;
@@ -405,20 +429,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   const bool opj = a.dh1 != nullptr;      // block-uniform
   const int GD = G * DH;                    // the workgroup's columns of dO
   float* dot = (float*)simg;                // opj: the dO tile [KT][GD] (fp32), in the image space until the loop
+  // the row statistics' operands (this lane's query row: o, the forward's row max / sum, dO without opj) and the
+  // keep words, loaded first: their round trips overlap the staging's instead of following its barrier
+  static_assert(KT == 64, "one query row per lane");
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = hgrp * G + w, hs = w * S::HS;
+  const long hr = ((long)b * a.H + h) * K;
+  f32x4 o_row[DH / 4], do_row[DH / 4];
+  float m_row = 0.f, l_row = 1.f;
+  if (lane < K) {
+    const float* op = a.o + ((long)b * K + lane) * D + h * DH;
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) {
+      o_row[q] = *(const f32x4*)(op + 4 * q);
+      do_row[q] = opj ? f32x4{0.f, 0.f, 0.f, 0.f} : *(const f32x4*)(a.dO + ((long)b * K + lane) * D + h * DH + 4 * q);
+    }
+    m_row = a.mrow[hr + lane];
+    l_row = a.lrow[hr + lane];
+  }
+  uint32_t words[KB::NW];
+#pragma unroll
+  for (int q = 0; q < KB::NW; ++q) words[q] = 0u;
+  if (DROP) {
+    const uint32_t* mk = a.mask + ((long)b * a.H + h) * (64 * KB::NW);
+#pragma unroll
+    for (int q = 0; q < KB::NW; ++q) words[q] = mk[64 * q + lane];
+  }
   if (opj) {
     // dO = dh1 W_out on v_mfma_f32_16x16x4f32 in rowgemm.hip's k order (lane group g: k = 8g + kk; + 0.f as its
     // bias-less epilogue): the same bits as the ctr_rowgemm launch it replaces.  Tiles: 4 row blocks x ncb column
     // blocks of the workgroup's GD columns, at most two per wave; operands straight from global (a lane's dh1
     // row segment is two 16-byte loads), issued before the q / k / v staging so the round trips overlap.
     const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63, g0 = l0 >> 4, c0 = l0 & 15;
-    const int ncb = (GD + 15) >> 4, cbase = wg_group(a) * GD;
-    const long r0 = (long)wg_sample(a) * K;
+    const int ncb = (GD + 15) >> 4, cbase = hgrp * GD;   // 1 or 2 (GD <= 32): tile t = (rb = t >> nsh, t & nm)
+    const int nsh = ncb - 1, nm = ncb - 1;
+    const long r0 = (long)b * K;
     f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     int tiles[2] = {-1, -1};
     for (int t = w0, q = 0; t < 4 * ncb && q < 2; t += G, ++q) {
       tiles[q] = t;
-      const int rb = t / ncb, i = 16 * rb + c0, n = cbase + 16 * (t % ncb) + c0;
-      const bool nin = 16 * (t % ncb) + c0 < GD;
+      const int rb = t >> nsh, i = 16 * rb + c0, n = cbase + 16 * (t & nm) + c0;
+      const bool nin = 16 * (t & nm) + c0 < GD;
       f32x4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = x0;
       if (i < K) {
         x0 = *(const f32x4*)(a.dh1 + (r0 + i) * 32 + 8 * g0);
@@ -431,7 +482,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       for (int kk = 0; kk < 8; ++kk)
         acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk < 4 ? x0[kk] : x1[kk - 4], wv[kk], acc[q], 0, 0, 0);
     }
-    stage<DH, NT, false>(a, sq, sk, sv, nullptr);
+    stage<DH, NT, false>(a, b, hgrp, sq, sk, sv, nullptr);
     for (int j = threadIdx.x; j < KT; j += blockDim.x) {   // sdo's mask / zero chunks
       *(bf16x4*)(sdo + j * S::RS + S::MOFF) = bf16x4{};
       *(bf16x4*)(sdo + j * S::RS + S::ZOFF) = bf16x4{};
@@ -440,7 +491,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if (tiles[q] < 0) continue;
-      const int rb = tiles[q] / ncb, col = 16 * (tiles[q] % ncb) + c0;
+      const int rb = tiles[q] >> nsh, col = 16 * (tiles[q] & nm) + c0;
       if (col >= GD) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -451,47 +502,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       }
     }
   } else {
-    stage<DH, NT, true>(a, sq, sk, sv, sdo);
+    stage<DH, NT, true>(a, b, hgrp, sq, sk, sv, sdo);
     if (BIAS) stage_rel<NT>(a, srel);
   }
-  __syncthreads();
-  const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int h = wg_group(a) * G + w, hs = w * S::HS;
+  lds_barrier();
   __bf16* ids = simg + w * 2 * IMG;
   __bf16* ipt = ids + IMG;
   const float* rb = srel + KT + a.tk + 4 * g - c;
-  const long hr = ((long)b * a.H + h) * K;
   // per query row i (lane): {max (log2), 1 / sum, D_i = do_i . o_i} in the wave's LDS row table, read back
   // per score tile (padded rows: p = 0, D = 0)
   f32x4* stw = (f32x4*)(srel + rel_floats<NT>(BIAS ? a.tk : 0)) + w * KT;
-  for (int row = lane; row < KT; row += 64) {
+  {
     f32x4 st = {0.f, 0.f, 0.f, 0.f};
-    if (row < K) {
-      const float* dp = opj ? dot + row * GD + w * DH : a.dO + ((long)b * K + row) * D + h * DH;
-      const float* op = a.o + ((long)b * K + row) * D + h * DH;
+    if (lane < K) {
       float s = 0.f;
 #pragma unroll
       for (int q = 0; q < DH / 4; ++q) {
-        const f32x4 x = *(const f32x4*)(dp + 4 * q), y = *(const f32x4*)(op + 4 * q);
+        const f32x4 x = opj ? *(const f32x4*)(dot + lane * GD + w * DH + 4 * q) : do_row[q], y = o_row[q];
         s = fmaf(x[0], y[0], s);
         s = fmaf(x[1], y[1], s);
         s = fmaf(x[2], y[2], s);
         s = fmaf(x[3], y[3], s);
       }
-      st = f32x4{a.mrow[hr + row], 1.0f / a.lrow[hr + row], s, 0.f};
+      st = f32x4{m_row, 1.0f / l_row, s, 0.f};
     }
-    stw[row] = st;
+    stw[lane] = st;
   }
   __builtin_amdgcn_wave_barrier();
-  if (opj) __syncthreads();                 // every wave's dO-tile reads before the images overwrite it
-  uint32_t words[KB::NW];
-#pragma unroll
-  for (int q = 0; q < KB::NW; ++q) words[q] = 0u;
-  if (DROP) {
-    const uint32_t* mk = a.mask + ((long)b * a.H + h) * (64 * KB::NW);
-#pragma unroll
-    for (int q = 0; q < KB::NW; ++q) words[q] = mk[64 * q + lane];
-  }
+  if (opj) lds_barrier();                 // every wave's dO-tile reads before the images overwrite it
   const uint32_t dsc_bits = __builtin_bit_cast(uint32_t, DROP ? a.drop.scale : 1.0f);
   f32x4 dq[NT];
   float dg[ND][4];
@@ -524,8 +562,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
         float dpk = dp[r], pt = p;
         if (DROP) {   // keep ? 1 / (1 - p) : 0, from the bit's sign-extension
           const int pos = 16 * ti + 4 * tj + r;
-          const float kf = __builtin_bit_cast(
-              float, (uint32_t)__builtin_amdgcn_sbfe((int)words[pos >> 5], pos & 31, 1) & dsc_bits);
+          const float kf = __builtin_bit_cast(float, bit_mask(words[pos >> 5], pos & 31) & dsc_bits);
           dpk *= kf;
           pt *= kf;
         }
@@ -565,25 +602,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   if (BIAS) {
     // diagonal sums of dS: register (dt, r) of lane (g, c) holds the sum over the tiles of diagonal dt of
     // element (a = 4g + r, c) = diagonal 16 (dt - (NT-1)) + a - c.  Heads first (fixed order), then diagonals.
-    __syncthreads();                                    // staging / image space is reused
+    lds_barrier();                                    // staging / image space is reused
     float* sd = (float*)smb;                            // [G][ND][16 a][16 c]
 #pragma unroll
     for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) sd[((w * ND + dt) * 16 + 4 * g + r) * 16 + c] = dg[dt][r];
-    __syncthreads();
-    float* sh = sd + G * ND * 256;                      // [ND][16][16] summed over heads
-    for (int e = threadIdx.x; e < ND * 256; e += blockDim.x) {
-      float s = 0.f;
-      for (int u = 0; u < G; ++u) s += sd[u * ND * 256 + e];
-      sh[e] = s;
+    lds_barrier();
+    // head sums (fixed order), stored diagonal-major: tile diagonal ee = a - c of tile-diagonal dt is a packed row
+    // of 16 - |ee| floats at dt * 256 + diag_off(ee), element min(a, c) -- a diagonal's sum then reads one row at
+    // immediate offsets (the [a][c] layout took a computed address per element).  A thread's loads are issued
+    // together (heads clamped in range, unused values dropped): the chains of dependent LDS round trips were this
+    // epilogue's cost.
+    float* sh = sd + G * ND * 256;                      // [ND][256] (+ 16 floats of read padding)
+    for (int p = threadIdx.x; p < 256; p += blockDim.x) {
+      const int aa = p >> 4, cc = p & 15;
+      const int o = diag_off(aa - cc) + (aa < cc ? aa : cc);
+      float v[ND][4];
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[dt][u] = sd[((u < G ? u : 0) * ND + dt) * 256 + p];
+#pragma unroll
+      for (int dt = 0; dt < ND; ++dt) {
+        float s = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u < G) s += v[dt][u];
+        sh[dt * 256 + o] = s;
+      }
     }
-    __syncthreads();
+    lds_barrier();
     // thread 2 x + half: diagonal d = x - (16 NT - 1); half 0 the tile diagonal with 0 <= d - 16 dt' <= 15,
-    // half 1 the one above it (-16 <= d - 16 dt' <= -1)
+    // half 1 the one above it (-16 <= d - 16 dt' <= -1; -16 is no diagonal of a tile).  Element order along a
+    // row = ascending a, the order of the sum it replaces.
     constexpr int NDG = 2 * 16 * NT - 1;
     const int nrel = 2 * a.tk + 1;
-    float* out = a.drel_part + ((long)b * a.ngrp + wg_group(a)) * nrel;
+    float* out = a.drel_part + ((long)b * a.ngrp + hgrp) * nrel;
     for (int t0 = 0; t0 < 2 * NDG; t0 += blockDim.x) {
       const int t = t0 + threadIdx.x;
       const int x = t >> 1, half = t & 1;
@@ -594,13 +649,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
         const int dtp = dth + half;
         const int e = d - 16 * dtp;
         const int dtx = dtp + NT - 1;
-        if (dtx >= 0 && dtx < ND) {
-#pragma unroll 4
-          for (int aa = 0; aa < 16; ++aa) {
-            const int cc = aa - e;
-            if (cc >= 0 && cc < 16) s += sh[(dtx * 16 + aa) * 16 + cc];
-          }
-        }
+        const bool tin = dtx >= 0 && dtx < ND && e > -16;
+        const int len = 16 - (e < 0 ? -e : e);
+        const float* row = sh + (tin ? dtx * 256 + diag_off(e) : 0);
+        float vv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) vv[k] = row[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (tin && k < len) s += vv[k];
       }
       // the pair (half 0, half 1) is lanes (2x, 2x+1): half 0 adds its neighbour's sum
       const float o = __shfl_xor(s, 1);
@@ -642,7 +699,8 @@ __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(ATT_WPE)))
 #endif
 void attn_bwd_mfl_kernel(AttnBfArgs a) {
-  if (wg_sample(a) >= a.B) return;      // the grid's tail past the last sample
+  const int b = wg_sample(a), hgrp = wg_group(a);
+  if (b >= a.B) return;      // the grid's tail past the last sample
   using S = Stg<DH, NT>;
   using KB = Kt<NT>;
   constexpr int KT = KB::KT, NDG = 32 * NT - 1, NDGP = (NDG + 3) & ~3;
@@ -654,10 +712,10 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
   __bf16* sdo = sv + S::IM;
   __bf16* simg = sdo + S::IM + S::PAD;              // per wave: 16 x 16 dS image, 16 x 16 p~ image (x2)
   float* srel = (float*)(simg + 4 * 4 * 256);
-  stage<DH, NT, true>(a, sq, sk, sv, sdo);
+  stage<DH, NT, true>(a, b, hgrp, sq, sk, sv, sdo);
   if (BIAS) stage_rel<NT>(a, srel);
-  const int b = wg_sample(a), w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
-  const int h = wg_group(a) * G + w, hs = w * S::HS;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int h = hgrp * G + w, hs = w * S::HS;
   __bf16* ids0 = simg + w * 4 * 256;
   const float* rb = srel + KT + a.tk + 4 * g - c;
   const long hr = ((long)b * a.H + h) * K;
@@ -801,7 +859,7 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
     __syncthreads();
     // heads of the group summed in a fixed order; diagonal d = x - (16 nt - 1) of the x-th sum
     const int nrel = 2 * a.tk + 1;
-    float* out = a.drel_part + ((long)b * a.ngrp + wg_group(a)) * nrel;
+    float* out = a.drel_part + ((long)b * a.ngrp + hgrp) * nrel;
     const float* base = (const float*)(stw + (4 - w) * KT);     // wave 0's scratch
     for (int e = threadIdx.x; e < nrel; e += blockDim.x) {
       const int d = e - a.tk, x = d + 16 * NT - 1;
@@ -898,7 +956,7 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
       srel[e] = v;
     }
   }
-  __syncthreads();
+  lds_barrier();
   // ---- in-projection: 4 row blocks x 6 column blocks of 16, K = 32 (8 MFMA k-steps of 4); tile t -> (rb, cb)
   for (int t = w; t < 24; t += G) {
     const int rb = t / 6, cb = t % 6;
@@ -920,7 +978,7 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
       dst[i * lf::RS + col] = (__bf16)(i < K ? (sec == 0 ? v * a.scale : v) : 0.f);
     }
   }
-  __syncthreads();
+  lds_barrier();
   // ---- attention, wave w = head h (attn_fwd_mf_kernel's per-head body at nt = 4)
   {
     const int h = w, hs = h * DH;
@@ -1015,7 +1073,7 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
       mk[64 + lane] = words[1];
     }
   }
-  __syncthreads();
+  lds_barrier();
   // ---- out-projection + bias + residual + RMSNorm: wave w < 4 takes row block w, both 16-column blocks, and
   // finishes it as rowgemm.hip's epilogue does (same k order, same per-row sum and 16-lane reduction: same bits)
   if (w < 4) {
@@ -1073,7 +1131,7 @@ template <int DH, int NT>
 size_t bwd_lds(int G, int tk) {
   const size_t main = ((size_t)4 * Stg<DH, NT>::IM + Stg<DH, NT>::PAD) * 2 + (size_t)4 * 2 * img_elems<NT>() * 2 +
                       (size_t)rel_floats<NT>(tk) * 4 + (size_t)4 * Kt<NT>::KT * 16;
-  const size_t ND = 2 * NT - 1, diag = ((size_t)G * ND * 256 + ND * 256) * 4;
+  const size_t ND = 2 * NT - 1, diag = ((size_t)G * ND * 256 + ND * 256 + 16) * 4;
   return main > diag ? main : diag;
 }
 

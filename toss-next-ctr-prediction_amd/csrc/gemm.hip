@@ -574,7 +574,13 @@ struct GemmBfArgs {
   const __bf16* B;
   int mt, nt;            // tiles along M, N
   int gm;                // tile order: -1 XCD column partition, 0 n fastest (bf_tile)
+  int vec;               // 4-element result stores legal (C / C2 / slab rows and nc multiples of 4, aligned)
+  int obf;               // C / C2 are bf16 (RNE of the fp32 accumulation): the reference's autocast output dtype
 };
+
+__device__ __forceinline__ __bf16* cptr_bf(const GemmArgs& g, int m, int n) {
+  return (g.C2 && n >= g.nc) ? (__bf16*)g.C2 + (long)m * g.ldc2 + (n - g.nc) : (__bf16*)g.C + (long)m * g.ldc + n;
+}
 
 __device__ __forceinline__ void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)src,
@@ -715,7 +721,7 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
       }
       bi ^= 1;
       if (kt + 1 < nkt) {
@@ -724,33 +730,60 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
       }
     }
 
+    // the products ran as C^T tiles (B fragment first): lane (g, c) holds row m = .. + c, columns n .. n + 3 of
+    // each 16 x 16 block in its four registers -- one 16-byte store per block instead of four 4-byte ones
     const ctr_gemm_epi_t& e = g.epi;
-    const int lrow = wm + (lane >> 4) * 4, lcol = wn + (lane & 15);
+    const int lrow = wm + (lane & 15), lcol = wn + (lane >> 4) * 4;
     if (g.ws) {   // split-K partial: raw slab, the reduce kernel applies the epilogue
       float* slab = g.ws + (long)z * g.M * g.N;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + lrow + i * 16;
+        if (m >= g.M) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int n = n0 + lcol + j * 16;
+          float* d = slab + (long)m * g.N + n;
+          if (p.vec && n + 3 < g.N) {
+            *(f32x4*)d = acc[i][j];
+          } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + lrow + i * 16 + r;
-            if (m < g.M && n < g.N) slab[(long)m * g.N + n] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r)
+              if (n + r < g.N) d[r] = acc[i][j][r];
           }
         }
+      }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + lrow + i * 16;
+        if (m >= g.M) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int n = n0 + lcol + j * 16;
+          if (n >= g.N) continue;
+          f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + lrow + i * 16 + r;
-            if (m < g.M && n < g.N) *cptr(g, m, n) = epi_elem(e, acc[i][j][r], m, n, g.N, g.ldc);
+          for (int r = 0; r < 4; ++r)     // columns past N: no epilogue (it stores pre-activations, reads aux / add)
+            if (n + r < g.N) v[r] = epi_elem(e, acc[i][j][r], m, n + r, g.N, g.ldc);
+          // a 4-column group never straddles nc (nc % 4 == 0 when vec)
+          if (p.obf) {
+            if (p.vec && n + 3 < g.N) {
+              *(bf16x4*)cptr_bf(g, m, n) = __builtin_convertvector(v, bf16x4);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < g.N) *cptr_bf(g, m, n + r) = (__bf16)v[r];
+            }
+          } else if (p.vec && n + 3 < g.N) {
+            *(f32x4*)cptr(g, m, n) = v;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < g.N) *cptr(g, m, n + r) = v[r];
           }
         }
+      }
     }
     if (!more) break;
     __builtin_amdgcn_s_waitcnt(0);           // the next tile's first slice (and this tile's stores)
@@ -902,16 +935,25 @@ extern "C" int ctr_gemm_bf16_ok(int M, int N, int K, int lda, int ta, int ldb, i
 extern "C" int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta, const void* B, int ldb, int tb,
                              float* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws,
                              const ctr_gemm_seg_t* seg, void* stream) {
+  return ctr_gemm_bf16_ex(M, N, K, A, lda, ta, B, ldb, tb, C, ldc, epi, splits, ws, seg, 0, stream);
+}
+
+extern "C" int ctr_gemm_bf16_ex(int M, int N, int K, const void* A, int lda, int ta, const void* B, int ldb, int tb,
+                                void* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws,
+                                const ctr_gemm_seg_t* seg, int flags, void* stream) {
+  CTR_REQUIRE((flags & ~CTR_GEMM_OUT_BF16) == 0, "ctr_gemm_bf16_ex: unknown flags");
+  const int obf = (flags & CTR_GEMM_OUT_BF16) ? 1 : 0;
   CTR_REQUIRE(ctr_gemm_bf16_ok(M, N, K, lda, ta, ldb, tb, splits), "ctr_gemm_bf16: unsupported shape / layout");
   CTR_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0, "ctr_gemm_bf16: operands need 16-byte alignment");
   CTR_REQUIRE(!seg || (!seg->A2 && !seg->B2), "ctr_gemm_bf16: only the C2 result segment is supported");
   GemmBfArgs p = {};
   GemmArgs& g = p.g;
-  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.C = C; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.lda = lda; g.ldb = ldb; g.C = (float*)C; g.ldc = ldc;
   ctr_gemm_epi_t zero = {};
   g.epi = epi ? *epi : zero;
   CTR_REQUIRE(!(g.epi.dact && !g.epi.aux), "dact needs aux");
   CTR_REQUIRE(!g.epi.norm_w, "ctr_gemm_bf16: no fused RMSNorm epilogue");
+  CTR_REQUIRE(!obf || !g.epi.pre, "ctr_gemm_bf16_ex: bf16 output has no pre-activation store");
   g.C2 = nullptr; g.ldc2 = 0; g.nc = N;
   if (seg && seg->C2) {
     CTR_REQUIRE(seg->nc >= 0 && seg->nc <= N && !g.epi.aux && !g.epi.pre && !g.epi.add,
@@ -923,9 +965,14 @@ extern "C" int ctr_gemm_bf16(int M, int N, int K, const void* A, int lda, int ta
   splits = (K + klen - 1) / klen;
   g.klen = klen;
   CTR_REQUIRE(splits == 1 || ws, "ctr_gemm_bf16: split-K needs ws");
+  CTR_REQUIRE(splits == 1 || !obf, "ctr_gemm_bf16_ex: bf16 output needs splits = 1");
   g.ws = splits > 1 ? ws : nullptr;
   p.A = (const __bf16*)A;
   p.B = (const __bf16*)B;
+  p.obf = obf;
+  const uintptr_t al = obf ? 7 : 15;       // bf16x4 / f32x4 stores
+  p.vec = (N % 4 == 0) && (ldc % 4 == 0) && (((uintptr_t)C & al) == 0) && (!ws || ((uintptr_t)ws & 15) == 0) &&
+          (!g.C2 || ((g.ldc2 % 4 == 0) && (g.nc % 4 == 0) && (((uintptr_t)g.C2 & al) == 0)));
   p.mt = cdiv(M, 128);
   p.nt = cdiv(N, 128);
   // XCD column partition where there are n-tiles for every XCD; persistent grid: two workgroups per CU (64 KB

@@ -165,12 +165,12 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
 // every fourth 16-row F block: dz_f = 2 w - 2 M z_f (+ dz_add) with M's C-layout registers as the B
 // operand (k-set {16i+4g+r}).  (One wave per sample left only 4 waves per SIMD at B = 4096, each a long
 // serial load -> MFMA chain.)
-template <int D>
+template <int D, class TA>
 __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restrict__ z, int B, int F,
                                                            const float* __restrict__ ucat, int QR,
                                                            const float* __restrict__ S,
                                                            const float* __restrict__ dquad,
-                                                           const float* __restrict__ dz_add, float* __restrict__ dz,
+                                                           const TA* __restrict__ dz_add, float* __restrict__ dz,
                                                            float* __restrict__ DS) {
   constexpr int NT = D / 16;
   extern __shared__ float sU[];
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
 #endif
   constexpr int PF = QNN_PF;
   const float* zb = z + (long)b * F * D;
-  const float* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
+  const TA* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
   f32x4 zpre[PF][NT];
   float apre[PF][4][NT];
   {
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
       for (int r = 0; r < 4; ++r) {
         const int f = f0 + 4 * g0 + r;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) apre[it][r][j] = (ab && f < F) ? ab[(long)f * D + 16 * j + c0] : 0.f;
+        for (int j = 0; j < NT; ++j) apre[it][r][j] = (ab && f < F) ? (float)ab[(long)f * D + 16 * j + c0] : 0.f;
       }
     }
   }
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
       for (int r = 0; r < 4; ++r) {
         const int f = f0 + 4 * g + r;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) aq[r][j] = (ab && f < F) ? ab[(long)f * D + 16 * j + c] : 0.f;
+        for (int j = 0; j < NT; ++j) aq[r][j] = (ab && f < F) ? (float)ab[(long)f * D + 16 * j + c] : 0.f;
       }
     }
 #pragma unroll
@@ -382,7 +382,8 @@ __global__ void scale_drop_kernel(const float* __restrict__ x, int B, int C, con
 }
 
 // dpost = drop_bwd(dout); dx_direct = dpost*gate; part(dgate) = sum_b dpost*x over row chunks
-__global__ __launch_bounds__(256) void se_bwd_partial(const float* __restrict__ dout, long dout_ld,
+template <class TD>
+__global__ __launch_bounds__(256) void se_bwd_partial(const TD* __restrict__ dout, long dout_ld,
                                                       const float* __restrict__ x, int B, int C,
                                                       const float* __restrict__ gate, Drop drop,
                                                       int rows_per_block, float* __restrict__ dx,
@@ -393,7 +394,7 @@ __global__ __launch_bounds__(256) void se_bwd_partial(const float* __restrict__ 
 #pragma unroll 4
     for (int b = b0; b < b1; ++b) {
       const long q = (long)b * C + c;
-      float g = dout[(long)b * dout_ld + c];
+      float g = (float)dout[(long)b * dout_ld + c];
       if (drop.thresh) g = drop_keep(drop, (uint32_t)q) ? g * drop.scale : 0.f;
       if (gate) {
         dx[q] = g * gate[c];
@@ -484,8 +485,27 @@ extern "C" int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float
   return check_launch("qnn_gram_fwd");
 }
 
+template <class TA>
+static void gram_bwd_launch(int D, int blocks, size_t sm, hipStream_t s, const float* z, int B, int F, const float* ucat,
+                            int QR, const float* S, const float* dquad, const TA* dz_add, float* dz, float* DS) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<16, TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<32, TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<64, TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr = true;
+  }
+  if (D == 16) qnn_gram_bwd_kernel<16, TA><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else if (D == 32) qnn_gram_bwd_kernel<32, TA><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else qnn_gram_bwd_kernel<64, TA><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+}
+
 extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
-                                const float* dquad, const float* dz_add, float* dz, float* DS, void* stream) {
+                                const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS,
+                                void* stream) {
   CTR_REQUIRE(D == 16 || D == 32 || D == 64, "qnn gram: D must be 16, 32 or 64");
   if (B == 0) return 0;
   const int QRp = (QR + 15) / 16 * 16, NT = D / 16;
@@ -493,20 +513,8 @@ extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float
                     sizeof(float);
   CTR_REQUIRE(sm <= 160 * 1024, "qnn gram bwd: U + M partials exceed LDS");
   hipStream_t s = (hipStream_t)stream;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
-  const int blocks = B;
-  if (D == 16) qnn_gram_bwd_kernel<16><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
-  else if (D == 32) qnn_gram_bwd_kernel<32><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
-  else qnn_gram_bwd_kernel<64><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  if (add_bf16) gram_bwd_launch(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const __bf16*)dz_add, dz, DS);
+  else gram_bwd_launch(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const float*)dz_add, dz, DS);
   return check_launch("qnn_gram_bwd");
 }
 
@@ -550,7 +558,8 @@ extern "C" size_t ctr_se_bwd_ws(int B, int C) {
   return ((size_t)cdiv(B, SE_RPB) * C + 3 * (size_t)C) * sizeof(float);
 }
 
-extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B, int C, int Cr, const float* gate,
+extern "C" int ctr_se_bwd(const void* dout, long dout_ld, int dout_bf16, const float* x, int B, int C, int Cr,
+                          const float* gate,
                           const float* g1, const float* mean, const float* W1, const float* W2, uint32_t drop_key,
                           uint32_t drop_thresh, float drop_scale, float* dx, float* dW1, float* db1, float* dW2,
                           float* db2, float* ws, void* stream) {
@@ -561,8 +570,12 @@ extern "C" int ctr_se_bwd(const float* dout, long dout_ld, const float* x, int B
   float* part = ws;                      // [np][C]
   float* dmean = ws + (size_t)np * C;    // [C]
   Drop d{drop_key, drop_thresh, drop_scale};
-  se_bwd_partial<<<dim3(cdiv(C, 256), np), 256, 0, s>>>(dout, dout_ld, x, B, C, gate, d, rpb, dx,
-                                                       gate ? part : nullptr);
+  if (dout_bf16)
+    se_bwd_partial<<<dim3(cdiv(C, 256), np), 256, 0, s>>>((const __bf16*)dout, dout_ld, x, B, C, gate, d, rpb, dx,
+                                                         gate ? part : nullptr);
+  else
+    se_bwd_partial<<<dim3(cdiv(C, 256), np), 256, 0, s>>>((const float*)dout, dout_ld, x, B, C, gate, d, rpb, dx,
+                                                         gate ? part : nullptr);
   if (gate) {
     float* dz2 = dmean + C;                // [C]
     float* dz1 = dz2 + C;                  // [Cr <= C]

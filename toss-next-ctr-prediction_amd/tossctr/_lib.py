@@ -61,6 +61,7 @@ SIGS = {
     "ctr_gemm_ex": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), i, p]),
     "ctr_gemm_bf16_ok": (i, [i, i, i, i, i, i, i, i]),
     "ctr_gemm_bf16": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), p]),
+    "ctr_gemm_bf16_ex": (i, [i, i, i, p, i, i, p, i, i, p, i, C.POINTER(GemmEpi), i, p, C.POINTER(GemmSeg), i, p]),
     "ctr_to_bf16": (i, [p, l, i, i, p, l, p]),
     "ctr_rowgemm_supported": (i, [i, i]),
     "ctr_rowgemm": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
@@ -113,13 +114,13 @@ SIGS = {
     "ctr_qnn_ucat": (i, [p, i, i, i, p, i, p]),
     "ctr_qnn_vfull": (i, [p, i, i, i, p, i, p]),
     "ctr_qnn_gram_fwd": (i, [p, i, i, i, p, i, p, p, p, p, p]),
-    "ctr_qnn_gram_bwd": (i, [p, i, i, i, p, i, p, p, p, p, p, p]),
+    "ctr_qnn_gram_bwd": (i, [p, i, i, i, p, i, p, p, p, i, p, p, p]),
     "ctr_qnn_du_combine": (i, [p, p, p, i, i, p, p]),
     "ctr_se_fwd_gate": (i, [p, i, i, p, p, p, p, p, p, p]),
     "ctr_scale_drop": (i, [p, i, i, p, u, u, f, p, l, p]),
     "ctr_scale_drop_bf": (i, [p, i, i, p, u, u, f, p, l, p, l, p]),
     "ctr_se_bwd_ws": (z, [i, i]),
-    "ctr_se_bwd": (i, [p, l, p, i, i, i, p, p, p, p, p, u, u, f, p, p, p, p, p, p, p]),
+    "ctr_se_bwd": (i, [p, l, i, p, i, i, i, p, p, p, p, p, u, u, f, p, p, p, p, p, p, p]),
     "ctr_rowgrad_ws_size": (z, [i]),
     "ctr_rowgrad": (i, [p, p, i, i, i, i, p, p, p, p, z, p]),
     "ctr_rowgrad2": (i, [p, p, p, i, i, i, i, p, p, p, p, p, z, p]),

@@ -318,13 +318,15 @@ class Engine:
         call("ctr_to_bf16", src, ld, rows, cols, ptr(out, off), ld_out, self.s())
         return out
 
-    def gemm_bf(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, seg=None):
+    def gemm_bf(self, M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi=None, seg=None, out_bf16=False):
         """C = op(A) op(B) on bf16 operand images (ctr_gemm_bf16, amp: bf16); split-K so that the
-        (tiles x splits) grid stays within one wave of 2 workgroups per CU."""
+        (tiles x splits) grid stays within one wave of 2 workgroups per CU.  ``out_bf16``: C (and the C2
+        segment) bf16, the output dtype autocast gives the reference's matmul (no split-K)."""
         tiles = math.ceil(M / 128) * math.ceil(N / 128)
-        splits = max(1, min(512 // max(tiles, 1), K // 512))
+        splits = 1 if out_bf16 else max(1, min(512 // max(tiles, 1), K // 512))
         wsp = ptr(self.splitk_ws(splits * M * N)) if splits > 1 else None
-        call("ctr_gemm_bf16", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg, self.s())
+        call("ctr_gemm_bf16_ex", M, N, K, A, lda, ta, Bm, ldb, tb, Cm, ldc, epi, splits, wsp, seg,
+             1 if out_bf16 else 0, self.s())     # CTR_GEMM_OUT_BF16
 
     def bf_ok(self, M, N, K, lda, ta, ldb, tb):
         return self.bf16 and bool(_lib.query("ctr_gemm_bf16_ok", M, N, K, lda, ta, ldb, tb, 1))
@@ -948,12 +950,14 @@ class Engine:
                               self.wgrad_splits(ncur, FD + C, B), seg=_lib.GemmSeg(B2=ptr(q["inter"]), ldb2=C, nb=FD))
                     self.colsum(ptr(dcur), ncur, B, ncur, ptr(G[bkey]))
         W0 = P["qnn.mlp.0.weight"]
-        dinter = W.get("dinter", (B, C))
-        dz_mlp = W.get("dz_mlp", (B, FD))
         bf_da = q.get("w0_bf") is not None and dcur_bf is not None and self.bf_ok(B, din, ncur, ncur, 0, din, 0)
-        if a.use_residual and bf_da:   # amp: [dz | dinter] = dcur W0 on bf16 images (W0 k-major: transposed reads)
+        dz_bf = a.use_residual and bf_da
+        dinter = W.get("dinter_bf" if dz_bf else "dinter", (B, C), torch.bfloat16 if dz_bf else torch.float32)
+        dz_mlp = W.get("dz_mlp_bf" if dz_bf else "dz_mlp", (B, FD), torch.bfloat16 if dz_bf else torch.float32)
+        if dz_bf:   # amp: [dz | dinter] = dcur W0 on bf16 images (W0 k-major: transposed reads), bf16 out as
+            # autocast's matmul returns it (the input grad the reference's cat backward splits is bf16)
             self.gemm_bf(B, din, ncur, ptr(dcur_bf), ncur, 0, ptr(q["w0_bf"]), din, 0, ptr(dz_mlp), FD,
-                         seg=_lib.GemmSeg(C2=ptr(dinter), ldc2=C, nc=FD))
+                         seg=_lib.GemmSeg(C2=ptr(dinter), ldc2=C, nc=FD), out_bf16=True)
         elif a.use_residual:     # [dz | dinter] = dcur W0: one GEMM, output split at column FD
             self.gemm(B, FD + C, ncur, ptr(dcur), ncur, 0, ptr(W0), din, 0, ptr(dz_mlp), FD,
                       seg=_lib.GemmSeg(C2=ptr(dinter), ldc2=C, nc=FD))
@@ -964,7 +968,7 @@ class Engine:
         dq_ = drop_args(seed, SITE_QNN, a.qnn_p, training)
         Cr = C // a.se_r if a.use_se else 1
         sws = W.get("se_ws", (_lib.query("ctr_se_bwd_ws", B, C) // 4 + 1,))
-        call("ctr_se_bwd", ptr(dinter), C, ptr(q["inter_pre"]), B, C, Cr, ptr(q["gate"]), ptr(q["g1"]),
+        call("ctr_se_bwd", ptr(dinter), C, int(dz_bf), ptr(q["inter_pre"]), B, C, Cr, ptr(q["gate"]), ptr(q["g1"]),
              ptr(q["mean"]), ptr(P.get("qnn.se.fc.0.weight")), ptr(P.get("qnn.se.fc.2.weight")), *dq_, ptr(dinter_pre),
              ptr(G.get("qnn.se.fc.0.weight")), ptr(G.get("qnn.se.fc.0.bias")), ptr(G.get("qnn.se.fc.2.weight")),
              ptr(G.get("qnn.se.fc.2.bias")), ptr(sws), st)
@@ -979,7 +983,7 @@ class Engine:
         dz = W.get("dz", (B, FD))
         DS = W.get("qDS", (B, QR))
         call("ctr_qnn_gram_bwd", ptr(q["z"]), B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]), ptr(dquad),
-             ptr(dz_mlp) if a.use_residual else None, ptr(dz), ptr(DS), st)
+             ptr(dz_mlp) if a.use_residual else None, int(dz_bf), ptr(dz), ptr(DS), st)
         # dUcat = 2 (zsum^T DS - sum_b G_b Ucat diag(dquad_b))
         T1 = W.get("qT1", (D, QR))
         T = W.get("qT", (D * D, QR))
