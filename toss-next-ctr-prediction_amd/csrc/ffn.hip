@@ -887,6 +887,24 @@ __device__ __forceinline__ f32x2 cdf_as2(f32x2 z, f32x2& e) {
   return f32x2{z.x < 0.f ? h.x : q.x, z.y < 0.f ? h.y : q.y};
 }
 
+// GELU of two elements for the forward (cdf_as2's erfc fit): z Phi(z) = max(z, 0) - |z| h with
+// h = erfc(|z| / sqrt 2) / 2 -- one fused multiply-add where z * (z < 0 ? h : 1 - h) took a subtract, two
+// compares, two selects and a multiply; the backward recomputes its fo as z * cdf_as2(z), the same value to
+// within fp32 rounding (both are rounded to bf16 for the products)
+__device__ __forceinline__ f32x2 gelu_as2(f32x2 z) {
+  const f32x2 az = {fabsf(z.x), fabsf(z.y)};
+  const f32x2 d = az * (0.70710678118654752f * 0.3275911f) + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * (0.5f * 1.061405429f) + (0.5f * -1.453152027f);
+  p = p * t + (0.5f * 1.421413741f);
+  p = p * t + (0.5f * -0.284496736f);
+  p = p * t + (0.5f * 0.254829592f);
+  const f32x2 ar = z * z * -0.72134752044448170f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(ar.x), __builtin_amdgcn_exp2f(ar.y)};
+  const f32x2 h = p * t * e;
+  return __builtin_elementwise_fma(-az, h, f32x2{fmaxf(z.x, 0.f), fmaxf(z.y, 0.f)});
+}
+
 // rows [m0, m0 + RT) of a (M, D) matrix -> fp32 LDS tile, row stride D + 4 (zero rows past M)
 template <int D, int RT>
 __device__ __forceinline__ void load_rows(const float* __restrict__ src, int M, int m0, float* dst) {
@@ -1143,7 +1161,7 @@ __global__ __launch_bounds__(256) void ffn_fwd_bfp_kernel(FfnArgs a) {
       for (int i = 0; i < T::NI; ++i)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-          p[i][s2] = f32x4{0.f, 0.f, 0.f, 0.f};
+          p[i][s2] = W.b[s2];      // pre^T accumulates onto b1 (register r of lane group g: column 4g + r)
 #pragma unroll
           for (int kh = 0; kh < T::KH; ++kh) p[i][s2] = mfma_bf(W.w1[s2][kh], xf[i][kh], p[i][s2]);
         }
@@ -1156,9 +1174,8 @@ __global__ __launch_bounds__(256) void ffn_fwd_bfp_kernel(FfnArgs a) {
         for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
-            const f32x2 z = {p[i][s2][2 * q] + W.b[s2][2 * q], p[i][s2][2 * q + 1] + W.b[s2][2 * q + 1]};
-            f32x2 e;
-            f32x2 v = z * cdf_as2(z, e);
+            const f32x2 z = {p[i][s2][2 * q], p[i][s2][2 * q + 1]};
+            f32x2 v = gelu_as2(z);
             if (DROP) {
               const uint32_t hb = drop_pair_bits(a.drop, (m * (uint32_t)FF + f0 + 16 * s2 + 4 * g + 2 * q) >> 1);
               const bool k0 = (hb & 0xFFFFu) >= thr, k1 = (hb >> 16) >= thr;
