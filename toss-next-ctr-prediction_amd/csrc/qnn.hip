@@ -160,12 +160,28 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
   }
 }
 
+// the residual addend of the Gram backward: fp32, or bf16 (amp) loaded as a zero-extended 16-bit word into a full
+// register and widened at its use -- as a __bf16 value the loads went to register halves (d16), each waiting
+// for the one before it
+template <class TA>
+struct GramAdd {
+  using R = float;
+  static __device__ __forceinline__ R load(const float* p) { return *p; }
+  static __device__ __forceinline__ float widen(R r) { return r; }
+};
+template <>
+struct GramAdd<__bf16> {
+  using R = uint32_t;
+  static __device__ __forceinline__ R load(const __bf16* p) { return *(const unsigned short*)p; }
+  static __device__ __forceinline__ float widen(R r) { return __builtin_bit_cast(float, r << 16); }
+};
+
 // One sample per 4-wave workgroup: M = U diag(dquad) U^T (MFMA over the QR columns; the waves share its
 // 16x16 tiles via LDS) and w = U (dquad o S) (QR quarters summed in fixed wave order); then the waves take
 // every fourth 16-row F block: dz_f = 2 w - 2 M z_f (+ dz_add) with M's C-layout registers as the B
 // operand (k-set {16i+4g+r}).  (One wave per sample left only 4 waves per SIMD at B = 4096, each a long
 // serial load -> MFMA chain.)
-template <int D, class TA>
+template <int D, class TA, bool ADD>
 __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restrict__ z, int B, int F,
                                                            const float* __restrict__ ucat, int QR,
                                                            const float* __restrict__ S,
@@ -189,9 +205,10 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
 #endif
   constexpr int PF = QNN_PF;
   const float* zb = z + (long)b * F * D;
-  const TA* ab = dz_add ? dz_add + (long)b * F * D : nullptr;
+  const TA* ab = ADD ? dz_add + (long)b * F * D : nullptr;
   f32x4 zpre[PF][NT];
-  float apre[PF][4][NT];
+  using AR = typename GramAdd<TA>::R;
+  AR apre[PF][4][NT];
   {
     const int w0 = threadIdx.x >> 6, l0 = threadIdx.x & 63, g0 = l0 >> 4, c0 = l0 & 15;
 #pragma unroll
@@ -199,12 +216,13 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
       const int f0 = 16 * w0 + 64 * it, fa = f0 + c0;
 #pragma unroll
       for (int i = 0; i < NT; ++i)
-        zpre[it][i] = fa < F ? *(const f32x4*)(zb + (long)fa * D + 16 * i + 4 * g0) : f32x4{0.f, 0.f, 0.f, 0.f};
+        zpre[it][i] = *(const f32x4*)(zb + (long)(fa < F ? fa : F - 1) * D + 16 * i + 4 * g0);   // rows past F: never stored
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = f0 + 4 * g0 + r;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) apre[it][r][j] = (ab && f < F) ? (float)ab[(long)f * D + 16 * j + c0] : 0.f;
+        for (int j = 0; j < NT; ++j)     // rows past F: row F - 1 re-read (in bounds, never stored)
+          apre[it][r][j] = ADD ? GramAdd<TA>::load(ab + (long)(f < F ? f : F - 1) * D + 16 * j + c0) : AR(0);
       }
     }
   }
@@ -267,7 +285,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
     for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the lane's four A values of a 16-column block are contiguous: one 16-byte load per block
     f32x4 zq[NT];
-    float aq[4][NT];
+    AR aq[4][NT];
     if (it < PF) {
 #pragma unroll
       for (int q = 0; q < PF; ++q)
@@ -282,12 +300,13 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
     } else {
 #pragma unroll
       for (int i = 0; i < NT; ++i)
-        zq[i] = fa < F ? *(const f32x4*)(zb + (long)fa * D + 16 * i + 4 * g) : f32x4{0.f, 0.f, 0.f, 0.f};
+        zq[i] = *(const f32x4*)(zb + (long)(fa < F ? fa : F - 1) * D + 16 * i + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = f0 + 4 * g + r;
 #pragma unroll
-        for (int j = 0; j < NT; ++j) aq[r][j] = (ab && f < F) ? (float)ab[(long)f * D + 16 * j + c] : 0.f;
+        for (int j = 0; j < NT; ++j)
+          aq[r][j] = ADD ? GramAdd<TA>::load(ab + (long)(f < F ? f : F - 1) * D + 16 * j + c) : AR(0);
       }
     }
 #pragma unroll
@@ -305,7 +324,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
         for (int j = 0; j < NT; ++j) {
           const int e = 16 * j + c;
           float v = wv[j] - 2.f * acc[j][r];
-          if (ab) v += aq[r][j];
+          if (ADD) v += GramAdd<TA>::widen(aq[r][j]);
           ob[(long)f * D + e] = v;
         }
       }
@@ -485,22 +504,22 @@ extern "C" int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float
   return check_launch("qnn_gram_fwd");
 }
 
-template <class TA>
+template <class TA, bool ADD>
 static void gram_bwd_launch(int D, int blocks, size_t sm, hipStream_t s, const float* z, int B, int F, const float* ucat,
                             int QR, const float* S, const float* dquad, const TA* dz_add, float* dz, float* DS) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<16, TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<32, TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<64, TA>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<16, TA, ADD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<32, TA, ADD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<64, TA, ADD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  if (D == 16) qnn_gram_bwd_kernel<16, TA><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
-  else if (D == 32) qnn_gram_bwd_kernel<32, TA><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
-  else qnn_gram_bwd_kernel<64, TA><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  if (D == 16) qnn_gram_bwd_kernel<16, TA, ADD><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else if (D == 32) qnn_gram_bwd_kernel<32, TA, ADD><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else qnn_gram_bwd_kernel<64, TA, ADD><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
 }
 
 extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
@@ -513,8 +532,9 @@ extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float
                     sizeof(float);
   CTR_REQUIRE(sm <= 160 * 1024, "qnn gram bwd: U + M partials exceed LDS");
   hipStream_t s = (hipStream_t)stream;
-  if (add_bf16) gram_bwd_launch(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const __bf16*)dz_add, dz, DS);
-  else gram_bwd_launch(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const float*)dz_add, dz, DS);
+  if (!dz_add) gram_bwd_launch<float, false>(D, B, sm, s, z, B, F, ucat, QR, S, dquad, nullptr, dz, DS);
+  else if (add_bf16) gram_bwd_launch<__bf16, true>(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const __bf16*)dz_add, dz, DS);
+  else gram_bwd_launch<float, true>(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const float*)dz_add, dz, DS);
   return check_launch("qnn_gram_bwd");
 }
 
