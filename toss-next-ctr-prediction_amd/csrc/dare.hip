@@ -116,12 +116,20 @@ __global__ __launch_bounds__(256) void topk_bwd_kernel(const int* __restrict__ t
   const int* tb = tok + (long)b * K;
   const float* dv = dvals + (long)b * K;
   // keys in chunks of TB_CH: the chunk's token / weight loads, then its row gathers, all independent (one memory
-  // round trip each per chunk instead of a token -> row dependency per key); summed in ascending k as before
+  // round trip each per chunk instead of a token -> row dependency per key); summed in ascending k as before.
+  // The att contributions dvals * q and the keys are written from the same chunk registers (a separate pass
+  // re-loaded the token and weight of every (k, d) one dependent round trip after another), and the gathers are
+  // unconditional -- the padding token reads row 0, its term dropped at the add (a conditional load put its use,
+  // and a wait, inside a branch per key)
   constexpr int TB_CH = 16;
+  float* ac = att_contrib + (long)b * K * D;
+  uint32_t* ak = att_keys + (long)b * K;
+  uint32_t* rk = rep_keys + (long)b * K;
   if (D <= 32) {    // two half-waves take the even / odd k, combined in a fixed order
     const int d = lane & 31, h = lane >> 5;
     float acc = 0.f;
     if (d < D) {
+      const float qd = q[(long)b * D + d];
       for (int k0 = h; k0 < K; k0 += 2 * TB_CH) {
         int t[TB_CH];
         float w[TB_CH], e[TB_CH];
@@ -132,16 +140,27 @@ __global__ __launch_bounds__(256) void topk_bwd_kernel(const int* __restrict__ t
           w[u] = k < K ? dv[k] : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < TB_CH; ++u) e[u] = t[u] != pad_id ? E_att[(long)t[u] * D + d] : 0.f;
+        for (int u = 0; u < TB_CH; ++u) e[u] = E_att[(long)(t[u] != pad_id ? t[u] : 0) * D + d];
 #pragma unroll
-        for (int u = 0; u < TB_CH; ++u)
+        for (int u = 0; u < TB_CH; ++u) {
+          const int k = k0 + 2 * u;
           if (t[u] != pad_id) acc = fmaf(w[u], e[u], acc);
+          if (k < K) {
+            ac[(long)k * D + d] = t[u] != pad_id ? w[u] * qd : 0.f;
+            if (d == 0) {
+              const uint32_t key = t[u] != pad_id ? (uint32_t)t[u] : INVALID_KEY;
+              ak[k] = key;
+              rk[k] = key;
+            }
+          }
+        }
       }
     }
     const float other = __shfl_down(acc, 32);
     if (h == 0 && d < D) dq[(long)b * D + d] = acc + other;
   } else if (lane < D) {
     float acc = 0.f;
+    const float qd = q[(long)b * D + lane];
     for (int k0 = 0; k0 < K; k0 += TB_CH) {
       int t[TB_CH];
       float w[TB_CH], e[TB_CH];
@@ -152,23 +171,22 @@ __global__ __launch_bounds__(256) void topk_bwd_kernel(const int* __restrict__ t
         w[u] = k < K ? dv[k] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < TB_CH; ++u) e[u] = t[u] != pad_id ? E_att[(long)t[u] * D + lane] : 0.f;
+      for (int u = 0; u < TB_CH; ++u) e[u] = E_att[(long)(t[u] != pad_id ? t[u] : 0) * D + lane];
 #pragma unroll
-      for (int u = 0; u < TB_CH; ++u)
+      for (int u = 0; u < TB_CH; ++u) {
+        const int k = k0 + u;
         if (t[u] != pad_id) acc = fmaf(w[u], e[u], acc);
+        if (k < K) {
+          ac[(long)k * D + lane] = t[u] != pad_id ? w[u] * qd : 0.f;
+          if (lane == 0) {
+            const uint32_t key = t[u] != pad_id ? (uint32_t)t[u] : INVALID_KEY;
+            ak[k] = key;
+            rk[k] = key;
+          }
+        }
+      }
     }
     dq[(long)b * D + lane] = acc;
-  }
-  for (int e = lane; e < K * D; e += 64) {
-    const int k = e / D, d = e % D;
-    const int t = tb[k];
-    att_contrib[((long)b * K + k) * D + d] = t != pad_id ? dv[k] * q[(long)b * D + d] : 0.f;
-  }
-  for (int k = lane; k < K; k += 64) {
-    const int t = tb[k];
-    const uint32_t key = t != pad_id ? (uint32_t)t : INVALID_KEY;
-    att_keys[(long)b * K + k] = key;
-    rep_keys[(long)b * K + k] = key;
   }
 }
 

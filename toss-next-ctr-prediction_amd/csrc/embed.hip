@@ -390,13 +390,25 @@ __device__ __forceinline__ float ctx_wave_mean(const float* __restrict__ x, int 
     const int dq = lane % Dq, pp = lane / Dq;
     f4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
     if (pp < P) {
+      // the part's features i = 0, 1, ... (f = pp + i P): even i into a0, odd into a1, eight loads issued before
+      // their adds (two per iteration left one round trip per pair of loads)
       const f4* x4 = (const f4*)x;
-      int f = pp;
-      for (; f + P < F; f += 2 * P) {
-        a0 += x4[(long)f * Dq + dq];
-        a1 += x4[(long)(f + P) * Dq + dq];
+      const int nf = F > pp ? (F - pp + P - 1) / P : 0;
+      for (int i0 = 0; i0 < nf; i0 += 8) {
+        f4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + u < nf ? i0 + u : nf - 1;
+          v[u] = x4[(long)(pp + i * P) * Dq + dq];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (i0 + u < nf) {
+            if (u & 1) a1 += v[u];
+            else a0 += v[u];
+          }
+        }
       }
-      if (f < F) a0 += x4[(long)f * Dq + dq];
     }
     const f4 v = a0 + a1;
     if (pp < P) *(f4*)&sp[(pp * Dq + dq) * 4] = v;

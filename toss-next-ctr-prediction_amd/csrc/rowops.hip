@@ -459,14 +459,28 @@ __global__ __launch_bounds__(1024) void loss_kernel(const float* __restrict__ z,
                                                     float* __restrict__ dza) {
   __shared__ float red[16][5];
   float npos = 0.f, sp = 0.f, sn = 0.f, spa = 0.f, sna = 0.f;
-  for (int i = threadIdx.x; i < B; i += 1024) {
-    const bool pos = y[i] > 0.5f;
-    npos += pos ? 1.f : 0.f;
-    if (pos) sp += softplus_f(-z[i]);
-    else sn += softplus_f(z[i]);
-    if (za) {
-      if (pos) spa += softplus_f(-za[i]);
-      else sna += softplus_f(za[i]);
+  // a thread's elements i = t, t + 1024, ... in chunks of four whose loads are issued together (one round trip
+  // per chunk instead of per element: the step's batch of 4096 is one chunk); the same per-thread order
+  for (int i0 = threadIdx.x; i0 < B; i0 += 4 * 1024) {
+    float yv[4], zv[4], zav[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(i0 + 1024 * u, B - 1);
+      yv[u] = y[i];
+      zv[u] = z[i];
+      zav[u] = za ? za[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + 1024 * u >= B) break;
+      const bool pos = yv[u] > 0.5f;
+      npos += pos ? 1.f : 0.f;
+      if (pos) sp += softplus_f(-zv[u]);
+      else sn += softplus_f(zv[u]);
+      if (za) {
+        if (pos) spa += softplus_f(-zav[u]);
+        else sna += softplus_f(zav[u]);
+      }
     }
   }
   {  // the five block sums in one LDS round (each: wave sums, then the 16 waves in order)
@@ -497,27 +511,40 @@ __global__ __launch_bounds__(1024) void loss_kernel(const float* __restrict__ z,
   }
   if (threadIdx.x == 0) loss[0] = L;
   // d softplus(x)/dx = sigmoid(x) (torch: 1 above the threshold 20)
-  for (int i = threadIdx.x; i < B; i += 1024) {
-    const bool pos = y[i] > 0.5f;
-    float g;
-    if (pos) {
-      const float x = -z[i];
-      g = -(x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / npos);
-    } else {
-      const float x = z[i];
-      g = (x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / nneg);
+  for (int i0 = threadIdx.x; i0 < B; i0 += 4 * 1024) {
+    float yv[4], zv[4], zav[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = min(i0 + 1024 * u, B - 1);
+      yv[u] = y[i];
+      zv[u] = z[i];
+      zav[u] = za ? za[i] : 0.f;
     }
-    dz[i] = g;
-    if (za) {
-      float ga;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + 1024 * u;
+      if (i >= B) break;
+      const bool pos = yv[u] > 0.5f;
+      float g;
       if (pos) {
-        const float x = -za[i];
-        ga = -(x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / npos);
+        const float x = -zv[u];
+        g = -(x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / npos);
       } else {
-        const float x = za[i];
-        ga = (x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / nneg);
+        const float x = zv[u];
+        g = (x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / nneg);
       }
-      dza[i] = aux_w * ga;
+      dz[i] = g;
+      if (za) {
+        float ga;
+        if (pos) {
+          const float x = -zav[u];
+          ga = -(x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / npos);
+        } else {
+          const float x = zav[u];
+          ga = (x > 20.f ? 1.f : sigmoid_f(x)) * (0.5f / nneg);
+        }
+        dza[i] = aux_w * ga;
+      }
     }
   }
 }
