@@ -135,7 +135,8 @@ int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const 
                       const long* proj_off, const int* dims, int row_ld, int D, float* cat_e, float* xf, long xf_ld,
                       uint32_t drop_key, uint32_t drop_thresh, float drop_scale, void* stream);
 size_t ctr_cat_embed_bwd_ws(int B, int Fc);
-/* backward: row-grad contributions (B*Fc rows x 64, zero-padded) keyed row_base[c] + X_cat[b,c] for
+/* backward: row-grad contributions (B*Fc rows x 64; columns k < d_c written, the rest left as they are --
+ * pass a buffer zero-filled once, as its padding is never written) keyed row_base[c] + X_cat[b,c] for
  * ctr_rowgrad, and dP_c written into grad_arena + proj_goff[c].                                    */
 int ctr_cat_embed_bwd(const int* xcat, int B, int Fc, const float* arena, const float* tab_base, const long* tab_off,
                       const long* proj_off, const int* dims, int row_ld, int D, const float* dcat,

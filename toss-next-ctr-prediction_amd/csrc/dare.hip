@@ -263,6 +263,7 @@ struct PoolBwdArgs {
 __global__ __launch_bounds__(64) void pool_bwd_kernel(PoolBwdArgs a) {
   __shared__ float sdu[64];
   __shared__ float sdw[256];
+  __shared__ float swk[256];
   const PoolArgs& f = a.f;
   const int b = blockIdx.x, lane = threadIdx.x;
   const int K = f.K, D = f.D;
@@ -273,24 +274,27 @@ __global__ __launch_bounds__(64) void pool_bwd_kernel(PoolBwdArgs a) {
     if (f.drop.thresh) g = drop_keep(f.drop, (uint32_t)((long)b * D + lane)) ? g * f.drop.scale : 0.f;
   }
   sdu[lane] = g;
-  __syncthreads();
   const float* xb = f.x + (long)b * K * D;
   const float* wb = f.w + (long)b * K;
+  // the sample's gate weights staged in LDS: read from global inside the dx loop they were re-loaded after every
+  // dx store (the pointers may alias), one round trip per element group
+  for (int k = lane; k < K; k += 64) swk[k] = wb[k];
+  __syncthreads();
   for (int e = lane; e < K * D; e += 64) {
     const int k = e / D, d = e % D;
-    a.dx[(long)b * K * D + e] = wb[k] * sdu[d];
+    a.dx[(long)b * K * D + e] = swk[k] * sdu[d];
   }
   float dot = 0.f;
   for (int k = lane; k < K; k += 64) {
     float s = 0.f;
     for (int d = 0; d < D; ++d) s = fmaf(xb[(long)k * D + d], sdu[d], s);
     sdw[k] = s;
-    dot += (f.gating == 0 ? wb[k] * s : s * fmaxf(f.vals[(long)b * K + k], 0.f));
+    dot += (f.gating == 0 ? swk[k] * s : s * fmaxf(f.vals[(long)b * K + k], 0.f));
   }
   dot = wave_sum(dot);
   __syncthreads();
   if (f.gating == 0) {
-    for (int k = lane; k < K; k += 64) a.dvals[(long)b * K + k] = wb[k] * (sdw[k] - dot);
+    for (int k = lane; k < K; k += 64) a.dvals[(long)b * K + k] = swk[k] * (sdw[k] - dot);
   } else {
     // w = r / (S + eps), r = relu(v): dv_k = [v_k>0] (dw_k/(S+eps) - sum_j dw_j r_j/(S+eps)^2)
     float S = 0.f;

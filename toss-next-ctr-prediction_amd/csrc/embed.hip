@@ -43,8 +43,16 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
     A = fmaf(sW[k], pk, A);
     Bv = fmaf(sB[k], pk, Bv);
   }
-  const int b1 = min(B, b0 + FE_ROWS);
-  for (int b = b0 + rg; b < b1; b += RG) out[(long)b * out_ld + (long)f * D + d] = fmaf(x[(long)b * F + f], A, Bv);
+  // the group's samples b0 + rg + RG i (i < FE_ROWS / RG <= 16 at D <= 64): every x load issued before the stores
+  const int b1 = min(B, b0 + FE_ROWS), nb = FE_ROWS / RG;
+  float xv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xv[i] = x[(long)min(b0 + rg + RG * i, B - 1) * F + f];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int b = b0 + rg + RG * i;
+    if (i < nb && b < b1) out[(long)b * out_ld + (long)f * D + d] = fmaf(xv[i], A, Bv);
+  }
 }
 
 // per (feature f, sample chunk): S1[f,d] = sum_b x[b,f] dout[b,f,d], S0[f,d] = sum_b dout[b,f,d]
@@ -59,10 +67,20 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restri
   const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
   float s1 = 0.f, s0 = 0.f;
   if (rg < RG)
-    for (int b = b0 + rg; b < b1; b += RG) {
-      const float g = dout[(long)b * dout_ld + (long)f * D + d];
-      s1 = fmaf(x[(long)b * F + f], g, s1);
-      s0 += g;
+    for (int bb = b0 + rg; bb < b1; bb += 8 * RG) {     // eight rows' loads issued together, summed in row order
+      float gv[8], xv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int b = min(bb + RG * i, b1 - 1);
+        gv[i] = dout[(long)b * dout_ld + (long)f * D + d];
+        xv[i] = x[(long)b * F + f];
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (bb + RG * i >= b1) break;
+        s1 = fmaf(xv[i], gv[i], s1);
+        s0 += gv[i];
+      }
     }
   r1[t] = s1;
   r0[t] = s0;
@@ -227,17 +245,20 @@ __global__ __launch_bounds__(256) void cat_embed_bwd_rows(const int* __restrict_
     sG[i * CE_LD + d] = dcat[((long)(b0 + i) * Fc + c) * D + d];
   }
   __syncthreads();
-  for (int e = tid; e < nb * 64; e += 256) {
-    const int i = e >> 6, k = e & 63;
+  // items (sample, k < dc) only: the columns past d_c of a contribution row stay zero from the buffer's first fill
+  // (a slot (b, c) always holds table c), so the 64-wide rows' padding is not rewritten every step
+  for (int e = tid; e < nb * dc; e += 256) {
+    const int i = e / dc, k = e - i * dc;
     const long bc = (long)(b0 + i) * Fc + c;
+    const float* g = sG + i * CE_LD;
     float acc = 0.f;
-    if (k < dc) {
-      const float* g = sG + i * CE_LD;
 #pragma unroll 8
-      for (int d = 0; d < D; ++d) acc = fmaf(g[d], sP[d * CE_LD + k], acc);
-    }
+    for (int d = 0; d < D; ++d) acc = fmaf(g[d], sP[d * CE_LD + k], acc);
     contrib[bc * 64 + k] = acc;
-    if (k == 0) keys[bc] = row_base[c] + (uint32_t)xcat[bc];
+  }
+  if (tid < nb) {
+    const long bc = (long)(b0 + tid) * Fc + c;
+    keys[bc] = row_base[c] + (uint32_t)xcat[bc];
   }
 }
 

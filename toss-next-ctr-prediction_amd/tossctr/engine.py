@@ -763,7 +763,7 @@ class Engine:
                  ptr(G["mask_embed.weight"]), None, ptr(G["mask_embed.out_proj.weight"]), ptr(fw), st)
         # ---------------- categorical tables + projections
         n_cat = B * a.Fc
-        cat_c = W.get("cat_contrib", (n_cat, 64))
+        cat_c = W.get_zeroed("cat_contrib", (n_cat, 64))     # columns past a table's d_c: zero, never written
         cat_k = W.get("cat_keys", (n_cat,), torch.int32)
         cws = W.get("cat_ws", (_lib.query("ctr_cat_embed_bwd_ws", B, a.Fc) // 4 + 1,))
         call("ctr_cat_embed_bwd", ptr(tv["xcat"]), B, a.Fc, ptr(self.arena.buf), tv["cat_tab"], tv["cat_off"],
