@@ -106,11 +106,25 @@ __global__ __launch_bounds__(1024) void feat_embed_bwd_final(int nchunk, int F, 
                                                             float* __restrict__ dP) {
   extern __shared__ float sS[];          // [2][F][D] | P [D][fe] | W [F][fe] | bias [F][fe]
   const int n2 = 2 * F * D;
-  for (int q = threadIdx.x; q < n2; q += blockDim.x) {
-    float v = 0.f;
-#pragma unroll 4
-    for (int c = 0; c < nchunk; ++c) v += part[(long)c * n2 + q];
-    sS[q] = v;
+  // two elements' chunk partials (nchunk <= 16 each) loaded together, then summed in chunk order: one round trip
+  // per two elements instead of one per four loads
+  for (int q0 = threadIdx.x; q0 < n2; q0 += 2 * blockDim.x) {
+    float v[2][16];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = min(q0 + h * (int)blockDim.x, n2 - 1);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) v[h][c] = part[(long)min(c, nchunk - 1) * n2 + q];
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int q = q0 + h * (int)blockDim.x;
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (c < nchunk) t += v[h][c];
+      if (q < n2) sS[q] = t;
+    }
   }
   float* sPm = sS + n2;
   float* sWm = sPm + D * fe;
@@ -584,14 +598,26 @@ __global__ __launch_bounds__(CTXB_T) void context_bwd_kernel(CtxBwdArgs a) {
   }
   __syncthreads();
   // dnum += g_num[d], dmask += g_mask[d]: 16-byte read-modify-writes when the rows allow it
+  // (each thread's read-modify-writes in groups of four: the group's loads issued before its stores -- in a plain
+  // loop every load followed the previous store to the same array, one round trip per element)
   auto bcast_add = [&](float* dst, int F, const float* g) {
     const int n = F * D;
     if ((D & 3) == 0 && (((uintptr_t)dst) & 15) == 0) {
       typedef float f4 __attribute__((ext_vector_type(4)));
       f4* d4 = (f4*)dst;
-      for (int e4 = t; e4 < (n >> 2); e4 += CTXB_T) {
-        const int d = (e4 << 2) % D;
-        d4[e4] += f4{g[d], g[d + 1], g[d + 2], g[d + 3]};
+      const int n4 = n >> 2;
+      for (int e0 = t; e0 < n4; e0 += 4 * CTXB_T) {
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = d4[min(e0 + u * CTXB_T, n4 - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e4 = e0 + u * CTXB_T;
+          if (e4 < n4) {
+            const int d = (e4 << 2) % D;
+            d4[e4] = v[u] + f4{g[d], g[d + 1], g[d + 2], g[d + 3]};
+          }
+        }
       }
     } else {
       for (int e = t; e < n; e += CTXB_T) dst[e] += g[e % D];
@@ -601,18 +627,27 @@ __global__ __launch_bounds__(CTXB_T) void context_bwd_kernel(CtxBwdArgs a) {
   if (f.Fm > 0) bcast_add(a.dmask + (long)b * f.mask_ld, f.Fm, sg[1]);
   const int fc0 = 1 + (f.Fn > 0) + (f.Fm > 0);
   const int n = f.Fc * D;
-  for (int e = t; e < n; e += CTXB_T) {
-    const int c = e / D, d = e - c * D;
-    const long q = (long)b * n + e;
-    float g = 0.f;
-    if (a.dxf_cat) {
-      const float gx = a.dxf_cat[(long)b * a.dxf_ld + e];
-      g = a.emb_drop.thresh ? (drop_keep(a.emb_drop, (uint32_t)q) ? gx * a.emb_drop.scale : 0.f) : gx;
+  for (int e0 = t; e0 < n; e0 += 8 * CTXB_T) {      // eight elements' loads per thread issued together
+    float gx[8], gf[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = min(e0 + u * CTXB_T, n - 1);
+      gx[u] = a.dxf_cat ? a.dxf_cat[(long)b * a.dxf_ld + e] : 0.f;
+      gf[u] = a.dfc ? a.dfc[(long)b * a.dfc_ld + (long)fc0 * D + e] : 0.f;
     }
-    if (a.dfc) g += a.dfc[(long)b * a.dfc_ld + (long)fc0 * D + e];
-    if (c == f.qi) g += sq[d];
-    g += sg[2][d];
-    a.dcat[q] = g;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = e0 + u * CTXB_T;
+      if (e >= n) break;
+      const int c = e / D, d = e - c * D;
+      const long q = (long)b * n + e;
+      float g = 0.f;
+      if (a.dxf_cat) g = a.emb_drop.thresh ? (drop_keep(a.emb_drop, (uint32_t)q) ? gx[u] * a.emb_drop.scale : 0.f) : gx[u];
+      if (a.dfc) g += gf[u];
+      if (c == f.qi) g += sq[d];
+      g += sg[2][d];
+      a.dcat[q] = g;
+    }
   }
 }
 
@@ -631,7 +666,7 @@ extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, 
   return check_launch("feat_embed_fwd");
 }
 
-static int fe_chunks(int B) { return std::max(1, std::min(16, cdiv(B, 256))); }
+static int fe_chunks(int B) { return std::max(1, std::min(16, cdiv(B, 256))); }   // <= 16: feat_embed_bwd_final
 
 extern "C" size_t ctr_feat_embed_bwd_ws(int B, int F, int D) {
   return (size_t)fe_chunks(B) * 2 * F * D * sizeof(float);

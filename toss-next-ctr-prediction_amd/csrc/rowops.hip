@@ -38,12 +38,18 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big_vec(const float* __restri
   const long row = blockIdx.x;
   const f4* xr = (const f4*)(x + row * ldx);
   const int n4 = N >> 2;
-  f4 v[NQ];
+  f4 v[NQ], wv[NQ];
   float ss = 0.f;
+  const f4* w4 = (const f4*)w;
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
     const int j = threadIdx.x + 256 * k;
     v[k] = j < n4 ? xr[j] : f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {       // the weights too, before the row reduction's barrier (not one round trip after)
+    const int j = threadIdx.x + 256 * k;
+    wv[k] = w4[j < n4 ? j : 0];
   }
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
@@ -56,12 +62,11 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big_vec(const float* __restri
   const float rr = 1.0f / sqrtf(ss / (float)N + eps);
   if (threadIdx.x == 0) r[row] = rr;
   f4* yr = (f4*)(y + row * ldy);
-  const f4* w4 = (const f4*)w;
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
     const int j = threadIdx.x + 256 * k;
     if (j < n4) {
-      const f4 o = w4[j] * v[k] * rr;
+      const f4 o = wv[k] * v[k] * rr;
       yr[j] = o;
       if (ybf) *(b4*)(ybf + row * ldybf + 4 * j) = __builtin_convertvector(o, b4);   // amp: the GEMM's bf16 image
     }
