@@ -5,14 +5,12 @@
 // 10M x D dense grad, contributions (key = row id, value = one grad row) are
 //   1. stably radix-sorted by key (rocPRIM, library primitive; stable => members of a key keep
 //      their contribution order),
-//   2. run-length encoded into (unique key, count), counts exclusive-scanned into offsets,
+//   2. run-length grouped into (unique key, first index) by two small kernels (rle_count / rle_write),
 //   3. summed per unique key by one wave each, in contribution order (bitwise reproducible).
 // The optimizer stream (optim.hip) then reads the compact (keys, rows) directly.
 // Keys equal to INVALID (0xFFFFFFFF: pad tokens, whose grads padding_idx drops) sort last.
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_run_length_encode.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 #include "common.h"
 #include "ctr_hip.h"
@@ -23,13 +21,92 @@ __global__ void iota_kernel(uint32_t* v, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = (uint32_t)i;
 }
 
+// Run-length groups of the sorted keys without rocPRIM's run_length_encode / exclusive_scan: their lookback scans
+// query hipGetDeviceProperties on the host at every call (is_sleep_scan_state_used), which stalled the host's
+// issue of the step's other stream for ~0.1 ms per dedupe.  Two passes over RLE_CH-key blocks: (1) each block
+// counts its run heads (i == 0 or key[i] != key[i-1]); (2) each block sums the counts of the blocks before it
+// (<= a few hundred words, in order), scans its threads' head counts in LDS and writes, per run, the unique key and
+// its first index; the last block writes n_uniq and offsets[n_uniq] = n, so a run's length is
+// offsets[u + 1] - offsets[u].  Deterministic and in key order, as the rocPRIM pair was.
+constexpr int RLE_T = 256, RLE_IPT = 8, RLE_CH = RLE_T * RLE_IPT;
+
+__device__ __forceinline__ uint32_t rle_heads(const uint32_t* __restrict__ skeys, int n, int i0, bool (&h)[RLE_IPT]) {
+  uint32_t k[RLE_IPT + 1];
+  k[0] = i0 > 0 && i0 - 1 < n ? skeys[i0 - 1] : 0u;
+#pragma unroll
+  for (int u = 0; u < RLE_IPT; ++u) k[u + 1] = skeys[min(i0 + u, n - 1)];
+  uint32_t c = 0;
+#pragma unroll
+  for (int u = 0; u < RLE_IPT; ++u) {
+    const int i = i0 + u;
+    h[u] = i < n && (i == 0 || k[u + 1] != k[u]);
+    c += h[u] ? 1u : 0u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ uint32_t rle_block_sum(uint32_t v, uint32_t* red) {
+  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int w = 0; w < RLE_T / 64; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+__global__ __launch_bounds__(RLE_T) void rle_count_kernel(const uint32_t* __restrict__ skeys, int n,
+                                                          uint32_t* __restrict__ bcount) {
+  __shared__ uint32_t red[RLE_T / 64];
+  bool h[RLE_IPT];
+  const uint32_t c = rle_heads(skeys, n, blockIdx.x * RLE_CH + threadIdx.x * RLE_IPT, h);
+  const uint32_t t = rle_block_sum(c, red);
+  if (threadIdx.x == 0) bcount[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(RLE_T) void rle_write_kernel(const uint32_t* __restrict__ skeys, int n,
+                                                          const uint32_t* __restrict__ bcount,
+                                                          uint32_t* __restrict__ uniq_keys,
+                                                          uint32_t* __restrict__ offsets,
+                                                          uint32_t* __restrict__ n_uniq) {
+  __shared__ uint32_t red[RLE_T / 64];
+  __shared__ uint32_t sc[RLE_T];
+  uint32_t pre = 0;
+  for (int q = threadIdx.x; q < (int)blockIdx.x; q += RLE_T) pre += bcount[q];
+  pre = rle_block_sum(pre, red);                 // the heads of the blocks before this one
+  bool h[RLE_IPT];
+  const int i0 = blockIdx.x * RLE_CH + threadIdx.x * RLE_IPT;
+  const uint32_t c = rle_heads(skeys, n, i0, h);
+  sc[threadIdx.x] = c;
+  __syncthreads();
+  for (int o = 1; o < RLE_T; o <<= 1) {          // inclusive scan of the threads' head counts
+    const uint32_t v = threadIdx.x >= o ? sc[threadIdx.x - o] : 0u;
+    __syncthreads();
+    sc[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t seg = pre + sc[threadIdx.x] - c;
+#pragma unroll
+  for (int u = 0; u < RLE_IPT; ++u)
+    if (h[u]) {
+      uniq_keys[seg] = skeys[i0 + u];
+      offsets[seg] = (uint32_t)(i0 + u);
+      ++seg;
+    }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == RLE_T - 1) {
+    const uint32_t total = pre + sc[RLE_T - 1];
+    n_uniq[0] = total;
+    offsets[total] = (uint32_t)n;
+  }
+}
+
 // one wave per unique key, lane = column; members summed in (stable) contribution order.  The
 // INVALID group (pad tokens: dropped by padding_idx) is skipped -- it is by far the largest group
 // (every short history contributes pads to its top-K) and its sum is never read.
 __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ contrib, int ld, int width,
                                                      const uint32_t* __restrict__ uniq_keys,
                                                      const uint32_t* __restrict__ sorted_idx,
-                                                     const uint32_t* __restrict__ counts,
                                                      const uint32_t* __restrict__ offsets,
                                                      const uint32_t* __restrict__ n_uniq, uint32_t n,
                                                      float* __restrict__ out) {
@@ -37,7 +114,7 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ c
   const int lane = threadIdx.x & 63;
   if (u >= n) return;
   // the slot's key / offset / count load beside the unique count (they followed it: one more round trip)
-  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = counts[u];
+  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = offsets[u + 1] - off;
   if (u >= *n_uniq) return;
   if (key == 0xFFFFFFFFu) {
     if (lane < width) out[(long)u * width + lane] = 0.f;
@@ -67,14 +144,13 @@ __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ c
 __global__ __launch_bounds__(256) void segsum2_kernel(const float* __restrict__ ca, const float* __restrict__ cb,
                                                       int ld, int width, const uint32_t* __restrict__ uniq_keys,
                                                       const uint32_t* __restrict__ sorted_idx,
-                                                      const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ offsets,
                                                       const uint32_t* __restrict__ n_uniq, uint32_t n,
                                                       float* __restrict__ oa, float* __restrict__ ob) {
   const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63, c = lane & 31;
   if (u >= n) return;
-  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = counts[u];   // beside the unique count
+  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = offsets[u + 1] - off;   // beside the unique count
   if (u >= *n_uniq) return;
   const float* __restrict__ src = lane < 32 ? ca : cb;
   float* __restrict__ dst = lane < 32 ? oa : ob;
@@ -102,28 +178,33 @@ __global__ __launch_bounds__(256) void segsum2_kernel(const float* __restrict__ 
 struct RowgradWs {
   size_t temp_bytes;
   size_t total;
-  size_t off_iota, off_skeys, off_sidx, off_counts, off_offsets;
+  size_t off_iota, off_skeys, off_sidx, off_bcount, off_offsets;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// the sort's temporary size depends on n only: the last few sizes cached (the step alternates two or three n)
 static RowgradWs rowgrad_layout(int n) {
+  static int cached_n[4] = {-1, -1, -1, -1};
+  static RowgradWs cached[4];
+  static int next = 0;
+  for (int q = 0; q < 4; ++q)
+    if (cached_n[q] == n) return cached[q];
   RowgradWs w{};
-  size_t t1 = 0, t2 = 0, t3 = 0;
+  size_t t1 = 0;
   (void)rocprim::radix_sort_pairs(nullptr, t1, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                            (uint32_t*)nullptr, (size_t)n, 0, 32);
-  (void)rocprim::run_length_encode(nullptr, t2, (const uint32_t*)nullptr, (unsigned)n, (uint32_t*)nullptr,
-                             (uint32_t*)nullptr, (uint32_t*)nullptr);
-  (void)rocprim::exclusive_scan(nullptr, t3, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)n,
-                          rocprim::plus<uint32_t>());
-  w.temp_bytes = align256(std::max(t1, std::max(t2, t3)));
+                                  (uint32_t*)nullptr, (size_t)n, 0, 32);
+  w.temp_bytes = align256(t1);
   const size_t a = align256((size_t)n * sizeof(uint32_t));
   w.off_iota = w.temp_bytes;
   w.off_skeys = w.off_iota + a;
   w.off_sidx = w.off_skeys + a;
-  w.off_counts = w.off_sidx + a;
-  w.off_offsets = w.off_counts + a;
-  w.total = w.off_offsets + a;
+  w.off_bcount = w.off_sidx + a;
+  w.off_offsets = w.off_bcount + align256((size_t)cdiv(n, RLE_CH) * sizeof(uint32_t));
+  w.total = w.off_offsets + align256(((size_t)n + 1) * sizeof(uint32_t));
+  cached_n[next] = n;
+  cached[next] = w;
+  next = (next + 1) & 3;
   return w;
 }
 
@@ -149,26 +230,23 @@ static int rowgrad_core(const uint32_t* keys, const float* const* contrib, float
   uint32_t* iota = (uint32_t*)(base + w.off_iota);
   uint32_t* skeys = (uint32_t*)(base + w.off_skeys);
   uint32_t* sidx = (uint32_t*)(base + w.off_sidx);
-  uint32_t* counts = (uint32_t*)(base + w.off_counts);
+  uint32_t* bcount = (uint32_t*)(base + w.off_bcount);
   uint32_t* offsets = (uint32_t*)(base + w.off_offsets);
   iota_kernel<<<std::min(cdiv(n, 256), 4096), 256, 0, s>>>(iota, n);
   size_t tb = w.temp_bytes;
   hipError_t e = rocprim::radix_sort_pairs(base, tb, keys, skeys, (const uint32_t*)iota, sidx, (size_t)n, 0,
                                            (unsigned)key_bits, s);
   CTR_REQUIRE(e == hipSuccess, "radix_sort_pairs failed");
-  tb = w.temp_bytes;
-  e = rocprim::run_length_encode(base, tb, (const uint32_t*)skeys, (unsigned)n, uniq_keys, counts, n_uniq, s);
-  CTR_REQUIRE(e == hipSuccess, "run_length_encode failed");
-  tb = w.temp_bytes;
-  e = rocprim::exclusive_scan(base, tb, (const uint32_t*)counts, offsets, 0u, (size_t)n, rocprim::plus<uint32_t>(), s);
-  CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
+  const int nb = cdiv(n, RLE_CH);
+  rle_count_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount);
+  rle_write_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount, uniq_keys, offsets, n_uniq);
   if (ncontrib == 2 && width <= 32)
-    segsum2_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, counts, offsets,
-                                              n_uniq, (uint32_t)n, uniq_grad[0], uniq_grad[1]);
+    segsum2_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, offsets, n_uniq,
+                                              (uint32_t)n, uniq_grad[0], uniq_grad[1]);
   else
     for (int q = 0; q < ncontrib; ++q)
-      segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, counts, offsets, n_uniq,
-                                               (uint32_t)n, uniq_grad[q]);
+      segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, offsets, n_uniq, (uint32_t)n,
+                                               uniq_grad[q]);
   return check_launch("rowgrad");
 }
 

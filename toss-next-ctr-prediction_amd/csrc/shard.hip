@@ -22,9 +22,9 @@
 // per-key widths, exclusive-scan offsets, per-owner float counts for the exchange's splits), not in the
 // 64-float fetched-row layout the forward kernels read.
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
 
 #include "common.h"
+#include "scan.h"
 #include "ctr_hip.h"
 
 namespace ctr {
@@ -209,12 +209,11 @@ static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static PlanWs plan_layout(long n) {
   PlanWs w{};
-  size_t t1 = 0, t2 = 0;
+  size_t t1 = 0;
   (void)rocprim::radix_sort_pairs(nullptr, t1, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                   (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0, 32);
-  (void)rocprim::inclusive_scan(nullptr, t2, (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n,
-                                rocprim::plus<uint32_t>());
-  w.temp_bytes = al256(std::max(t1, t2));
+  // the sort's temporary space doubles as the scan's block sums (the sort is done when the scan runs)
+  w.temp_bytes = al256(std::max(t1, (size_t)scan_ws_words(n) * sizeof(uint32_t)));
   const size_t a = al256((size_t)n * sizeof(uint32_t));
   w.off_okeys = w.temp_bytes;
   w.off_iota = w.off_okeys + a;
@@ -265,9 +264,7 @@ extern "C" int ctr_shard_plan(const int32_t* X, long n, int ncols, int mode, int
                                            (size_t)n, 0, (unsigned)key_bits, s);
   CTR_REQUIRE(e == hipSuccess, "radix_sort_pairs failed");
   shard_flags_kernel<<<g, 256, 0, s>>>(skeys, n, flags);
-  tb = w.temp_bytes;
-  e = rocprim::inclusive_scan(base, tb, (const uint32_t*)flags, seg, (size_t)n, rocprim::plus<uint32_t>(), s);
-  CTR_REQUIRE(e == hipSuccess, "inclusive_scan failed");
+  scan_u32(flags, seg, n, true, (uint32_t*)base, s);
   shard_finalize_kernel<<<g, 256, 0, s>>>(skeys, sidx, flags, seg, n, uniq, n_uniq, remap);
   shard_counts_kernel<<<1, 64, 0, s>>>(uniq, n_uniq, world, lbits, send_counts);
   return check_launch("shard_plan");
@@ -291,10 +288,7 @@ extern "C" int ctr_shard_gather(const int32_t* local, long n, int mode, const ct
 }
 
 extern "C" size_t ctr_shard_offsets_ws_size(long cap) {
-  size_t t = 0;
-  (void)rocprim::exclusive_scan(nullptr, t, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)cap + 1,
-                                rocprim::plus<uint32_t>());
-  return al256(t) + al256(((size_t)cap + 1) * sizeof(uint32_t));
+  return al256((size_t)scan_ws_words(cap + 1) * sizeof(uint32_t)) + al256(((size_t)cap + 1) * sizeof(uint32_t));
 }
 
 extern "C" int ctr_shard_offsets(const uint32_t* keys, const uint32_t* n_ptr, long n, long cap, uint32_t mask,
@@ -304,17 +298,12 @@ extern "C" int ctr_shard_offsets(const uint32_t* keys, const uint32_t* n_ptr, lo
   CTR_REQUIRE(cap >= 0 && ntabs >= 1, "ctr_shard_offsets: bad sizes");
   CTR_REQUIRE(ws_bytes >= ctr_shard_offsets_ws_size(cap), "ctr_shard_offsets: workspace too small");
   CTR_REQUIRE(!float_counts || (n_ptr && world >= 1 && world <= 64), "ctr_shard_offsets: per-owner counts need n_uniq");
-  size_t tb = 0;
-  (void)rocprim::exclusive_scan(nullptr, tb, (const uint32_t*)nullptr, (uint32_t*)nullptr, 0u, (size_t)cap + 1,
-                                rocprim::plus<uint32_t>());
+  const size_t tb = al256((size_t)scan_ws_words(cap + 1) * sizeof(uint32_t));
   char* base = (char*)ws;
-  uint32_t* width = (uint32_t*)(base + al256(tb));
+  uint32_t* width = (uint32_t*)(base + tb);
   // cap + 1 widths (the last one 0) -> cap + 1 exclusive offsets: offsets[i + 1] - offsets[i] = width i
   shard_widths_kernel<<<grid_for(cap + 1), 256, 0, s>>>(keys, n_ptr, n, cap + 1, mask, lbase, dims, ntabs, width);
-  size_t t2 = al256(tb);
-  hipError_t e = rocprim::exclusive_scan(base, t2, (const uint32_t*)width, offsets, 0u, (size_t)cap + 1,
-                                         rocprim::plus<uint32_t>(), s);
-  CTR_REQUIRE(e == hipSuccess, "exclusive_scan failed");
+  scan_u32(width, offsets, cap + 1, false, (uint32_t*)base, s);
   if (float_counts) shard_float_counts_kernel<<<1, 64, 0, s>>>(keys, n_ptr, offsets, world, lbits, float_counts);
   return check_launch("shard_offsets");
 }
