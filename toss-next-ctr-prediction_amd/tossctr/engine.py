@@ -246,8 +246,9 @@ class Engine:
         return buf
 
     class _Side:
-        def __init__(self, eng):
+        def __init__(self, eng, after=None):
             self.eng = eng
+            self.after = after
 
         def __enter__(self):
             e = self.eng
@@ -256,8 +257,10 @@ class Engine:
             if e._side is None:
                 e._side = torch.cuda.Stream(device=e.device)
             self.main = torch.cuda.current_stream(e.device)
-            ev = e._event()
-            ev.record(self.main)
+            ev = self.after
+            if ev is None:
+                ev = e._event()
+                ev.record(self.main)
             e._side.wait_event(ev)
             self.ctx = torch.cuda.stream(e._side)
             self.ctx.__enter__()
@@ -279,10 +282,21 @@ class Engine:
         self._ev_i = (getattr(self, "_ev_i", -1) + 1) % len(ring)
         return ring[self._ev_i]
 
-    def side(self):
+    def side(self, after=None):
         """Context: the enclosed launches go to the side stream, after everything issued so far on the
-        current stream.  Their inputs must not be overwritten by later main-stream work before join()."""
-        return Engine._Side(self)
+        current stream (or, with ``after``, after the point that event marks: see mark()).  Their inputs must
+        not be overwritten by later main-stream work before join()."""
+        return Engine._Side(self, after)
+
+    def mark(self):
+        """An event recorded on the current stream now: side(after=mark) launched later in host order still
+        starts behind only the work issued before the mark -- so a long host-side launch sequence (the rocPRIM
+        sort's ~20 dispatches) can be issued after the main stream's next kernels are already queued."""
+        if not self.side_stream:
+            return None
+        ev = self._event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
 
     def join(self):
         """Current stream waits for the side stream's work."""
@@ -731,8 +745,8 @@ class Engine:
         tg["fx"] = tv["fx"]
         call("ctr_dare_topk_bwd", ptr(sv["tok"]), B, K, ptr(sv["query"]), tv["att"], D, ptr(dvals), tv["pad"], ptr(dq),
              ptr(att_c), ptr(att_k), ptr(rep_k), st)
-        # att and rep contributions share their keys (the top-K tokens): one sort for both, on the side
-        # stream beside the context / embedding backward (its inputs are final; its own sort workspace)
+        # att and rep contributions share their keys (the top-K tokens): one sort for both, on the side stream
+        # beside the context / embedding backward (its own sort workspace), issued below
         # ---------------- context / query
         mode = QUERY_MODES[a.query_mode]
         dcat = W.get("dcat", (B, a.Fc, D))
@@ -742,8 +756,10 @@ class Engine:
              B, mode, self.qi, ptr(P["ctx_mlp.0.weight"]), ptr(sv["hq"]), ptr(dq),
              ptr(dxF, cat_off) if a.use_qnn else None, FD, *dk, ptr(dfc), dfc.shape[1] if dfc is not None else 0,
              ptr(dxF, num_off), ptr(dxF, mask_off), ptr(dcat), ptr(dpre), st)
-        with self.side():     # the side-stream sort after the main stream's next product is queued
-            tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
+        # the DARE rows' dedupe runs on the side stream from here (its inputs are final); its ~20 launches are
+        # issued after the main stream's embedding backward is queued (step time unchanged in A/B either way:
+        # the two branches meet at the join)
+        seq_ready = self.mark()
         if mode != 0:
             self.wgrad(ptr(dpre), D, ptr(sv["ctx"]), a.nctx * D, B, D, a.nctx * D, ptr(G["ctx_mlp.0.weight"]),
                        bias_grad=ptr(G["ctx_mlp.0.bias"]))
@@ -769,6 +785,8 @@ class Engine:
         call("ctr_cat_embed_bwd", ptr(tv["xcat"]), B, a.Fc, ptr(self.arena.buf), tv["cat_tab"], tv["cat_off"],
              ptr(self.cat_proj_off), ptr(self.cat_dims_t), tv["cat_ld"], D, ptr(dcat), tv["row_base"], ptr(cat_c),
              ptr(cat_k), ptr(self.arena.grad), ptr(self.cat_proj_off), ptr(cws), st)
+        with self.side(after=seq_ready):
+            tg["att"], tg["rep"] = self._rowgrad2(W, att_k, att_c, dx, M, D, tv["seq_bits"], ws="rowgrad_ws_side")
         tg["cat"] = self._rowgrad(W, "cat", cat_k, cat_c, n_cat, 64, 64, tv["cat_bits"])
         self.join()
         return tg
