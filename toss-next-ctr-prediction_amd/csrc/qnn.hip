@@ -400,30 +400,53 @@ __global__ void scale_drop_kernel(const float* __restrict__ x, int B, int C, con
   }
 }
 
-// dpost = drop_bwd(dout); dx_direct = dpost*gate; part(dgate) = sum_b dpost*x over row chunks
-template <class TD>
+// dpost = drop_bwd(dout); dx_direct = dpost*gate; part(dgate) = sum_b dpost*x over row chunks.  A thread's rows go
+// in chunks of 16 whose loads are issued together (the per-row flag branches had put a wait behind every load)
+template <class TD, bool GATE, bool DROP>
 __global__ __launch_bounds__(256) void se_bwd_partial(const TD* __restrict__ dout, long dout_ld,
                                                       const float* __restrict__ x, int B, int C,
                                                       const float* __restrict__ gate, Drop drop,
                                                       int rows_per_block, float* __restrict__ dx,
                                                       float* __restrict__ part) {
+  constexpr int CH = 16;
   const int b0 = blockIdx.y * rows_per_block, b1 = min(B, b0 + rows_per_block);
   for (int c = blockIdx.x * 256 + threadIdx.x; c < C; c += gridDim.x * 256) {
     float acc = 0.f;
-#pragma unroll 4
-    for (int b = b0; b < b1; ++b) {
-      const long q = (long)b * C + c;
-      float g = (float)dout[(long)b * dout_ld + c];
-      if (drop.thresh) g = drop_keep(drop, (uint32_t)q) ? g * drop.scale : 0.f;
-      if (gate) {
-        dx[q] = g * gate[c];
-        acc = fmaf(g, x[q], acc);
-      } else {
-        dx[q] = g;
+    const float gc = GATE ? gate[c] : 1.f;
+    for (int r0 = b0; r0 < b1; r0 += CH) {
+      float gv[CH], xv[CH];
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int b = min(r0 + u, b1 - 1);
+        gv[u] = (float)dout[(long)b * dout_ld + c];
+        xv[u] = GATE ? x[(long)b * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u) {
+        const int b = r0 + u;
+        if (b >= b1) break;
+        const long q = (long)b * C + c;
+        float g = gv[u];
+        if (DROP) g = drop_keep(drop, (uint32_t)q) ? g * drop.scale : 0.f;
+        if (GATE) {
+          dx[q] = g * gc;
+          acc = fmaf(g, xv[u], acc);
+        } else {
+          dx[q] = g;
+        }
       }
     }
-    if (part) part[(long)blockIdx.y * C + c] = acc;
+    if (GATE && part) part[(long)blockIdx.y * C + c] = acc;
   }
+}
+
+template <class TD>
+static void se_bwd_partial_launch(dim3 grid, hipStream_t s, const TD* dout, long dout_ld, const float* x, int B, int C,
+                                  const float* gate, Drop d, int rpb, float* dx, float* part) {
+  if (gate && d.thresh) se_bwd_partial<TD, true, true><<<grid, 256, 0, s>>>(dout, dout_ld, x, B, C, gate, d, rpb, dx, part);
+  else if (gate) se_bwd_partial<TD, true, false><<<grid, 256, 0, s>>>(dout, dout_ld, x, B, C, gate, d, rpb, dx, part);
+  else if (d.thresh) se_bwd_partial<TD, false, true><<<grid, 256, 0, s>>>(dout, dout_ld, x, B, C, gate, d, rpb, dx, part);
+  else se_bwd_partial<TD, false, false><<<grid, 256, 0, s>>>(dout, dout_ld, x, B, C, gate, d, rpb, dx, part);
 }
 
 // dgate[c] = sum of the row-block partials (fixed order); dz2 = dgate * sigmoid'(.)  -> db2, dz2
@@ -590,12 +613,11 @@ extern "C" int ctr_se_bwd(const void* dout, long dout_ld, int dout_bf16, const f
   float* part = ws;                      // [np][C]
   float* dmean = ws + (size_t)np * C;    // [C]
   Drop d{drop_key, drop_thresh, drop_scale};
+  const dim3 grid(cdiv(C, 256), np);
   if (dout_bf16)
-    se_bwd_partial<<<dim3(cdiv(C, 256), np), 256, 0, s>>>((const __bf16*)dout, dout_ld, x, B, C, gate, d, rpb, dx,
-                                                         gate ? part : nullptr);
+    se_bwd_partial_launch(grid, s, (const __bf16*)dout, dout_ld, x, B, C, gate, d, rpb, dx, gate ? part : nullptr);
   else
-    se_bwd_partial<<<dim3(cdiv(C, 256), np), 256, 0, s>>>((const float*)dout, dout_ld, x, B, C, gate, d, rpb, dx,
-                                                         gate ? part : nullptr);
+    se_bwd_partial_launch(grid, s, (const float*)dout, dout_ld, x, B, C, gate, d, rpb, dx, gate ? part : nullptr);
   if (gate) {
     float* dz2 = dmean + C;                // [C]
     float* dz1 = dz2 + C;                  // [Cr <= C]
