@@ -11,9 +11,8 @@
 //     holds whole 16-column strips of a row per lane group -> the RMSNorm row sum is a 16-lane
 //     reduction.
 //   ctr_rowgemm_wgrad dW = dY^T X over all rows, plus db = colsum(dY), for one nn.Linear
-//     Each workgroup owns a contiguous row range (its four waves interleaved 32-row groups); a k-step of the
-//     MFMA is 4 rows (lane group g = row), the bias grad is one more 16-column block whose B operand is the
-//     ones column.  Each workgroup writes its partial [dW | db] slab row laid out like the gradient arena
+//     Each workgroup owns a contiguous row range (its four waves interleaved row groups); a k-step of the
+//     MFMA is 4 rows (lane group g = row); the bias grad is a VALU sum of the same dY loads.  Each workgroup writes its partial [dW | db] slab row laid out like the gradient arena
 //     (weight, then the bias at o_db); ctr_colsum reduces the slab rows in a fixed order -- deterministic,
 //     no atomics.
 // f32-input MFMA = an exact fmaf chain per lane: results differ from torch's sgemm only in summation
@@ -164,74 +163,105 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
 }
 
 // dW[NO x NIN] partial of one workgroup over rows [m_begin, m_end): C tile (I, J) = dY[:, 16I..]^T X[:, 16J..].
-// Four waves take interleaved 32-row groups of the range (eight 4-row k-steps of loads in flight each, four
-// waves per SIMD's worth of latency hiding: one wave per SIMD ran the streams at 2-2.5 TB/s); their partials
-// are summed in LDS in a fixed wave order and the workgroup writes one slab row -- deterministic.
+// Four waves take interleaved groups of 4U rows of the range; a wave's next group is loaded into a second register
+// set while the MFMAs of the current one run (loads stay in flight through the whole loop; the loads are
+// unconditional, at rows clamped into the range, and dY of a row past it is zeroed at use).  db = colsum(dY) is a
+// per-lane VALU sum over the lane's rows, reduced over the four lane groups at the end.  The waves' partials are
+// summed in LDS in a fixed wave order and the workgroup writes one slab row -- deterministic.
 template <int NO, int NIN>
 __global__ __launch_bounds__(256) void rowgemm_wgrad_kernel(const float* __restrict__ dY, int ldy,
                                                             const float* __restrict__ X, int ldx, int M,
                                                             int rows_per_wg, float* __restrict__ slab,
                                                             long ld_slab, int o_db) {
   constexpr int IO = NO / 16, JW = NIN / 16;
-  constexpr int U = NO >= 96 ? 4 : 8;                       // k-steps (4 rows each) loaded together
-  constexpr int NA = IO * (JW + 1) * 4;                      // accumulator floats per lane
+  constexpr int U = NO >= 96 ? 4 : 8;                       // k-steps (4 rows each) of one group
+  constexpr int NA = IO * JW * 4 + IO;                       // accumulator floats per lane (+ the bias sums)
+  constexpr int STEP = 4 * 4 * U;                            // rows of one pass of the four waves
   __shared__ float red[3][NA][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
+  const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);    // wave-uniform: the loop runs on scalars
   const int m_begin = blockIdx.x * rows_per_wg, m_end = min(M, m_begin + rows_per_wg);
-  f32x4 acc[IO][JW + 1];                                     // + the ones block (bias grad)
+  f32x4 acc[IO][JW];
+  float db[IO];
 #pragma unroll
-  for (int i = 0; i < IO; ++i)
+  for (int i = 0; i < IO; ++i) {
+    db[i] = 0.f;
 #pragma unroll
-    for (int j = 0; j <= JW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float one = c == 0 ? 1.f : 0.f;
-  for (int m0 = m_begin + 4 * U * w; m0 < m_end; m0 += 4 * 4 * U) {
-    float ay[U][IO], bx[U][JW];
+    for (int j = 0; j < JW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  auto load = [&](int m0, float (&ay)[U][IO], float (&bx)[U][JW]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int m = m0 + 4 * u + g;
-      const bool ok = m < m_end;
+      const long m = min(m0 + 4 * u + g, m_end - 1);
 #pragma unroll
-      for (int i = 0; i < IO; ++i) ay[u][i] = ok ? dY[(long)m * ldy + 16 * i + c] : 0.f;
+      for (int i = 0; i < IO; ++i) ay[u][i] = dY[m * ldy + 16 * i + c];
 #pragma unroll
-      for (int j = 0; j < JW; ++j) bx[u][j] = ok ? X[(long)m * ldx + 16 * j + c] : 0.f;
+      for (int j = 0; j < JW; ++j) bx[u][j] = X[m * ldx + 16 * j + c];
     }
+  };
+  auto compute = [&](int m0, const float (&ay)[U][IO], const float (&bx)[U][JW]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      const bool ok = m0 + 4 * u + g < m_end;
 #pragma unroll
       for (int i = 0; i < IO; ++i) {
+        const float y = ok ? ay[u][i] : 0.f;
+        db[i] += y;
 #pragma unroll
-        for (int j = 0; j < JW; ++j) acc[i][j] = rg_mfma(ay[u][i], bx[u][j], acc[i][j]);
-        acc[i][JW] = rg_mfma(ay[u][i], one, acc[i][JW]);
+        for (int j = 0; j < JW; ++j) acc[i][j] = rg_mfma(y, bx[u][j], acc[i][j]);
       }
+    }
+  };
+  float ya[U][IO], xa[U][JW], yb[U][IO], xb[U][JW];
+  const int mw = m_begin + 4 * U * w;
+  if (mw < m_end) load(mw, ya, xa);
+  // Two groups per trip and no branch inside: a skipped load (or a break between a load and its use, which lets
+  // the compiler sink the loads past it) makes the wait counts assume the newest loads are the ones a compute
+  // needs.  A group past the range (at most one per wave) runs on clamped rows with dY zeroed.
+  for (int m0 = mw; m0 < m_end; m0 += 2 * STEP) {
+    load(m0 + STEP, yb, xb);
+    compute(m0, ya, xa);
+    load(m0 + 2 * STEP, ya, xa);
+    compute(m0 + STEP, yb, xb);
+  }
+#pragma unroll
+  for (int i = 0; i < IO; ++i) {                             // lane (g, c) -> column 16i + c over all four g
+    db[i] += __shfl_xor(db[i], 16, 64);
+    db[i] += __shfl_xor(db[i], 32, 64);
   }
   if (w > 0) {
 #pragma unroll
-    for (int i = 0; i < IO; ++i)
+    for (int i = 0; i < IO; ++i) {
 #pragma unroll
-      for (int j = 0; j <= JW; ++j)
+      for (int j = 0; j < JW; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red[w - 1][(i * (JW + 1) + j) * 4 + r][lane] = acc[i][j][r];
+        for (int r = 0; r < 4; ++r) red[w - 1][(i * JW + j) * 4 + r][lane] = acc[i][j][r];
+      red[w - 1][IO * JW * 4 + i][lane] = db[i];
+    }
   }
   __syncthreads();
   if (w != 0) return;
 #pragma unroll 1
   for (int src = 0; src < 3; ++src)
 #pragma unroll
-    for (int i = 0; i < IO; ++i)
+    for (int i = 0; i < IO; ++i) {
 #pragma unroll
-      for (int j = 0; j <= JW; ++j)
+      for (int j = 0; j < JW; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[src][(i * (JW + 1) + j) * 4 + r][lane];
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[src][(i * JW + j) * 4 + r][lane];
+      db[i] += red[src][IO * JW * 4 + i][lane];
+    }
   float* out = slab + (long)blockIdx.x * ld_slab;
 #pragma unroll
-  for (int i = 0; i < IO; ++i)
+  for (int i = 0; i < IO; ++i) {
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int o = 16 * i + 4 * g + rr;
 #pragma unroll
       for (int j = 0; j < JW; ++j) out[(long)o * NIN + 16 * j + c] = acc[i][j][rr];
-      if (c == 0) out[o_db + o] = acc[i][JW][rr];
     }
+    if (g == 0) out[o_db + 16 * i + c] = db[i];
+  }
 }
 
 // persistent grid: as many workgroups as fit the chip at once (register-limited occupancy)
@@ -265,6 +295,7 @@ static bool wgrad_shape(int NO, int NIN) {
 
 // workgroup b of the weight-grad kernel owns rows [b*rpw, (b+1)*rpw): ~512 workgroups of four waves (two per
 // CU), rpw a multiple of 128 (one 32-row group per wave per pass) -- a <= 512-row slab for the column sum
+// (1024 or 2048 workgroups measured 7-10% slower at cfg2)
 static void wgrad_split(int M, int* rpw, int* waves) {
   const int target = std::max(1, std::min(512, (M + 255) / 256));
   *rpw = ((M + target - 1) / target + 127) / 128 * 128;
