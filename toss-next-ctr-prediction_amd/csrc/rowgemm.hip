@@ -89,15 +89,16 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
     const int b0 = blk * 16 * NI;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int row = b0 + 16 * i + c;
+      // rows clamped into range, not skipped (a conditional load is a branch that waits for every load before
+      // it); the results of rows past M are never stored
+      const long row = min(b0 + 16 * i + c, a.M - 1);
 #pragma unroll
-      for (int q = 0; q < KQ / 4; ++q)
-        A[i][q] = row < a.M ? *(const f32x4*)(a.A + (long)row * a.lda + g * KQ + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < KQ / 4; ++q) A[i][q] = *(const f32x4*)(a.A + row * a.lda + g * KQ + 4 * q);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        const int orow = b0 + 16 * i + 4 * g + rr;
+        const long orow = min(b0 + 16 * i + 4 * g + rr, a.M - 1);
 #pragma unroll
-        for (int j = 0; j < NS; ++j) S[i][rr][j] = (SIDE && orow < a.M) ? side[(long)orow * ld_side + 16 * j + c] : 0.f;
+        for (int j = 0; j < NS; ++j) S[i][rr][j] = SIDE ? side[orow * ld_side + 16 * j + c] : 0.f;
       }
     }
   };
