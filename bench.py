@@ -439,8 +439,26 @@ def main():
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
                           "ctr_adamw_ema", "ctr_adamw_ema_hist", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
+    # a HIP event recorded between two kernels costs a boundary of its own (≈ 5 µs each on MI355X: 10–12 µs gaps around
+    # every bracketed launch), so the candidates are ranked on a few untimed probe steps first and the timed steps
+    # bracket only the dominant one -- the roofline kernel, still timed live in the timed region
+    probe, roof_kernel = {}, None
     if args.kernel_events == "all":
+        a_ = model.arch
         _lib.time_calls(roof_timed)
+        for _ in range(PROFILE_STEPS):
+            run(g, g)
+            g += 1
+        torch.cuda.synchronize()
+        probe = _lib.timed_ms()
+        _lib.time_calls(())
+        fm_ = args.batch * a_.K_eff(args.seq_len)
+        ranked = sorted(probe, key=lambda n: probe[n][0] * probe[n][1], reverse=True)
+        roof_kernel = next((n for n in ranked if price(n, a_, args.batch, fm_, args.amp, model.engine.ffn_flags,
+                                                       probe[n][1]) is not None), None)
+        if roof_kernel is not None:
+            _lib.time_calls((roof_kernel,))
+        torch.cuda.synchronize()
     if args.markers:
         _lib.call("ctr_step_marker", 1, torch.cuda.current_stream(dev).cuda_stream)
     t0 = time.perf_counter()
@@ -506,15 +524,20 @@ def main():
                     "work_unit": unit,
                     "avg_launch_ms": round(kstats_timed[n][1], 4), "ms_per_step": round(per_step_t[n], 4),
                     "share_of_step": round(per_step_t[n] / ms, 4), "timing": "HIP events in the timed steps"}
-            # every priced kernel of the timed steps, dominant first (the roofline object is the first)
+            # every priced candidate, dominant first: the roofline kernel from the timed steps, the others from the
+            # probe steps before them (ranked there; only the dominant one is bracketed in the timed region)
             roof["priced"] = {}
-            for m_ in sorted(per_step_t, key=per_step_t.get, reverse=True):
-                pr_ = price(m_, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, kstats_timed[m_][1])
+            per_step_p = {m_: c * t_ / PROFILE_STEPS for m_, (c, t_) in probe.items()}
+            src = [(n, kstats_timed[n], per_step_t[n], "timed")] + [
+                (m_, probe[m_], per_step_p[m_], "probe") for m_ in sorted(per_step_p, key=per_step_p.get, reverse=True)
+                if m_ != n]
+            for m_, (c_, t_), ps_, how in src:
+                pr_ = price(m_, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, t_)
                 if pr_ is None:
                     continue
-                roof["priced"][m_] = {"bound": pr_[0], "ms_per_step": round(per_step_t[m_], 4),
-                                      "avg_launch_ms": round(kstats_timed[m_][1], 4), "achieved": round(pr_[2], 2),
-                                      "peak": round(pr_[3], 1), "unit": pr_[4], "frac": round(pr_[2] / pr_[3], 4)}
+                roof["priced"][m_] = {"bound": pr_[0], "ms_per_step": round(ps_, 4), "avg_launch_ms": round(t_, 4),
+                                      "achieved": round(pr_[2], 2), "peak": round(pr_[3], 1), "unit": pr_[4],
+                                      "frac": round(pr_[2] / pr_[3], 4), "steps": how}
             break
         rec = {
             "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref"
@@ -536,7 +559,8 @@ def main():
             "roofline": roof,
             "kernels": kernels,
             "kernels_note": f"HIP events on {PROFILE_STEPS} extra steps after the timed region (the flush: once, over those "
-                            f"{PROFILE_STEPS} ticks; the timed region's flush is flush_ms)",
+                            f"{PROFILE_STEPS} ticks; the timed region's flush is flush_ms); the roofline candidates ranked "
+                            f"on {PROFILE_STEPS} untimed probe steps before it, only the dominant one bracketed while timed",
             "opt_ms_per_step": round(opt_ms, 3) if opt_ms is not None else None,
             "table_update": "dense stream" if args.dense_opt else "exact lazy (replay on read/grad; final flush timed)",
             "flush_ms": round(flush_ms, 3),
