@@ -101,78 +101,98 @@ __global__ __launch_bounds__(RLE_T) void rle_write_kernel(const uint32_t* __rest
   }
 }
 
-// one wave per unique key, lane = column; members summed in (stable) contribution order.  The
-// INVALID group (pad tokens: dropped by padding_idx) is skipped -- it is by far the largest group
-// (every short history contributes pads to its top-K) and its sum is never read.
+// one wave per SS_KPW consecutive unique keys, lane = column; each key's members summed in (stable) contribution
+// order.  The keys' slot loads, their first members' indices and the first members' rows are each issued for all
+// SS_KPW keys together (most keys have one member: three dependent round trips per key became three per SS_KPW
+// keys); a key with more than SS_CH members continues in chunks of SS_CH.  The sums add in member order exactly
+// as one key per wave did.  The INVALID group (pad tokens: dropped by padding_idx) is skipped -- it is by far the
+// largest group (every short history contributes pads to its top-K) and its sum is never read.
+constexpr int SS_KPW = 4, SS_CH = 4;
+
+template <int NA>
+__device__ __forceinline__ void segsum_keys(const float* const (&src)[NA], float* const (&dst)[NA], int ld, int width,
+                                            int col, const uint32_t* __restrict__ uniq_keys,
+                                            const uint32_t* __restrict__ sorted_idx,
+                                            const uint32_t* __restrict__ offsets, const uint32_t* __restrict__ n_uniq,
+                                            uint32_t n, uint32_t u0, int a) {
+  uint32_t key[SS_KPW], off[SS_KPW], cnt[SS_KPW];
+#pragma unroll
+  for (int j = 0; j < SS_KPW; ++j) {      // slots past n_uniq read in-bounds workspace words; they are not used
+    const uint32_t u = min(u0 + j, n - 1);
+    key[j] = uniq_keys[u];
+    off[j] = offsets[u];
+    cnt[j] = offsets[u + 1];
+  }
+  const uint32_t nu = *n_uniq;
+#pragma unroll
+  for (int j = 0; j < SS_KPW; ++j) cnt[j] -= off[j];
+  if (col >= width) return;
+  bool live[SS_KPW];
+  uint32_t ix[SS_KPW][SS_CH];
+#pragma unroll
+  for (int j = 0; j < SS_KPW; ++j) {
+    live[j] = u0 + j < nu && key[j] != 0xFFFFFFFFu;
+    const uint32_t c1 = live[j] && cnt[j] > 0 ? cnt[j] - 1 : 0;
+#pragma unroll
+    for (int q = 0; q < SS_CH; ++q) ix[j][q] = sorted_idx[min(off[j] + min((uint32_t)q, c1), n - 1)];
+  }
+  float v[SS_KPW][SS_CH];
+#pragma unroll
+  for (int j = 0; j < SS_KPW; ++j)
+#pragma unroll
+    for (int q = 0; q < SS_CH; ++q) v[j][q] = src[a][(long)ix[j][q] * ld + col];
+#pragma unroll
+  for (int j = 0; j < SS_KPW; ++j) {
+    const uint32_t u = u0 + j;
+    if (u >= nu) break;
+    if (!live[j]) {                        // the INVALID group: zero row (never read)
+      dst[a][(long)u * width + col] = 0.f;
+      continue;
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int q = 0; q < SS_CH; ++q)
+      if ((uint32_t)q < cnt[j]) acc += v[j][q];
+    for (uint32_t i = SS_CH; i < cnt[j]; i += SS_CH) {      // long groups: further chunks, loads issued together
+      float w[SS_CH];
+#pragma unroll
+      for (int q = 0; q < SS_CH; ++q)
+        w[q] = src[a][(long)sorted_idx[off[j] + min(i + q, cnt[j] - 1)] * ld + col];
+#pragma unroll
+      for (int q = 0; q < SS_CH; ++q)
+        if (i + q < cnt[j]) acc += w[q];
+    }
+    dst[a][(long)u * width + col] = acc;
+  }
+}
+
 __global__ __launch_bounds__(256) void segsum_kernel(const float* __restrict__ contrib, int ld, int width,
                                                      const uint32_t* __restrict__ uniq_keys,
                                                      const uint32_t* __restrict__ sorted_idx,
                                                      const uint32_t* __restrict__ offsets,
                                                      const uint32_t* __restrict__ n_uniq, uint32_t n,
                                                      float* __restrict__ out) {
-  const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (u >= n) return;
-  // the slot's key / offset / count load beside the unique count (they followed it: one more round trip)
-  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = offsets[u + 1] - off;
-  if (u >= *n_uniq) return;
-  if (key == 0xFFFFFFFFu) {
-    if (lane < width) out[(long)u * width + lane] = 0.f;
-    return;
-  }
-  if (lane < width) {
-    float acc = 0.f;
-    uint32_t i = 0;
-    for (; i + 4 <= cnt; i += 4) {   // issue 4 independent row loads, add in order
-      const float a0 = contrib[(long)sorted_idx[off + i] * ld + lane];
-      const float a1 = contrib[(long)sorted_idx[off + i + 1] * ld + lane];
-      const float a2 = contrib[(long)sorted_idx[off + i + 2] * ld + lane];
-      const float a3 = contrib[(long)sorted_idx[off + i + 3] * ld + lane];
-      acc += a0;
-      acc += a1;
-      acc += a2;
-      acc += a3;
-    }
-    for (; i < cnt; ++i) acc += contrib[(long)sorted_idx[off + i] * ld + lane];
-    out[(long)u * width + lane] = acc;
-  }
+  const uint32_t u0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * SS_KPW;
+  if (u0 >= n) return;
+  const float* const src[1] = {contrib};
+  float* const dst[1] = {out};
+  segsum_keys<1>(src, dst, ld, width, threadIdx.x & 63, uniq_keys, sorted_idx, offsets, n_uniq, n, u0, 0);
 }
 
-// Two contribution arrays sharing the keys (the DARE att / rep rows, width <= 32): one wave per unique
-// key, lanes [0, 32) sum array a and lanes [32, 64) array b -- one set of index loads for both and no
-// idle half-wave (two segsum_kernel launches at width 32 left half of every wave idle).
+// Two contribution arrays sharing the keys (the DARE att / rep rows, width <= 32): lanes [0, 32) sum array a and
+// lanes [32, 64) array b -- one set of index loads for both and no idle half-wave.
 __global__ __launch_bounds__(256) void segsum2_kernel(const float* __restrict__ ca, const float* __restrict__ cb,
                                                       int ld, int width, const uint32_t* __restrict__ uniq_keys,
                                                       const uint32_t* __restrict__ sorted_idx,
                                                       const uint32_t* __restrict__ offsets,
                                                       const uint32_t* __restrict__ n_uniq, uint32_t n,
                                                       float* __restrict__ oa, float* __restrict__ ob) {
-  const uint32_t u = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63, c = lane & 31;
-  if (u >= n) return;
-  const uint32_t key = uniq_keys[u], off = offsets[u], cnt = offsets[u + 1] - off;   // beside the unique count
-  if (u >= *n_uniq) return;
-  const float* __restrict__ src = lane < 32 ? ca : cb;
-  float* __restrict__ dst = lane < 32 ? oa : ob;
-  if (c >= width) return;
-  if (key == 0xFFFFFFFFu) {
-    dst[(long)u * width + c] = 0.f;
-    return;
-  }
-  float acc = 0.f;
-  uint32_t i = 0;
-  for (; i + 4 <= cnt; i += 4) {   // issue 4 independent row loads, add in order
-    const float a0 = src[(long)sorted_idx[off + i] * ld + c];
-    const float a1 = src[(long)sorted_idx[off + i + 1] * ld + c];
-    const float a2 = src[(long)sorted_idx[off + i + 2] * ld + c];
-    const float a3 = src[(long)sorted_idx[off + i + 3] * ld + c];
-    acc += a0;
-    acc += a1;
-    acc += a2;
-    acc += a3;
-  }
-  for (; i < cnt; ++i) acc += src[(long)sorted_idx[off + i] * ld + c];
-  dst[(long)u * width + c] = acc;
+  const uint32_t u0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * SS_KPW;
+  if (u0 >= n) return;
+  const int lane = threadIdx.x & 63;
+  const float* const src[2] = {ca, cb};
+  float* const dst[2] = {oa, ob};
+  segsum_keys<2>(src, dst, ld, width, lane & 31, uniq_keys, sorted_idx, offsets, n_uniq, n, u0, lane >> 5);
 }
 
 struct RowgradWs {
@@ -241,12 +261,12 @@ static int rowgrad_core(const uint32_t* keys, const float* const* contrib, float
   rle_count_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount);
   rle_write_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount, uniq_keys, offsets, n_uniq);
   if (ncontrib == 2 && width <= 32)
-    segsum2_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, offsets, n_uniq,
-                                              (uint32_t)n, uniq_grad[0], uniq_grad[1]);
+    segsum2_kernel<<<cdiv(n, 4 * SS_KPW), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, offsets,
+                                                         n_uniq, (uint32_t)n, uniq_grad[0], uniq_grad[1]);
   else
     for (int q = 0; q < ncontrib; ++q)
-      segsum_kernel<<<cdiv(n, 4), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, offsets, n_uniq, (uint32_t)n,
-                                               uniq_grad[q]);
+      segsum_kernel<<<cdiv(n, 4 * SS_KPW), 256, 0, s>>>(contrib[q], ld, width, uniq_keys, sidx, offsets, n_uniq,
+                                                          (uint32_t)n, uniq_grad[q]);
   return check_launch("rowgrad");
 }
 
