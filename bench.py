@@ -71,61 +71,97 @@ MFMA_BF16_PEAK_TFS = 16 * MFMA_F32_PEAK_TFS   # dense bf16 MFMA = 16x the fp32 r
 PROFILE_STEPS = 5       # untimed steps after the timed region that fill the per-kernel table
 
 
-def kernel_work(name, a, B, ffn_M):
-    """(bound, algorithmic units per launch, unit) of the timed entry points -- SURVEY §8(d) per-unit
-    figures x the units one launch processes ("Roofline accounting").
-    FFN: the four products (8 FF D flop per row backward, 4 forward; the backward's pre-activation
-    recompute not counted).  Attention core (src/models/dare.py:39-70, MHA over K candidates, dh = D / H):
-    amp none -- the fp32 VALU kernels (attn.hip): per (sample, head) QK^T and PV = 4 K^2 dh flop forward, dP, dV,
-    dQ, dK = 8 K^2 dh backward (the score recompute not counted), priced against the fp32 vector peak; amp bf16
-    -- the bf16-MFMA kernels (attn_mf.hip), whose products are a few % of the bf16 peak: priced against HBM by
-    the bytes each launch must move (below)."""
+def kernel_work(name, a, B, ffn_M, amp="bf16", ffn_flags=0):
+    """Algorithmic work of one launch of a timed entry point: {"flops": [(flop, peak dtype)], "bytes": HBM bytes,
+    "flop_note": ...} or None -- SURVEY §8(d)'s per-unit figures x the units one launch processes (DESIGN.md §5,
+    "Roofline accounting").  Every kernel is then priced on its BINDING roof (price()): its floor time is
+    max(sum flop / peak of its dtype, bytes / 8 TB/s).
+
+    FFN (src/models/dare.py:45-48,66-69): the four products, 8 FF D flop per row backward, 4 forward (the backward's
+    pre-activation recompute not counted); bytes per row: forward reads x (4 D) and writes the output and the
+    pre-norm sum (8 D), the norm's rsqrt (4) and the dropout keep bits (FF / 8); the norm-fused backward reads x1,
+    dy, h2, h1 (16 D) and r1, r2 (8), the keep bits, and writes dh1 (4 D) -- the weight-grad outputs are a few
+    hundred KB.  Attention core (dare.py:53-62, MHA over K candidates): QK^T and PV = 4 K^2 D flop per sample forward,
+    dP, dS K, dK, dV = 8 K^2 D backward; bytes per (sample, candidate) row: qkv (12 D), o (4 D), row max / sum
+    (8 H) forward, + dO, and dqkv written (32 D) backward, plus the keep bits per (sample, head) in the kernels' lane
+    layout.  The fused layer forward adds in_proj and out_proj (8 D^2 flop per row on fp32 MFMA) and reads x (4 D),
+    writes h1, x1 (8 D) and r1 (4); ``_oproj`` forms dO = dh1 W_out inside (2 D^2 flop per row, fp32 MFMA).
+    QNN pair interaction (src/models/qnn_alpha.py:86-97): the reference's A = z U projection, 2 F D QR flop per
+    sample (the north star's "feature_embed_dim x proj_dim projection"), forward; its backward recomputes A and forms
+    dz = dA U^T, 4 F D QR (the Gram form executes fewer flops -- priced at the reference's); bytes: z (4 F D) read,
+    and the per-sample outputs.  QNN MLP first layer (qnn_alpha.py:123-129) on bf16 operands: 2 M N K flop; bytes:
+    both bf16 operands once and the output (fp32, or bf16 for the input grad)."""
     D, FF = a.D, a.ffn_hidden
-    if name in ("ctr_ffn_bwd", "ctr_ffn_bwd_norms"):     # dfo = dh W2, dW2 = dh^T fo, dW1 = dact^T x, dx = dact W1 (pre recompute excluded)
-        return "mfma", 8.0 * ffn_M * FF * D, "flop"
-    if name == "ctr_ffn_fwd":     # pre = x W1^T, y = fo W2^T
-        return "mfma", 4.0 * ffn_M * FF * D, "flop"
+    kb = (FF // 8) if a.ffn_p > 0 else 0
+    fdt = "bf16" if (amp == "bf16" and ffn_flags) else "f32"
+    if name in ("ctr_ffn_bwd", "ctr_ffn_bwd_norms"):
+        per_row = (20 * D + 8 + kb) if name == "ctr_ffn_bwd_norms" else (12 * D + kb)
+        return {"flops": [(8.0 * ffn_M * FF * D, fdt)], "bytes": float(ffn_M * per_row)}
+    if name == "ctr_ffn_fwd":
+        return {"flops": [(4.0 * ffn_M * FF * D, fdt)], "bytes": float(ffn_M * (12 * D + 4 + kb))}
     K = ffn_M // max(1, B)
-    if name == "ctr_attn_fwd":
-        return "valu", 4.0 * B * K * K * D, "flop"
-    if name == "ctr_attn_bwd":
-        return "valu", 8.0 * B * K * K * D, "flop"
-    # amp: the bf16-MFMA attention (attn_mf.hip) -- its products take a few % of the bf16 MFMA peak, so its
-    # roofline is HBM: per (sample, candidate) row the fp32 qkv read (12 D B), o write (4 D), row max / sum
-    # (8 H); per (sample, head) the keep bits in the kernels' lane layout, 64 lanes x NW words (NW = 2 for
-    # nt = ceil(K / 16) <= 4 tiles a side: 512 B; ceil(4 nt^2 / 32) beyond: 3.3 KB at K = 148); the backward
-    # reads qkv, o, dO (20 D), the row stats and bits, and writes dqkv (12 D)
     H = a.H
     nt = (K + 15) // 16
-    mask = B * H * 64 * 4 * (2 if nt <= 4 else (4 * nt * nt + 31) // 32)
+    mask_bf = B * H * 64 * 4 * (2 if nt <= 4 else (4 * nt * nt + 31) // 32) if a.mha_p > 0 else 0
+    mask_f32 = B * H * K * ((K + 31) // 32) * 4 if a.mha_p > 0 else 0
+    fwd_b, bwd_b = B * K * (16 * D + 8 * H), B * K * (32 * D + 8 * H)
+    if name == "ctr_attn_fwd":
+        return {"flops": [(4.0 * B * K * K * D, "f32")], "bytes": float(fwd_b + mask_f32)}
+    if name == "ctr_attn_bwd":
+        return {"flops": [(8.0 * B * K * K * D, "f32")], "bytes": float(bwd_b + mask_f32)}
     if name == "ctr_attn_fwd_bf":
-        return "hbm", float(B * K * (16 * D + 8 * H) + mask), "B"
-    if name in ("ctr_attn_bwd_bf", "ctr_attn_bwd_bf_oproj"):     # _oproj reads dh1 rows in place of dO
-        return "hbm", float(B * K * (32 * D + 8 * H) + mask), "B"
-    # the fused layer forward (in_proj -> attention -> out_proj + residual + RMSNorm, attn_mf.hip): reads x (4 D)
-    # and writes qkv (12 D), o (4 D), h1 and x1 (8 D), r1 (4), the row stats (8 H) and the keep bits per row
+        return {"flops": [(4.0 * B * K * K * D, "bf16")], "bytes": float(fwd_b + mask_bf)}
+    if name == "ctr_attn_bwd_bf":
+        return {"flops": [(8.0 * B * K * K * D, "bf16")], "bytes": float(bwd_b + mask_bf)}
+    if name == "ctr_attn_bwd_bf_oproj":     # reads dh1 rows in place of dO (same bytes)
+        return {"flops": [(8.0 * B * K * K * D, "bf16"), (2.0 * B * K * D * D, "f32")], "bytes": float(bwd_b + mask_bf)}
     if name == "ctr_attn_layer_fwd_bf":
-        return "hbm", float(B * K * (28 * D + 4 + 8 * H) + mask), "B"
+        return {"flops": [(4.0 * B * K * K * D, "bf16"), (8.0 * B * K * D * D, "f32")],
+                "bytes": float(B * K * (28 * D + 4 + 8 * H) + mask_bf)}
+    if name in ("ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd") and a.use_qnn:
+        F, QR = a.F, a.qh * a.qr
+        if name == "ctr_qnn_gram_fwd":     # z read; zsum, G (D x D), S, quad written
+            return {"flops": [(2.0 * B * F * D * QR, "f32")], "bytes": float(B * (4 * F * D + 4 * D + 4 * D * D + 8 * QR)),
+                    "flop_note": "reference A = z U (2 F D QR per sample); the Gram form executes 2 F D^2 + 2 D^2 QR"}
+        add = 2 if amp == "bf16" else 4    # the MLP's input grad, bf16 under amp
+        return {"flops": [(4.0 * B * F * D * QR, "f32")],
+                "bytes": float(B * ((8 + add) * F * D + 12 * QR)),
+                "flop_note": "reference A recompute + dz = dA U^T (4 F D QR per sample); the Gram form executes less"}
+    if name.startswith("ctr_gemm_bf16_ex@"):
+        shp = name.split("@")[1]
+        bf_out = shp.endswith("b")
+        M, N, Kk = (int(x) for x in shp.rstrip("b").split("x"))
+        return {"flops": [(2.0 * M * N * Kk, "bf16")], "bytes": float(2 * (M * Kk + Kk * N) + (2 if bf_out else 4) * M * N)}
     return None
 
 
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, MI355X_MICROARCH.md
+PEAK_TFS = {"f32": MFMA_F32_PEAK_TFS, "bf16": MFMA_BF16_PEAK_TFS}   # dense MFMA (f32 = the f32 vector rate too)
 
 
 def price(name, a, B, ffn_M, amp, ffn_flags, launch_ms):
-    """(bound, work, achieved, peak, unit, mfma dtype) of one timed entry point, or None."""
-    w = kernel_work(name, a, B, ffn_M)
+    """The roofline of one timed entry point, or None: its binding roof is the larger of the compute floor
+    (sum over its products of flop / dense peak of their dtype) and the HBM floor (algorithmic bytes / 8 TB/s);
+    frac = that floor / the measured launch time.  ``achieved`` / ``peak`` are in the binding roof's units
+    (GB/s against 8 TB/s, or TFLOP/s against the products' combined peak)."""
+    w = kernel_work(name, a, B, ffn_M, amp, ffn_flags)
     if w is None:
         return None
-    bound, work, _ = w
-    if bound == "hbm":
-        return bound, w, work / (launch_ms * 1e-3) / 1e9, HBM_PEAK_GBS, "GB/s", None
-    # amp bf16: the FFN kernels' products run on bf16 MFMA -> priced against the bf16 dense peak; the fp32
-    # attention core runs on the fp32 vector units (its peak = the fp32 rate, 157.3 TF)
-    bf = amp == "bf16" and name.startswith("ctr_ffn") and ffn_flags
-    peak = MFMA_BF16_PEAK_TFS if bf else MFMA_F32_PEAK_TFS
-    return bound, w, work / (launch_ms * 1e-3) / 1e12, peak, "TFLOP/s", (None if bound == "valu" else
-                                                                        "bf16" if bf else "f32")
+    t = launch_ms * 1e-3
+    flops = sum(f for f, _ in w["flops"])
+    t_f = sum(f / (PEAK_TFS[d] * 1e12) for f, d in w["flops"])
+    t_b = w["bytes"] / (HBM_PEAK_GBS * 1e9)
+    dts = sorted({d for _, d in w["flops"]})
+    out = {"bound": "hbm" if t_b >= t_f else "mfma", "flops": flops, "bytes": w["bytes"],
+           "floor_us": round(max(t_f, t_b) * 1e6, 2), "compute_floor_us": round(t_f * 1e6, 2),
+           "hbm_floor_us": round(t_b * 1e6, 2), "frac": max(t_f, t_b) / t, "mfma_dtype": "+".join(dts),
+           "hbm_frac": t_b / t, "mfma_frac": t_f / t}
+    if "flop_note" in w:
+        out["flop_note"] = w["flop_note"]
+    if out["bound"] == "hbm":
+        out.update(achieved=w["bytes"] / t / 1e9, peak=HBM_PEAK_GBS, unit="GB/s")
+    else:
+        out.update(achieved=flops / t / 1e12, peak=flops / t_f / 1e12, unit="TFLOP/s")
+    return out
 
 
 def step_bytes_dense_equiv(a, B, L, with_ema):
@@ -435,10 +471,11 @@ def main():
     # host-issue sensitive), so the timed steps bracket only the roofline candidates (the kernels with an
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd",
-                  "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj")
+                  "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj",
+                  "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd", "ctr_gemm_bf16_ex")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
-                          "ctr_adamw_ema", "ctr_adamw_ema_hist", "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd")
+                          "ctr_adamw_ema", "ctr_adamw_ema_hist")
     # a HIP event recorded between two kernels costs a boundary of its own (≈ 5 µs each on MI355X: 10–12 µs gaps around
     # every bracketed launch), so the candidates are ranked on a few untimed probe steps first and the timed steps
     # bracket only the dominant one -- the roofline kernel, still timed live in the timed region
@@ -455,7 +492,7 @@ def main():
         fm_ = args.batch * a_.K_eff(args.seq_len)
         ranked = sorted(probe, key=lambda n: probe[n][0] * probe[n][1], reverse=True)
         roof_kernel = next((n for n in ranked if price(n, a_, args.batch, fm_, args.amp, model.engine.ffn_flags,
-                                                       probe[n][1]) is not None), None)
+                                                       probe[n][1]) is not None), None)     # may carry a shape key
         if roof_kernel is not None:
             _lib.time_calls((roof_kernel,))
         torch.cuda.synchronize()
@@ -517,13 +554,16 @@ def main():
             pr = price(n, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, kstats_timed[n][1])
             if pr is None:
                 continue
-            bound, (_, work, unit), ach, peak, runit, mdt = pr
-            roof = {"bound": bound, "kernel": n, "achieved": round(ach, 2), "peak": round(peak, 1),
-                    "unit": runit, "frac": round(ach / peak, 4), "mfma_dtype": mdt,
-                    "traffic": pmc_traffic(n) if args.config == "cfg2" else None, "work_per_launch": work,
-                    "work_unit": unit,
+            roof = {"bound": pr["bound"], "kernel": n, "achieved": round(pr["achieved"], 2), "peak": round(pr["peak"], 1),
+                    "unit": pr["unit"], "frac": round(pr["frac"], 4), "mfma_dtype": pr["mfma_dtype"],
+                    "traffic": pmc_traffic(n) if args.config == "cfg2" else None,
+                    "algorithmic_bytes": pr["bytes"], "algorithmic_flops": pr["flops"],
+                    "floor_us": pr["floor_us"], "hbm_floor_us": pr["hbm_floor_us"],
+                    "compute_floor_us": pr["compute_floor_us"],
                     "avg_launch_ms": round(kstats_timed[n][1], 4), "ms_per_step": round(per_step_t[n], 4),
-                    "share_of_step": round(per_step_t[n] / ms, 4), "timing": "HIP events in the timed steps"}
+                    "share_of_step": round(per_step_t[n] / ms, 4), "timing": "HIP events in the timed steps",
+                    "pricing": "binding roof: frac = max(sum flop / dense MFMA peak of the dtype, algorithmic bytes / "
+                               "8 TB/s) / measured launch time (kernel_work)"}
             # every priced candidate, dominant first: the roofline kernel from the timed steps, the others from the
             # probe steps before them (ranked there; only the dominant one is bracketed in the timed region)
             roof["priced"] = {}
@@ -535,9 +575,14 @@ def main():
                 pr_ = price(m_, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, t_)
                 if pr_ is None:
                     continue
-                roof["priced"][m_] = {"bound": pr_[0], "ms_per_step": round(ps_, 4), "avg_launch_ms": round(t_, 4),
-                                      "achieved": round(pr_[2], 2), "peak": round(pr_[3], 1), "unit": pr_[4],
-                                      "frac": round(pr_[2] / pr_[3], 4), "steps": how}
+                ent = {"bound": pr_["bound"], "ms_per_step": round(ps_, 4), "avg_launch_ms": round(t_, 4),
+                       "achieved": round(pr_["achieved"], 2), "peak": round(pr_["peak"], 1), "unit": pr_["unit"],
+                       "frac": round(pr_["frac"], 4), "hbm_frac": round(pr_["hbm_frac"], 4),
+                       "mfma_frac": round(pr_["mfma_frac"], 4), "mfma_dtype": pr_["mfma_dtype"],
+                       "bytes": pr_["bytes"], "flops": pr_["flops"], "steps": how}
+                if "flop_note" in pr_:
+                    ent["flop_note"] = pr_["flop_note"]
+                roof["priced"][m_] = ent
             break
         rec = {
             "metric": "training samples/sec at bs=4096 seq_len=100, 1/2/4/8 MI355X vs CPU ref"

@@ -155,17 +155,30 @@ def run(rank, world, port, args):
     if args.config == "cfg5r":
         _dump_touched(model, opt, ema, batches, arch, rank, world, losses, args)
     else:
+        if args.sync_eval:        # every table row brought current before the evaluation reads it
+            model.sync()
         model.eval()
         eb = make_batch(Bs, Fn, Fm, list(cards.values()), L, vocab, seed=4242 + 7 * rank)
         with torch.no_grad():
             logits = model(to_torch_batch(eb), seed=1)[0].cpu()
+        # the eval forward's DARE top-K selection (tokens in slot order, scores): where two runs' selections differ
+        # the logits of that sample move discontinuously (tests/test_gpu_shard.py::_compare)
+        Wk = model.engine.ws(Bs, L)
+        eval_tok = Wk.get("topk_tok", (Bs, model.arch.K_eff(L)), torch.int32).cpu()
+        eval_vals = Wk.get("topk_vals", (Bs, model.arch.K_eff(L))).cpu()
+        eval_idx = Wk.get("topk_idx", (Bs, model.arch.K_eff(L)), torch.int32).cpu()
+        if args.eval_check and model.shards is not None:
+            _eval_check(model, eb, rank, logits)
+        if args.dump_ws and rank == 0:      # the evaluation forward's workspace (tools/shard_logit_diag.py)
+            torch.save({k: v.detach().cpu() for k, v in model.engine.ws(Bs, L).t.items()}, args.out + ".ws")
         sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         shadow = {k: v.detach().cpu() for k, v in ema.state_dict()["shadow_params"].items()}
         mom = {k: model.full_table(opt.m, k).detach().cpu() for k in model.arena.order}
         vel = {k: model.full_table(opt.v, k).detach().cpu() for k in model.arena.order}
         local_rows = int(model.arena.shapes["dare.emb_att.weight"][0])
         if rank == 0:
-            torch.save({"sd": sd, "ema": shadow, "m": mom, "v": vel, "losses": losses, "logits": logits,
+            torch.save({"sd": sd, "ema": shadow, "m": mom, "v": vel, "losses": losses, "logits": logits, "eval_tok": eval_tok, "eval_vals": eval_vals,
+                        "eval_idx": eval_idx,
                         "gnorm": float(opt.norm_out[0]), "local_rows": local_rows, "vocab": vocab, "cards": cards,
                         "cfg": cfg, "Fn": Fn, "Fm": Fm, "L": L, "B": Bs, "lr0": lr0, "clip": clip,
                         "init": "reference" if args.config == "cfg5w" else "synthetic"},
@@ -173,6 +186,32 @@ def run(rank, world, port, args):
     if pg is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _eval_check(model, eb, rank, logits):
+    """Diagnostics (tools/shard_logit_diag.py): the rows the sharded fetch hands the evaluation forward against the
+    full tables gathered from the shards, and a second evaluation forward of the same batch."""
+    import torch
+    from golden_util import to_torch_batch
+    X_num, X_mask, X_cat, seq = model.stage(to_torch_batch(eb))
+    model.sync()
+    full = {k: model.full_table(model.arena.buf, k) for k in ("dare.emb_att.weight", "dare.emb_rep.weight")}
+    fx = model.shards.fetch(X_cat, seq)
+    r = fx["seq"].long()
+    for name, k in (("att", "dare.emb_att.weight"), ("rep", "dare.emb_rep.weight")):
+        got = fx[name][r]
+        want = full[k][seq.long()]
+        print(f"rank {rank} eval fetch {name}: max |fetched - full| {float((got - want).abs().max()):.3e}", flush=True)
+    for c in range(min(3, X_cat.shape[1])):
+        k = f"cat_embs.{model.arch.cat_names[c]}.weight"
+        ft = model.full_table(model.arena.buf, k)
+        w = ft.shape[1]
+        got = fx["cat"][fx["xcat"][:, c].long(), :w]
+        want = ft[X_cat[:, c].long()]
+        print(f"rank {rank} eval fetch cat {c}: max |fetched - full| {float((got - want).abs().max()):.3e}", flush=True)
+    with torch.no_grad():
+        z2 = model(to_torch_batch(eb), seed=1)[0].cpu()
+    print(f"rank {rank} second eval: max |dz| {float((z2 - logits).abs().max()):.3e}", flush=True)
 
 
 def _dump_touched(model, opt, ema, batches, arch, rank, world, losses, args):
@@ -225,6 +264,9 @@ def main():
                          "through the host)")
     ap.add_argument("--interleave-eval", type=int, default=0, help="an eval forward between steps 1 and 2")
     ap.add_argument("--short-last", type=int, default=0, help="rank 1 contributes nothing on the last step")
+    ap.add_argument("--dump-ws", type=int, default=0, help="save the evaluation forward's workspace to OUT.ws")
+    ap.add_argument("--eval-check", type=int, default=0, help="diagnostics of the sharded evaluation fetch")
+    ap.add_argument("--sync-eval", type=int, default=0, help="flush the lazy tables before the evaluation forward")
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     if args.mode == "single":

@@ -45,10 +45,26 @@ def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0, p
 
 def _compare(a, b, rtol, atol=1e-6, what=""):
     close_enough(np.asarray(a["losses"], np.float64), np.asarray(b["losses"], np.float64), rtol, atol, what + "loss")
-    # the eval logits after the last step: the MHA key bias (see below) moves in lr-sized steps on rounding noise, and
-    # the amp attention rounds q . (k + b_k) to bf16, so the exact shift invariance holds only to ~1e-3 -- the runs
-    # agree bitwise after step 1 and to ~1e-8 after step 2 (tiny config); the parameters themselves are held to rtol
-    close_enough(a["logits"].double().numpy(), b["logits"].double().numpy(), max(rtol, 1e-3), atol, what + "logits")
+    # the eval logits after the last step, at rtol -- unless the evaluation's DARE top-K put two candidates in a
+    # different slot order.  The runs' parameters agree to ~1e-8 (the clip norm's cross-rank summation order moves
+    # the clip coefficient by an ulp), so the selection scores agree to a few fp32 ulps; two candidates of one sample
+    # whose scores tie to that precision can swap slots (measured, tools/shard_logit_diag.py: scores -1.0807130 /
+    # -1.0807132 at positions 28 / 31, the tiny config after 4 steps).  The encoder sees the slot order (its
+    # positional bias), so that sample's logit moves (9.8e-4), and the SE gate's batch mean carries a share of it to
+    # every other sample (~2e-5).  Every slot-order difference must be such a tie (the same positions, scores within
+    # 8 ulps); only then are the logits held to 1e-3.
+    ia, ib = a["eval_idx"].numpy(), b["eval_idx"].numpy()
+    flip = ~(ia == ib).all(1)
+    lt = rtol
+    if flip.any():
+        va = a["eval_vals"].numpy()
+        for i in np.where(flip)[0]:
+            d = ia[i] != ib[i]
+            assert sorted(ia[i][d]) == sorted(ib[i][d]), (what, i, ia[i], ib[i])
+            sc = va[i][d]
+            assert sc.max() - sc.min() <= 8 * np.spacing(np.float32(np.abs(sc).max())), (what, i, sc)
+        lt = max(rtol, 1e-3)
+    close_enough(a["logits"].double().numpy(), b["logits"].double().numpy(), lt, atol, what + "logits")
     assert a["sd"].keys() == b["sd"].keys()
     for k in a["sd"]:
         assert a["sd"][k].shape == b["sd"][k].shape, k

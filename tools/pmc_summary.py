@@ -6,7 +6,8 @@ non-PMC kernel duration from a kernel-trace summary (PMC runs serialise dispatch
 timestamps are not used).  Derived columns:
   * HBM bytes  = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024; gfx950 FETCH_SIZE counts half of wide
     streaming reads, MI355X_MICROARCH.md "HBM")
-  * MFMA TF/s  = (SQ_INSTS_VALU_MFMA_MOPS_F32 + _BF16 when collected) x 512 FLOP / duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
+  * MFMA TF/s  = (SQ_INSTS_VALU_MFMA_MOPS_F32 + _BF16, each when collected -- the f32 one comes from the "mops" pass
+    of tools/profile.sh; without it f32-MFMA kernels read 0) x 512 FLOP / duration; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES /
     (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
   * VALU issue = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction on a 32-wide SIMD) / (duration x
     2.4 GHz x 1024 SIMDs): the fraction of the chip's VALU issue slots the kernel's vector instructions fill

@@ -31,6 +31,9 @@ pmc_groups() {  # suffix config
   pmc "write$1" "$2" WRITE_SIZE
   pmc "valu$1" "$2" SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
       SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
+  # f32 MFMA ops (the QNN Gram products, the fused layer forward's projections) in their own pass: the valu pass
+  # holds 7 SQ counters already
+  pmc "mops$1" "$2" SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE
   pmc "lds$1" "$2" SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU \
       SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY
 }

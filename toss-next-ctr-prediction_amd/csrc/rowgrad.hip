@@ -14,6 +14,7 @@
 
 #include "common.h"
 #include "ctr_hip.h"
+#include "scan.h"
 
 namespace ctr {
 
@@ -25,10 +26,10 @@ __global__ void iota_kernel(uint32_t* v, int n) {
 // query hipGetDeviceProperties on the host at every call (is_sleep_scan_state_used), which stalled the host's
 // issue of the step's other stream for ~0.1 ms per dedupe.  Two passes over RLE_CH-key blocks: (1) each block
 // counts its run heads (i == 0 or key[i] != key[i-1]); (2) each block sums the counts of the blocks before it
-// (<= a few hundred words, in order), scans its threads' head counts in LDS and writes, per run, the unique key and
+// (in order; beyond SCAN_FLAT_MAX blocks they are scanned once first, scan.h), scans its threads' head counts in LDS and writes, per run, the unique key and
 // its first index; the last block writes n_uniq and offsets[n_uniq] = n, so a run's length is
 // offsets[u + 1] - offsets[u].  Deterministic and in key order, as the rocPRIM pair was.
-constexpr int RLE_T = 256, RLE_IPT = 8, RLE_CH = RLE_T * RLE_IPT;
+constexpr int RLE_T = SCAN_T, RLE_IPT = SCAN_IPT, RLE_CH = SCAN_CH;     // scan.h's block shape (shared helpers)
 
 __device__ __forceinline__ uint32_t rle_heads(const uint32_t* __restrict__ skeys, int n, int i0, bool (&h)[RLE_IPT]) {
   uint32_t k[RLE_IPT + 1];
@@ -45,36 +46,23 @@ __device__ __forceinline__ uint32_t rle_heads(const uint32_t* __restrict__ skeys
   return c;
 }
 
-__device__ __forceinline__ uint32_t rle_block_sum(uint32_t v, uint32_t* red) {
-  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-#pragma unroll
-  for (int w = 0; w < RLE_T / 64; ++w) t += red[w];
-  __syncthreads();
-  return t;
-}
-
 __global__ __launch_bounds__(RLE_T) void rle_count_kernel(const uint32_t* __restrict__ skeys, int n,
                                                           uint32_t* __restrict__ bcount) {
   __shared__ uint32_t red[RLE_T / 64];
   bool h[RLE_IPT];
   const uint32_t c = rle_heads(skeys, n, blockIdx.x * RLE_CH + threadIdx.x * RLE_IPT, h);
-  const uint32_t t = rle_block_sum(c, red);
+  const uint32_t t = scan_block_sum(c, red);
   if (threadIdx.x == 0) bcount[blockIdx.x] = t;
 }
 
 __global__ __launch_bounds__(RLE_T) void rle_write_kernel(const uint32_t* __restrict__ skeys, int n,
-                                                          const uint32_t* __restrict__ bcount,
+                                                          const uint32_t* __restrict__ bcount, int prescanned,
                                                           uint32_t* __restrict__ uniq_keys,
                                                           uint32_t* __restrict__ offsets,
                                                           uint32_t* __restrict__ n_uniq) {
   __shared__ uint32_t red[RLE_T / 64];
   __shared__ uint32_t sc[RLE_T];
-  uint32_t pre = 0;
-  for (int q = threadIdx.x; q < (int)blockIdx.x; q += RLE_T) pre += bcount[q];
-  pre = rle_block_sum(pre, red);                 // the heads of the blocks before this one
+  const uint32_t pre = scan_block_prefix(bcount, prescanned != 0, red);   // the heads of the blocks before this one
   bool h[RLE_IPT];
   const int i0 = blockIdx.x * RLE_CH + threadIdx.x * RLE_IPT;
   const uint32_t c = rle_heads(skeys, n, i0, h);
@@ -203,13 +191,16 @@ struct RowgradWs {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// the sort's temporary size depends on n only: the last few sizes cached (the step alternates two or three n)
+// the sort's temporary size depends on n (and the device's arch): the last few (device, n) cached per host thread
+// (the step alternates two or three n; ctypes releases the GIL, so two threads may be in here at once)
 static RowgradWs rowgrad_layout(int n) {
-  static int cached_n[4] = {-1, -1, -1, -1};
-  static RowgradWs cached[4];
-  static int next = 0;
+  thread_local int cached_n[4] = {-1, -1, -1, -1}, cached_dev[4] = {-1, -1, -1, -1};
+  thread_local RowgradWs cached[4];
+  thread_local int next = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
   for (int q = 0; q < 4; ++q)
-    if (cached_n[q] == n) return cached[q];
+    if (cached_n[q] == n && cached_dev[q] == dev) return cached[q];
   RowgradWs w{};
   size_t t1 = 0;
   (void)rocprim::radix_sort_pairs(nullptr, t1, (const uint32_t*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr,
@@ -223,6 +214,7 @@ static RowgradWs rowgrad_layout(int n) {
   w.off_offsets = w.off_bcount + align256((size_t)cdiv(n, RLE_CH) * sizeof(uint32_t));
   w.total = w.off_offsets + align256(((size_t)n + 1) * sizeof(uint32_t));
   cached_n[next] = n;
+  cached_dev[next] = dev;
   cached[next] = w;
   next = (next + 1) & 3;
   return w;
@@ -259,7 +251,9 @@ static int rowgrad_core(const uint32_t* keys, const float* const* contrib, float
   CTR_REQUIRE(e == hipSuccess, "radix_sort_pairs failed");
   const int nb = cdiv(n, RLE_CH);
   rle_count_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount);
-  rle_write_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount, uniq_keys, offsets, n_uniq);
+  const int pre = nb > SCAN_FLAT_MAX;         // > 2M keys: the block counts scanned once (scan.h)
+  if (pre) scan_prefix_kernel<<<1, SCAN_T, 0, s>>>(bcount, nb);
+  rle_write_kernel<<<nb, RLE_T, 0, s>>>(skeys, n, bcount, pre, uniq_keys, offsets, n_uniq);
   if (ncontrib == 2 && width <= 32)
     segsum2_kernel<<<cdiv(n, 4 * SS_KPW), 256, 0, s>>>(contrib[0], contrib[1], ld, width, uniq_keys, sidx, offsets,
                                                          n_uniq, (uint32_t)n, uniq_grad[0], uniq_grad[1]);

@@ -194,25 +194,32 @@ class CtrError(RuntimeError):
     pass
 
 
-_timed = {}     # entry name -> list of (start, end) torch.cuda.Event pairs, while timing is on
+_timed = {}     # entry name -> list of (start, end, key) torch.cuda.Event pairs + report key, while timing is on
+# entry points reported per call shape: one entry serves launches of different shapes (the three QNN MLP products)
+_TIME_KEY = {"ctr_gemm_bf16_ex": lambda a: f"ctr_gemm_bf16_ex@{a[0]}x{a[1]}x{a[2]}" + ("b" if a[15] else "")}
 
 
 def time_calls(names):
     """Bracket every call of the named entry points with HIP events on the current stream (the stream
-    the library launches on); ``timed_ms()`` reads the per-call averages.  ``time_calls(())`` stops."""
+    the library launches on); ``timed_ms()`` reads the per-call averages.  ``time_calls(())`` stops.
+    A name may carry a shape key (``ctr_gemm_bf16_ex@MxNxK``): the entry point is bracketed."""
     _timed.clear()
     for n in names:
-        _timed[n] = []
+        _timed[n.split("@")[0]] = []
 
 
 def timed_ms():
-    """{name: (calls, average ms per call)} of the calls bracketed since time_calls()."""
+    """{key: (calls, average ms per call)} of the calls bracketed since time_calls(); the key is the entry name, or
+    the name and the call's shape for the entries of _TIME_KEY."""
     import torch
     torch.cuda.synchronize()
     out = {}
-    for n, evs in _timed.items():
-        if evs:
-            out[n] = (len(evs), sum(a.elapsed_time(b) for a, b in evs) / len(evs))
+    for evs in _timed.values():
+        acc = {}
+        for a, b, key in evs:
+            acc.setdefault(key, []).append(a.elapsed_time(b))
+        for key, ts in acc.items():
+            out[key] = (len(ts), sum(ts) / len(ts))
     return out
 
 
@@ -229,7 +236,8 @@ def call(name, *args):
         ev[0].record()
         rc = fn(*args)
         ev[1].record()
-        _timed[name].append(ev)
+        kf = _TIME_KEY.get(name)
+        _timed[name].append((ev[0], ev[1], kf(args) if kf else name))
     else:
         rc = fn(*args)
     if rc != 0:
