@@ -1214,6 +1214,184 @@ __global__ __launch_bounds__(256) void ffn_fwd_bfp_kernel(FfnArgs a) {
   }
 }
 
+// Wave-independent forward (D = 32, round 5): no x tile in LDS and no barrier after the weight staging, so a
+// workgroup's eight waves run free of each other and two workgroups (51 KB of weight images each) fit a CU at four
+// waves per SIMD (<= 128 registers).  A wave owns 32-row tiles t = wave, + total waves, ...; its x rows are read
+// straight into registers in the k order the products use -- lane (g, c) holds x[row 16 i + c][4g .. 4g+3] and
+// [16 + 4g .. 16 + 4g+3] -- which is both the B operand of pre^T = W1 x^T (the staged W1 image carries the same d
+// order) and, because the output is formed TRANSPOSED (y^T = W2 fo^T: A = the W2 image, B = fo straight from the
+// pre^T accumulators), exactly the fp32 residual the epilogue adds to lane (g, c)'s outputs y[row 16 i + c][16 j +
+// 4g + r]: a row's 32 outputs sit in its four lane groups, the RMSNorm sum takes two lane swaps, h and y go out as
+// 16-byte stores of whole rows.  The next tile's rows are loaded while the current one computes.  Keep bits, their
+// "row words" layout, the weight images for the backward: as the per-tile kernels.
+struct FfnFw {
+  static constexpr int D = 32, RW = 32, NI = 2, NWAVE = 8;
+};
+
+template <bool DROP>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ffn_fwd_bfw_kernel(FfnArgs a) {
+  constexpr int D = 32;
+  extern __shared__ __attribute__((aligned(16))) char fsm[];
+  const int FF = a.FF, NCH = FF / 32;
+  bf16x8* iw1 = (bf16x8*)fsm;                        // [NCH][2][64]: W1[32 ch + 16 s + c][4g .. +3 | 16 + 4g .. +3]
+  bf16x8* iw2 = iw1 + NCH * 2 * 64;                  // [NCH][2][64]: W2[16 j + c][32 ch + 4g .. +3 | 32 ch + 16 + 4g ..]
+  float* sb1 = (float*)(iw2 + NCH * 2 * 64);         // [FF]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
+  if (a.wbf) {     // bf16 weight images for the backward: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF)
+    const int n = FF * D;
+    for (int e = blockIdx.x * 512 + tid; e < 3 * n; e += gridDim.x * 512) {
+      float v;
+      if (e < n) {
+        v = a.W1[e];
+      } else if (e < 2 * n) {
+        const int q = e - n;
+        v = a.W2[(q % D) * FF + q / D];
+      } else {
+        const int q = e - 2 * n;
+        v = a.W1[(q % FF) * D + q / FF];
+      }
+      a.wbf[e] = (__bf16)v;
+    }
+  }
+  for (int u = tid; u < NCH * 2 * 64; u += 512) {
+    const int l = u & 63, sc = u >> 6, s2 = sc & 1, ch = sc >> 1, lg = l >> 4;
+    const float* p = a.W1 + (long)(32 * ch + 16 * s2 + (l & 15)) * D + 4 * lg;
+    iw1[u] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 16));
+  }
+  for (int u = tid; u < NCH * 2 * 64; u += 512) {
+    const int l = u & 63, q = u >> 6, j = q & 1, ch = q >> 1;
+    const float* p = a.W2 + (long)(16 * j + (l & 15)) * FF + 32 * ch + 4 * (l >> 4);
+    iw2[u] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 16));
+  }
+  for (int u = tid; u < FF; u += 512) sb1[u] = a.b1[u];
+  __syncthreads();
+
+  const int nb16 = (a.M + 15) / 16;
+  const auto rmask = buf_rsrc(a.mask, DROP ? (uint32_t)nb16 * 16 * (FF / 32) * 4 : 0u);
+  const uint32_t xbytes = (uint32_t)a.M * D * 4;
+  const auto rx = buf_rsrc(a.x, xbytes);
+  const auto rh = buf_rsrc(a.h, xbytes);
+  const auto ry = buf_rsrc(a.y, xbytes);
+  const auto rr = buf_rsrc(a.r, (uint32_t)a.M * 4);
+  const uint32_t thr = a.drop.thresh;
+  const float dsc = a.drop.scale;
+  // x rows of a tile: xr[i][j] = x[m0 + 16 i + c][16 j + 4g .. +3] (0 past M)
+  f32x4 xr[2][2];
+  auto fetch_x = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        xr[i][j] = buf_ld4(rx, (uint32_t)(((t * 32 + 16 * i + c) * D) + 16 * j + 4 * g) * 4, 0);
+  };
+  struct Wc {
+    bf16x8 w1[2], w2[2];
+    f32x4 b[2];
+  };
+  auto load_w = [&](int ch, Wc& W) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      W.w1[s2] = iw1[(ch * 2 + s2) * 64 + lane];
+      W.w2[s2] = iw2[(ch * 2 + s2) * 64 + lane];
+      W.b[s2] = *(const f32x4*)(sb1 + 32 * ch + 16 * s2 + 4 * g);
+    }
+  };
+  const int ntiles = (a.M + 31) / 32;
+  const int gw = blockIdx.x * FfnFw::NWAVE + w, nw = gridDim.x * FfnFw::NWAVE;
+  if (gw < ntiles) fetch_x(gw);
+  for (int tile = gw; tile < ntiles; tile += nw) {
+    const int m0 = tile * 32;
+    bf16x8 xf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) xf[i] = pack8(xr[i][0], xr[i][1]);
+    if (tile + nw < ntiles) fetch_x(tile + nw);
+    f32x4 yacc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ch = 0; ch < NCH; ++ch) {
+      Wc W;
+      load_w(ch, W);
+      const int f0 = 32 * ch;
+      f32x4 p[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) p[i][s2] = mfma_bf(W.w1[s2], xf[i], W.b[s2]);   // pre^T [ff][row], + b1
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t m = (uint32_t)(m0 + 16 * i + c);
+        uint32_t kb = 0;
+        f32x4 fo[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const f32x2 z = {p[i][s2][2 * q], p[i][s2][2 * q + 1]};
+            f32x2 v = gelu_as2(z);
+            if (DROP) {
+              const uint32_t hb = drop_pair_bits(a.drop, (m * (uint32_t)FF + f0 + 16 * s2 + 4 * g + 2 * q) >> 1);
+              const bool k0 = (hb & 0xFFFFu) >= thr, k1 = (hb >> 16) >= thr;
+              v = v * f32x2{k0 ? dsc : 0.f, k1 ? dsc : 0.f};
+              kb |= (k0 ? 1u : 0u) << (4 * s2 + 2 * q);
+              kb |= (k1 ? 1u : 0u) << (4 * s2 + 2 * q + 1);
+            }
+            fo[s2][2 * q] = v.x;
+            fo[s2][2 * q + 1] = v.y;
+          }
+        const bf16x8 bf = pack8(fo[0], fo[1]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) yacc[i][j] = mfma_bf(W.w2[j], bf, yacc[i][j]);          // y^T [d][row]
+        if (DROP) {
+          uint32_t kw = ((kb & 0xFu) << (4 * g)) | ((kb >> 4) << (16 + 4 * g));
+          kw |= (uint32_t)__shfl_xor((int)kw, 16, 64);
+          kw |= (uint32_t)__shfl_xor((int)kw, 32, 64);
+          const uint32_t wi = rw_word(ch, nb16, m0 / 16 + i, c);
+          buf_st_u32(kw, rmask, (g == 0 && (int)m < a.M) ? wi * 4 : BUF_OOB);
+        }
+      }
+    }
+    // epilogue: h = x + (y + b2), r = 1 / rms(h), y = nw h r -- row 16 i + c over the four lane groups; the x rows
+    // (this wave's own, read at the tile's start) are read again rather than held across the chunk loop
+    f32x4 xc[2][2], bb[2], nn[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        xc[i][j] = buf_ld4(rx, (uint32_t)(((m0 + 16 * i + c) * D) + 16 * j + 4 * g) * 4, 0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      bb[j] = *(const f32x4*)(a.b2 + 16 * j + 4 * g);
+      nn[j] = *(const f32x4*)(a.nw + 16 * j + 4 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x4 hv[2];
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        hv[j] = xc[i][j] + (yacc[i][j] + bb[j]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss = fmaf(hv[j][r], hv[j][r], ss);
+      }
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      const float rs = 1.0f / sqrtf(ss / (float)D + a.eps);
+      const uint32_t row = (uint32_t)(m0 + 16 * i + c);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t off = (row * D + 16 * j + 4 * g) * 4;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hv[j]), rh, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nn[j] * hv[j] * rs), ry, off, 0, 0);
+      }
+      buf_st(rs, rr, g == 0 ? row * 4 : BUF_OOB);
+    }
+  }
+}
+
+static size_t ffn_fwdw_lds(int FF) { return (size_t)FF * 32 * 2 * 2 + (size_t)FF * 4; }
+
 template <int D>
 static size_t ffn_fwdp_lds(int FF) {
   return (size_t)FF * D * 2 * 2 + (size_t)FF * 4 + (size_t)FfnBf<D>::RT * FfnBf<D>::S * 4;
@@ -2296,19 +2474,19 @@ static void launch_ffn_bf(const FfnArgs& a, bool bwd, hipStream_t s) {
   const bool drop = a.drop.thresh != 0;
   if (!bwd) {
     if constexpr (D == 32) {
-      const size_t sm = ffn_fwdp_lds<D>(a.FF);
-      if (sm <= 80 * 1024) {      // two workgroups per CU
+      const size_t sm = ffn_fwdw_lds(a.FF);
+      if (sm <= 76 * 1024) {      // two workgroups of eight waves per CU
         static bool attr = false;
         if (!attr) {
-          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfp_kernel<D, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    80 * 1024);
-          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfp_kernel<D, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    80 * 1024);
+          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfw_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    76 * 1024);
+          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfw_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    76 * 1024);
           attr = true;
         }
-        const int grid = std::min(cdiv(a.M, FfnBf<D>::RT), 2 * 256);
-        if (drop) ffn_fwd_bfp_kernel<D, true><<<grid, 256, sm, s>>>(a);
-        else ffn_fwd_bfp_kernel<D, false><<<grid, 256, sm, s>>>(a);
+        const int grid = std::min(cdiv(a.M, 32 * FfnFw::NWAVE), 2 * 256);
+        if (drop) ffn_fwd_bfw_kernel<true><<<grid, 512, sm, s>>>(a);
+        else ffn_fwd_bfw_kernel<false><<<grid, 512, sm, s>>>(a);
         return;
       }
     }
