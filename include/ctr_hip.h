@@ -98,6 +98,8 @@ int ctr_gemm_bf16_ex(int M, int N, int K, const void* A, int lda, int ta, const 
                      void* C, int ldc, const ctr_gemm_epi_t* epi, int splits, float* ws, const ctr_gemm_seg_t* seg,
                      int flags, void* stream);
 int ctr_to_bf16(const float* src, long lds, int rows, int cols, void* dst, long ldd, void* stream);
+/* test / bench hook: the bf16 GEMM kernel form (0 automatic, 1 two-stage 128 x 128, 2 ring 256 x 128, 3 ring 128 x 128) */
+void ctr_gemm_bf16_set_variant(int v);
 
 
 /* Row-streaming GEMMs of the DARE encoder layer (MHA in_proj / out_proj, src/models/dare.py:53-62, and

@@ -19,10 +19,16 @@ def bf16_image(L, x):
 
 @pytest.mark.parametrize("M,N,K,ta,tb", [(4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0),
                                          (300, 136, 192, 0, 1), (136, 264, 128, 1, 0), (72, 200, 64, 1, 1),
-                                         (257, 88, 320, 0, 0)])
+                                         (257, 88, 320, 0, 0),
+                                         # the ring kernel (M >= 256): every operand layout, one or two k-steps per
+                                         # tile (epilogue stores inside the counted-wait window), row / column tails
+                                         (520, 264, 192, 1, 1), (1024, 1000, 64, 0, 1), (600, 520, 128, 0, 0),
+                                         (384, 2048, 64, 1, 0), (2000, 7552, 512, 0, 0)])
 @pytest.mark.parametrize("splits", [1, 3])
-def test_gemm_bf16_vs_torch(M, N, K, ta, tb, splits):
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])     # automatic, two-stage, ring 256 x 128, ring 128 x 128
+def test_gemm_bf16_vs_torch(M, N, K, ta, tb, splits, variant):
     L = _lib()
+    L.query("ctr_gemm_bf16_set_variant", variant)
     assert L.query("ctr_gemm_bf16_ok", M, N, K, M if ta else K, ta, K if tb else N, tb, splits)
     g = torch.Generator(device="cuda").manual_seed(M * 13 + N + K)
     A = torch.randn((K, M) if ta else (M, K), device="cuda", generator=g)
@@ -37,6 +43,12 @@ def test_gemm_bf16_vs_torch(M, N, K, ta, tb, splits):
     ref = a64 @ b64
     assert torch.isfinite(C).all()
     assert rel(C.double(), ref) < 1e-5
+    # deterministic: a second call writes the same bits (a staged tile read before its DMA landed would not)
+    C2 = torch.full_like(C, float("nan"))
+    L.call("ctr_gemm_bf16", M, N, K, ptr(Ab), Ab.shape[1], ta, ptr(Bb), Bb.shape[1], tb, ptr(C2), N, None, splits,
+           ptr(ws), None, stream())
+    L.query("ctr_gemm_bf16_set_variant", 0)
+    assert torch.equal(C, C2)
 
 
 def test_gemm_bf16_epilogue_and_c2():

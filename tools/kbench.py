@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--bf16", action="store_true", help="ffn: the amp bf16 kernels (CTR_FFN_BF16)")
     ap.add_argument("--norms", action="store_true", help="ffn: the norm-fused backward (ctr_ffn_bwd_norms, as the step)")
     ap.add_argument("--shapes", default="", help="gemm: comma-separated indices of the shape list")
+    ap.add_argument("--variant", type=int, default=0, help="gemmig: ctr_gemm_bf16_set_variant")
     args = ap.parse_args()
     torch.manual_seed(0)
     st = torch.cuda.current_stream().cuda_stream
@@ -147,20 +148,36 @@ def main():
                 t = timeit(lambda: torch.matmul(a_op, b_op, out=Cg), args.iters)
             res.append(f"torch:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}")
             print(f"gemm M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
-    if "gemmbf" in which:      # ctr_gemm_bf16 (bf16 operands in HBM) on the QNN MLP's three big products
-        for (Mg, Ng, Kg, ta, tb) in [(4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0)]:
-            Ag = torch.randn((Kg, Mg) if ta else (Mg, Kg), device="cuda").bfloat16()
-            Bg = torch.randn((Ng, Kg) if tb else (Kg, Ng), device="cuda").bfloat16()
-            Cg = torch.empty(Mg, Ng, device="cuda")
-            res = []
-            for sp in (1, 2, 3, 4, 6, 8):
-                ws = torch.empty(sp * Mg * Ng + 16, device="cuda")
-                fn = lambda: call("ctr_gemm_bf16", Mg, Ng, Kg, ptr(Ag), Ag.shape[1], ta, ptr(Bg), Bg.shape[1], tb,
-                                  ptr(Cg), Ng, None, sp, ptr(ws), None, st)
-                t = timeit(fn, args.iters)
-                res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}({t * 1e3:.0f}us)")
-            print(f"gemm_bf16 M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
-        # the input grad as the step runs it: bf16 [dz | dinter] output split at column 6400
+    if "gemmbf" in which:      # ctr_gemm_bf16 (bf16 operands in HBM) on the QNN MLP's three big products, per kernel form
+        for var in (1, 2, 3):      # ctr_gemm_bf16_set_variant: two-stage 128 x 128, ring 256 x 128, ring 128 x 128
+            _lib.query("ctr_gemm_bf16_set_variant", var)
+            for (Mg, Ng, Kg, ta, tb) in [(4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0)]:
+                Ag = torch.randn((Kg, Mg) if ta else (Mg, Kg), device="cuda").bfloat16()
+                Bg = torch.randn((Ng, Kg) if tb else (Kg, Ng), device="cuda").bfloat16()
+                Cg = torch.empty(Mg, Ng, device="cuda")
+                res = []
+                for sp in (1, 2, 4, 8):
+                    ws = torch.empty(sp * Mg * Ng + 16, device="cuda")
+                    fn = lambda: call("ctr_gemm_bf16", Mg, Ng, Kg, ptr(Ag), Ag.shape[1], ta, ptr(Bg), Bg.shape[1], tb,
+                                      ptr(Cg), Ng, None, sp, ptr(ws), None, st)
+                    t = timeit(fn, args.iters)
+                    res.append(f"s{sp}:{2.0 * Mg * Ng * Kg / t / 1e9:.0f}({t * 1e3:.0f}us)")
+                print(f"v{var} gemm_bf16 M={Mg} N={Ng} K={Kg} ta={ta} tb={tb} TF/s: " + " ".join(res))
+            # the input grad as the step runs it: bf16 [dz | dinter] output split at column 6400
+            Mg, Ng, Kg, nc = 4096, 7552, 512, 6400
+            Ag = torch.randn(Mg, Kg, device="cuda").bfloat16()
+            Bg = torch.randn(Kg, Ng, device="cuda").bfloat16()
+            C1 = torch.empty(Mg, nc, device="cuda", dtype=torch.bfloat16)
+            C2 = torch.empty(Mg, Ng - nc, device="cuda", dtype=torch.bfloat16)
+            seg = _lib.GemmSeg(C2=ptr(C2), ldc2=Ng - nc, nc=nc)
+            fn = lambda: call("ctr_gemm_bf16_ex", Mg, Ng, Kg, ptr(Ag), Kg, 0, ptr(Bg), Ng, 0, ptr(C1), nc, None, 1, None,
+                              seg, 1, st)
+            t = timeit(fn, args.iters)
+            print(f"v{var} gemm_bf16 out bf16 + C2 M={Mg} N={Ng} K={Kg}: {2.0 * Mg * Ng * Kg / t / 1e9:.0f} TF/s "
+                  f"({t * 1e3:.0f}us)")
+        _lib.query("ctr_gemm_bf16_set_variant", 0)
+    if "gemmig" in which:      # the QNN MLP's input grad alone (bf16 [dz | dinter] out), one kernel form: PMC passes
+        _lib.query("ctr_gemm_bf16_set_variant", args.variant)
         Mg, Ng, Kg, nc = 4096, 7552, 512, 6400
         Ag = torch.randn(Mg, Kg, device="cuda").bfloat16()
         Bg = torch.randn(Kg, Ng, device="cuda").bfloat16()
@@ -170,7 +187,8 @@ def main():
         fn = lambda: call("ctr_gemm_bf16_ex", Mg, Ng, Kg, ptr(Ag), Kg, 0, ptr(Bg), Ng, 0, ptr(C1), nc, None, 1, None,
                           seg, 1, st)
         t = timeit(fn, args.iters)
-        print(f"gemm_bf16 out bf16 + C2 M={Mg} N={Ng} K={Kg}: {2.0 * Mg * Ng * Kg / t / 1e9:.0f} TF/s ({t * 1e3:.0f}us)")
+        print(f"v{args.variant} input grad: {2.0 * Mg * Ng * Kg / t / 1e9:.0f} TF/s ({t * 1e3:.0f}us)")
+        _lib.query("ctr_gemm_bf16_set_variant", 0)
     if "attn" in which or "attnbf" in which:
         qkv = torch.randn(M, 3 * D, device="cuda")
         rel = torch.randn(2 * K + 1, device="cuda") * 0.1

@@ -588,6 +588,8 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
 }
 
 typedef short s16x4_g __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_g __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_g __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ bf16x4 lds_tr4_g(const __bf16* p) {
   return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
                                         (__attribute__((address_space(3))) s16x4_g*)p));
@@ -794,6 +796,317 @@ __global__ __launch_bounds__(256) void gemm_bf_kernel(GemmBfArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// bf16-operand GEMM, ring form (round 5): ONE 512-thread workgroup per CU walks its tiles' 64-deep k-steps as
+// one flat sequence through a ring of NS LDS stages filled by global_load_lds, NS - 1 steps ahead --
+// across tile boundaries, so a tile's first steps are in flight while the previous tile computes and stores.
+// Each step: a COUNTED s_waitcnt vmcnt (this wave's pieces of the step have landed; the younger steps' DMA and
+// the recent epilogue stores stay in flight), a raw s_barrier (every wave's pieces landed, and every wave is
+// done reading the stage the next DMA overwrites), the DMA of step + NS - 1, then the MFMAs.  The
+// two-stage kernel above waited for vmcnt(0) -- every DMA and store in flight -- at each of its barriers.
+// Tile 256 x 128 (8 waves as 4 (M) x 2 (N) of 64 x 64, C^T accumulators as above): operand re-reads from L2 are
+// 3/4 of the 128 x 128 tile's per output element.  The epilogue's stores are raw buffer stores, exactly 16 per
+// lane per tile (32 with a C2 segment: one to each, the other dropped) -- out-of-range rows / columns dropped
+// by the resource bound instead of skipped -- so the counted waits stay exact; epilogues with operands of their
+// own (bias, activation, ...) take a vmcnt(0) at the next two steps.
+constexpr int G8_BN = 128;
+template <int BM, int NS>
+struct G8 {
+  static constexpr int A = BM * 64, B = G8_BN * 64, STAGE = A + B;   // bf16 elements
+  static constexpr int LDS = NS * STAGE * 2;
+  static constexpr int PL = (BM + G8_BN) * 128 / 1024 / 8;         // DMA pieces per lane per step
+  static constexpr int WR = BM / 64, WC = 8 / WR;                   // wave grid (each 64 rows)
+  static constexpr int WN = G8_BN / WC, NJ = WN / 16;               // wave columns, 16-col blocks
+  static_assert(LDS <= 160 * 1024, "G8: LDS");
+};
+int g_gemm_bf_variant = 0;     // test / bench hook (ctr_gemm_bf16_set_variant): 0 auto, 1 two-stage, 2 ring 256, 3 ring 128
+
+// rows [r0, r0 + NR) x k [k0, k0 + 64) of a k-contiguous operand into a swizzled [NR][64] image (as stage_kc)
+template <int NR>
+__device__ __forceinline__ void stage_kc8(const __bf16* __restrict__ src, long ld, int r0, int nvalid, int k0,
+                                          __bf16* tile, int w, int lane) {
+  constexpr int PW = NR / 64;
+#pragma unroll
+  for (int t = 0; t < PW; ++t) {
+    const int q = w * PW + t, r = q * 8 + (lane >> 3);
+    const int kc = (lane & 7) ^ ((r >> 1) & 7);
+    const int gr = min(r0 + r, nvalid - 1);
+    glds16(src + (long)gr * ld + k0 + 8 * kc, tile + q * 512);
+  }
+}
+// k [k0, k0 + 64) x cols [c0, c0 + NC) of a k-major operand into [8 k-blocks][NC / 16 col-blocks][8][16] (as stage_km)
+template <int NC>
+__device__ __forceinline__ void stage_km8(const __bf16* __restrict__ src, long ld, int c0, int nvalid, int k0,
+                                          __bf16* tile, int w, int lane) {
+  constexpr int PW = NC / 64, QB = NC / 64;     // pieces per wave; pieces per k-block (4 col-blocks each)
+#pragma unroll
+  for (int t = 0; t < PW; ++t) {
+    const int q = w * PW + t, kb = q / QB, cb = 4 * (q % QB) + (lane >> 4);
+    const int row = ((lane & 15) >> 1) ^ (4 * (kb & 1));
+    const int col = min(c0 + 16 * cb + 8 * (lane & 1), nvalid - 8);
+    glds16(src + (long)(k0 + 8 * kb + row) * ld + col, tile + q * 512);
+  }
+}
+template <int NCB>
+__device__ __forceinline__ bf16x8 frag_km8(const __bf16* tile, int cb16, int ks, int lane) {
+  const int kb = 4 * ks + (lane >> 4), l = lane & 15;
+  const __bf16* blk = tile + (kb * NCB + cb16) * 128;
+  const int sw = 4 * (kb & 1);
+  const bf16x4 lo = lds_tr4_g(blk + ((l >> 2) ^ sw) * 16 + 4 * (l & 3));
+  const bf16x4 hi = lds_tr4_g(blk + (((l >> 2) + 4) ^ sw) * 16 + 4 * (l & 3));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// s_waitcnt vmcnt(n) (n <= 63), lgkmcnt / expcnt not waited for
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 1: wait_vm<1>(); break;
+    case 2: wait_vm<2>(); break;
+    case 3: wait_vm<3>(); break;
+    case 4: wait_vm<4>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    case 8: wait_vm<8>(); break;
+    case 9: wait_vm<9>(); break;
+    case 10: wait_vm<10>(); break;
+    case 11: wait_vm<11>(); break;
+    case 12: wait_vm<12>(); break;
+    case 13: wait_vm<13>(); break;
+    case 14: wait_vm<14>(); break;
+    case 15: wait_vm<15>(); break;
+    case 16: wait_vm<16>(); break;
+    case 17: wait_vm<17>(); break;
+    case 18: wait_vm<18>(); break;
+    case 19: wait_vm<19>(); break;
+    case 20: wait_vm<20>(); break;
+    case 21: wait_vm<21>(); break;
+    case 22: wait_vm<22>(); break;
+    case 23: wait_vm<23>(); break;
+    case 24: wait_vm<24>(); break;
+    case 25: wait_vm<25>(); break;
+    case 26: wait_vm<26>(); break;
+    case 27: wait_vm<27>(); break;
+    case 28: wait_vm<28>(); break;
+    case 29: wait_vm<29>(); break;
+    case 30: wait_vm<30>(); break;
+    case 31: wait_vm<31>(); break;
+    case 32: wait_vm<32>(); break;
+    case 33: wait_vm<33>(); break;
+    case 34: wait_vm<34>(); break;
+    case 35: wait_vm<35>(); break;
+    case 36: wait_vm<36>(); break;
+    case 37: wait_vm<37>(); break;
+    case 38: wait_vm<38>(); break;
+    case 39: wait_vm<39>(); break;
+    case 40: wait_vm<40>(); break;
+    case 41: wait_vm<41>(); break;
+    case 42: wait_vm<42>(); break;
+    case 43: wait_vm<43>(); break;
+    case 44: wait_vm<44>(); break;
+    case 45: wait_vm<45>(); break;
+    case 46: wait_vm<46>(); break;
+    case 47: wait_vm<47>(); break;
+    case 48: wait_vm<48>(); break;
+    case 49: wait_vm<49>(); break;
+    case 50: wait_vm<50>(); break;
+    case 51: wait_vm<51>(); break;
+    case 52: wait_vm<52>(); break;
+    case 53: wait_vm<53>(); break;
+    case 54: wait_vm<54>(); break;
+    case 55: wait_vm<55>(); break;
+    case 56: wait_vm<56>(); break;
+    case 57: wait_vm<57>(); break;
+    case 58: wait_vm<58>(); break;
+    case 59: wait_vm<59>(); break;
+    case 60: wait_vm<60>(); break;
+    case 61: wait_vm<61>(); break;
+    case 62: wait_vm<62>(); break;
+    case 63: wait_vm<63>(); break;
+    default: wait_vm<0>(); break;     // never under-waits
+  }
+}
+
+template <bool TA, bool TB, int BM, int NS>
+__global__ __launch_bounds__(512) void gemm_bf8_kernel(GemmBfArgs p) {
+  using C8 = G8<BM, NS>;
+  constexpr int NJ = C8::NJ;
+  extern __shared__ __attribute__((aligned(16))) __bf16 sm8[];
+  const GemmArgs& g = p.g;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nsplit = (g.K + g.klen - 1) / g.klen;
+  const int wm = (w / C8::WC) * 64, wn = (w % C8::WC) * C8::WN;
+  auto nk_of = [&](int z) {
+    const int k0 = z * g.klen, k1 = min(g.K, k0 + g.klen);
+    return k1 > k0 ? (k1 - k0) / 64 : 0;
+  };
+  // producer cursor: the next k-step to stage
+  int pt = 0, pk = 0, pz = 0, pm = 0, pn = 0;
+  bool pv = bf_tile(p, nsplit, 0, pz, pm, pn);
+  int pnk = pv ? nk_of(pz) : 0;
+  int nprod = 0;       // k-steps staged so far
+  auto produce = [&](int st) {
+    if (!pv) return;
+    ++nprod;
+    __bf16* ta = sm8 + st * C8::STAGE;
+    __bf16* tb = ta + C8::A;
+    const int k0 = pz * g.klen + pk * 64;
+    if (TA) stage_km8<BM>(p.A, g.lda, pm * BM, g.M, k0, ta, w, lane);
+    else stage_kc8<BM>(p.A, g.lda, pm * BM, g.M, k0, ta, w, lane);
+    if (TB) stage_kc8<G8_BN>(p.B, g.ldb, pn * G8_BN, g.N, k0, tb, w, lane);
+    else stage_km8<G8_BN>(p.B, g.ldb, pn * G8_BN, g.N, k0, tb, w, lane);
+    if (++pk == pnk) {
+      pk = 0;
+      ++pt;
+      pv = bf_tile(p, nsplit, pt, pz, pm, pn);
+      pnk = pv ? nk_of(pz) : 0;
+    }
+  };
+  int ct = 0, cz, cm, cn;
+  if (!bf_tile(p, nsplit, 0, cz, cm, cn)) return;
+  int cnk = nk_of(cz), ck = 0;
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) produce(st);
+
+  // epilogue store plan: fast = raw buffer stores only (exactly SPT per lane per tile)
+  const ctr_gemm_epi_t& e = g.epi;
+  const bool plain = !e.dact && !e.bias && !e.add && !e.pre && !e.act && !e.drop_thresh;
+  const bool fast = p.vec && (g.ws || plain);
+  const bool two = !g.ws && g.C2 != nullptr;
+  const int SPT = (two ? 2 : 1) * 4 * NJ;
+  const int esz = g.ws ? 4 : (p.obf ? 2 : 4);
+  const __amdgpu_buffer_rsrc_t rc = g.ws ? buf_rsrc(g.ws, 0x7FFFFFFF)
+                                         : buf_rsrc(g.C, (uint32_t)(((long)(g.M - 1) * g.ldc + min(g.N, g.nc)) * esz));
+  const __amdgpu_buffer_rsrc_t rc2 = two ? buf_rsrc(g.C2, (uint32_t)(((long)(g.M - 1) * g.ldc2 + (g.N - g.nc)) * esz))
+                                         : rc;
+  int epi_iter[2] = {-99, -99};     // iterations of the last two epilogues (their stores are younger than some DMA)
+  bool epi_slow[2] = {false, false};
+
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int sidx = 0;; ++sidx) {
+    // this step's DMA was issued NS - 1 iterations ago (or in the prologue); younger than it: the DMA of the
+    // steps issued after it, and the stores of every epilogue since (iterations sidx - NS + 1 .. sidx - 1)
+    int younger = C8::PL * (nprod - sidx - 1);
+    {
+      bool slow = false;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int age = sidx - epi_iter[q];
+        if (age >= 1 && age <= NS - 1) {
+          younger += SPT;
+          slow |= epi_slow[q];
+        }
+      }
+      if (slow) younger = 0;
+    }
+    wait_vm_n(min(younger, 63));
+    // raw barrier, no fence (a workgroup fence would drain the DMA in flight: vmcnt(0)); the empty asm keeps the
+    // compiler from moving LDS reads or the next DMA across it
+    __asm__ volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+    produce((sidx + NS - 1) % NS);
+    const __bf16* ta = sm8 + (sidx % NS) * C8::STAGE;
+    const __bf16* tb = ta + C8::A;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = TA ? frag_km8<BM / 16>(ta, (wm >> 4) + i, ks, lane) : frag_kc(ta, wm + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bfr[j] = TB ? frag_kc(tb, wn + 16 * j, ks, lane) : frag_km8<G8_BN / 16>(tb, (wn >> 4) + j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (++ck < cnk) continue;
+    // ---- epilogue of tile (cz, cm, cn)
+    const int m0 = cm * BM, n0 = cn * G8_BN;
+    const int lrow = wm + (lane & 15), lcol = wn + (lane >> 4) * 4;
+    if (fast) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + lrow + i * 16;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = n0 + lcol + j * 16;
+          const bool ok = m < g.M && n < g.N;
+          if (g.ws) {
+            const long off = (((long)cz * g.M + m) * g.N + n) * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_g, acc[i][j]), rc,
+                                                   ok ? (uint32_t)off : BUF_OOB, 0, 0);
+          } else {
+            const bool in2 = two && n >= g.nc;
+            const long o1 = ((long)m * g.ldc + n) * esz, o2 = ((long)m * g.ldc2 + (n - g.nc)) * esz;
+            if (p.obf) {
+              const bf16x4 v = __builtin_convertvector(acc[i][j], bf16x4);
+              __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_g, v), rc,
+                                                    ok && !in2 ? (uint32_t)o1 : BUF_OOB, 0, 0);
+              if (two)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_g, v), rc2,
+                                                      ok && in2 ? (uint32_t)o2 : BUF_OOB, 0, 0);
+            } else {
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_g, acc[i][j]), rc,
+                                                     ok && !in2 ? (uint32_t)o1 : BUF_OOB, 0, 0);
+              if (two)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_g, acc[i][j]), rc2,
+                                                       ok && in2 ? (uint32_t)o2 : BUF_OOB, 0, 0);
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + lrow + i * 16;
+        if (m >= g.M) continue;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int n = n0 + lcol + j * 16;
+          if (n >= g.N) continue;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (n + r >= g.N) continue;
+            if (g.ws) {
+              g.ws[((long)cz * g.M + m) * g.N + n + r] = acc[i][j][r];
+            } else {
+              const float v = epi_elem(e, acc[i][j][r], m, n + r, g.N, g.ldc);
+              if (p.obf) *cptr_bf(g, m, n + r) = (__bf16)v;
+              else *cptr(g, m, n + r) = v;
+            }
+          }
+        }
+      }
+    }
+    epi_iter[1] = epi_iter[0];
+    epi_slow[1] = epi_slow[0];
+    epi_iter[0] = sidx;
+    epi_slow[0] = !fast;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ck = 0;
+    ++ct;
+    if (!bf_tile(p, nsplit, ct, cz, cm, cn)) break;
+    cnk = nk_of(cz);
+  }
+  wait_vm<0>();
+}
+
 // fp32 (rows, cols) with row stride lds -> bf16 with row stride ldd (RNE); 4 elements per thread
 __global__ void to_bf16_kernel(const float* __restrict__ src, long lds, int rows, int cols, __bf16* __restrict__ dst,
                                long ldd) {
@@ -920,6 +1233,30 @@ extern "C" int ctr_to_bf16(const float* src, long lds, int rows, int cols, void*
   return check_launch("ctr_to_bf16");
 }
 
+template <bool TA, bool TB, int BM, int NS>
+static void launch_g8_t(const GemmBfArgs& p, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_bf8_kernel<TA, TB, BM, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              G8<BM, NS>::LDS);
+    attr = true;
+  }
+  gemm_bf8_kernel<TA, TB, BM, NS><<<grid, 512, G8<BM, NS>::LDS, s>>>(p);
+}
+template <int BM, int NS>
+static void launch_g8_b(const GemmBfArgs& p, int ta, int tb, int grid, hipStream_t s) {
+  if (!ta && tb) launch_g8_t<false, true, BM, NS>(p, grid, s);
+  else if (!ta && !tb) launch_g8_t<false, false, BM, NS>(p, grid, s);
+  else if (ta && !tb) launch_g8_t<true, false, BM, NS>(p, grid, s);
+  else launch_g8_t<true, true, BM, NS>(p, grid, s);
+}
+static void launch_g8(const GemmBfArgs& p, int ta, int tb, int BM, int grid, hipStream_t s) {
+  if (BM == 256) launch_g8_b<256, 3>(p, ta, tb, grid, s);
+  else launch_g8_b<128, 4>(p, ta, tb, grid, s);
+}
+
+extern "C" void ctr_gemm_bf16_set_variant(int v) { g_gemm_bf_variant = v; }
+
 extern "C" int ctr_gemm_bf16_ok(int M, int N, int K, int lda, int ta, int ldb, int tb, int splits) {
   if (M < 8 || N < 8 || K <= 0 || K % 64) return 0;
   if (splits < 1) splits = 1;
@@ -973,18 +1310,31 @@ extern "C" int ctr_gemm_bf16_ex(int M, int N, int K, const void* A, int lda, int
   const uintptr_t al = obf ? 7 : 15;       // bf16x4 / f32x4 stores
   p.vec = (N % 4 == 0) && (ldc % 4 == 0) && (((uintptr_t)C & al) == 0) && (!ws || ((uintptr_t)ws & 15) == 0) &&
           (!g.C2 || ((g.ldc2 % 4 == 0) && (g.nc % 4 == 0) && (((uintptr_t)g.C2 & al) == 0)));
-  p.mt = cdiv(M, 128);
-  p.nt = cdiv(N, 128);
-  // XCD column partition where there are n-tiles for every XCD; persistent grid: two workgroups per CU (64 KB
-  // of LDS each) at most, a multiple of 8 for the partition
-  p.gm = p.nt >= 8 ? -1 : 0;
-  const int tiles = p.gm < 0 ? 8 * p.mt * cdiv(p.nt, 8) * splits : p.mt * p.nt * splits;
-  const int grid = std::min(tiles, 512);
   hipStream_t s = (hipStream_t)stream;
-  if (!ta && tb) gemm_bf_kernel<false, true><<<grid, 256, 0, s>>>(p);
-  else if (!ta && !tb) gemm_bf_kernel<false, false><<<grid, 256, 0, s>>>(p);
-  else if (ta && !tb) gemm_bf_kernel<true, false><<<grid, 256, 0, s>>>(p);
-  else gemm_bf_kernel<true, true><<<grid, 256, 0, s>>>(p);
+  // the ring kernel where it measured faster: wide outputs (the QNN MLP's input grad, N = 7552); the forward
+  // (N = 512) and the k-major weight grad keep the two-stage kernel (tools/kbench.py --which gemmbf)
+  int var = g_gemm_bf_variant;
+  if (var == 0) var = (M >= 256 && N >= 2048 && !ta) ? 2 : 1;
+  if (var >= 2 && M >= 128) {
+    const int BM = var == 2 ? 256 : 128;
+    p.mt = cdiv(M, BM);
+    p.nt = cdiv(N, G8_BN);
+    p.gm = p.nt >= 8 ? -1 : 0;
+    const int tiles = p.gm < 0 ? 8 * p.mt * cdiv(p.nt, 8) * splits : p.mt * p.nt * splits;
+    const int grid = std::min(tiles, 256);
+    launch_g8(p, ta, tb, BM, grid, s);  } else {
+    p.mt = cdiv(M, 128);
+    p.nt = cdiv(N, 128);
+    // XCD column partition where there are n-tiles for every XCD; persistent grid: two workgroups per CU (64 KB
+    // of LDS each) at most, a multiple of 8 for the partition
+    p.gm = p.nt >= 8 ? -1 : 0;
+    const int tiles = p.gm < 0 ? 8 * p.mt * cdiv(p.nt, 8) * splits : p.mt * p.nt * splits;
+    const int grid = std::min(tiles, 512);
+    if (!ta && tb) gemm_bf_kernel<false, true><<<grid, 256, 0, s>>>(p);
+    else if (!ta && !tb) gemm_bf_kernel<false, false><<<grid, 256, 0, s>>>(p);
+    else if (ta && !tb) gemm_bf_kernel<true, false><<<grid, 256, 0, s>>>(p);
+    else gemm_bf_kernel<true, true><<<grid, 256, 0, s>>>(p);
+  }
   if (splits > 1) {
     const long MN = (long)M * N;
     int blocks = (int)std::min<long>((MN + 255) / 256, 4096);

@@ -83,6 +83,7 @@ SIGS = {
     "ctr_pos_bias_grad": (i, [p, i, i, i, p, p]),
     "ctr_attn_mask_words": (i, [i, i, i]),
     "ctr_attn_set_generic": (None, [i]),
+    "ctr_gemm_bf16_set_variant": (None, [i]),
     "ctr_attn_fwd": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
     "ctr_attn_bwd_nparts": (i, [i, i, i]),
     "ctr_attn_bwd": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
