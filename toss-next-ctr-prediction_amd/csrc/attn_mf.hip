@@ -911,7 +911,7 @@ struct LayerFwdArgs {
 };
 
 template <int DH, bool BIAS, int DROPK>
-__global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) void attn_layer_fwd_kernel(LayerFwdArgs L) {
   constexpr int NT = 4, KT = 64, G = lf::D / DH;     // all heads of the sample
   const AttnBfArgs& a = L.at;
   __shared__ __attribute__((aligned(16))) __bf16 sq[KT * lf::RS + 16];
@@ -990,40 +990,20 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
     }
     const float* rb = srel + KT + a.tk + 4 * g - c;
     const long hr = ((long)b * a.H + h) * K;
-    uint32_t words[2] = {0u, 0u};
     const float dsc = DROPK ? a.drop.scale : 1.0f;
     const int nt = (K + 15) >> 4;
     const uint32_t dmask = nt >= 4 ? 0xFFFFu : (1u << (4 * nt)) - 1u;
+    // the dropout decisions of all four query tiles first, as 64 bits (query tile ti: bits 16 (ti & 1) .. of
+    // word ti >> 1, bit 4 tj + r = key 16 tj + 4 g + r): the hashes' temporaries are then not live beside the
+    // score tiles (104 registers otherwise, two workgroups per CU instead of four)
+    uint32_t dbits[2] = {0u, 0u};
+    if (DROPK) {
 #pragma unroll
-    for (int ti = 0; ti < NT; ++ti) {
-      __builtin_amdgcn_sched_barrier(0);
-      const bf16x4 qop = lf_row<DH>(sq, 16 * ti + c, hs, g);
-      const int i = 16 * ti + c;
-      const uint32_t rowbase = (uint32_t)((hr + i) * K);
-      f32x4 t[NT];
-      float mx = -INFINITY;
+      for (int ti = 0; ti < NT; ++ti) {
+        const uint32_t rowbase = (uint32_t)((hr + 16 * ti + c) * K);
+        uint32_t dropped = 0u;
 #pragma unroll
-      for (int tj = 0; tj < NT; ++tj) {
-        const f32x4 sc = mma(kop[tj], qop, f32x4{0.f, 0.f, 0.f, 0.f});
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          t[tj][r] = BIAS ? fmaf(sc[r], L2E, rb[16 * (tj - ti) + r]) : sc[r] * L2E;
-          mx = fmaxf(mx, t[tj][r]);
-        }
-      }
-      mx = grp_max(mx);
-      float l = 0.f;
-      uint32_t dropped = 0u;
-      bf16x4 pb[NT];
-#pragma unroll
-      for (int tj = 0; tj < NT; ++tj) {
-        float pe[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pe[r] = __builtin_amdgcn_exp2f(t[tj][r] - mx);
-          l += pe[r];
-        }
-        if (DROPK) {
+        for (int tj = 0; tj < NT; ++tj) {
           const uint32_t j0 = 16 * tj + 4 * g;
           uint32_t half[4];
           if (DROPK == 1) {
@@ -1042,11 +1022,39 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
             }
           }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const uint32_t m = sign_mask(half[r] - a.drop.thresh);
-            pe[r] = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, pe[r]) & ~m);
-            dropped |= m & (1u << (4 * tj + r));
-          }
+          for (int r = 0; r < 4; ++r) dropped |= (half[r] < a.drop.thresh ? 1u : 0u) << (4 * tj + r);
+        }
+        dbits[ti >> 1] |= dropped << (16 * (ti & 1));
+      }
+    }
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+      __builtin_amdgcn_sched_barrier(0);
+      const bf16x4 qop = lf_row<DH>(sq, 16 * ti + c, hs, g);
+      const int i = 16 * ti + c;
+      f32x4 t[NT];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) {
+        const f32x4 sc = mma(kop[tj], qop, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          t[tj][r] = BIAS ? fmaf(sc[r], L2E, rb[16 * (tj - ti) + r]) : sc[r] * L2E;
+          mx = fmaxf(mx, t[tj][r]);
+        }
+      }
+      mx = grp_max(mx);
+      float l = 0.f;
+      const uint32_t dropped = dbits[ti >> 1] >> (16 * (ti & 1));
+      bf16x4 pb[NT];
+#pragma unroll
+      for (int tj = 0; tj < NT; ++tj) {
+        float pe[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pe[r] = __builtin_amdgcn_exp2f(t[tj][r] - mx);
+          l += pe[r];
+          if (DROPK && ((dropped >> (4 * tj + r)) & 1u)) pe[r] = 0.f;
         }
         pb[tj] = __builtin_bit_cast(bf16x4, pk_bf4(f32x4{pe[0], pe[1], pe[2], pe[3]}));
       }
@@ -1064,11 +1072,13 @@ __global__ __launch_bounds__(512) void attn_layer_fwd_kernel(LayerFwdArgs L) {
         a.mrow[hr + i] = mx;
         a.lrow[hr + i] = l;
       }
-      // the words attn_fwd_mf_kernel writes at nt = ceil(K / 16): key tiles >= nt kept, query tiles >= nt none
-      if (DROPK && ti < nt) words[ti >> 1] |= (~(dropped & dmask) & 0xFFFFu) << (16 * (ti & 1));
     }
-    if (DROPK) {
+    if (DROPK) {   // the keep words attn_fwd_mf_kernel writes at nt = ceil(K / 16): key tiles >= nt kept, query tiles >= nt none
       uint32_t* mk = a.mask + ((long)b * a.H + h) * 128;
+      uint32_t words[2] = {0u, 0u};
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti)
+        if (ti < nt) words[ti >> 1] |= (~((dbits[ti >> 1] >> (16 * (ti & 1))) & dmask) & 0xFFFFu) << (16 * (ti & 1));
       mk[lane] = words[0];
       mk[64 + lane] = words[1];
     }
