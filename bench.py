@@ -13,6 +13,7 @@ replicated all-gathers row grads instead).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
 """
 import argparse
+import gc
 import json
 import math
 import os
@@ -398,6 +399,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-events", choices=("all", "none"), default="all",
                     help="HIP events around the big kernels' calls in the timed steps (none: no roofline)")
+    ap.add_argument("--gc-in-steps", action="store_true",
+                    help="leave Python's cyclic garbage collector running in the timed steps (A/B of its host stalls)")
     ap.add_argument("--markers", action="store_true",
                     help="launch an empty step_marker_kernel around the timed region (tools/prof_summary.py)")
     ap.add_argument("--dense-opt", action="store_true",
@@ -496,6 +499,12 @@ def main():
         if roof_kernel is not None:
             _lib.time_calls((roof_kernel,))
         torch.cuda.synchronize()
+    # the host issues the step a few hundred dispatches ahead of the device at most (the HIP queue depth): a cyclic
+    # garbage collection of the interpreter's heap mid-step (≈ 2 ms, once in ~20 steps in the kernel trace) leaves the
+    # GPU idle that long (level at 20 + 5 steps after the collect below: 3.549 vs 3.554 ms, tools/_ab_gc.sh).
+    gc.collect()
+    if not args.gc_in_steps:
+        gc.disable()
     if args.markers:
         _lib.call("ctr_step_marker", 1, torch.cuda.current_stream(dev).cuda_stream)
     t0 = time.perf_counter()
@@ -514,6 +523,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     flush_ms = fl[0].elapsed_time(fl[1])
     kstats_timed = _lib.timed_ms()
     _lib.time_calls(())
