@@ -593,6 +593,45 @@ def test_attn_bwd_oproj_equals_two_launches(K, H, p, bias):
         assert torch.equal(r_drp.view(torch.int32), f_drp.view(torch.int32))
 
 
+@pytest.mark.parametrize("B,F,D,fe,bias", [(4096, 82, 32, 16, True), (4096, 82, 32, 16, False), (1000, 35, 64, 8, True),
+                                           (37, 5, 16, 4, True), (300, 3, 256, 16, True), (257, 7, 48, 24, False)])
+def test_feat_embed_vs_fp64(B, F, D, fe, bias):
+    """NumericFeatureEmbedding / BinaryFeatureEmbedding (src/models/feature_embed.py:19-27, 42-48): out = (x W + b) P^T
+    and its backward (dW, dbias, dP) against an fp64 torch reference; B = 4096 / F = 82 / D = 32 is the bench's."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(B + F + D)
+    x = torch.randn(B, F, device="cuda", generator=g)
+    W = torch.randn(F, fe, device="cuda", generator=g)
+    bv = torch.randn(F, fe, device="cuda", generator=g) if bias else None
+    P = torch.randn(D, fe, device="cuda", generator=g) / fe ** 0.5
+    out_ld = F * D + 5                        # a row stride wider than the block, as in the stacked token matrix
+    out = torch.full((B, out_ld), float("nan"), device="cuda")
+    st = stream()
+    L.call("ctr_feat_embed_fwd", ptr(x), B, F, ptr(W), ptr(bv) if bias else None, ptr(P), fe, D, ptr(out), out_ld, st)
+    xd, Wd, Pd = x.double(), W.double(), P.double()
+    h = xd[:, :, None] * Wd[None] + (bv.double()[None] if bias else 0.0)
+    ref = torch.einsum("bfk,dk->bfd", h, Pd).reshape(B, F * D)
+    torch.cuda.synchronize()
+    got = out[:, :F * D].double()
+    assert torch.isnan(out[:, F * D:]).all(), "wrote past the block"
+    assert float((got - ref).norm() / ref.norm()) < 1e-6
+    dout_t = torch.randn(B, out_ld, device="cuda", generator=g)
+    ws = torch.empty(L.query("ctr_feat_embed_bwd_ws", B, F, D) // 4 + 1, device="cuda")
+    dW = torch.full_like(W, float("nan"))
+    db = torch.full_like(W, float("nan"))
+    dP = torch.full_like(P, float("nan"))
+    L.call("ctr_feat_embed_bwd", ptr(x), B, F, ptr(W), ptr(bv) if bias else None, ptr(P), fe, D, ptr(dout_t), out_ld,
+           ptr(dW), ptr(db) if bias else None, ptr(dP), ptr(ws), st)
+    go = dout_t[:, :F * D].double().reshape(B, F, D)
+    gh = torch.einsum("bfd,dk->bfk", go, Pd)                       # dL/dh
+    r_dW = (gh * xd[:, :, None]).sum(0)
+    r_db = gh.sum(0)
+    r_dP = torch.einsum("bfd,bfk->dk", go, h)
+    torch.cuda.synchronize()
+    for name, a, r in (("dW", dW, r_dW), ("dP", dP, r_dP)) + ((("dbias", db, r_db),) if bias else ()):
+        assert float((a.double() - r).norm() / r.norm()) < 1e-5, name
+
+
 @pytest.mark.parametrize("L_,K,D", [(100, 60, 32), (40, 40, 16), (400, 148, 64), (7, 3, 8)])
 def test_topk_select_vs_torch(L_, K, D):
     L = _lib()

@@ -15,8 +15,11 @@ namespace ctr {
 // out[b, f, d] = sum_k (x[b,f] W[f,k] + bias[f,k]) P[d,k] = x[b,f] * A[f,d] + Bv[f,d] with
 // A[f,d] = W[f,:].P[d,:], Bv[f,d] = bias[f,:].P[d,:] formed once per workgroup: the stream is then one
 // FMA per output (the reference's per-k rounding differs by a few ulp).  Workgroup = (feature f, chunk
-// of FE_ROWS samples); lanes = d, so each sample's D outputs are one contiguous store.
-constexpr int FE_ROWS = 64;
+// of fe_rows(D) samples); lanes = d, so each sample's D outputs are one contiguous store.  A thread takes 32
+// samples (one round trip for their x values; the per-workgroup projection staging amortised over 32 x 256 / D
+// samples -- 64 per workgroup before, 5,248 workgroups a call at cfg2, ~21 us for 43 MB).
+constexpr int FE_NB = 32;                           // samples per thread
+__host__ __device__ __forceinline__ int fe_rows_d(int D) { return FE_NB * (256 / D); }
 
 __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __restrict__ x, int B, int F,
                                                              const float* __restrict__ W,
@@ -24,7 +27,7 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
                                                              const float* __restrict__ P, int fe, int D,
                                                              float* __restrict__ out, long out_ld) {
   extern __shared__ float sfe[];         // P [D][fe+1] | W row [fe] | bias row [fe]
-  const int f = blockIdx.y, b0 = blockIdx.x * FE_ROWS;
+  const int f = blockIdx.y, b0 = blockIdx.x * fe_rows_d(D);
   const int RG = 256 / D, d = threadIdx.x % D, rg = threadIdx.x / D;
   const int FP = fe + 1;
   float* sP = sfe;
@@ -43,15 +46,14 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
     A = fmaf(sW[k], pk, A);
     Bv = fmaf(sB[k], pk, Bv);
   }
-  // the group's samples b0 + rg + RG i (i < FE_ROWS / RG <= 16 at D <= 64): every x load issued before the stores
-  const int b1 = min(B, b0 + FE_ROWS), nb = FE_ROWS / RG;
-  float xv[16];
+  // the group's samples b0 + rg + RG i (i < FE_NB): every x load issued before the stores
+  float xv[FE_NB];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) xv[i] = x[(long)min(b0 + rg + RG * i, B - 1) * F + f];
+  for (int i = 0; i < FE_NB; ++i) xv[i] = x[(long)min(b0 + rg + RG * i, B - 1) * F + f];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < FE_NB; ++i) {
     const int b = b0 + rg + RG * i;
-    if (i < nb && b < b1) out[(long)b * out_ld + (long)f * D + d] = fmaf(xv[i], A, Bv);
+    if (b < B) out[(long)b * out_ld + (long)f * D + d] = fmaf(xv[i], A, Bv);
   }
 }
 
@@ -67,16 +69,16 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restri
   const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
   float s1 = 0.f, s0 = 0.f;
   if (rg < RG)
-    for (int bb = b0 + rg; bb < b1; bb += 8 * RG) {     // eight rows' loads issued together, summed in row order
-      float gv[8], xv[8];
+    for (int bb = b0 + rg; bb < b1; bb += 32 * RG) {    // 32 rows' loads issued together (a chunk's rows at D = 32),
+      float gv[32], xv[32];                             // summed in row order
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 32; ++i) {
         const int b = min(bb + RG * i, b1 - 1);
         gv[i] = dout[(long)b * dout_ld + (long)f * D + d];
         xv[i] = x[(long)b * F + f];
       }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 32; ++i) {
         if (bb + RG * i >= b1) break;
         s1 = fmaf(xv[i], gv[i], s1);
         s0 += gv[i];
@@ -97,68 +99,66 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restri
   }
 }
 
-// one workgroup: S = sum over chunks (fixed order) into LDS, then
-// dW = S1 @ P, dbias = S0 @ P, dP = sum_f S1^T W + S0^T bias
-__global__ __launch_bounds__(1024) void feat_embed_bwd_final(int nchunk, int F, int D, int fe,
-                                                            const float* __restrict__ part, const float* W,
-                                                            const float* bias, const float* P,
-                                                            float* __restrict__ dW, float* __restrict__ dbias,
-                                                            float* __restrict__ dP) {
-  extern __shared__ float sS[];          // [2][F][D] | P [D][fe] | W [F][fe] | bias [F][fe]
-  const int n2 = 2 * F * D;
-  // two elements' chunk partials (nchunk <= 16 each) loaded together, then summed in chunk order: one round trip
-  // per two elements instead of one per four loads
-  for (int q0 = threadIdx.x; q0 < n2; q0 += 2 * blockDim.x) {
-    float v[2][16];
+// F + D workgroups (one per output row; one workgroup for all of it took ~19 us, a chain of round trips):
+// workgroup f < F sums the chunk partials of S1[f, :], S0[f, :] (fixed chunk order) and forms dW[f, :] = S1[f] @ P,
+// dbias[f, :] = S0[f] @ P; workgroup F + d sums those of S1[:, d], S0[:, d] and forms dP[d, :] = sum_f (S1[f, d]
+// W[f, :] + S0[f, d] bias[f, :]) in feature order -- the same sums, products and orders as the one-workgroup form
+__global__ __launch_bounds__(256) void feat_embed_bwd_final(int nchunk, int F, int D, int fe,
+                                                           const float* __restrict__ part, const float* __restrict__ W,
+                                                           const float* __restrict__ bias, const float* __restrict__ P,
+                                                           float* __restrict__ dW, float* __restrict__ dbias,
+                                                           float* __restrict__ dP) {
+  extern __shared__ float sfb[];       // row f: S [2][D] | P [D][fe];  column d: S [2][F] | W [F][fe] | bias [F][fe]
+  const int tid = threadIdx.x;
+  const long n2 = 2L * F * D;
+  const bool rowf = blockIdx.x < F;
+  const int f = blockIdx.x, dd = blockIdx.x - F;
+  const int nS = rowf ? 2 * D : 2 * F;
+  for (int q = tid; q < nS; q += 256) {
+    // element of S (S1 then S0): row f -> (h, d) = (q / D, q % D); column d -> (h, f) = (q / F, q % F)
+    const long idx = rowf ? (long)(q / D) * F * D + (long)f * D + q % D : (long)(q / F) * F * D + (long)(q % F) * D + dd;
+    float v[16];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int q = min(q0 + h * (int)blockDim.x, n2 - 1);
+    for (int c = 0; c < 16; ++c) v[c] = part[(long)min(c, nchunk - 1) * n2 + idx];
+    float t = 0.f;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) v[h][c] = part[(long)min(c, nchunk - 1) * n2 + q];
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int q = q0 + h * (int)blockDim.x;
-      float t = 0.f;
-#pragma unroll
-      for (int c = 0; c < 16; ++c)
-        if (c < nchunk) t += v[h][c];
-      if (q < n2) sS[q] = t;
-    }
+    for (int c = 0; c < 16; ++c)
+      if (c < nchunk) t += v[c];
+    sfb[q] = t;
   }
-  float* sPm = sS + n2;
-  float* sWm = sPm + D * fe;
-  float* sBm = sWm + F * fe;
-  for (int q = threadIdx.x; q < D * fe; q += blockDim.x) sPm[q] = P[q];
-  for (int q = threadIdx.x; q < F * fe; q += blockDim.x) {
-    sWm[q] = W[q];
-    sBm[q] = bias ? bias[q] : 0.f;
+  float* sw = sfb + nS;
+  if (rowf) {
+    for (int q = tid; q < D * fe; q += 256) sw[q] = P[q];
+  } else {
+    for (int q = tid; q < F * fe; q += 256) {
+      sw[q] = W[q];
+      sw[F * fe + q] = bias ? bias[q] : 0.f;
+    }
   }
   __syncthreads();
-  P = sPm;
-  W = sWm;
-  bias = bias ? sBm : nullptr;
-  const float* S1 = sS;
-  const float* S0 = sS + F * D;
-  for (int q = threadIdx.x; q < (F + D) * fe; q += blockDim.x) {
-    if (q < F * fe) {
-      const int f = q / fe, k = q % fe;
+  if (rowf) {
+    const float* S1 = sfb;
+    const float* S0 = sfb + D;
+    for (int k = tid; k < fe; k += 256) {
       float a = 0.f, c = 0.f;
       for (int d = 0; d < D; ++d) {
-        a = fmaf(S1[f * D + d], P[d * fe + k], a);
-        c = fmaf(S0[f * D + d], P[d * fe + k], c);
+        a = fmaf(S1[d], sw[d * fe + k], a);
+        c = fmaf(S0[d], sw[d * fe + k], c);
       }
-      dW[q] = a;
-      if (dbias) dbias[q] = c;
-    } else {
-      const int r = q - F * fe;
-      const int d = r / fe, k = r % fe;
+      dW[(long)f * fe + k] = a;
+      if (dbias) dbias[(long)f * fe + k] = c;
+    }
+  } else {
+    const float* S1 = sfb;
+    const float* S0 = sfb + F;
+    const float* sb = sw + F * fe;
+    for (int k = tid; k < fe; k += 256) {
       float a = 0.f;
-      for (int f = 0; f < F; ++f) {
-        a = fmaf(S1[f * D + d], W[f * fe + k], a);
-        if (bias) a = fmaf(S0[f * D + d], bias[f * fe + k], a);
+      for (int ff = 0; ff < F; ++ff) {
+        a = fmaf(S1[ff], sw[ff * fe + k], a);
+        if (bias) a = fmaf(S0[ff], sb[ff * fe + k], a);
       }
-      dP[r] = a;
+      dP[(long)dd * fe + k] = a;
     }
   }
 }
@@ -661,8 +661,8 @@ extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, 
   CTR_REQUIRE(D <= 256, "D > 256");
   const size_t sm = ((size_t)D * (fe + 1) + 2 * fe) * sizeof(float);
   CTR_REQUIRE(sm <= 64 * 1024, "feat_embed: D x fe projection exceeds LDS");
-  feat_embed_fwd_kernel<<<dim3(cdiv(B, FE_ROWS), F), 256, sm, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D, out,
-                                                                                      out_ld);
+  feat_embed_fwd_kernel<<<dim3(cdiv(B, fe_rows_d(D)), F), 256, sm, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D,
+                                                                                          out, out_ld);
   return check_launch("feat_embed_fwd");
 }
 
@@ -677,19 +677,17 @@ extern "C" int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, 
                                   float* dP, float* ws, void* stream) {
   if (F == 0) return 0;
   CTR_REQUIRE(D <= 256, "D > 256");
-  const size_t sm = ((size_t)2 * F * D + (size_t)D * fe + (size_t)2 * F * fe) * sizeof(float);
+  const size_t sm_row = ((size_t)2 * D + (size_t)D * fe) * sizeof(float);
+  const size_t sm_col = ((size_t)2 * F + (size_t)2 * F * fe) * sizeof(float);
+  const size_t sm = sm_row > sm_col ? sm_row : sm_col;
   CTR_REQUIRE(sm <= 160 * 1024, "feat_embed_bwd: sums + weights exceed LDS");
   hipStream_t s = (hipStream_t)stream;
   const int nch = fe_chunks(B);
   const int rpc = cdiv(B, nch);
   feat_embed_bwd_sums<<<dim3(F, nch), 256, 0, s>>>(x, B, F, D, dout, dout_ld, rpc, ws);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)feat_embed_bwd_final, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr = true;
-  }
-  feat_embed_bwd_final<<<1, 1024, sm, s>>>(nch, F, D, fe, ws, W, bias, P, dW, dbias, dP);
+  if (sm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)feat_embed_bwd_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  feat_embed_bwd_final<<<F + D, 256, sm, s>>>(nch, F, D, fe, ws, W, bias, P, dW, dbias, dP);
   return check_launch("feat_embed_bwd");
 }
 
