@@ -319,6 +319,16 @@ int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int
  * bf16 when add_bf16 -- the MLP's input grad under amp: bf16); DS = dquad o S (for dUcat)           */
 int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
                      const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS, void* stream);
+/* the same over one feature block of the rows (pair_grouping 'block', src/models/qnn_alpha.py:99-116, block slices
+ * src/models/wrapper.py:66-75): z (and dz_add, dz) rows of stride ld >= F D, F the block's features; accumulate != 0
+ * adds G and quad to what the buffers hold (the blocks' quads summed, qnn_alpha.py:108), zsum / S per block     */
+int ctr_qnn_gram_fwd_ex(const float* z, long ld, int B, int F, int D, const float* ucat, int QR, float* zsum, float* G,
+                        float* S, float* quad, int accumulate, void* stream);
+int ctr_qnn_gram_bwd_ex(const float* z, long ld, int B, int F, int D, const float* ucat, int QR, const float* S,
+                        const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS, void* stream);
+/* dst (B, ncols; row stride ld) = add (fp32, or bf16 when add_bf16; row stride ld_add; null: 0) -- the columns of the
+ * block form's z rows outside every interaction block                                                  */
+int ctr_qnn_passthrough(const void* add, int add_bf16, long ld_add, int B, int ncols, float* dst, long ld, void* stream);
 /* dUcat = 2 (T1 - sum_e Ucat[e,c] T[d*D+e, c]) with T1 = zsum^T DS (D x QR), T = G^T dquad (D*D x QR) */
 int ctr_qnn_du_combine(const float* T1, const float* T, const float* ucat, int D, int QR, float* ducat,
                        void* stream);

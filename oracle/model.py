@@ -162,6 +162,16 @@ class Arch:
             self.F = 1 + self.Fn + self.Fm + self.Fc
         self.aux_w = float(qa.get("aux_head_weight", 0.0))
 
+    def qnn_blocks(self):
+        """src/models/wrapper.py:66-75: the feature blocks of the QNN input [u | num | mask | cat], in that order
+        (a block only when its features are present)."""
+        sizes = [1] + [n for n in (self.Fn, self.Fm) if n > 0] + [self.Fc]     # seq, num?, mask?, cat
+        out, o = [], 0
+        for n in sizes:
+            out.append((o, o + n))
+            o += n
+        return out
+
     def param_shapes(self):
         """state_dict keys/shapes in reference registration order (src/models/wrapper.py:24-100)."""
         D, fe = self.D, self.f_embed
@@ -293,17 +303,26 @@ def forward(P, batch, A: Arch, drop: Dropper, dtype=torch.float32, record=None):
     return logits, torch.sigmoid(logits), aux
 
 
-def qnn_forward(P, feats, A: Arch, drop):
-    # src/models/qnn_alpha.py:109-130 (pair_grouping 'all', :86-97)
-    B, Fq, D = feats.shape
-    z = rmsnorm(feats.reshape(B, Fq * D), P["qnn.pre_norm.w"]).reshape(B, Fq, D)
+def _pair_all(P, z, A: Arch):
+    # src/models/qnn_alpha.py:86-97
     outs = []
     for h in range(A.qh):
         Ah = z @ P["qnn.U"][h]
         s = Ah.sum(dim=1)
         quad = s * s - (Ah * Ah).sum(dim=1)
         outs.append(quad @ P["qnn.V"][h])
-    inter = torch.cat(outs, dim=1)
+    return torch.cat(outs, dim=1)
+
+
+def qnn_forward(P, feats, A: Arch, drop):
+    # src/models/qnn_alpha.py:109-130
+    B, Fq, D = feats.shape
+    z = rmsnorm(feats.reshape(B, Fq * D), P["qnn.pre_norm.w"]).reshape(B, Fq, D)
+    blocks = [(s, e) for s, e in A.qnn_blocks() if e - s > 1] if A.pair_grouping == "block" else []
+    if blocks:   # :99-108: the interaction within each block of more than one feature, summed over the blocks
+        inter = torch.stack([_pair_all(P, z[:, s:e, :], A) for s, e in blocks], dim=0).sum(dim=0)
+    else:
+        inter = _pair_all(P, z, A)
     if A.use_se:   # src/models/qnn_alpha.py:17-26
         m = inter.mean(dim=0, keepdim=True)
         g = torch.relu(m @ P["qnn.se.fc.0.weight"].t() + P["qnn.se.fc.0.bias"])

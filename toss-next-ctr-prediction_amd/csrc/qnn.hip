@@ -63,11 +63,14 @@ __device__ __forceinline__ void stage_ucat(const float* __restrict__ ucat, int Q
 // One wave per sample.  G = z^T z by MFMA with the F rows as the contraction (A and B operands are the
 // same loaded values: lane (g, c) holds z[4s+g][16i+c]); then H = G Ucat using the symmetric G's
 // C-layout registers directly as A operands (k-set {16i + 4g + r}), and sum_f A^2 = sum_d U o H.
+// ld: a sample's z row stride (F D, or wider for one feature block of the rows); acc: G and quad are added to
+// what the buffers hold (pair_grouping 'block': the blocks' Gram matrices and quads summed, zsum / S per block)
 template <int D>
-__global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restrict__ z, int B, int F,
+__global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restrict__ z, long ld, int B, int F,
                                                            const float* __restrict__ ucat, int QR,
                                                            float* __restrict__ zsum_out, float* __restrict__ G_out,
-                                                           float* __restrict__ S_out, float* __restrict__ quad_out) {
+                                                           float* __restrict__ S_out, float* __restrict__ quad_out,
+                                                           int acc_out) {
   constexpr int NT = D / 16;
   extern __shared__ float sU[];
   const int QRp = (QR + 15) / 16 * 16, US = QRp + 1;
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int b = blockIdx.x * 4 + w;
   if (b >= B) return;
-  const float* zb = z + (long)b * F * D;
+  const float* zb = z + (long)b * ld;
   f32x4 acc[NT][NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i)
@@ -131,7 +134,10 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < NT; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Gb[(16 * i + 4 * g + r) * D + 16 * j + c] = acc[i][j][r];
+      for (int r = 0; r < 4; ++r) {
+        float* gp = Gb + (16 * i + 4 * g + r) * D + 16 * j + c;
+        *gp = acc_out ? *gp + acc[i][j][r] : acc[i][j][r];
+      }
   __builtin_amdgcn_wave_barrier();
   for (int t = 0; t < QRp / 16; ++t) {
     const int cc = 16 * t + c;
@@ -155,7 +161,8 @@ __global__ __launch_bounds__(256) void qnn_gram_fwd_kernel(const float* __restri
     sa2 += __shfl_xor(sa2, 32);
     if (g == 0 && cc < QR) {
       S_out[(long)b * QR + cc] = sv;
-      quad_out[(long)b * QR + cc] = sv * sv - sa2;
+      float* qp = quad_out + (long)b * QR + cc;
+      *qp = acc_out ? *qp + (sv * sv - sa2) : sv * sv - sa2;
     }
   }
 }
@@ -182,7 +189,7 @@ struct GramAdd<__bf16> {
 // operand (k-set {16i+4g+r}).  (One wave per sample left only 4 waves per SIMD at B = 4096, each a long
 // serial load -> MFMA chain.)
 template <int D, class TA, bool ADD>
-__global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restrict__ z, int B, int F,
+__global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restrict__ z, long ld, int B, int F,
                                                            const float* __restrict__ ucat, int QR,
                                                            const float* __restrict__ S,
                                                            const float* __restrict__ dquad,
@@ -204,8 +211,8 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
 #define QNN_PF 2
 #endif
   constexpr int PF = QNN_PF;
-  const float* zb = z + (long)b * F * D;
-  const TA* ab = ADD ? dz_add + (long)b * F * D : nullptr;
+  const float* zb = z + (long)b * ld;                 // z, dz_add and dz share the row stride ld
+  const TA* ab = ADD ? dz_add + (long)b * ld : nullptr;
   f32x4 zpre[PF][NT];
   using AR = typename GramAdd<TA>::R;
   AR apre[PF][4][NT];
@@ -276,7 +283,7 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
     const int e = 16 * j + c;
     wv[j] = 2.f * (((sW[e] + sW[D + e]) + sW[2 * D + e]) + sW[3 * D + e]);
   }
-  float* ob = dz + (long)b * F * D;
+  float* ob = dz + (long)b * ld;
   int it = 0;
   for (int f0 = 16 * w; f0 < F; f0 += 64, ++it) {
     const int fa = f0 + c;                       // A-operand row of this lane
@@ -513,23 +520,30 @@ static size_t gram_lds(int D, int QR) {
   return ((size_t)D * (QRp + 1) + 8 * (size_t)std::max(D, QRp)) * sizeof(float);
 }
 
-extern "C" int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int QR, float* zsum,
-                                float* G, float* S, float* quad, void* stream) {
+extern "C" int ctr_qnn_gram_fwd_ex(const float* z, long ld, int B, int F, int D, const float* ucat, int QR,
+                                   float* zsum, float* G, float* S, float* quad, int accumulate, void* stream) {
   CTR_REQUIRE(D == 16 || D == 32 || D == 64, "qnn gram: D must be 16, 32 or 64");
+  CTR_REQUIRE(ld >= (long)F * D, "qnn gram: row stride shorter than F D");
   if (B == 0) return 0;
   const size_t sm = gram_lds(D, QR);
   CTR_REQUIRE(sm <= 64 * 1024, "qnn gram: U exceeds LDS");
   hipStream_t s = (hipStream_t)stream;
   const int blocks = cdiv(B, 4);
-  if (D == 16) qnn_gram_fwd_kernel<16><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, zsum, G, S, quad);
-  else if (D == 32) qnn_gram_fwd_kernel<32><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, zsum, G, S, quad);
-  else qnn_gram_fwd_kernel<64><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, zsum, G, S, quad);
+  if (D == 16) qnn_gram_fwd_kernel<16><<<blocks, 256, sm, s>>>(z, ld, B, F, ucat, QR, zsum, G, S, quad, accumulate);
+  else if (D == 32) qnn_gram_fwd_kernel<32><<<blocks, 256, sm, s>>>(z, ld, B, F, ucat, QR, zsum, G, S, quad, accumulate);
+  else qnn_gram_fwd_kernel<64><<<blocks, 256, sm, s>>>(z, ld, B, F, ucat, QR, zsum, G, S, quad, accumulate);
   return check_launch("qnn_gram_fwd");
 }
 
+extern "C" int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int QR, float* zsum,
+                                float* G, float* S, float* quad, void* stream) {
+  return ctr_qnn_gram_fwd_ex(z, (long)F * D, B, F, D, ucat, QR, zsum, G, S, quad, 0, stream);
+}
+
 template <class TA, bool ADD>
-static void gram_bwd_launch(int D, int blocks, size_t sm, hipStream_t s, const float* z, int B, int F, const float* ucat,
-                            int QR, const float* S, const float* dquad, const TA* dz_add, float* dz, float* DS) {
+static void gram_bwd_launch(int D, int blocks, size_t sm, hipStream_t s, const float* z, long ld, int B, int F,
+                            const float* ucat, int QR, const float* S, const float* dquad, const TA* dz_add, float* dz,
+                            float* DS) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_kernel<16, TA, ADD>,
@@ -540,25 +554,58 @@ static void gram_bwd_launch(int D, int blocks, size_t sm, hipStream_t s, const f
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  if (D == 16) qnn_gram_bwd_kernel<16, TA, ADD><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
-  else if (D == 32) qnn_gram_bwd_kernel<32, TA, ADD><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
-  else qnn_gram_bwd_kernel<64, TA, ADD><<<blocks, 256, sm, s>>>(z, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  if (D == 16) qnn_gram_bwd_kernel<16, TA, ADD><<<blocks, 256, sm, s>>>(z, ld, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else if (D == 32) qnn_gram_bwd_kernel<32, TA, ADD><<<blocks, 256, sm, s>>>(z, ld, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else qnn_gram_bwd_kernel<64, TA, ADD><<<blocks, 256, sm, s>>>(z, ld, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
 }
 
-extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
-                                const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS,
-                                void* stream) {
+extern "C" int ctr_qnn_gram_bwd_ex(const float* z, long ld, int B, int F, int D, const float* ucat, int QR,
+                                   const float* S, const float* dquad, const void* dz_add, int add_bf16, float* dz,
+                                   float* DS, void* stream) {
   CTR_REQUIRE(D == 16 || D == 32 || D == 64, "qnn gram: D must be 16, 32 or 64");
+  CTR_REQUIRE(ld >= (long)F * D, "qnn gram: row stride shorter than F D");
   if (B == 0) return 0;
   const int QRp = (QR + 15) / 16 * 16, NT = D / 16;
   const size_t sm = ((size_t)D * (QRp + 1) + 2 * (size_t)QRp + (size_t)NT * NT * 4 * 64 + 4 * (size_t)D) *
                     sizeof(float);
   CTR_REQUIRE(sm <= 160 * 1024, "qnn gram bwd: U + M partials exceed LDS");
   hipStream_t s = (hipStream_t)stream;
-  if (!dz_add) gram_bwd_launch<float, false>(D, B, sm, s, z, B, F, ucat, QR, S, dquad, nullptr, dz, DS);
-  else if (add_bf16) gram_bwd_launch<__bf16, true>(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const __bf16*)dz_add, dz, DS);
-  else gram_bwd_launch<float, true>(D, B, sm, s, z, B, F, ucat, QR, S, dquad, (const float*)dz_add, dz, DS);
+  if (!dz_add) gram_bwd_launch<float, false>(D, B, sm, s, z, ld, B, F, ucat, QR, S, dquad, nullptr, dz, DS);
+  else if (add_bf16)
+    gram_bwd_launch<__bf16, true>(D, B, sm, s, z, ld, B, F, ucat, QR, S, dquad, (const __bf16*)dz_add, dz, DS);
+  else gram_bwd_launch<float, true>(D, B, sm, s, z, ld, B, F, ucat, QR, S, dquad, (const float*)dz_add, dz, DS);
   return check_launch("qnn_gram_bwd");
+}
+
+extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
+                                const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS,
+                                void* stream) {
+  return ctr_qnn_gram_bwd_ex(z, (long)F * D, B, F, D, ucat, QR, S, dquad, dz_add, add_bf16, dz, DS, stream);
+}
+
+// pair_grouping 'block': the rows' columns outside every interaction block (single-feature blocks, e.g. the DARE
+// output u) take no interaction gradient -- dz = the MLP's input-grad addend (fp32 or bf16), or 0 without one
+__global__ void qnn_passthrough_kernel(const void* __restrict__ add, int add_bf16, long ld_add, int B, int ncols,
+                                       float* __restrict__ dst, long ld) {
+  const long n = (long)B * ncols;
+  for (long q = blockIdx.x * (long)blockDim.x + threadIdx.x; q < n; q += (long)gridDim.x * blockDim.x) {
+    const long b = q / ncols, j = q - b * ncols;
+    float v = 0.f;
+    if (add) {
+      if (add_bf16) v = __builtin_bit_cast(float, (uint32_t)((const unsigned short*)add)[b * ld_add + j] << 16);
+      else v = ((const float*)add)[b * ld_add + j];
+    }
+    dst[b * ld + j] = v;
+  }
+}
+
+extern "C" int ctr_qnn_passthrough(const void* add, int add_bf16, long ld_add, int B, int ncols, float* dst, long ld,
+                                   void* stream) {
+  if (B == 0 || ncols == 0) return 0;
+  const long n = (long)B * ncols;
+  qnn_passthrough_kernel<<<(unsigned)std::min<long>(cdiv(n, 256L), 2048), 256, 0, (hipStream_t)stream>>>(
+      add, add_bf16, ld_add, B, ncols, dst, ld);
+  return check_launch("qnn_passthrough");
 }
 
 extern "C" int ctr_qnn_du_combine(const float* T1, const float* T, const float* ucat, int D, int QR, float* ducat,

@@ -114,6 +114,9 @@ SIGS = {
     "ctr_loss": (i, [p, p, p, i, f, p, p, p, p]),
     "ctr_qnn_ucat": (i, [p, i, i, i, p, i, p]),
     "ctr_qnn_vfull": (i, [p, i, i, i, p, i, p]),
+    "ctr_qnn_gram_fwd_ex": (i, [p, l, i, i, i, p, i, p, p, p, p, i, p]),
+    "ctr_qnn_gram_bwd_ex": (i, [p, l, i, i, i, p, i, p, p, p, i, p, p, p]),
+    "ctr_qnn_passthrough": (i, [p, i, l, i, i, p, l, p]),
     "ctr_qnn_gram_fwd": (i, [p, i, i, i, p, i, p, p, p, p, p]),
     "ctr_qnn_gram_bwd": (i, [p, i, i, i, p, i, p, p, p, i, p, p, p]),
     "ctr_qnn_du_combine": (i, [p, p, p, i, i, p, p]),

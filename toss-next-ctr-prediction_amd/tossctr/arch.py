@@ -65,6 +65,20 @@ class Arch:
     def C(self):
         return self.qh * self.qP
 
+    def qnn_blocks(self):
+        """The QNN's interaction blocks (pair_grouping 'block', src/models/qnn_alpha.py:99-108): the slices of the
+        input [u | num | mask | cat] (src/models/wrapper.py:66-75) holding more than one feature, in that order;
+        empty for 'all' (or when no block has two features: the reference then falls back to all pairs)."""
+        if self.pair_grouping != "block":
+            return []
+        sizes = [1] + [n for n in (self.Fn, self.Fm) if n > 0] + [self.Fc]
+        out, o = [], 0
+        for n in sizes:
+            if n > 1:
+                out.append((o, o + n))
+            o += n
+        return out
+
     @property
     def nctx(self):
         return (self.Fn > 0) + (self.Fm > 0) + 1
@@ -117,8 +131,8 @@ class Arch:
             raise NotImplementedError("only norm: rms encoder layers are implemented (all reference configs use rms)")
         if self.use_qnn and self.qnn_norm.lower() != "rms":
             raise NotImplementedError("only QNN norm: rms is implemented (all reference configs use rms)")
-        if self.use_qnn and self.pair_grouping != "all":
-            raise NotImplementedError("pair_grouping 'block' is not implemented (no reference config uses it)")
+        if self.use_qnn and self.pair_grouping not in ("all", "block"):
+            raise ValueError(f"unknown pair_grouping {self.pair_grouping!r}")
         if self.amp not in ("none", "bf16"):
             raise NotImplementedError(f"amp: {self.amp!r} -- the MI355X path runs fp32 or bf16 (amp: bf16)")
         if self.gating not in ("softmax", "relu"):

@@ -597,11 +597,18 @@ class Engine:
         ucat = W.get("ucat", (D, QR))
         call("ctr_qnn_ucat", ptr(P["qnn.U"]), a.qh, D, a.qr, ptr(ucat), 0, st)
         # pair interaction through per-sample Gram matrices: A = z @ Ucat is never formed (qnn.hip)
-        zsum = W.get("qzsum", (B, D))
+        blocks = a.qnn_blocks()
+        nb = max(1, len(blocks))
+        zsum = W.get("qzsum", (nb, B, D))
         gram = W.get("qgram", (B, D * D))
-        S = W.get("qS", (B, QR))
+        S = W.get("qS", (nb, B, QR))
         quad = W.get("qquad", (B, QR))
-        call("ctr_qnn_gram_fwd", ptr(z), B, F, D, ptr(ucat), QR, ptr(zsum), ptr(gram), ptr(S), ptr(quad), st)
+        if blocks:     # pair_grouping 'block' (qnn_alpha.py:99-108): quad and G summed over the blocks
+            for i, (f0, f1) in enumerate(blocks):
+                call("ctr_qnn_gram_fwd_ex", ptr(z, f0 * D), FD, B, f1 - f0, D, ptr(ucat), QR, ptr(zsum[i]), ptr(gram),
+                     ptr(S[i]), ptr(quad), int(i > 0), st)
+        else:
+            call("ctr_qnn_gram_fwd", ptr(z), B, F, D, ptr(ucat), QR, ptr(zsum), ptr(gram), ptr(S), ptr(quad), st)
         vfull = W.get("qvfull", (QR, C))
         call("ctr_qnn_vfull", ptr(P["qnn.V"]), a.qh, a.qr, a.qP, ptr(vfull), 0, st)
         inter_pre = W.get("inter_pre", (B, C))
@@ -999,15 +1006,31 @@ class Engine:
                       self.wgrad_splits(QR, C, B))
             call("ctr_qnn_vfull", ptr(dvfull), a.qh, a.qr, a.qP, ptr(G["qnn.V"]), 1, self.s())
         dz = W.get("dz", (B, FD))
-        DS = W.get("qDS", (B, QR))
-        call("ctr_qnn_gram_bwd", ptr(q["z"]), B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]), ptr(dquad),
-             ptr(dz_mlp) if a.use_residual else None, int(dz_bf), ptr(dz), ptr(DS), st)
-        # dUcat = 2 (zsum^T DS - sum_b G_b Ucat diag(dquad_b))
+        blocks = a.qnn_blocks()
+        DS = W.get("qDS", (max(1, len(blocks)), B, QR))
+        dadd = dz_mlp if a.use_residual else None
+        if blocks:
+            # the features of no block take no interaction grad: dz = the MLP's input grad there
+            f_prev = 0
+            for f0, f1 in blocks + [(F, F)]:
+                if f0 > f_prev:
+                    call("ctr_qnn_passthrough", ptr(dadd, f_prev * D), int(dz_bf), FD, B, (f0 - f_prev) * D,
+                         ptr(dz, f_prev * D), FD, st)
+                f_prev = f1
+            for i, (f0, f1) in enumerate(blocks):
+                call("ctr_qnn_gram_bwd_ex", ptr(q["z"], f0 * D), FD, B, f1 - f0, D, ptr(q["ucat"]), QR,
+                     ptr(q["S"][i]), ptr(dquad), ptr(dadd, f0 * D), int(dz_bf), ptr(dz, f0 * D), ptr(DS[i]), st)
+        else:
+            call("ctr_qnn_gram_bwd", ptr(q["z"]), B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]), ptr(dquad),
+                 ptr(dadd), int(dz_bf), ptr(dz), ptr(DS), st)
+        # dUcat = 2 (zsum^T DS - sum_b G_b Ucat diag(dquad_b)); the block form sums zsum_k^T DS_k over the blocks
         T1 = W.get("qT1", (D, QR))
         T = W.get("qT", (D * D, QR))
         ducat = W.get("ducat", (D, QR))
         with self.side():
-            self.gemm(D, QR, B, ptr(q["zsum"]), D, 1, ptr(DS), QR, 0, ptr(T1), QR, None, self.wgrad_splits(D, QR, B))
+            for i in range(max(1, len(blocks))):
+                self.gemm(D, QR, B, ptr(q["zsum"][i]), D, 1, ptr(DS[i]), QR, 0, ptr(T1), QR,
+                          GemmEpi(add=ptr(T1), ld_add=QR) if i > 0 else None, self.wgrad_splits(D, QR, B))
             self.gemm(D * D, QR, B, ptr(q["gram"]), D * D, 1, ptr(dquad), QR, 0, ptr(T), QR, None,
                       self.wgrad_splits(D * D, QR, B))
             call("ctr_qnn_du_combine", ptr(T1), ptr(T), ptr(q["ucat"]), D, QR, ptr(ducat), self.s())
