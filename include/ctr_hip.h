@@ -117,6 +117,17 @@ int ctr_rowgemm(int M, int K, int N, const float* A, int lda, const float* W, in
 int ctr_rowgemm_wgrad_rows(int M);
 int ctr_rowgemm_wgrad(const float* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN, float* slab,
                       long ld_slab, int o_db, void* stream);
+/* amp: bf16 forms of the two above for D = 64 (cfgs/v3_k148_s1.yaml; the reference's autocast F.linear,
+ * src/train.py:158-168 over src/models/dare.py:53-62): operands rounded to bf16 (RNE), fp32 accumulation
+ * and fp32 outputs, same arguments and epilogues.  (K, N): (64,64) (64,192) (192,64); wgrad (NO, NIN):
+ * (64,64) (192,64), its slab rows counted by ctr_rowgemm_bf_wgrad_rows(M); db sums the fp32 dY.    (rowgemm_bf.hip) */
+int ctr_rowgemm_bf_supported(int K, int N);
+int ctr_rowgemm_bf(int M, int K, int N, const float* A, int lda, const float* W, int tb, float* C, int ldc,
+                   const float* bias, const float* add, int ld_add, const float* resid, int ld_resid,
+                   const float* norm_w, float* norm_h, float* norm_r, float eps, void* stream);
+int ctr_rowgemm_bf_wgrad_rows(int M);
+int ctr_rowgemm_bf_wgrad(const float* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN, float* slab,
+                         long ld_slab, int o_db, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Feature embeddings / context                                                    (embed.hip)

@@ -1101,6 +1101,88 @@ def test_rowgemm_wgrad_vs_torch(NO, NIN, M):
     assert float(out[NO * NIN:o_db].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("M,N", [(300, 20), (300, 64), (77, 1000), (64, 5000), (4096, 9024), (33, 16384),
+                                  (17, 20000)])
+def test_rmsnorm_bwd_vs_torch(M, N):
+    """ctr_rmsnorm_bwd (dh and the per-block dw partials) vs torch fp64 for every row-width form: small rows,
+    256-thread rows, the 16-byte forms up to 8192 and (1024 threads) 16384 wide, the two-pass fallback beyond.
+    (4096, 9024): a QNN input norm width of the cfg4 shape class."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N)
+    dy = torch.randn(M, N, device="cuda", generator=g)
+    h = torch.randn(M, N, device="cuda", generator=g)
+    w = torch.rand(N, device="cuda", generator=g) + 0.5
+    r = torch.rsqrt(h.double().pow(2).mean(-1) + 1e-6).float()
+    nparts = L.query("ctr_rmsnorm_bwd_nparts", M, N)
+    dwp = torch.full((nparts, N), float("nan"), device="cuda")
+    dh = torch.full((M, N), float("nan"), device="cuda")
+    L.call("ctr_rmsnorm_bwd", ptr(dy), N, ptr(h), N, ptr(r), ptr(w), M, N, ptr(dh), N, None, 0, ptr(dwp), stream())
+    gd, hd, rd, wd = dy.double(), h.double(), r.double()[:, None], w.double()
+    dot = (wd * gd * hd).sum(-1, keepdim=True)
+    ref = wd * gd * rd - hd * rd.pow(3) / N * dot
+    assert rel(dh.double(), ref) < 1e-5
+    assert rel(dwp.double().sum(0), (gd * hd * rd).sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("K,N", [(64, 192), (64, 64), (192, 64)])
+@pytest.mark.parametrize("M", [606208, 1000, 77, 5])
+def test_rowgemm_bf_vs_emulation(K, N, M):
+    """rowgemm_bf.hip (amp, D = 64): C = A W^T (+bias) / A W (+add) / fused residual + RMSNorm on bf16-rounded
+    operands, vs an fp64 emulation with the same rounded operands (only the fp32 summation order differs).
+    M = 606,208 is cfg4's B*K (4096 x 148): the persistent walk over every row block."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(K * 1000 + N + M)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    Wt = torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)      # nn.Linear layout (tb = 1)
+    Wn = torch.randn(K, N, device="cuda", generator=g) / math.sqrt(K)      # (K, N) layout (tb = 0)
+    b = torch.randn(N, device="cuda", generator=g)
+    add = torch.randn(M, N, device="cuda", generator=g)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    st = stream()
+    Ab = _bfr(A)
+    L.call("ctr_rowgemm_bf", M, K, N, ptr(A), K, ptr(Wt), 1, ptr(C), N, ptr(b), None, 0, None, 0, None, None, None,
+           0.0, st)
+    assert rel(C.double(), Ab @ _bfr(Wt).t() + b.double()) < 1e-6
+    L.call("ctr_rowgemm_bf", M, K, N, ptr(A), K, ptr(Wn), 0, ptr(C), N, None, ptr(add), N, None, 0, None, None, None,
+           0.0, st)
+    assert rel(C.double(), Ab @ _bfr(Wn) + add.double()) < 1e-6
+    # an fp32 product would differ from the bf16 one by ~2^-9 relative: the emulation pins the operand rounding
+    assert rel(C.double(), A.double() @ Wn.double() + add.double()) > 1e-4
+    if K == N:      # out_proj: residual + RMSNorm epilogue
+        res = torch.randn(M, N, device="cuda", generator=g)
+        w = torch.rand(N, device="cuda", generator=g) + 0.5
+        h, r = torch.empty(M, N, device="cuda"), torch.empty(M, device="cuda")
+        L.call("ctr_rowgemm_bf", M, K, N, ptr(A), K, ptr(Wt), 1, ptr(C), N, ptr(b), None, 0, ptr(res), N, ptr(w),
+               ptr(h), ptr(r), 1e-6, st)
+        h_ref = res.double() + (Ab @ _bfr(Wt).t() + b.double())
+        r_ref = torch.rsqrt(h_ref.pow(2).mean(-1) + 1e-6)
+        assert rel(h.double(), h_ref) < 1e-6 and rel(r.double(), r_ref) < 1e-6
+        assert rel(C.double(), w.double() * h_ref * r_ref[:, None]) < 1e-6
+
+
+@pytest.mark.parametrize("NO,NIN", [(192, 64), (64, 64)])
+@pytest.mark.parametrize("M", [606208, 1001, 5])
+def test_rowgemm_bf_wgrad_vs_emulation(NO, NIN, M):
+    """amp, D = 64: dW = dY^T X on bf16-rounded operands (fp64 emulation) and db = colsum of the fp32 dY, slab
+    rows reduced by ctr_colsum."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(NO + NIN + M)
+    dY = torch.randn(M, NO, device="cuda", generator=g)
+    X = torch.randn(M, NIN, device="cuda", generator=g)
+    o_db = NO * NIN + 8                     # a padding gap before the bias, as in the grad arena
+    n_sl = o_db + NO
+    ld = (n_sl + 3) // 4 * 4
+    rows = L.query("ctr_rowgemm_bf_wgrad_rows", M)
+    slab = torch.zeros(rows, ld, device="cuda")
+    L.call("ctr_rowgemm_bf_wgrad", ptr(dY), NO, ptr(X), NIN, M, NO, NIN, ptr(slab), ld, o_db, stream())
+    out = torch.full((n_sl,), float("nan"), device="cuda")
+    ws = torch.empty(L.query("ctr_colsum_ws_size", rows, n_sl) // 4 + 1, device="cuda")
+    L.call("ctr_colsum", ptr(slab), ld, rows, n_sl, 1.0, ptr(out), ptr(ws), stream())
+    assert rel(out[:NO * NIN].double().view(NO, NIN), _bfr(dY).t() @ _bfr(X)) < 1e-6
+    assert rel(out[o_db:].double(), dY.double().sum(0)) < 1e-6
+    assert float(out[NO * NIN:o_db].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("M,N,ld", [(1, 4, 4), (7, 3, 3), (4096, 512, 512), (4096, 513, 516), (1023, 8432, 8432),
                                     (5000, 257, 260), (64, 1, 1), (129, 260, 264), (0, 8, 8)])
 def test_colsum_vs_torch(M, N, ld):

@@ -67,6 +67,10 @@ SIGS = {
     "ctr_rowgemm": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
     "ctr_rowgemm_wgrad_rows": (i, [i]),
     "ctr_rowgemm_wgrad": (i, [p, i, p, i, i, i, i, p, l, i, p]),
+    "ctr_rowgemm_bf_supported": (i, [i, i]),
+    "ctr_rowgemm_bf": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
+    "ctr_rowgemm_bf_wgrad_rows": (i, [i]),
+    "ctr_rowgemm_bf_wgrad": (i, [p, i, p, i, i, i, i, p, l, i, p]),
     "ctr_feat_embed_fwd": (i, [p, i, i, p, p, p, i, i, p, l, p]),
     "ctr_feat_embed_bwd_ws": (z, [i, i, i]),
     "ctr_feat_embed_bwd": (i, [p, i, i, p, p, p, i, i, p, l, p, p, p, p, p]),

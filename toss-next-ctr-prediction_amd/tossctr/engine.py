@@ -175,6 +175,12 @@ class Engine:
         # row-streaming in/out-projection kernels (rowgemm.hip) for the D they are built for
         self.rowgemm = a.n_layers > 0 and all(bool(_lib.query("ctr_rowgemm_supported", k, n))
                                               for k, n in ((a.D, 3 * a.D), (a.D, a.D), (3 * a.D, a.D)))
+        # amp: bf16 at the widths the fp32 row kernels do not cover (D = 64): their bf16-operand forms
+        # (rowgemm_bf.hip), as the reference's autocast F.linear
+        self.rowgemm_bf = bool(self.bf16 and a.n_layers > 0 and not self.rowgemm and
+                               all(bool(_lib.query("ctr_rowgemm_bf_supported", k, n))
+                                   for k, n in ((a.D, 3 * a.D), (a.D, a.D), (3 * a.D, a.D))))
+        self.rowgemm = self.rowgemm or self.rowgemm_bf
         self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden, 0)) and \
             self._ffn_contiguous()
         # amp: bf16 -> the fused FFN's bf16-MFMA kernels where their shape constraints hold (D in {32, 64},
@@ -362,9 +368,10 @@ class Engine:
 
     def rowgemm_call(self, M, K, N, A, W, tb, C, bias=None, add=None, resid=None, norm_w=None, norm_h=None,
                      norm_r=None):
-        """C (M, N) = A (M, K) W^T (tb) or A W, + bias / + add / residual + RMSNorm (rowgemm.hip)."""
-        call("ctr_rowgemm", M, K, N, A, K, W, tb, C, N, bias, add, N if add else 0, resid, N if resid else 0, norm_w,
-             norm_h, norm_r, 1e-6, self.s())
+        """C (M, N) = A (M, K) W^T (tb) or A W, + bias / + add / residual + RMSNorm (rowgemm.hip; amp at
+        D = 64: rowgemm_bf.hip)."""
+        call("ctr_rowgemm_bf" if self.rowgemm_bf else "ctr_rowgemm", M, K, N, A, K, W, tb, C, N, bias, add,
+             N if add else 0, resid, N if resid else 0, norm_w, norm_h, norm_r, 1e-6, self.s())
 
     def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey, tag="", defer=False):
         """dW = dY^T X and db = colsum(dY) of one nn.Linear in one pass (rowgemm.hip): per-wave partial
@@ -373,9 +380,10 @@ class Engine:
         o_db = self.arena.offsets[bkey] - o0
         n_sl = o_db + n_out
         ld = (n_sl + 3) // 4 * 4
-        rows = _lib.query("ctr_rowgemm_wgrad_rows", M)
+        bf = "_bf" if self.rowgemm_bf else ""
+        rows = _lib.query(f"ctr_rowgemm{bf}_wgrad_rows", M)
         slab = W.get_zeroed(f"wg_slab_{n_out}x{n_in}_{tag}", (rows, ld))     # padding columns stay zero
-        call("ctr_rowgemm_wgrad", dY, n_out, X, n_in, M, n_out, n_in, ptr(slab), ld, o_db, self.s())
+        call(f"ctr_rowgemm{bf}_wgrad", dY, n_out, X, n_in, M, n_out, n_in, ptr(slab), ld, o_db, self.s())
         self.colsum(ptr(slab), ld, rows, n_sl, ptr(self.arena.grad, o0), defer=defer)
 
     def colsum(self, X, ld, M, N, out, div=1.0, defer=False):
