@@ -877,7 +877,7 @@ BF_TOL = 2e-4     # bf16 emulation: only rare rounding-boundary flips of an oper
 @pytest.mark.parametrize("M,D,FF,p", [(300, 32, 384, 0.1), (130, 64, 384, 0.15), (4097, 32, 384, 0.0),
                                       (517, 32, 64, 0.2), (64, 32, 32, 0.5), (70001, 32, 384, 0.1),
                                       (140003, 64, 96, 0.1), (70001, 64, 384, 0.1), (4097, 64, 128, 0.15),
-                                      (9001, 64, 256, 0.0)])
+                                      (9001, 64, 256, 0.0), (606208, 64, 384, 0.15)])
 def test_fused_ffn_bf16_vs_emulation(M, D, FF, p):
     """amp bf16 FFN kernels (CTR_FFN_BF16) vs an fp64 emulation with bf16-rounded product operands; the
     persistent backward (M > 512 tiles: several tiles per workgroup, slab rows accumulated) included."""

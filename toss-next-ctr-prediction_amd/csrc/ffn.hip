@@ -1224,22 +1224,28 @@ __global__ __launch_bounds__(256) void ffn_fwd_bfp_kernel(FfnArgs a) {
 // 4g + r]: a row's 32 outputs sit in its four lane groups, the RMSNorm sum takes two lane swaps, h and y go out as
 // 16-byte stores of whole rows.  The next tile's rows are loaded while the current one computes.  Keep bits, their
 // "row words" layout, the weight images for the backward: as the per-tile kernels.
+// D = 64 (round 5): the same with 16-row tiles (NI = 1; 99 KB of weight images) and one workgroup of sixteen waves
+// per CU (four per SIMD); the d order of step kh of a D-contraction is {32 kh + 4g .. +3} u {32 kh + 16 + 4g .. +3}.
+template <int D_>
 struct FfnFw {
-  static constexpr int D = 32, RW = 32, NI = 2, NWAVE = 8;
+  static constexpr int D = D_, NI = D == 32 ? 2 : 1, RW = 16 * NI, NWAVE = D == 32 ? 8 : 16;
+  static constexpr int KH = D / 32, NJ = D / 16;
 };
 
-template <bool DROP>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ffn_fwd_bfw_kernel(FfnArgs a) {
-  constexpr int D = 32;
+template <int D, bool DROP>
+__global__ __launch_bounds__(FfnFw<D>::NWAVE * 64) __attribute__((amdgpu_waves_per_eu(4))) void ffn_fwd_bfw_kernel(
+    FfnArgs a) {
+  using T = FfnFw<D>;
+  constexpr int NI = T::NI, KH = T::KH, NJ = T::NJ, NT = T::NWAVE * 64;
   extern __shared__ __attribute__((aligned(16))) char fsm[];
   const int FF = a.FF, NCH = FF / 32;
-  bf16x8* iw1 = (bf16x8*)fsm;                        // [NCH][2][64]: W1[32 ch + 16 s + c][4g .. +3 | 16 + 4g .. +3]
-  bf16x8* iw2 = iw1 + NCH * 2 * 64;                  // [NCH][2][64]: W2[16 j + c][32 ch + 4g .. +3 | 32 ch + 16 + 4g ..]
-  float* sb1 = (float*)(iw2 + NCH * 2 * 64);         // [FF]
+  bf16x8* iw1 = (bf16x8*)fsm;                 // [NCH][2][KH][64]: W1[32 ch + 16 s + c][32 kh + 4g .. +3 | 32 kh + 16 + 4g ..]
+  bf16x8* iw2 = iw1 + NCH * 2 * KH * 64;      // [NCH][NJ][64]: W2[16 j + c][32 ch + 4g .. +3 | 32 ch + 16 + 4g ..]
+  float* sb1 = (float*)(iw2 + NCH * NJ * 64);  // [FF]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
   if (a.wbf) {     // bf16 weight images for the backward: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF)
     const int n = FF * D;
-    for (int e = blockIdx.x * 512 + tid; e < 3 * n; e += gridDim.x * 512) {
+    for (int e = blockIdx.x * NT + tid; e < 3 * n; e += gridDim.x * NT) {
       float v;
       if (e < n) {
         v = a.W1[e];
@@ -1253,17 +1259,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
       a.wbf[e] = (__bf16)v;
     }
   }
-  for (int u = tid; u < NCH * 2 * 64; u += 512) {
-    const int l = u & 63, sc = u >> 6, s2 = sc & 1, ch = sc >> 1, lg = l >> 4;
-    const float* p = a.W1 + (long)(32 * ch + 16 * s2 + (l & 15)) * D + 4 * lg;
+  for (int u = tid; u < NCH * 2 * KH * 64; u += NT) {
+    const int l = u & 63, q = u >> 6, kh = q % KH, sc = q / KH, s2 = sc & 1, ch = sc >> 1, lg = l >> 4;
+    const float* p = a.W1 + (long)(32 * ch + 16 * s2 + (l & 15)) * D + 32 * kh + 4 * lg;
     iw1[u] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 16));
   }
-  for (int u = tid; u < NCH * 2 * 64; u += 512) {
-    const int l = u & 63, q = u >> 6, j = q & 1, ch = q >> 1;
+  for (int u = tid; u < NCH * NJ * 64; u += NT) {
+    const int l = u & 63, q = u >> 6, j = q % NJ, ch = q / NJ;
     const float* p = a.W2 + (long)(16 * j + (l & 15)) * FF + 32 * ch + 4 * (l >> 4);
     iw2[u] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 16));
   }
-  for (int u = tid; u < FF; u += 512) sb1[u] = a.b1[u];
+  for (int u = tid; u < FF; u += NT) sb1[u] = a.b1[u];
   __syncthreads();
 
   const int nb16 = (a.M + 15) / 16;
@@ -1276,51 +1282,59 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
   const uint32_t thr = a.drop.thresh;
   const float dsc = a.drop.scale;
   // x rows of a tile: xr[i][j] = x[m0 + 16 i + c][16 j + 4g .. +3] (0 past M)
-  f32x4 xr[2][2];
+  f32x4 xr[NI][NJ];
   auto fetch_x = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        xr[i][j] = buf_ld4(rx, (uint32_t)(((t * 32 + 16 * i + c) * D) + 16 * j + 4 * g) * 4, 0);
+      for (int j = 0; j < NJ; ++j)
+        xr[i][j] = buf_ld4(rx, (uint32_t)(((t * T::RW + 16 * i + c) * D) + 16 * j + 4 * g) * 4, 0);
   };
   struct Wc {
-    bf16x8 w1[2], w2[2];
+    bf16x8 w1[2][KH], w2[NJ];
     f32x4 b[2];
   };
   auto load_w = [&](int ch, Wc& W) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      W.w1[s2] = iw1[(ch * 2 + s2) * 64 + lane];
-      W.w2[s2] = iw2[(ch * 2 + s2) * 64 + lane];
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) W.w1[s2][kh] = iw1[((ch * 2 + s2) * KH + kh) * 64 + lane];
       W.b[s2] = *(const f32x4*)(sb1 + 32 * ch + 16 * s2 + 4 * g);
     }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) W.w2[j] = iw2[(ch * NJ + j) * 64 + lane];
   };
-  const int ntiles = (a.M + 31) / 32;
-  const int gw = blockIdx.x * FfnFw::NWAVE + w, nw = gridDim.x * FfnFw::NWAVE;
+  const int ntiles = (a.M + T::RW - 1) / T::RW;
+  const int gw = blockIdx.x * T::NWAVE + w, nw = gridDim.x * T::NWAVE;
   if (gw < ntiles) fetch_x(gw);
   for (int tile = gw; tile < ntiles; tile += nw) {
-    const int m0 = tile * 32;
-    bf16x8 xf[2];
+    const int m0 = tile * T::RW;
+    bf16x8 xf[NI][KH];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) xf[i] = pack8(xr[i][0], xr[i][1]);
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) xf[i][kh] = pack8(xr[i][2 * kh], xr[i][2 * kh + 1]);
     if (tile + nw < ntiles) fetch_x(tile + nw);
-    f32x4 yacc[2][2];
+    f32x4 yacc[NI][NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int ch = 0; ch < NCH; ++ch) {
       Wc W;
       load_w(ch, W);
       const int f0 = 32 * ch;
-      f32x4 p[2][2];
+      f32x4 p[NI][2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) p[i][s2] = mfma_bf(W.w1[s2], xf[i], W.b[s2]);   // pre^T [ff][row], + b1
+        for (int s2 = 0; s2 < 2; ++s2) {
+          p[i][s2] = mfma_bf(W.w1[s2][0], xf[i][0], W.b[s2]);                            // pre^T [ff][row], + b1
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+          for (int kh = 1; kh < KH; ++kh) p[i][s2] = mfma_bf(W.w1[s2][kh], xf[i][kh], p[i][s2]);
+        }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
         const uint32_t m = (uint32_t)(m0 + 16 * i + c);
         uint32_t kb = 0;
         f32x4 fo[2];
@@ -1342,7 +1356,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
           }
         const bf16x8 bf = pack8(fo[0], fo[1]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) yacc[i][j] = mfma_bf(W.w2[j], bf, yacc[i][j]);          // y^T [d][row]
+        for (int j = 0; j < NJ; ++j) yacc[i][j] = mfma_bf(W.w2[j], bf, yacc[i][j]);         // y^T [d][row]
         if (DROP) {
           uint32_t kw = ((kb & 0xFu) << (4 * g)) | ((kb >> 4) << (16 + 4 * g));
           kw |= (uint32_t)__shfl_xor((int)kw, 16, 64);
@@ -1354,23 +1368,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     }
     // epilogue: h = x + (y + b2), r = 1 / rms(h), y = nw h r -- row 16 i + c over the four lane groups; the x rows
     // (this wave's own, read at the tile's start) are read again rather than held across the chunk loop
-    f32x4 xc[2][2], bb[2], nn[2];
+    f32x4 xc[NI][NJ], bb[NJ], nn[NJ];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < NJ; ++j)
         xc[i][j] = buf_ld4(rx, (uint32_t)(((m0 + 16 * i + c) * D) + 16 * j + 4 * g) * 4, 0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       bb[j] = *(const f32x4*)(a.b2 + 16 * j + 4 * g);
       nn[j] = *(const f32x4*)(a.nw + 16 * j + 4 * g);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      f32x4 hv[2];
+    for (int i = 0; i < NI; ++i) {
+      f32x4 hv[NJ];
       float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         hv[j] = xc[i][j] + (yacc[i][j] + bb[j]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) ss = fmaf(hv[j][r], hv[j][r], ss);
@@ -1380,7 +1394,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
       const float rs = 1.0f / sqrtf(ss / (float)D + a.eps);
       const uint32_t row = (uint32_t)(m0 + 16 * i + c);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const uint32_t off = (row * D + 16 * j + 4 * g) * 4;
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hv[j]), rh, off, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nn[j] * hv[j] * rs), ry, off, 0, 0);
@@ -1390,7 +1404,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
   }
 }
 
-static size_t ffn_fwdw_lds(int FF) { return (size_t)FF * 32 * 2 * 2 + (size_t)FF * 4; }
+template <int D>
+static size_t ffn_fwdw_lds(int FF) { return (size_t)FF * D * 2 * 2 + (size_t)FF * 4; }
 
 template <int D>
 static size_t ffn_fwdp_lds(int FF) {
@@ -2473,20 +2488,23 @@ template <int D>
 static void launch_ffn_bf(const FfnArgs& a, bool bwd, hipStream_t s) {
   const bool drop = a.drop.thresh != 0;
   if (!bwd) {
-    if constexpr (D == 32) {
-      const size_t sm = ffn_fwdw_lds(a.FF);
-      if (sm <= 76 * 1024) {      // two workgroups of eight waves per CU
+    {
+      // D = 32: two workgroups of eight waves per CU; D = 64: one of sixteen
+      constexpr size_t lim = D == 32 ? 76 * 1024 : 150 * 1024;
+      const size_t sm = ffn_fwdw_lds<D>(a.FF);
+      if (sm <= lim) {
         static bool attr = false;
         if (!attr) {
-          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfw_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    76 * 1024);
-          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfw_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    76 * 1024);
+          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfw_kernel<D, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lim);
+          (void)hipFuncSetAttribute((const void*)ffn_fwd_bfw_kernel<D, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lim);
           attr = true;
         }
-        const int grid = std::min(cdiv(a.M, 32 * FfnFw::NWAVE), 2 * 256);
-        if (drop) ffn_fwd_bfw_kernel<true><<<grid, 512, sm, s>>>(a);
-        else ffn_fwd_bfw_kernel<false><<<grid, 512, sm, s>>>(a);
+        using T = FfnFw<D>;
+        const int grid = std::min(cdiv(a.M, T::RW * T::NWAVE), (D == 32 ? 2 : 1) * 256);
+        if (drop) ffn_fwd_bfw_kernel<D, true><<<grid, T::NWAVE * 64, sm, s>>>(a);
+        else ffn_fwd_bfw_kernel<D, false><<<grid, T::NWAVE * 64, sm, s>>>(a);
         return;
       }
     }

@@ -180,22 +180,23 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_big(const float* __restrict__
   }
 }
 
-// big rows with 16-byte loads (N % 4 == 0, aligned rows; NQ float4 per thread): the next row's dy and h
-// are loaded before this row's block reduction, so the load latency hides behind the reduction barrier.
-template <int NQ>
-__global__ __launch_bounds__(256) void rmsnorm_bwd_big_vec(const float* __restrict__ dy, long ldy,
+// big rows with 16-byte loads (N % 4 == 0, aligned rows; NQ float4 per thread, NT threads): the next row's dy
+// and h are loaded before this row's block reduction, so the load latency hides behind the reduction barrier.
+// NT = 1024 covers rows up to 16384 wide in one pass over dy and h (the QNN input norm at D = 64).
+template <int NQ, int NT = 256>
+__global__ __launch_bounds__(NT) void rmsnorm_bwd_big_vec(const float* __restrict__ dy, long ldy,
                                                            const float* __restrict__ h, long ldh,
                                                            const float* __restrict__ r, const float* __restrict__ w,
                                                            int M, int N, float* __restrict__ dh, long lddh,
                                                            int rows_per_block, float* __restrict__ dw_part) {
   typedef float f4 __attribute__((ext_vector_type(4)));
-  __shared__ float red[4];
+  __shared__ float red[NT / 64];
   const int m0 = blockIdx.x * rows_per_block, m1 = min(M, m0 + rows_per_block);
   const int n4 = N >> 2;
   f4 wv[NQ], acc[NQ], g[NQ], hh[NQ];
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
-    const int j = threadIdx.x + 256 * k;
+    const int j = threadIdx.x + NT * k;
     wv[k] = j < n4 ? ((const f4*)w)[j] : f4{0.f, 0.f, 0.f, 0.f};
     acc[k] = f4{0.f, 0.f, 0.f, 0.f};
   }
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_big_vec(const float* __restri
     const f4* hr = (const f4*)(h + (long)m * ldh);
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      const int j = threadIdx.x + 256 * k;
+      const int j = threadIdx.x + NT * k;
       gg[k] = j < n4 ? gy[j] : f4{0.f, 0.f, 0.f, 0.f};
       hv[k] = j < n4 ? hr[j] : f4{0.f, 0.f, 0.f, 0.f};
     }
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_big_vec(const float* __restri
     f4* o = (f4*)(dh + (long)m * lddh);
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      const int j = threadIdx.x + 256 * k;
+      const int j = threadIdx.x + NT * k;
       if (j < n4) o[j] = wv[k] * g[k] * rm - hh[k] * coef;
     }
     if (m + 1 < m1) {
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(256) void rmsnorm_bwd_big_vec(const float* __restri
   f4* dp = (f4*)(dw_part + (long)blockIdx.x * N);
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
-    const int j = threadIdx.x + 256 * k;
+    const int j = threadIdx.x + NT * k;
     if (j < n4) dp[j] = acc[k];
   }
 }
@@ -613,6 +614,8 @@ extern "C" int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long l
                       15) == 0;
     if (vec && N > 256 * 8 && N <= 1024 * 8)
       rmsnorm_bwd_big_vec<8><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
+    else if (vec && N > 1024 * 8 && N <= 1024 * 16)
+      rmsnorm_bwd_big_vec<4, 1024><<<nb, 1024, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
     else if (N <= 256 * 8) rmsnorm_bwd_big<8><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
     else if (N <= 256 * 16) rmsnorm_bwd_big<16><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
     else if (N <= 256 * 32) rmsnorm_bwd_big<32><<<nb, 256, 0, s>>>(dy, ldy, h, ldh, r, w, M, N, dh, lddh, rpb, dw_part);
