@@ -1101,6 +1101,19 @@ def test_rowgemm_wgrad_vs_torch(NO, NIN, M):
     assert float(out[NO * NIN:o_db].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("nparts,n,H", [(8192, 297, 8), (4096, 201, 4), (13, 65, 2), (1, 3, 4), (0, 9, 4)])
+def test_pos_bias_grad_vs_torch(nparts, n, H):
+    """ctr_pos_bias_grad: drel[d, h] = sum_p part[p, d] / H for every head (the head-mean bias's grad), the
+    partials reduced in place in chunks; (8192, 297): cfg4's B x head groups and 2 top_k + 1."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(nparts + n)
+    part = torch.randn(max(nparts, 1), n, device="cuda", generator=g)
+    ref = part[:nparts].double().sum(0) / H
+    drel = torch.full((n, H), float("nan"), device="cuda")
+    L.call("ctr_pos_bias_grad", ptr(part), nparts, H, n, ptr(drel), stream())
+    assert rel(drel.double(), ref[:, None].expand(n, H)) < 1e-6 if nparts else float(drel.abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("M,N", [(300, 20), (300, 64), (77, 1000), (64, 5000), (4096, 9024), (33, 16384),
                                   (17, 20000)])
 def test_rmsnorm_bwd_vs_torch(M, N):

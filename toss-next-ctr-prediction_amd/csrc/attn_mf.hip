@@ -712,6 +712,16 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
   __bf16* sdo = sv + S::IM;
   __bf16* simg = sdo + S::IM + S::PAD;              // per wave: 16 x 16 dS image, 16 x 16 p~ image (x2)
   float* srel = (float*)(simg + 4 * 4 * 256);
+  // keep words: key tile tj's 4 nt bits start at bit 4 nt tj of the lane's word row and span up to three words;
+  // the next tile's words are loaded while the current one runs (tile 0's during the staging)
+  const uint32_t* mk = a.mask + ((long)b * a.H + hgrp * G + (threadIdx.x >> 6)) * (64 * KB::NW) + (threadIdx.x & 63);
+  auto fetch_kw = [&](int t, uint32_t (&kw)[3]) {
+    const int w0 = (4 * NT * t) >> 5;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) kw[u] = mk[64 * min(w0 + u, KB::NW - 1)];
+  };
+  uint32_t kwn[3] = {0u, 0u, 0u};
+  if (DROP) fetch_kw(0, kwn);
   stage<DH, NT, true>(a, b, hgrp, sq, sk, sv, sdo);
   if (BIAS) stage_rel<NT>(a, srel);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
@@ -743,7 +753,6 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
   if (BIAS)
     for (int e = lane; e < NDGP; e += 64) dsum[e] = 0.f;
   __syncthreads();
-  const uint32_t* mk = a.mask + ((long)b * a.H + h) * (64 * KB::NW) + lane;
   const uint32_t dsc_bits = __builtin_bit_cast(uint32_t, DROP ? a.drop.scale : 1.0f);
   // fold the finished tile diagonal dt (values v[r] of element (a = 4g + r, c): diagonal 16 (dt - nt + 1) + a - c)
   // into dsum: lane e + 15 (e = a - c in [-15, 15]) sums its diagonal over a, ascending
@@ -778,10 +787,12 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
     const bf16x4 ktop = op_col<DH, NT>(sk, 16 * tj, hs, g, c);                         // A = k^T [d][j]
     uint64_t kb = 0;
     if (DROP) {
+      const uint32_t kw[3] = {kwn[0], kwn[1], kwn[2]};
+      fetch_kw(min(tj + 1, NT - 1), kwn);
       const int p0 = 4 * NT * tj, w0 = p0 >> 5;
-      const uint64_t lo = mk[64 * w0], hi = w0 + 1 < KB::NW ? mk[64 * (w0 + 1)] : 0u;
+      const uint64_t lo = kw[0], hi = w0 + 1 < KB::NW ? kw[1] : 0u;
       kb = ((hi << 32) | lo) >> (p0 & 31);
-      if ((p0 & 31) + 4 * NT > 64) kb |= (uint64_t)mk[64 * (w0 + 2)] << (64 - (p0 & 31));
+      if ((p0 & 31) + 4 * NT > 64) kb |= (uint64_t)kw[2] << (64 - (p0 & 31));
     }
     const float* rbt = rb + 16 * tj;
     f32x4 dk = {0.f, 0.f, 0.f, 0.f}, dv = dk;
