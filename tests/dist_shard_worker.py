@@ -111,9 +111,15 @@ def run(rank, world, port, args):
             for k, v in make_params(dense, 5, arch.pad_id).items():
                 model.arena.views[k].copy_(torch.from_numpy(v))
             _fill_tables_by_index(model, rank, world)
-    ema = ArenaEMA(model, base_decay=0.9)
-    opt = FusedAdamW(model, lr=lr0, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
-                     lazy=bool(args.lazy))
+    if args.autograd:
+        # the reference loop itself (src/train.py:185-195): loss.backward(), clip, torch.optim.AdamW; row-sharded
+        # tables clip through model.clip_grad_norm_ (the global norm)
+        ema = opt = None
+        opt_t = torch.optim.AdamW(model.parameters(), lr=lr0, weight_decay=0.05)
+    else:
+        ema = ArenaEMA(model, base_decay=0.9)
+        opt = FusedAdamW(model, lr=lr0, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
+                         lazy=bool(args.lazy))
     losses, batches, staged = [], [], []
     for t in range(args.steps):
         bseed = 1000 + t + (0 if args.same_batch else 100 * rank)
@@ -121,7 +127,23 @@ def run(rank, world, port, args):
         batches.append(b)
         staged.append((model.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda()))
     model.train()
-    for t in range(args.steps):
+    for t in range(args.steps if args.autograd else 0):
+        for grp in opt_t.param_groups:
+            grp["lr"] = lr0 * (1.0 - 0.2 * t)
+        z, _, aux = model(to_torch_batch(batches[t]), seed=(9 << 32) | t)
+        y = staged[t][1]
+        loss = _bce_wll(z, y)
+        if model.aux_weight > 0:
+            loss = loss + model.aux_weight * _bce_wll(aux, y)
+        opt_t.zero_grad(set_to_none=True)
+        loss.backward()
+        if model.shards is not None:
+            model.clip_grad_norm_(clip)
+        else:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
+        opt_t.step()
+        losses.append(loss.detach())
+    for t in range(0 if args.autograd else args.steps):
         opt.param_groups[0]["lr"] = lr0 * (1.0 - 0.2 * t)
         inputs, y = staged[t]
         if args.interleave_eval and t == 2:
@@ -142,10 +164,10 @@ def run(rank, world, port, args):
         if args.sync_check and t == 2:
             torch.cuda.set_sync_debug_mode("error")
         loss = model.train_step(inputs, y, opt, global_step=t + 1, seed=(9 << 32) | t, next_inputs=nxt, **kw)
-        losses.append(loss)
+        losses.append(loss.clone())     # the step's loss lives in a workspace buffer the next step overwrites
     torch.cuda.set_sync_debug_mode("default")
     losses = [float(x.item()) for x in losses]
-    if model.shards is not None and args.prefetch:
+    if model.shards is not None and args.prefetch and not args.autograd:
         # every step after the first consumed the plan made beside the step before it, except the one an
         # evaluation forward came in front of (--interleave-eval)
         sh = model.shards
@@ -172,20 +194,30 @@ def run(rank, world, port, args):
         if args.dump_ws and rank == 0:      # the evaluation forward's workspace (tools/shard_logit_diag.py)
             torch.save({k: v.detach().cpu() for k, v in model.engine.ws(Bs, L).t.items()}, args.out + ".ws")
         sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
-        shadow = {k: v.detach().cpu() for k, v in ema.state_dict()["shadow_params"].items()}
-        mom = {k: model.full_table(opt.m, k).detach().cpu() for k in model.arena.order}
-        vel = {k: model.full_table(opt.v, k).detach().cpu() for k in model.arena.order}
+        shadow = {k: v.detach().cpu() for k, v in ema.state_dict()["shadow_params"].items()} if ema else {}
+        mom = {k: model.full_table(opt.m, k).detach().cpu() for k in model.arena.order} if opt else {}
+        vel = {k: model.full_table(opt.v, k).detach().cpu() for k in model.arena.order} if opt else {}
         local_rows = int(model.arena.shapes["dare.emb_att.weight"][0])
         if rank == 0:
             torch.save({"sd": sd, "ema": shadow, "m": mom, "v": vel, "losses": losses, "logits": logits, "eval_tok": eval_tok, "eval_vals": eval_vals,
                         "eval_idx": eval_idx,
-                        "gnorm": float(opt.norm_out[0]), "local_rows": local_rows, "vocab": vocab, "cards": cards,
+                        "gnorm": float(opt.norm_out[0]) if opt else float("nan"), "local_rows": local_rows, "vocab": vocab, "cards": cards,
                         "cfg": cfg, "Fn": Fn, "Fm": Fm, "L": L, "B": Bs, "lr0": lr0, "clip": clip,
                         "init": "reference" if args.config == "cfg5w" else "synthetic"},
                        args.out)
     if pg is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _bce_wll(z, y):
+    """bce_wll_style (src/train.py:71-90): the two classes' mean softplus losses, half each (a missing class
+    contributes 0)."""
+    import torch
+    pos = y > 0.5
+    pl = torch.nn.functional.softplus(-z[pos]).mean() if pos.any() else z.sum() * 0
+    nl = torch.nn.functional.softplus(z[~pos]).mean() if (~pos).any() else z.sum() * 0
+    return 0.5 * (pl + nl)
 
 
 def _eval_check(model, eb, rank, logits):
@@ -258,6 +290,8 @@ def main():
     ap.add_argument("--steps", type=int, default=STEPS)
     ap.add_argument("--config", choices=("tiny", "cfg5w", "cfg5r"), default="tiny")
     ap.add_argument("--nccl", type=int, default=0, help="world 1 over RCCL instead of world 2 over gloo")
+    ap.add_argument("--autograd", type=int, default=0,
+                    help="the reference loop (model(batch), loss.backward(), clip, torch.optim.AdamW) instead of train_step")
     ap.add_argument("--prefetch", type=int, default=1, help="plan the next batch's exchange beside each step")
     ap.add_argument("--sync-check", type=int, default=0,
                     help="steps >= 2 under torch.cuda.set_sync_debug_mode('error') (needs --nccl 1: gloo stages "

@@ -26,14 +26,15 @@ _cache = {}
 
 
 def _run(tmp_path_factory, mode, same, lazy=1, steps=4, config="tiny", nccl=0, prefetch=1, sync_check=0,
-         interleave=0, short_last=0):
-    key = (mode, same, lazy, steps, config, nccl, prefetch, sync_check, interleave, short_last)
+         interleave=0, short_last=0, autograd=0):
+    key = (mode, same, lazy, steps, config, nccl, prefetch, sync_check, interleave, short_last, autograd)
     if key not in _cache:
         out = str(tmp_path_factory.mktemp("shard") / ("_".join(map(str, key)) + ".pt"))
         r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", mode,
                             "--same-batch", str(same), "--lazy", str(lazy), "--steps", str(steps), "--config", config,
                             "--nccl", str(nccl), "--prefetch", str(prefetch), "--sync-check", str(sync_check),
-                            "--interleave-eval", str(interleave), "--short-last", str(short_last), "--out", out], capture_output=True, text=True, timeout=250)
+                            "--interleave-eval", str(interleave), "--short-last", str(short_last), "--autograd", str(autograd),
+                            "--out", out], capture_output=True, text=True, timeout=250)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         if config in ("tiny", "cfg5w"):
             _cache[key] = torch.load(out, weights_only=True)
@@ -242,3 +243,20 @@ def test_rccl_sharded_step_never_blocks_the_host(tmp_path_factory):
     single = _run(tmp_path_factory, "single", 1, steps=6)
     got = _run(tmp_path_factory, "sharded", 1, steps=6, nccl=1, sync_check=1)
     _compare(got, single, 1e-5, what="RCCL world-1 sharded (sync-checked) vs single: ")
+
+
+def test_sharded_autograd_loop_matches_fused_step(tmp_path_factory):
+    """The reference loop (src/train.py:185-195) on row-sharded tables, world 2, different batches per rank:
+    ``model(batch)``, ``loss.backward()`` -- collective: the dense grads averaged over the ranks, every table row
+    grad sent to its owner and averaged, a table's ``.grad`` its local shard's -- ``model.clip_grad_norm_`` (the
+    global norm, FSDP-style) and ``torch.optim.AdamW`` on the local parameters.  It must land where the fused
+    sharded step does (``train_step``: the same DDP mean, global clip and AdamW; FusedAdamW's hardware sqrt /
+    reciprocal differ from torch's by a few ulp of the update term): losses, and every parameter with the full
+    tables gathered from the shards, after 4 steps."""
+    a = _run(tmp_path_factory, "sharded", 0, autograd=1)
+    b = _run(tmp_path_factory, "sharded", 0)
+    close_enough(np.asarray(a["losses"], np.float64), np.asarray(b["losses"], np.float64), 1e-5, 1e-6, "loss")
+    assert a["sd"].keys() == b["sd"].keys()
+    for k in a["sd"]:
+        assert a["sd"][k].shape == b["sd"][k].shape, k
+        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), 1e-4, 1e-6, k)

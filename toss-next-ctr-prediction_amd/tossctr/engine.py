@@ -1068,20 +1068,25 @@ class Engine:
         return dfcin
 
     # ------------------------------------------------------------------ compat: dense table grads
-    def dense_table_grad(self, key):
-        """Materialise the dense gradient of one embedding table from the compact rows (autograd path)."""
-        if self.shards is not None:
-            raise NotImplementedError("row-sharded tables train through the fused step (model.train_step)")
+    def dense_table_grad(self, key, tg=None, scale=1.0):
+        """Materialise the dense gradient of one embedding table from the compact rows (autograd path).
+        Row-sharded tables: ``tg`` = the grads routed to this rank's rows (TableShards.route: local keys, the
+        local row bases), the result this rank's shard, times ``scale``."""
+        if self.shards is not None and tg is None:
+            raise RuntimeError("row-sharded tables: pass the routed grads (CTRModel._reduce_sharded_grads)")
+        tg = self.tg if tg is None else tg
         a = self.a
         shp = self.arena.shapes[key]
         out = torch.zeros(shp, dtype=torch.float32, device=self.device)
         if key == "dare.emb_att.weight":
-            t, base = self.tg["att"], 0
+            t, base = tg["att"], 0
         elif key == "dare.emb_rep.weight":
-            t, base = self.tg["rep"], 0
+            t, base = tg["rep"], 0
         else:
             c = a.cat_names.index(key[len("cat_embs."):-len(".weight")])
-            t, base = self.tg["cat"], int(self.cat_row_base_np[c])
+            t, base = tg["cat"], int(self.cat_row_base_np[c])
         call("ctr_scatter_rows", ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["n"], shp[1], t["G"].shape[1],
              base, shp[0], ptr(out), self.s())
+        if scale != 1.0:
+            out.mul_(scale)
         return out

@@ -7,7 +7,9 @@ engine.ParamArena).  The compute is libctrhip.so; there is no torch/CPU fallback
 Two training paths:
   * reference-style: ``logits, prob, aux = model(batch); loss = f(...); loss.backward()`` works --
     a custom autograd.Function runs the HIP backward and hands torch ordinary dense ``.grad`` tensors
-    (tables included; fine for tests / small vocabularies);
+    (tables included; fine for tests / small vocabularies).  With row-sharded tables the backward is
+    collective (dense grads averaged over the ranks, row grads sent to their owners; a table's ``.grad``
+    is its local shard's) and ``model.clip_grad_norm_`` replaces ``nn.utils.clip_grad_norm_`` (global norm);
   * fused (what tossctr.train and bench.py use): ``model.train_step(...)`` via tossctr.optim --
     table grads stay compact (sorted unique rows) and clip + AdamW + EMA run as one HBM stream.
 """
@@ -54,10 +56,24 @@ class _CTRFunction(torch.autograd.Function):
             dz = dz + g_prob * p * (1 - p)
         daux = None if g_aux is None else g_aux.float().contiguous()
         eng.backward(sv, dz, daux, overlap=False)     # torch reads the grads right after: no async reduce
+        sh, routed = model.shards, None
+        fused = model.__dict__.get("_fused_opt")
+        if sh is not None and fused is None:
+            # row-sharded tables under a plain torch optimizer: DDP semantics here, in the backward -- the dense
+            # grads all-reduced and averaged, each table's row grads sent to their owners (the fused step's
+            # exchange, tossctr/shard.py route) and averaged; .grad of a table is then its local shard's
+            routed = model._reduce_sharded_grads()
         grads = []
         for k in model.arena.order:
             if model.arena.kind[k] == "table":
-                grads.append(eng.dense_table_grad(k))
+                if sh is None:
+                    grads.append(eng.dense_table_grad(k))
+                elif routed is None:
+                    # FusedAdamW bound: its step() routes the engine's compact row grads and clips on the global
+                    # norm itself, so no dense shard grad is materialised
+                    grads.append(None)
+                else:
+                    grads.append(eng.dense_table_grad(k, routed, 1.0 / sh.world))
             elif k in model.no_grad and not (k.startswith("dare.aux_head") and daux is not None):
                 grads.append(None)
             else:
@@ -209,13 +225,46 @@ class CTRModel(nn.Module):
     def forward(self, batch, seed=None):
         inputs = self._stage(batch)
         if self.training and torch.is_grad_enabled():
-            if self.shards is not None:
-                raise NotImplementedError("row-sharded tables train through the fused step (model.train_step)")
             seed = self.next_seed() if seed is None else seed
             return _CTRFunction.apply(self, inputs, seed, *[getattr(*_tree_module(self, k)) for k in self.arena.order])
         logits, prob, aux, _ = self.engine.forward(*inputs, training=self.training,
                                                    seed=self.next_seed() if seed is None else seed, save=False)
         return logits.clone(), prob.clone(), aux.clone()
+
+    # ------------------------------------------------------------------ row-sharded tables, autograd path
+    def _reduce_sharded_grads(self):
+        """Collective (every rank, in the backward): dense grads all-reduced and divided by the world size
+        (DDP's mean), the compact table row grads routed to their owners; returns the routed grads."""
+        from . import dist as D
+        sh, ar = self.shards, self.arena
+        n = ar.n_dense_grad
+        D.allreduce_sum_(ar.grad[:n], sh.group)
+        ar.grad[:n].mul_(1.0 / sh.world)
+        return sh.route(self.engine.tg, self.engine.tg["fx"])
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float, norm_type: float = 2.0):
+        """``torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm)`` over the WHOLE model when its tables
+        are row-sharded (collective; as FSDP's ``clip_grad_norm_``): the dense grads are replicated, each rank
+        holds its shards' grads, so the squared norm is the dense part plus the all-reduced table parts.  Same
+        coefficient as torch (``max_norm / (norm + 1e-6)``, clamped to 1, always multiplied).  Without sharded
+        tables it is torch's own function.  Returns the total norm."""
+        params = [p for p in self.parameters() if p.grad is not None]
+        if self.shards is None:
+            return torch.nn.utils.clip_grad_norm_(params, max_norm, norm_type)
+        if float(norm_type) != 2.0:
+            raise NotImplementedError("row-sharded clip_grad_norm_: norm_type 2 only")
+        from . import dist as D
+        tab = {id(v) for k, v in self.named_parameters() if self.arena.kind[k] == "table"}
+        sq = torch.zeros(2, dtype=torch.float32, device=self.arena.device)
+        for p in params:
+            sq[1 if id(p) in tab else 0] += p.grad.float().pow(2).sum()
+        D.allreduce_sum_(sq[1:], self.shards.group)
+        total = sq.sum().sqrt()
+        coef = (max_norm / (total + 1e-6)).clamp(max=1.0)
+        for p in params:
+            p.grad.mul_(coef)
+        return total
 
     # ------------------------------------------------------------------ fused training step
     def train_step(self, inputs, y, opt, global_step, seed=None, contribute=True, contributors=None,
