@@ -291,6 +291,16 @@ int ctr_rmsnorm_bwd_nparts(int M, int N);
 /* RMSNorm backward: dh = w*dy*r - h*r^3/N*sum(w*dy*h) (+ add); dw partials (nparts, N) */
 int ctr_rmsnorm_bwd(const float* dy, long ldy, const float* h, long ldh, const float* r, const float* w, int M, int N,
                     float* dh, long lddh, const float* add, long ld_add, float* dw_part, void* stream);
+/* LayerNorm (norm options other than "rms": src/models/dare.py:15-18 make_norm -> nn.LayerNorm(d), eps 1e-5) over
+ * rows of N <= 16384: y = (x - mean) rstd w + b, mean / rstd saved per row; ybf (nullable) y's bf16 image.
+ * Backward: dx = rstd (g w - mean(g w) - xhat mean(g w xhat)) (+ add); dw / db partial rows (nparts, N) each,
+ * reduced by ctr_colsum.                                                                          (layernorm.hip) */
+int ctr_layernorm_fwd(const float* x, long ldx, int M, int N, const float* w, const float* b, float eps, float* y,
+                      long ldy, float* mean, float* rstd, void* ybf, long ldybf, void* stream);
+int ctr_layernorm_bwd_nparts(int M, int N);
+int ctr_layernorm_bwd(const float* dy, long ldy, const float* x, long ldx, const float* mean, const float* rstd,
+                      const float* w, int M, int N, float* dx, long lddx, const float* add, long ld_add,
+                      float* dw_part, float* db_part, void* stream);
 size_t ctr_colsum_ws_size(int M, int N);
 /* out[n] = sum_m X[m,n] / div  (bias grads; div = B gives torch .mean(dim=0)) */
 int ctr_colsum(const float* X, long ld, int M, int N, float div, float* out, float* ws, void* stream);

@@ -64,6 +64,18 @@ def rmsnorm(x, w, eps=1e-6):
     return w * x * torch.rsqrt(x.pow(2).mean(dim=-1, keepdim=True) + eps)
 
 
+def norm(x, P, name, layer):
+    # src/models/dare.py:15-18 make_norm: "rms" -> RMSNorm (weight `w`), any other name -> nn.LayerNorm(d) (weight,
+    # bias, eps 1e-5)
+    if layer:
+        return F.layer_norm(x, (x.shape[-1],), P[name + ".weight"], P[name + ".bias"], 1e-5)
+    return rmsnorm(x, P[name + ".w"])
+
+
+def norm_params(name, d, layer):
+    return [(name + ".weight", (d,)), (name + ".bias", (d,))] if layer else [(name + ".w", (d,))]
+
+
 def decay_log_table(L: int, tau: float, dtype=torch.float32) -> torch.Tensor:
     # src/models/dare.py:126-130
     pos = torch.arange(L)
@@ -93,7 +105,7 @@ def topk_select(P, seq, q, K, tau, pad_id, dtype):
     return sel, vals, idx
 
 
-def encoder_layer(P, pre, x, H, mha_p, ffn_p, add_pos, top_k, drop, li):
+def encoder_layer(P, pre, x, H, mha_p, ffn_p, add_pos, top_k, drop, li, layer_norm=False):
     # src/models/dare.py:53-70; MHA explicit (need_weights=True) path of
     # torch.nn.functional.multi_head_attention_forward (batch_first)
     B, K, D = x.shape
@@ -112,11 +124,11 @@ def encoder_layer(P, pre, x, H, mha_p, ffn_p, add_pos, top_k, drop, li):
     a = drop(site_attn(li), a, mha_p)
     o = (a @ v).transpose(1, 2).reshape(B, K, D)
     h = o @ P[pre + "mha.out_proj.weight"].t() + P[pre + "mha.out_proj.bias"]
-    x = rmsnorm(x + h, P[pre + "norm1.w"])
+    x = norm(x + h, P, pre + "norm1", layer_norm)
     f = F.gelu(x @ P[pre + "ffn.0.weight"].t() + P[pre + "ffn.0.bias"])
     f = drop(site_ffn(li), f, ffn_p)
     f = f @ P[pre + "ffn.3.weight"].t() + P[pre + "ffn.3.bias"]
-    return rmsnorm(x + f, P[pre + "norm2.w"])
+    return norm(x + f, P, pre + "norm2", layer_norm)
 
 
 class Arch:
@@ -150,6 +162,8 @@ class Arch:
         self.ffn_p = t.get("ffn_dropout", 0.1)
         self.add_pos = t.get("add_positional_bias", True)
         self.gating = t.get("gating", "softmax") if t else "softmax"
+        self.layer_norm = self.tb and str(t.get("norm", "rms")).lower() != "rms"
+        self.qnn_layer_norm = bool(qa["enabled"]) and str(qa.get("norm", "rms")).lower() != "rms"
         self.use_qnn = bool(qa["enabled"])
         if self.use_qnn:
             self.qh, self.qr, self.qP = qa["heads"], qa["rank"], qa["proj_dim"]
@@ -192,10 +206,10 @@ class Arch:
             p = f"dare.layers.{i}."
             out += [(p + "mha.in_proj_weight", (3 * D, D)), (p + "mha.in_proj_bias", (3 * D,)),
                     (p + "mha.out_proj.weight", (D, D)), (p + "mha.out_proj.bias", (D,)),
-                    (p + "norm1.w", (D,)),
+                    *norm_params(p + "norm1", D, self.layer_norm),
                     (p + "ffn.0.weight", (self.ffn_hidden, D)), (p + "ffn.0.bias", (self.ffn_hidden,)),
                     (p + "ffn.3.weight", (D, self.ffn_hidden)), (p + "ffn.3.bias", (D,)),
-                    (p + "norm2.w", (D,))]
+                    *norm_params(p + "norm2", D, self.layer_norm)]
             if self.add_pos:
                 out.append((p + "pbias.rel.weight", (2 * self.top_k + 1, self.H)))
         out += [("dare.aux_head.weight", (1, D)), ("dare.aux_head.bias", (1,))]
@@ -203,7 +217,7 @@ class Arch:
             FD = self.F * D
             C = self.qh * self.qP
             out += [("qnn.U", (self.qh, D, self.qr)), ("qnn.V", (self.qh, self.qr, self.qP)),
-                    ("qnn.pre_norm.w", (FD,))]
+                    *norm_params("qnn.pre_norm", FD, self.qnn_layer_norm)]
             if self.use_se:
                 Cr = C // self.se_r
                 out += [("qnn.se.fc.0.weight", (Cr, C)), ("qnn.se.fc.0.bias", (Cr,)),
@@ -272,7 +286,8 @@ def forward(P, batch, A: Arch, drop: Dropper, dtype=torch.float32, record=None):
     if record is not None:
         record["topk_idx"], record["topk_vals"], record["query"] = idx, vals, query
     for li in range(A.n_layers):                              # src/models/dare.py:142-146
-        x = encoder_layer(P, f"dare.layers.{li}.", x, A.H, A.mha_p, A.ffn_p, A.add_pos, A.top_k, drop, li)
+        x = encoder_layer(P, f"dare.layers.{li}.", x, A.H, A.mha_p, A.ffn_p, A.add_pos, A.top_k, drop, li,
+                          A.layer_norm)
     if A.gating == "relu":                                    # src/models/dare.py:150-155
         w = torch.relu(vals)
         w = w / (w.sum(dim=1, keepdim=True) + 1e-12)
@@ -317,7 +332,7 @@ def _pair_all(P, z, A: Arch):
 def qnn_forward(P, feats, A: Arch, drop):
     # src/models/qnn_alpha.py:109-130
     B, Fq, D = feats.shape
-    z = rmsnorm(feats.reshape(B, Fq * D), P["qnn.pre_norm.w"]).reshape(B, Fq, D)
+    z = norm(feats.reshape(B, Fq * D), P, "qnn.pre_norm", A.qnn_layer_norm).reshape(B, Fq, D)
     blocks = [(s, e) for s, e in A.qnn_blocks() if e - s > 1] if A.pair_grouping == "block" else []
     if blocks:   # :99-108: the interaction within each block of more than one feature, summed over the blocks
         inter = torch.stack([_pair_all(P, z[:, s:e, :], A) for s, e in blocks], dim=0).sum(dim=0)

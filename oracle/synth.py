@@ -26,8 +26,10 @@ def make_params(shapes, seed: int, pad_id: int = 0):
             a = r.standard_normal(shp)
             if ("emb_att" in k or "emb_rep" in k):
                 a[pad_id] = 0.0
-        elif k.endswith("norm1.w") or k.endswith("norm2.w") or k.endswith("pre_norm.w"):
+        elif k.endswith(("norm1.w", "norm2.w", "pre_norm.w", "norm1.weight", "norm2.weight", "pre_norm.weight")):
             a = 1.0 + 0.1 * r.standard_normal(shp)
+        elif k.endswith(("norm1.bias", "norm2.bias", "pre_norm.bias")):       # LayerNorm bias
+            a = 0.1 * r.standard_normal(shp)
         elif k in ("qnn.U", "qnn.V"):
             a = 0.2 * r.standard_normal(shp)
         elif k in ("num_embed.weight", "mask_embed.weight"):
@@ -97,16 +99,25 @@ def reference_init(A, seed: int):
         out[p + "mha.in_proj_weight"] = w
         out[p + "mha.in_proj_bias"] = torch.zeros(3 * D)
         out[p + "mha.out_proj.bias"].zero_()
-        out[p + "norm1.w"] = torch.ones(D)
+        if A.layer_norm:
+            out[p + "norm1.weight"], out[p + "norm1.bias"] = torch.ones(D), torch.zeros(D)
+        else:
+            out[p + "norm1.w"] = torch.ones(D)
         linear(p + "ffn.0", A.ffn_hidden, D)
         linear(p + "ffn.3", D, A.ffn_hidden)
-        out[p + "norm2.w"] = torch.ones(D)
+        if A.layer_norm:
+            out[p + "norm2.weight"], out[p + "norm2.bias"] = torch.ones(D), torch.zeros(D)
+        else:
+            out[p + "norm2.w"] = torch.ones(D)
         if A.add_pos:
             embedding(p + "pbias.rel.weight", 2 * A.top_k + 1, A.H)
     linear("dare.aux_head", 1, D)
     if A.use_qnn:
         FD, C = A.F * D, A.qh * A.qP
-        out["qnn.pre_norm.w"] = torch.ones(FD)
+        if A.qnn_layer_norm:
+            out["qnn.pre_norm.weight"], out["qnn.pre_norm.bias"] = torch.ones(FD), torch.zeros(FD)
+        else:
+            out["qnn.pre_norm.w"] = torch.ones(FD)
         out["qnn.U"] = torch.randn(A.qh, D, A.qr) * 0.02
         out["qnn.V"] = torch.randn(A.qh, A.qr, A.qP) * 0.02
         if A.use_se:

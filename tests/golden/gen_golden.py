@@ -352,16 +352,16 @@ def run_case(name, cfg, B, L, vocab, Fn, Fm, cat_cards, steps, pseed, bseed, sto
 
 
 def tiny_cfg(query_mode="concat", gating="softmax", emb_drop=0.0, aux_w=0.1, qnn=True, tb=True,
-             D=16, K=16, H=4, layers=2, ema=True, ffn_hidden=48, pair_grouping="all"):
+             D=16, K=16, H=4, layers=2, ema=True, ffn_hidden=48, pair_grouping="all", norm="rms", qnn_norm="rms"):
     dims = {"c0": 8, "c1": 12, "c2": 16, "c3": 4, "c4": 20}
     cfg = {
         "model": {"emb_dim": D, "embedding_dropout": emb_drop, "cat_embedding_dims": dims, "dare_dropout": 0.2,
                   "qnn_alpha": {"enabled": qnn, "feature_embed_dim": 8, "heads": 2, "rank": 4, "proj_dim": 16,
                                 "mlp_hidden": [32, 16], "dropout": 0.2, "use_se": True, "se_reduction": 4,
-                                "use_residual": True, "norm": "rms", "pair_grouping": pair_grouping,
+                                "use_residual": True, "norm": qnn_norm, "pair_grouping": pair_grouping,
                                 "aux_head_weight": aux_w}},
         "sequence": {"tfm": {"n_layers": layers, "n_heads": H, "mha_dropout": 0.1, "ffn_hidden": ffn_hidden,
-                             "ffn_dropout": 0.1, "norm": "rms", "gating": gating, "add_positional_bias": True},
+                             "ffn_dropout": 0.1, "norm": norm, "gating": gating, "add_positional_bias": True},
                      "query_mode": query_mode, "transformer_block": tb, "top_k": K, "recency_tau": 16,
                      "pad_id": 0, "query_key": "c1"},
     }
@@ -547,11 +547,15 @@ def main():
 def gen_r5():
     """Round 5: QNN pair_grouping 'block' (src/models/qnn_alpha.py:99-108, block slices src/models/wrapper.py:66-75):
     [u | 6 numeric | 1 mask | 5 categorical] features -- u and the single mask feature fall in one-feature blocks,
-    which the block form leaves out of every interaction."""
+    which the block form leaves out of every interaction; and LayerNorm norms (tiny_ln)."""
     tr = dict(lr=3e-3, wd=1e-4, clip=0.5, steps_per_epoch=4, warmup_epochs=1, epochs=3)
     cards = {"c0": 300, "c1": 500, "c2": 1000, "c3": 200, "c4": 700}
     run_case("tiny_block", tiny_cfg(pair_grouping="block"), B=48, L=24, vocab=4000, Fn=6, Fm=1, cat_cards=cards,
              steps=3, pseed=15, bseed=500, store_params=True, train_cfg=tr)
+    # LayerNorm (src/models/dare.py:15-18: any norm name but "rms" is nn.LayerNorm) in the encoder layers and the
+    # QNN pre-norm
+    run_case("tiny_ln", tiny_cfg(norm="layer", qnn_norm="layer"), B=40, L=24, vocab=4000, Fn=6, Fm=3,
+             cat_cards=cards, steps=3, pseed=16, bseed=520, store_params=True, train_cfg=tr)
 
 
 def gen_r3(only_cfg4=False):

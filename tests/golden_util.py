@@ -12,7 +12,7 @@ from oracle.model import make_arch
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["tiny_concat", "tiny_s1_relu", "tiny_s2", "base_fc", "cfg2_dims", "cfg3_dims", "k148", "k120", "cfg4_full",
-         "tiny_ffn40", "cfg2_ref", "tiny_block"]
+         "tiny_ffn40", "cfg2_ref", "tiny_block", "tiny_ln"]
 # amp: bf16 twins (gen_golden.gen_bf16): the reference under torch.autocast(bfloat16) on the inputs,
 # seeds and parameters of the fp32 fixture named in meta["twin"]
 BF16_CASES = ["tiny_concat_bf16", "cfg2_dims_bf16", "cfg3_dims_bf16", "k148_bf16", "cfg4_full_bf16", "cfg2_ref_bf16"]

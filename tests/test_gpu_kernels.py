@@ -1101,6 +1101,42 @@ def test_rowgemm_wgrad_vs_torch(NO, NIN, M):
     assert float(out[NO * NIN:o_db].abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("M,N", [(1000, 16), (77, 32), (300, 64), (50, 100), (40, 300), (33, 2000), (64, 6400),
+                                  (9, 12800), (5000, 64)])
+def test_layernorm_vs_torch(M, N):
+    """layernorm.hip (norm != "rms": nn.LayerNorm, eps 1e-5): y, the saved mean / rstd, y's bf16 image, and the
+    backward's dx (+ add) and dw / db partial rows against torch fp64, for every row-width form."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(M * 13 + N)
+    x = torch.randn(M, N, device="cuda", generator=g) * 2 + 0.5
+    w = 1 + 0.2 * torch.randn(N, device="cuda", generator=g)
+    b = 0.1 * torch.randn(N, device="cuda", generator=g)
+    y = torch.full((M, N), float("nan"), device="cuda")
+    mu, rs = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+    ybf = torch.empty(M, N + 8, device="cuda", dtype=torch.bfloat16)
+    L.call("ctr_layernorm_fwd", ptr(x), N, M, N, ptr(w), ptr(b), 1e-5, ptr(y), N, ptr(mu), ptr(rs), ptr(ybf), N + 8,
+           stream())
+    xd = x.double().requires_grad_(True)
+    wd, bd = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(xd, (N,), wd, bd, 1e-5)
+    assert rel(y.double(), ref.detach()) < 1e-6
+    assert rel(mu.double(), x.double().mean(-1)) < 1e-6
+    assert rel(rs.double(), torch.rsqrt(x.double().var(-1, unbiased=False) + 1e-5)) < 1e-6
+    assert torch.equal(ybf[:, :N], y.to(torch.bfloat16))
+    dy = torch.randn(M, N, device="cuda", generator=g)
+    add = torch.randn(M, N, device="cuda", generator=g)
+    ref.backward(dy.double())
+    nparts = L.query("ctr_layernorm_bwd_nparts", M, N)
+    dwp = torch.full((nparts, N), float("nan"), device="cuda")
+    dbp = torch.full((nparts, N), float("nan"), device="cuda")
+    dx = torch.full((M, N), float("nan"), device="cuda")
+    L.call("ctr_layernorm_bwd", ptr(dy), N, ptr(x), N, ptr(mu), ptr(rs), ptr(w), M, N, ptr(dx), N, ptr(add), N,
+           ptr(dwp), ptr(dbp), stream())
+    assert rel(dx.double(), xd.grad + add.double()) < 1e-5
+    assert rel(dwp.double().sum(0), wd.grad) < 1e-5
+    assert rel(dbp.double().sum(0), bd.grad) < 1e-5
+
+
 @pytest.mark.parametrize("nparts,n,H", [(8192, 297, 8), (4096, 201, 4), (13, 65, 2), (1, 3, 4), (0, 9, 4)])
 def test_pos_bias_grad_vs_torch(nparts, n, H):
     """ctr_pos_bias_grad: drel[d, h] = sum_p part[p, d] / H for every head (the head-mean bias's grad), the

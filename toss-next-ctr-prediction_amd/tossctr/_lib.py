@@ -110,6 +110,9 @@ SIGS = {
     "ctr_rmsnorm_fwd_bf": (i, [p, l, i, i, p, f, p, l, p, p, l, p]),
     "ctr_rmsnorm_bwd_nparts": (i, [i, i]),
     "ctr_rmsnorm_bwd": (i, [p, l, p, l, p, p, i, i, p, l, p, l, p, p]),
+    "ctr_layernorm_fwd": (i, [p, l, i, i, p, p, f, p, l, p, p, p, l, p]),
+    "ctr_layernorm_bwd_nparts": (i, [i, i]),
+    "ctr_layernorm_bwd": (i, [p, l, p, l, p, p, p, i, i, p, l, p, l, p, p, p]),
     "ctr_colsum_ws_size": (z, [i, i]),
     "ctr_colsum": (i, [p, l, i, i, f, p, p, p]),
     "ctr_colsum_multi_ok": (i, [C.POINTER(ColsumSeg)]),

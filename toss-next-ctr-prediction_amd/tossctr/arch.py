@@ -127,10 +127,6 @@ class Arch:
             raise ValueError(f"unknown query_mode {self.query_mode}")
         if self.query_mode != "S2" and self.query_key not in self.cat_cols:
             raise ValueError(f"query_key {self.query_key} not in cat columns")
-        if self.tb and self.norm.lower() != "rms":
-            raise NotImplementedError("only norm: rms encoder layers are implemented (all reference configs use rms)")
-        if self.use_qnn and self.qnn_norm.lower() != "rms":
-            raise NotImplementedError("only QNN norm: rms is implemented (all reference configs use rms)")
         if self.use_qnn and self.pair_grouping not in ("all", "block"):
             raise ValueError(f"unknown pair_grouping {self.pair_grouping!r}")
         if self.amp not in ("none", "bf16"):
@@ -144,6 +140,15 @@ class Arch:
         for d in self.cat_dims:
             if d < 4 or d > 64:
                 raise NotImplementedError("cat_embedding_dims must be in [4, 64]")
+
+    @property
+    def layer_norm(self):
+        """src/models/dare.py:15-18 make_norm: any norm name but "rms" is nn.LayerNorm (weight + bias, eps 1e-5)."""
+        return bool(self.tb) and self.norm.lower() != "rms"
+
+    @property
+    def qnn_layer_norm(self):
+        return bool(self.use_qnn) and self.qnn_norm.lower() != "rms"
 
     def param_shapes(self):
         """(state_dict key, shape, kind) in reference order; kind: 'dense' or 'table'."""
@@ -164,17 +169,17 @@ class Arch:
             p = f"dare.layers.{i}."
             out += [(p + "mha.in_proj_weight", (3 * D, D)), (p + "mha.in_proj_bias", (3 * D,)),
                     (p + "mha.out_proj.weight", (D, D)), (p + "mha.out_proj.bias", (D,)),
-                    (p + "norm1.w", (D,)),
+                    *self._norm_params(p + "norm1", D, self.layer_norm),
                     (p + "ffn.0.weight", (self.ffn_hidden, D)), (p + "ffn.0.bias", (self.ffn_hidden,)),
                     (p + "ffn.3.weight", (D, self.ffn_hidden)), (p + "ffn.3.bias", (D,)),
-                    (p + "norm2.w", (D,))]
+                    *self._norm_params(p + "norm2", D, self.layer_norm)]
             if self.add_pos:
                 out.append((p + "pbias.rel.weight", (2 * self.top_k + 1, self.H)))
         out += [("dare.aux_head.weight", (1, D)), ("dare.aux_head.bias", (1,))]
         if self.use_qnn:
             FD, C = self.F * D, self.C
             out += [("qnn.U", (self.qh, D, self.qr)), ("qnn.V", (self.qh, self.qr, self.qP)),
-                    ("qnn.pre_norm.w", (FD,))]
+                    *self._norm_params("qnn.pre_norm", FD, self.qnn_layer_norm)]
             if self.use_se:
                 Cr = C // self.se_r
                 out += [("qnn.se.fc.0.weight", (Cr, C)), ("qnn.se.fc.0.bias", (Cr,)),
@@ -190,6 +195,11 @@ class Arch:
             out += [("fc.0.weight", (512, nin)), ("fc.0.bias", (512,)), ("fc.3.weight", (1, 512)),
                     ("fc.3.bias", (1,))]
         return [(k, s, "table" if k.startswith("cat_embs.") or ".emb_" in k else "dense") for k, s in out]
+
+    @staticmethod
+    def _norm_params(name, d, layer):
+        """RMSNorm: `w` (src/models/dare.py:10); nn.LayerNorm: `weight`, `bias`."""
+        return [(name + ".weight", (d,)), (name + ".bias", (d,))] if layer else [(name + ".w", (d,))]
 
     def no_grad_keys(self):
         """Params whose .grad stays None in the reference step (AdamW skips them; EMA still tracks them)."""

@@ -181,8 +181,11 @@ class Engine:
                                all(bool(_lib.query("ctr_rowgemm_bf_supported", k, n))
                                    for k, n in ((a.D, 3 * a.D), (a.D, a.D), (3 * a.D, a.D))))
         self.rowgemm = self.rowgemm or self.rowgemm_bf
-        self.ffn_fused = a.n_layers > 0 and bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden, 0)) and \
-            self._ffn_contiguous()
+        # LayerNorm encoder layers (norm != "rms", layernorm.hip) take the unfused forms: the fused kernels carry
+        # RMSNorm in their epilogues
+        self.ln = a.layer_norm
+        self.ffn_fused = a.n_layers > 0 and not self.ln and \
+            bool(_lib.query("ctr_ffn_supported", a.D, a.ffn_hidden, 0)) and self._ffn_contiguous()
         # amp: bf16 -> the fused FFN's bf16-MFMA kernels where their shape constraints hold (D in {32, 64},
         # FF % 32 == 0); other shapes keep the fp32 kernels (more precise than the reference's bf16)
         self.ffn_flags = 1 if (self.bf16 and self.ffn_fused and
@@ -192,7 +195,7 @@ class Engine:
         self.attn_bf = bool(self.bf16 and a.n_layers > 0 and _lib.query("ctr_attn_bf_ok", a.top_k, a.H, a.D))
         # ... and the layer's in_proj -> attention -> out_proj + residual + RMSNorm in one launch where it fits
         # (attn_mf.hip: K <= 64, D = 32; the same bits as the three launches)
-        self.attn_layer = bool(self.attn_bf and self.rowgemm and
+        self.attn_layer = bool(self.attn_bf and self.rowgemm and not self.ln and
                                _lib.query("ctr_attn_layer_fwd_ok", a.top_k, a.H, a.D))
         # ... and in the backward the out-projection's input grad dO = dh1 W_out inside the attention backward
         # (ctr_attn_bwd_bf_oproj: same bits, dO never written)
@@ -366,6 +369,22 @@ class Engine:
         """Split-K factor for weight-gradient GEMMs (tiny M x N, huge K = rows), splits >= 64 rows deep."""
         return Engine._split_factor(M, N, K, 64)
 
+    def _ln_fwd(self, h, M, N, name, y, mu, rs, ybf=None, ldybf=0):
+        """y = LayerNorm(h) with weight / bias ``name``.weight / .bias (nn.LayerNorm, eps 1e-5); the row mean and
+        rstd saved for the backward; ybf: y's bf16 image too (row stride ldybf)."""
+        call("ctr_layernorm_fwd", ptr(h), N, M, N, ptr(self.P[name + ".weight"]), ptr(self.P[name + ".bias"]), 1e-5,
+             ptr(y), N, ptr(mu), ptr(rs), ptr(ybf) if ybf is not None else None, ldybf, self.s())
+
+    def _ln_bwd(self, W, dy, h, mu, rs, M, N, name, dh):
+        """LayerNorm backward: dh, and the weight / bias grads of ``name`` through per-block partial rows."""
+        npart = _lib.query("ctr_layernorm_bwd_nparts", M, N)
+        dwp = W.get(f"ln_dw_part{N}", (npart, N))
+        dbp = W.get(f"ln_db_part{N}", (npart, N))
+        call("ctr_layernorm_bwd", ptr(dy), N, ptr(h), N, ptr(mu), ptr(rs), ptr(self.P[name + ".weight"]), M, N,
+             ptr(dh), N, None, 0, ptr(dwp), ptr(dbp), self.s())
+        self.colsum(ptr(dwp), N, npart, N, ptr(self.G[name + ".weight"]))
+        self.colsum(ptr(dbp), N, npart, N, ptr(self.G[name + ".bias"]))
+
     def rowgemm_call(self, M, K, N, A, W, tb, C, bias=None, add=None, resid=None, norm_w=None, norm_h=None,
                      norm_r=None):
         """C (M, N) = A (M, K) W^T (tb) or A W, + bias / + add / residual + RMSNorm (rowgemm.hip; amp at
@@ -502,7 +521,15 @@ class Engine:
                               GemmEpi(bias=ptr(P[pre + "mha.in_proj_bias"])))
                 call("ctr_attn_fwd_bf" if self.attn_bf else "ctr_attn_fwd", ptr(qkv), B, K, a.H, D, ptr(relmean),
                      a.top_k, scale, *da, ptr(amask), ptr(o), ptr(mrow), ptr(lrow), st)
-                if self.rowgemm:
+                if self.ln:     # h1 = x + out_proj(o), then x1 = LayerNorm(h1)
+                    if self.rowgemm:
+                        self.rowgemm_call(M, D, D, ptr(o), ptr(P[pre + "mha.out_proj.weight"]), 1, ptr(h1),
+                                          bias=ptr(P[pre + "mha.out_proj.bias"]), add=ptr(x))
+                    else:
+                        self.gemm(M, D, D, ptr(o), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 1, ptr(h1), D,
+                                  GemmEpi(bias=ptr(P[pre + "mha.out_proj.bias"]), add=ptr(x), ld_add=D))
+                    self._ln_fwd(h1, M, D, pre + "norm1", x1, W.get(f"mu1_{li}", (M,)), r1)
+                elif self.rowgemm:
                     self.rowgemm_call(M, D, D, ptr(o), ptr(P[pre + "mha.out_proj.weight"]), 1, ptr(x1),
                                       bias=ptr(P[pre + "mha.out_proj.bias"]), resid=ptr(x),
                                       norm_w=ptr(P[pre + "norm1.w"]), norm_h=ptr(h1), norm_r=ptr(r1))
@@ -531,9 +558,14 @@ class Engine:
                 self.gemm(M, FF, D, ptr(x1), D, 0, ptr(P[pre + "ffn.0.weight"]), D, 1, ptr(fo), FF,
                           GemmEpi(bias=ptr(P[pre + "ffn.0.bias"]), act=2, pre=ptr(act), drop_key=dfk[0],
                                   drop_thresh=dfk[1], drop_scale=dfk[2]))
-                self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(x2), D,
-                          GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
-                                  norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
+                if self.ln:     # h2 = x1 + ffn(x1), then x2 = LayerNorm(h2)
+                    self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(h2), D,
+                              GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), add=ptr(x1), ld_add=D))
+                    self._ln_fwd(h2, M, D, pre + "norm2", x2, W.get(f"mu2_{li}", (M,)), r2)
+                else:
+                    self.gemm(M, D, FF, ptr(fo), FF, 0, ptr(P[pre + "ffn.3.weight"]), FF, 1, ptr(x2), D,
+                              GemmEpi(bias=ptr(P[pre + "ffn.3.bias"]), resid=ptr(x1), ld_resid=D,
+                                      norm_w=ptr(P[pre + "norm2.w"]), norm_h=ptr(h2), norm_r=ptr(r2), norm_eps=1e-6))
             Ls.update(qkv=qkv, relmean=relmean, o=o, mrow=mrow, lrow=lrow, amask=amask, h1=h1, r1=r1, x1=x1,
                       act=act, fo=fo, fmask=fmask, fwbf=fwbf if self.ffn_fused else None,
                       h2=h2, r2=r2)
@@ -597,7 +629,9 @@ class Engine:
         # amp: the MLP's first GEMM runs on a bf16 image of [z | inter], written by z's and inter's producers
         zi_bf = W.get("zi_bf", (B, din), torch.bfloat16) if (self.bf_ok(B, H0, din, din, 0, din, 1) and
                                                               FD % 8 == 0 and FD % 4 == 0) else None
-        if zi_bf is not None:
+        if a.qnn_layer_norm:
+            self._ln_fwd(xF, B, FD, "qnn.pre_norm", z, W.get("muq", (B,)), rq, ybf=zi_bf, ldybf=din)
+        elif zi_bf is not None:
             call("ctr_rmsnorm_fwd_bf", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq),
                  ptr(zi_bf), din, st)
         else:
@@ -860,11 +894,14 @@ class Engine:
             slab_sum = None
             # x2 = norm2(x1 + ffn(x1))
             dh2 = W.get("dh2", (M, D))
-            npart = _lib.query("ctr_rmsnorm_bwd_nparts", M, D)
-            dwp = W.get("dw_part", (npart, D))
-            call("ctr_rmsnorm_bwd", ptr(dx2), D, ptr(Ls["h2"]), D, ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]), M, D,
-                 ptr(dh2), D, None, 0, ptr(dwp), st)
-            self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm2.w"]))
+            if self.ln:
+                self._ln_bwd(W, dx2, Ls["h2"], W.get(f"mu2_{li}", (M,)), Ls["r2"], M, D, pre + "norm2", dh2)
+            else:
+                npart = _lib.query("ctr_rmsnorm_bwd_nparts", M, D)
+                dwp = W.get("dw_part", (npart, D))
+                call("ctr_rmsnorm_bwd", ptr(dx2), D, ptr(Ls["h2"]), D, ptr(Ls["r2"]), ptr(P[pre + "norm2.w"]), M, D,
+                     ptr(dh2), D, None, 0, ptr(dwp), st)
+                self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm2.w"]))
             dx1 = W.get("dx1", (M, D))
             # ffn.3: f @ W2^T + b2
             self.wgrad(ptr(dh2), D, ptr(Ls["fo"]), FF, M, D, FF, ptr(G[pre + "ffn.3.weight"]),
@@ -880,9 +917,12 @@ class Engine:
             # x1 = norm1(x + attn(x)); per layer: the side stream's out_proj weight grad reads it while the
             # next layer's backward runs on the main stream
             dh1 = W.get(f"dh1_{li}", (M, D))
-            call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,
-                 ptr(dh1), D, None, 0, ptr(dwp), st)
-            self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
+            if self.ln:
+                self._ln_bwd(W, dx1, Ls["h1"], W.get(f"mu1_{li}", (M,)), Ls["r1"], M, D, pre + "norm1", dh1)
+            else:
+                call("ctr_rmsnorm_bwd", ptr(dx1), D, ptr(Ls["h1"]), D, ptr(Ls["r1"]), ptr(P[pre + "norm1.w"]), M, D,
+                     ptr(dh1), D, None, 0, ptr(dwp), st)
+                self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
         # out_proj
         do = W.get("do", (M, D))
         if self.attn_oproj:              # dO is formed inside the attention backward below
@@ -1044,6 +1084,9 @@ class Engine:
             call("ctr_qnn_du_combine", ptr(T1), ptr(T), ptr(q["ucat"]), D, QR, ptr(ducat), self.s())
             call("ctr_qnn_ucat", ptr(ducat), a.qh, D, a.qr, ptr(G["qnn.U"]), 1, self.s())
         # pre-norm
+        if a.qnn_layer_norm:
+            self._ln_bwd(W, dz, sv["xF"], W.get("muq", (B,)), q["rq"], B, FD, "qnn.pre_norm", dxF)
+            return
         npart = _lib.query("ctr_rmsnorm_bwd_nparts", B, FD)
         dwp = W.get("dwq_part", (npart, FD))
         call("ctr_rmsnorm_bwd", ptr(dz), FD, ptr(sv["xF"]), FD, ptr(q["rq"]), ptr(P["qnn.pre_norm.w"]), B, FD,

@@ -170,7 +170,8 @@ class CTRModel(nn.Module):
     @torch.no_grad()
     def reset_parameters(self, generator=None):
         """Reference default init: nn.Embedding N(0,1) (pad row 0), nn.Linear kaiming-uniform /
-        U(+-1/sqrt(fan_in)) biases, RMSNorm w = 1, feature slopes N(0, 0.02^2), U/V N(0, 0.02^2)."""
+        U(+-1/sqrt(fan_in)) biases, RMSNorm w = 1 (LayerNorm weight 1, bias 0), feature slopes N(0, 0.02^2),
+        U/V N(0, 0.02^2)."""
         a = self.arch
         g = generator
         gt = g     # row-sharded tables: every rank draws its own rows (dense params stay identical)
@@ -180,8 +181,10 @@ class CTRModel(nn.Module):
                 (base * 1000003 + 7919 * (self.shards.rank + 1)) % (1 << 63))
         for k in self.arena.order:
             t = self.arena.views[k]
-            if k.endswith(".w"):
-                t.fill_(1.0)
+            if k.endswith(".w") or k.endswith(("norm1.weight", "norm2.weight", "pre_norm.weight")):
+                t.fill_(1.0)          # RMSNorm w / nn.LayerNorm weight
+            elif k.endswith(("norm1.bias", "norm2.bias", "pre_norm.bias")):
+                t.zero_()
             elif ".emb_" in k or k.startswith("cat_embs."):
                 t.normal_(0.0, 1.0, generator=gt)
                 if ".emb_" in k:
