@@ -44,7 +44,7 @@ def main():
     ap.add_argument("--H", type=int, default=8)
     ap.add_argument("--p", type=float, default=0.1, help="dropout probability (0: no dropout)")
     ap.add_argument("--nobias", action="store_true", help="attn: no positional bias")
-    ap.add_argument("--bf16", action="store_true", help="ffn: the amp bf16 kernels (CTR_FFN_BF16)")
+    ap.add_argument("--bf16", action="store_true", help="ffn: the amp bf16 kernels (CTR_FFN_BF16); rowgemm: rowgemm_bf")
     ap.add_argument("--norms", action="store_true", help="ffn: the norm-fused backward (ctr_ffn_bwd_norms, as the step)")
     ap.add_argument("--shapes", default="", help="gemm: comma-separated indices of the shape list")
     ap.add_argument("--variant", type=int, default=0, help="gemmig: ctr_gemm_bf16_set_variant")
@@ -89,6 +89,7 @@ def main():
         print(f"ffn_fwd M={M} D={D} FF={FF}: {tf * 1e3:.1f} us  {4.0 * M * FF * D / tf / 1e9:.1f} TF/s")
         print(f"ffn_bwd M={M} D={D} FF={FF}: {tb * 1e3:.1f} us  {8.0 * M * FF * D / tb / 1e9:.1f} TF/s")
     if "rowgemm" in which:
+        rg = "ctr_rowgemm_bf" if args.bf16 else "ctr_rowgemm"     # --bf16: the amp D = 64 row kernels
         x = torch.randn(M, D, device="cuda")
         Win, bin_ = torch.randn(3 * D, D, device="cuda"), torch.randn(3 * D, device="cuda")
         Wout, bout = torch.randn(D, D, device="cuda"), torch.randn(D, device="cuda")
@@ -97,26 +98,26 @@ def main():
         dh1, do, dq, dx = (torch.randn(M, D, device="cuda"), torch.empty(M, D, device="cuda"),
                            torch.randn(M, 3 * D, device="cuda"), torch.empty(M, D, device="cuda"))
         cases = {
-            "qkv": lambda: call("ctr_rowgemm", M, D, 3 * D, ptr(x), D, ptr(Win), 1, ptr(qkv), 3 * D, ptr(bin_), None, 0,
+            "qkv": lambda: call(rg, M, D, 3 * D, ptr(x), D, ptr(Win), 1, ptr(qkv), 3 * D, ptr(bin_), None, 0,
                                 None, 0, None, None, None, 0.0, st),
-            "out+norm": lambda: call("ctr_rowgemm", M, D, D, ptr(o), D, ptr(Wout), 1, ptr(x1), D, ptr(bout), None, 0,
+            "out+norm": lambda: call(rg, M, D, D, ptr(o), D, ptr(Wout), 1, ptr(x1), D, ptr(bout), None, 0,
                                      ptr(x), D, ptr(nw), ptr(h1), ptr(r1), 1e-6, st),
-            "do": lambda: call("ctr_rowgemm", M, D, D, ptr(dh1), D, ptr(Wout), 0, ptr(do), D, None, None, 0, None, 0,
+            "do": lambda: call(rg, M, D, D, ptr(dh1), D, ptr(Wout), 0, ptr(do), D, None, None, 0, None, 0,
                                None, None, None, 0.0, st),
-            "dx": lambda: call("ctr_rowgemm", M, 3 * D, D, ptr(dq), 3 * D, ptr(Win), 0, ptr(dx), D, None, ptr(dh1), D,
+            "dx": lambda: call(rg, M, 3 * D, D, ptr(dq), 3 * D, ptr(Win), 0, ptr(dx), D, None, ptr(dh1), D,
                                None, 0, None, None, None, 0.0, st),
         }
         mb = {"qkv": 4 * M * 4 * D, "out+norm": 4 * M * (5 * D + 1), "do": 8 * M * D, "dx": 4 * M * 5 * D}
         for n, fn in cases.items():
             t = timeit(fn, args.iters)
-            print(f"rowgemm {n} M={M} D={D}: {t * 1e3:.1f} us  {mb[n] / t / 1e6:.0f} GB/s")
+            print(f"{rg} {n} M={M} D={D}: {t * 1e3:.1f} us  {mb[n] / t / 1e6:.0f} GB/s")
         for no, ni, dy, xx in ((3 * D, D, dq, x), (D, D, dh1, o)):
-            rows = _lib.query("ctr_rowgemm_wgrad_rows", M)
+            rows = _lib.query(rg + "_wgrad_rows", M)
             ld = (no * ni + 64 + no + 3) // 4 * 4
             slab = torch.zeros(rows, ld, device="cuda")
-            fn = lambda: call("ctr_rowgemm_wgrad", ptr(dy), no, ptr(xx), ni, M, no, ni, ptr(slab), ld, no * ni + 64, st)
+            fn = lambda: call(rg + "_wgrad", ptr(dy), no, ptr(xx), ni, M, no, ni, ptr(slab), ld, no * ni + 64, st)
             t = timeit(fn, args.iters)
-            print(f"rowgemm_wgrad {no}x{ni} M={M}: {t * 1e3:.1f} us  {4 * M * (no + ni) / t / 1e6:.0f} GB/s")
+            print(f"{rg}_wgrad {no}x{ni} M={M}: {t * 1e3:.1f} us  {4 * M * (no + ni) / t / 1e6:.0f} GB/s")
     if "gemm" in which:        # the QNN MLP's big GEMMs at each split-K factor
         shapes = [(4096, 512, 6400, 0, 1), (4096, 512, 7552, 0, 1), (512, 7552, 4096, 1, 0), (4096, 7552, 512, 0, 0), (512, 6400, 4096, 1, 0), (4096, 6400, 512, 0, 0),
                   (4096, 1152, 512, 0, 0), (4096, 512, 1152, 0, 1), (512, 1152, 4096, 1, 0),
