@@ -291,7 +291,7 @@ def opt_algorithmic_bytes(opt, with_ema):
     return b
 
 
-PMC_ROUNDS = ("r04", "r03", "r02", "r01")      # newest committed PMC summaries first
+PMC_ROUNDS = ("r05", "r04", "r03", "r02", "r01")      # newest committed PMC summaries first
 
 
 def pmc_traffic(name):
@@ -301,7 +301,7 @@ def pmc_traffic(name):
     x2).  None when the summaries are absent."""
     import csv
     bwd = ("ffn_bwd_own_kernel", "ffn_bwd_bf_kernel", "ffn_bwd_cols_kernel", "ffn_bwd_kernel")   # preferred first
-    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bfp_kernel", "ffn_fwd_bf_kernel", "ffn_fwd_kernel"),
+    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bfw_kernel", "ffn_fwd_bfp_kernel", "ffn_fwd_bf_kernel", "ffn_fwd_kernel"),
              "ctr_attn_bwd": ("attn_bwd_wave_kernel", "attn_bwd_kernel"),
              "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel"),
              "ctr_attn_bwd_bf": ("attn_bwd_mf_kernel",), "ctr_attn_fwd_bf": ("attn_fwd_mf_kernel",),
