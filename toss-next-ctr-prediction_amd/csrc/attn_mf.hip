@@ -722,33 +722,46 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
   };
   uint32_t kwn[3] = {0u, 0u, 0u};
   if (DROP) fetch_kw(0, kwn);
-  stage<DH, NT, true>(a, b, hgrp, sq, sk, sv, sdo);
-  if (BIAS) stage_rel<NT>(a, srel);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   const int h = hgrp * G + w, hs = w * S::HS;
+  const long hr = ((long)b * a.H + h) * K;
+  // the row statistics' operands (dO, o, the forward's row max / sum of the lane's rows) loaded before the
+  // staging, all of them at once: their round trips overlap the staging's instead of following it one row at a time
+  constexpr int NR = (KT + 63) / 64;
+  f32x4 rdo[NR][DH / 4], ro[NR][DH / 4];
+  float rm[NR], rl[NR];
+#pragma unroll
+  for (int u = 0; u < NR; ++u) {
+    const int row = min(lane + 64 * u, K - 1);     // clamped (rows past K are zeroed below)
+    const float* dp = a.dO + ((long)b * K + row) * D + h * DH;
+    const float* op = a.o + ((long)b * K + row) * D + h * DH;
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) {
+      rdo[u][q] = *(const f32x4*)(dp + 4 * q);
+      ro[u][q] = *(const f32x4*)(op + 4 * q);
+    }
+    rm[u] = a.mrow[hr + row];
+    rl[u] = a.lrow[hr + row];
+  }
+  stage<DH, NT, true>(a, b, hgrp, sq, sk, sv, sdo);
+  if (BIAS) stage_rel<NT>(a, srel);
   __bf16* ids0 = simg + w * 4 * 256;
   const float* rb = srel + KT + a.tk + 4 * g - c;
-  const long hr = ((long)b * a.H + h) * K;
   f32x4* stw = (f32x4*)(srel + rel_floats<NT>(BIAS ? a.tk : 0)) + w * KT;
   float* sdg = (float*)(stw + (4 - w) * KT) + w * (256 + NDGP);   // per wave: [16][16] scratch, NDG diagonal sums
   float* dsum = sdg + 256;
-  for (int row = lane; row < KT; row += 64) {
-    f32x4 st = {0.f, 0.f, 0.f, 0.f};
-    if (row < K) {
-      const float* dp = a.dO + ((long)b * K + row) * D + h * DH;
-      const float* op = a.o + ((long)b * K + row) * D + h * DH;
-      float s = 0.f;
 #pragma unroll
-      for (int q = 0; q < DH / 4; ++q) {
-        const f32x4 x = *(const f32x4*)(dp + 4 * q), y = *(const f32x4*)(op + 4 * q);
-        s = fmaf(x[0], y[0], s);
-        s = fmaf(x[1], y[1], s);
-        s = fmaf(x[2], y[2], s);
-        s = fmaf(x[3], y[3], s);
-      }
-      st = f32x4{a.mrow[hr + row], 1.0f / a.lrow[hr + row], s, 0.f};
+  for (int u = 0; u < NR; ++u) {
+    const int row = lane + 64 * u;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < DH / 4; ++q) {
+      s = fmaf(rdo[u][q][0], ro[u][q][0], s);
+      s = fmaf(rdo[u][q][1], ro[u][q][1], s);
+      s = fmaf(rdo[u][q][2], ro[u][q][2], s);
+      s = fmaf(rdo[u][q][3], ro[u][q][3], s);
     }
-    stw[row] = st;
+    if (row < KT) stw[row] = row < K ? f32x4{rm[u], 1.0f / rl[u], s, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if (BIAS)
     for (int e = lane; e < NDGP; e += 64) dsum[e] = 0.f;
