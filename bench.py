@@ -301,7 +301,7 @@ def pmc_traffic(name):
     x2).  None when the summaries are absent."""
     import csv
     bwd = ("ffn_bwd_own_kernel", "ffn_bwd_bf_kernel", "ffn_bwd_cols_kernel", "ffn_bwd_kernel")   # preferred first
-    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bfw_kernel", "ffn_fwd_bfp_kernel", "ffn_fwd_bf_kernel", "ffn_fwd_kernel"),
+    kerns = {"ctr_ffn_bwd": bwd, "ctr_ffn_bwd_norms": bwd, "ctr_ffn_fwd": ("ffn_fwd_bfw_kernel", "ffn_fwd_bf_kernel", "ffn_fwd_kernel"),
              "ctr_attn_bwd": ("attn_bwd_wave_kernel", "attn_bwd_kernel"),
              "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel"),
              "ctr_attn_bwd_bf": ("attn_bwd_mf_kernel",), "ctr_attn_fwd_bf": ("attn_fwd_mf_kernel",),
@@ -387,59 +387,40 @@ def cpu_baseline(cfg, B, L, seed=0, timed=3):
                       f"({', '.join(f'{x:.1f}' for x in times[1:])} s)"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)    # 20 warm-up, >= 100 timed steps
-    ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=4096)
-    ap.add_argument("--seq-len", type=int, default=None, help="default: the config's (100; cfg4 400)")
-    ap.add_argument("--config", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2",
-                    help="BASELINE.json config (the metric is quoted on cfg2; cfg5 needs 8 GPUs)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel-events", choices=("all", "none"), default="all",
-                    help="HIP events around the big kernels' calls in the timed steps (none: no roofline)")
-    ap.add_argument("--gc-in-steps", action="store_true",
-                    help="leave Python's cyclic garbage collector running in the timed steps (A/B of its host stalls)")
-    ap.add_argument("--markers", action="store_true",
-                    help="launch an empty step_marker_kernel around the timed region (tools/prof_summary.py)")
-    ap.add_argument("--dense-opt", action="store_true",
-                    help="step the tables in the dense AdamW/EMA stream instead of the exact lazy path")
-    ap.add_argument("--amp", choices=("none", "bf16"), default="bf16",
-                    help="cfg['amp'] (src/train.py:133-139): bf16 (BASELINE.json config 2 is quoted at bf16) = bf16 "
-                         "MFMA operands, fp32 accumulation, fp32 master weights / optimizer state / tables; none = fp32")
-    ap.add_argument("--tables", choices=("sharded", "replicated"), default="sharded",
-                    help="N > 1: row-shard the embedding tables over the ranks (all-to-all row fetch / grad "
-                         "routing) or replicate them (all-gather of row grads)")
-    args = ap.parse_args()
+def launch_ranks(n):
+    """``bench.py --gpus N`` without a launcher: start the N ranks (one process per GPU) as children under
+    torch.distributed.run on 127.0.0.1, with this process's own arguments, and return their exit status (non-zero when
+    any rank fails).  Rank 0 prints the JSON line to the stdout this process shares with it.  Nothing here touches
+    the GPU: the children initialise it, each on its own card (LOCAL_RANK)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")    # dmabuf IPC: what RCCL needs on this host driver
+    return subprocess.run(cmd, env=env).returncode
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())   # ranks > cards: rehearsal
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    pg = None
-    if world > 1:
-        import torch.distributed as dist
-        backend = os.environ.get("CTR_DIST_BACKEND", "nccl")    # gloo: functional rehearsal on one card
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
-        pg = dist.group.WORLD
 
+def build_run(args, amp, dev, pg, rank, shard):
+    """The benchmarked training setup: the config's model (random init of the reference's architecture), EMA, the
+    fused AdamW (exact-lazy tables unless --dense-opt), min(steps + warmup, 256) distinct synthetic batches resident
+    in HBM, and ``run(i, gstep)`` = one training step on batch i at global step gstep (lr from the reference's
+    cosine-warmup schedule)."""
     from tossctr import CTRModel, FusedAdamW, build_ema
-    from tossctr.configs import N_NUM_NEXT, cat_cardinals, dare_qnn_next
+    from tossctr.configs import BENCH_CONFIGS, N_NUM_NEXT, cat_cardinals
     from tossctr.train import cosine_warmup_lr
-
-    from tossctr.configs import BENCH_CONFIGS
     cfg = BENCH_CONFIGS[args.config](batch_size=args.batch)
     if args.seq_len is None:
         args.seq_len = int(cfg["sequence"]["max_len"])
     cfg["sequence"]["max_len"] = args.seq_len
-    cfg["amp"] = args.amp
+    cfg["amp"] = amp
     cards = cat_cardinals(cfg)
     cols = list(cfg["data"]["cat_cols"])
     vocab = 10_000_000                                   # src/train.py:116
     torch.manual_seed(cfg["seed"])
-    shard = pg is not None and args.tables == "sharded"
     model = CTRModel(cfg, vocab, N_NUM_NEXT, N_NUM_NEXT, cards, cols, device=dev, process_group=pg,
                      shard_tables=shard)
     model.reset_parameters(torch.Generator(device=dev).manual_seed(cfg["seed"]))
@@ -459,6 +440,91 @@ def main():
         # row-sharded tables: the next batch's exchange is planned beside this step (tossctr/shard.py)
         nxt = data[(i + 1) % nb][0] if shard else None
         return model.train_step(inp, y, opt, global_step=gstep + 1, next_inputs=nxt)
+    return cfg, model, ema, opt, data, run
+
+
+def fp32_secondary(args, dev):
+    """``secondary.fp32``: the same protocol (args.warmup untimed + args.steps timed steps, the exact-lazy flush of
+    the timed ticks inside the timed region) on a FRESH model at ``amp: none`` -- the precision every reference yaml
+    trains at (cfgs/dare_qnn_next.yaml:5 ``amp: none``) -- beside the bf16 headline BASELINE.json quotes cfg2 at."""
+    cfg, model, ema, opt, data, run = build_run(args, "none", dev, None, 0, False)
+    g = 0
+    for _ in range(args.warmup):
+        run(g, g)
+        g += 1
+    model.sync()
+    torch.cuda.synchronize()
+    gc.collect()
+    gc.disable()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = run(g, g)
+        g += 1
+    model.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    gc.enable()
+    if not math.isfinite(float(loss.item())):
+        raise RuntimeError("non-finite loss (fp32 secondary)")
+    ms = elapsed / args.steps * 1e3
+    out = {"value": round(args.batch * args.steps / elapsed, 1), "unit": "samples/s", "ms_per_step": round(ms, 3),
+           "steps": args.steps, "warmup": args.warmup, "dtype": "fp32",
+           "precision": "fp32 everywhere (amp: none, the reference yamls' setting): fp32 VALU attention, fp32 FFN and "
+                        "GEMM kernels (fp32 MFMA where they use it)",
+           "protocol": "fresh model, same warm-up / timed steps / timed flush as the headline"}
+    del model, opt, ema, data
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)    # SURVEY §8(d): 20 warm-up, >= 100 timed steps
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--seq-len", type=int, default=None, help="default: the config's (100; cfg4 400)")
+    ap.add_argument("--config", choices=("cfg2", "cfg3", "cfg4", "cfg5"), default="cfg2",
+                    help="BASELINE.json config (the metric is quoted on cfg2; cfg5 needs 8 GPUs)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fp32-secondary", action="store_true",
+                    help="skip secondary.fp32 (the same protocol at amp: none, on a fresh model; N = 1 only)")
+    ap.add_argument("--kernel-events", choices=("all", "none"), default="all",
+                    help="HIP events around the big kernels' calls in the timed steps (none: no roofline)")
+    ap.add_argument("--gc-in-steps", action="store_true",
+                    help="leave Python's cyclic garbage collector running in the timed steps (A/B of its host stalls)")
+    ap.add_argument("--markers", action="store_true",
+                    help="launch an empty step_marker_kernel around the timed region (tools/prof_summary.py)")
+    ap.add_argument("--dense-opt", action="store_true",
+                    help="step the tables in the dense AdamW/EMA stream instead of the exact lazy path")
+    ap.add_argument("--amp", choices=("none", "bf16"), default="bf16",
+                    help="cfg['amp'] (src/train.py:133-139): bf16 (BASELINE.json config 2 is quoted at bf16) = bf16 "
+                         "MFMA operands, fp32 accumulation, fp32 master weights / optimizer state / tables; none = fp32")
+    ap.add_argument("--tables", choices=("sharded", "replicated"), default="sharded",
+                    help="N > 1: row-shard the embedding tables over the ranks (all-to-all row fetch / grad "
+                         "routing) or replicate them (all-gather of row grads)")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+                         f"(bench.py --gpus N starts them itself when WORLD_SIZE is unset)")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())   # ranks > cards: rehearsal
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = os.environ.get("CTR_DIST_BACKEND", "nccl")    # gloo: functional rehearsal on one card
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        pg = dist.group.WORLD
+
+    shard = pg is not None and args.tables == "sharded"
+    cfg, model, ema, opt, data, run = build_run(args, args.amp, dev, pg, rank, shard)
+    nb = len(data)
 
     g = 0
     for _ in range(args.warmup):
@@ -639,8 +705,12 @@ def main():
                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": round(tb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         rec["dense_equivalent_bytes"] = step_bytes_dense_equiv(a, args.batch, args.seq_len, ema is not None)
+        if world == 1 and not args.no_fp32_secondary:
+            del data, model, opt, ema, run
+            gc.collect()
+            torch.cuda.empty_cache()
+            rec["secondary"] = {"fp32": fp32_secondary(args, dev)}
         if world == 1 and not args.no_cpu_baseline and args.config == "cfg2":
-            del data
             rec["cpu_baseline"] = cpu_baseline(cfg, args.batch, args.seq_len)
         else:
             rec["cpu_baseline"] = None

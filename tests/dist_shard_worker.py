@@ -111,16 +111,23 @@ def run(rank, world, port, args):
             for k, v in make_params(dense, 5, arch.pad_id).items():
                 model.arena.views[k].copy_(torch.from_numpy(v))
             _fill_tables_by_index(model, rank, world)
-    if args.autograd:
+    if args.autograd == 3:
+        # loss.backward() with FusedAdamW bound: the table grads stay compact, step() routes them and clips on the
+        # global norm (no EMA: the loop calls step() without a global step)
+        ema = None
+        opt = opt_t = FusedAdamW(model, lr=lr0, weight_decay=0.05, max_grad_norm=clip, process_group=pg,
+                                 lazy=bool(args.lazy))
+    elif args.autograd:
         # the reference loop itself (src/train.py:185-195): loss.backward(), clip, torch.optim.AdamW; row-sharded
-        # tables clip through model.clip_grad_norm_ (the global norm)
+        # tables clip through model.clip_grad_norm_ (the global norm) -- with --autograd 2 through the reference's
+        # own nn.utils.clip_grad_norm_ (a per-rank norm there), which the optimizer step must refuse
         ema = opt = None
         opt_t = torch.optim.AdamW(model.parameters(), lr=lr0, weight_decay=0.05)
     else:
         ema = ArenaEMA(model, base_decay=0.9)
         opt = FusedAdamW(model, lr=lr0, weight_decay=0.05, max_grad_norm=clip, ema=ema, process_group=pg,
                          lazy=bool(args.lazy))
-    losses, batches, staged = [], [], []
+    losses, batches, staged, raised = [], [], [], []
     for t in range(args.steps):
         bseed = 1000 + t + (0 if args.same_batch else 100 * rank)
         b = make_batch(Bs, Fn, Fm, list(cards.values()), L, vocab, seed=bseed)
@@ -137,11 +144,20 @@ def run(rank, world, port, args):
             loss = loss + model.aux_weight * _bce_wll(aux, y)
         opt_t.zero_grad(set_to_none=True)
         loss.backward()
-        if model.shards is not None:
+        if args.autograd == 3:
+            pass                                # FusedAdamW.step clips
+        elif model.shards is not None and args.autograd == 1:
             model.clip_grad_norm_(clip)
         else:
             torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
-        opt_t.step()
+        if args.autograd == 2:
+            try:
+                opt_t.step()
+            except RuntimeError as e:
+                raised.append(str(e))
+                break
+        else:
+            opt_t.step()
         losses.append(loss.detach())
     for t in range(0 if args.autograd else args.steps):
         opt.param_groups[0]["lr"] = lr0 * (1.0 - 0.2 * t)
@@ -167,6 +183,14 @@ def run(rank, world, port, args):
         losses.append(loss.clone())     # the step's loss lives in a workspace buffer the next step overwrites
     torch.cuda.set_sync_debug_mode("default")
     losses = [float(x.item()) for x in losses]
+    if args.autograd == 2:
+        # every rank refuses the step (the check is collective), at the first step: nothing has drifted
+        with open(f"{args.out}.raised{rank}", "w") as fh:
+            fh.write(raised[0] if raised else "")
+        if pg is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     if model.shards is not None and args.prefetch and not args.autograd:
         # every step after the first consumed the plan made beside the step before it, except the one an
         # evaluation forward came in front of (--interleave-eval)
@@ -291,7 +315,9 @@ def main():
     ap.add_argument("--config", choices=("tiny", "cfg5w", "cfg5r"), default="tiny")
     ap.add_argument("--nccl", type=int, default=0, help="world 1 over RCCL instead of world 2 over gloo")
     ap.add_argument("--autograd", type=int, default=0,
-                    help="the reference loop (model(batch), loss.backward(), clip, torch.optim.AdamW) instead of train_step")
+                    help="the reference loop instead of train_step: 1 = model(batch), loss.backward(), model.clip_grad_norm_, "
+                         "torch.optim.AdamW; 2 = the same with nn.utils.clip_grad_norm_ (must be refused on sharded "
+                         "tables); 3 = loss.backward() + FusedAdamW.step()")
     ap.add_argument("--prefetch", type=int, default=1, help="plan the next batch's exchange beside each step")
     ap.add_argument("--sync-check", type=int, default=0,
                     help="steps >= 2 under torch.cuda.set_sync_debug_mode('error') (needs --nccl 1: gloo stages "

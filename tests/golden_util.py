@@ -351,3 +351,35 @@ def check_topk(fx, t, idx_got, vals_got, label=""):
 def to_torch_batch(b):
     return {"X_num": torch.from_numpy(b["X_num"]).float(), "X_mask": torch.from_numpy(b["X_mask"]).float(),
             "X_cat": torch.from_numpy(b["X_cat"]).long(), "seq": torch.from_numpy(b["seq"]).long()}
+
+
+# The full-shape step cases (tests/test_gpu_fullshape.py; their reference bf16 bands: tests/golden/gen_amp_band_full.py):
+# the BASELINE configs as bench.py runs them, at the production batch (cfg4 at 1024, the size SURVEY §6 ran the
+# reference at on CPU -- 4096 does not fit a 62 GB host there), from the reference's own initialisation
+FULL_SHAPE = {"cfg2": dict(B=4096), "cfg3": dict(B=4096), "cfg4": dict(B=1024)}
+FULL_SHAPE_PSEED = 2024            # torch.manual_seed before CTRModel(...): oracle.synth.reference_init
+FULL_SHAPE_BSEED = 31337
+FULL_SHAPE_DSEED = (777 << 32) | 1  # dropout seed of the step (the cfg seed 777, step 1)
+
+
+def full_shape_case(name):
+    """(cfg, cards, cols, arch, B, L, vocab, Fn, batch) of a FULL_SHAPE case: tossctr.configs.BENCH_CONFIGS[name] (the
+    reference yaml restated with BASELINE.json's overrides), vocab 10M (src/train.py:116), the yaml's max_len, the
+    SURVEY §8(d) batch distributions (oracle.synth.make_batch, positive rate 0.019)."""
+    from tossctr.configs import BENCH_CONFIGS, N_NUM_NEXT, cat_cardinals
+    B = FULL_SHAPE[name]["B"]
+    cfg = BENCH_CONFIGS[name](batch_size=B)
+    cards = cat_cardinals(cfg)
+    cols = list(cards)
+    vocab, L, Fn = 10_000_000, int(cfg["sequence"]["max_len"]), N_NUM_NEXT
+    A = make_arch(cfg, vocab, Fn, Fn, cards, cols)
+    b = synth.make_batch(B, Fn, Fn, list(cards.values()), L, vocab, seed=FULL_SHAPE_BSEED, pos_rate=0.019)
+    return cfg, cards, cols, A, B, L, vocab, Fn, b
+
+
+def full_shape_touched(b, cols):
+    """Table key -> the rows the batch reads (unique token ids for both DARE tables, per column for the cats)."""
+    out = {"dare.emb_att.weight": np.unique(b["seq"]), "dare.emb_rep.weight": np.unique(b["seq"])}
+    for i, c in enumerate(cols):
+        out[f"cat_embs.{c}.weight"] = np.unique(b["X_cat"][:, i])
+    return out

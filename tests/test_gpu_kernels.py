@@ -492,6 +492,72 @@ def test_attn_layer_bf16_full_batch_vs_emulation(p):
     assert max(errs) < ATT_BF_TOL, errs
 
 
+@pytest.mark.parametrize("K,H,D,p", [(100, 8, 32, 0.1), (148, 8, 64, 0.1)])
+def test_attention_bf16_full_batch_k_gt_64(K, H, D, p):
+    """The K > 64 bf16 attention (ctr_attn_fwd_bf / ctr_attn_bwd_bf: attn_bwd_mfl_kernel's compact staging) at the
+    production batch of BASELINE cfg3 (K = 100, D = 32, dh 4) and cfg4 (K = 148, D = 64, dh 8): B = 4096 samples over
+    the full grid, against the fp64 emulation (attn_bf_emulate) at ATT_BF_TOL, evaluated in sample chunks (norms
+    accumulated over the whole batch); the keep bits exactly the oracle's in every chunk."""
+    L = _lib()
+    assert L.query("ctr_attn_bf_ok", K, H, D) == 1
+    from tossctr.rng import drop_args
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import rng as orng
+    B, dh, tk = 4096, D // H, K
+    g = torch.Generator(device="cuda").manual_seed(K * 4099 + D)
+    qkv = torch.randn(B * K, 3 * D, device="cuda", generator=g)
+    rel_w = torch.randn(2 * tk + 1, H, device="cuda", generator=g)
+    dk = drop_args(9876, 11, p, True)
+    relmean = torch.empty(2 * tk + 1, device="cuda")
+    st = stream()
+    L.call("ctr_pos_bias_mean", ptr(rel_w), H, 2 * tk + 1, ptr(relmean), st)
+    o = torch.full((B * K, D), float("nan"), device="cuda")
+    mrow = torch.empty(B * H * K, device="cuda")
+    lrow = torch.empty(B * H * K, device="cuda")
+    scale = float(np.float32(math.sqrt(1.0 / dh)))
+    nmask = L.query("ctr_attn_mask_words", B, K, H)
+    mask = torch.zeros(nmask, dtype=torch.int32, device="cuda")
+    L.call("ctr_attn_fwd_bf", ptr(qkv), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mask), ptr(o), ptr(mrow),
+           ptr(lrow), st)
+    do = torch.randn(B * K, D, device="cuda", generator=g)
+    dqkv = torch.full((B * K, 3 * D), float("nan"), device="cuda")
+    nparts = L.query("ctr_attn_bwd_bf_nparts", H) * B
+    drp = torch.full((nparts, 2 * tk + 1), float("nan"), device="cuda")
+    L.call("ctr_attn_bwd_bf", ptr(qkv), ptr(o), ptr(do), B, K, H, D, ptr(relmean), tk, scale, *dk, ptr(mask),
+           ptr(mrow), ptr(lrow), ptr(dqkv), ptr(drp), st)
+    drel = torch.empty(2 * tk + 1, H, device="cuda")
+    L.call("ctr_pos_bias_grad", ptr(drp), nparts, H, 2 * tk + 1, ptr(drel), st)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o).all() and torch.isfinite(dqkv).all()
+    km = orng.keep_mask(9876, 11, p, (B * H, K, K))
+    nt = (K + 15) // 16
+    wps = H * 64 * (2 if nt <= 4 else (4 * nt * nt + 31) // 32)      # mask words per sample
+    assert nmask >= B * wps
+    rt = rel_table(relmean, K, tk)
+    err = np.zeros(4)
+    nrm = np.zeros(4)
+    diag = torch.zeros(2 * K - 1, dtype=torch.float64, device="cuda")
+    CH = 256
+    for c0 in range(0, B, CH):
+        c1 = min(B, c0 + CH)
+        n = c1 - c0
+        kc = km[c0 * H:c1 * H]
+        assert np.array_equal(attn_bf_keep_bits(mask[c0 * wps:c1 * wps], n, H, K), kc), c0
+        keep = torch.from_numpy(kc).cuda().view(n, H, K, K)
+        r0, r1 = c0 * K, c1 * K
+        o_r, dq_r, dk_r, dv_r, dg = attn_bf_emulate(qkv[r0:r1], n, K, H, D, scale, rt, keep, dk[2], do[r0:r1],
+                                                    o_kernel=o[r0:r1])
+        diag += dg
+        dq, dkk, dv = (t.double() for t in dqkv[r0:r1].split(D, -1))
+        for i, (x, y) in enumerate(((o[r0:r1].double(), o_r), (dq, dq_r), (dkk, dk_r), (dv, dv_r))):
+            err[i] += float(((x - y) ** 2).sum())
+            nrm[i] += float((y ** 2).sum())
+        del keep, o_r, dq_r, dk_r, dv_r
+    errs = list(np.sqrt(err / nrm)) + [rel(drel.double(), drel_from_diag(diag, K, tk, H))]
+    assert max(errs) < ATT_BF_TOL, errs
+
+
 @pytest.mark.parametrize("K,H,p", [(60, 8, 0.1), (64, 8, 0.1), (61, 8, 0.1), (48, 4, 0.2), (33, 8, 0.0),
                                    (17, 4, 0.1), (1, 8, 0.1), (50, 4, 0.0)])
 @pytest.mark.parametrize("bias", [True, False])
@@ -1197,6 +1263,10 @@ def test_rowgemm_bf_vs_emulation(K, N, M):
     assert rel(C.double(), Ab @ _bfr(Wn) + add.double()) < 1e-6
     # an fp32 product would differ from the bf16 one by ~2^-9 relative: the emulation pins the operand rounding
     assert rel(C.double(), A.double() @ Wn.double() + add.double()) > 1e-4
+    # tb = 1 with bias AND add: the LayerNorm encoder's out_proj + residual h = x + o W^T + b (engine.py, amp D = 64)
+    L.call("ctr_rowgemm_bf", M, K, N, ptr(A), K, ptr(Wt), 1, ptr(C), N, ptr(b), ptr(add), N, None, 0, None, None, None,
+           0.0, st)
+    assert rel(C.double(), Ab @ _bfr(Wt).t() + b.double() + add.double()) < 1e-6
     if K == N:      # out_proj: residual + RMSNorm epilogue
         res = torch.randn(M, N, device="cuda", generator=g)
         w = torch.rand(N, device="cuda", generator=g) + 0.5

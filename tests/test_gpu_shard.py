@@ -260,3 +260,31 @@ def test_sharded_autograd_loop_matches_fused_step(tmp_path_factory):
     for k in a["sd"]:
         assert a["sd"][k].shape == b["sd"][k].shape, k
         close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), 1e-4, 1e-6, k)
+
+
+def test_sharded_autograd_fused_optimizer_matches_fused_step(tmp_path_factory):
+    """``loss.backward()`` followed by ``FusedAdamW.step()`` on row-sharded tables (world 2, different batches per
+    rank): the backward leaves the table grads compact (``.grad`` None), ``step()`` all-reduces the dense grads,
+    routes the row grads to their owners and clips on the global norm -- it must land where ``train_step`` does
+    (the loss gradient comes from torch's autograd of the loss instead of the fused loss kernel: ulps)."""
+    a = _run(tmp_path_factory, "sharded", 0, autograd=3)
+    b = _run(tmp_path_factory, "sharded", 0)
+    close_enough(np.asarray(a["losses"], np.float64), np.asarray(b["losses"], np.float64), 1e-5, 1e-6, "loss")
+    for k in b["sd"]:
+        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), 1e-5, 1e-6, k)
+        close_enough(a["m"][k].double().numpy().ravel(), b["m"][k].double().numpy().ravel(), 1e-4, 1e-9, "m:" + k)
+
+
+def test_sharded_autograd_reference_clip_is_refused(tmp_path_factory):
+    """The reference's own ``nn.utils.clip_grad_norm_(model.parameters(), clip)`` on row-sharded tables takes each
+    rank's LOCAL shard norm, so the ranks would scale their replicated dense grads differently and drift apart;
+    the optimizer step after such a backward raises on every rank (the check is collective) at the first step."""
+    out = str(tmp_path_factory.mktemp("shard") / "refclip.pt")
+    r = subprocess.run([sys.executable, os.path.join(HERE, "dist_shard_worker.py"), "--mode", "sharded",
+                        "--same-batch", "0", "--steps", "2", "--autograd", "2", "--out", out],
+                       capture_output=True, text=True, timeout=250)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    for rank in range(2):
+        with open(f"{out}.raised{rank}") as fh:
+            msg = fh.read()
+        assert "model.clip_grad_norm_" in msg, (rank, msg)

@@ -1051,169 +1051,6 @@ __global__ __launch_bounds__(256) void ffn_fwd_bf_kernel(FfnArgs a) {
   ffn_fwd_epilogue<D, T>(a, yacc, xw, m0 + rb);
 }
 
-// Persistent forward (D = 32): a workgroup stages the layer's weights ONCE as bf16 MFMA operand images in LDS --
-// W1 [chunk][s][kh][lane] and W2 [chunk][j][lane], 16 bytes per lane in exactly the register order of the
-// per-tile kernel above (one conflict-free ds_read_b128 per operand) -- plus b1, then walks row tiles
-// t = blockIdx.x, + gridDim.x, ...  The per-tile form re-read every chunk's fp32 weights from L2 and
-// converted them (12 chunks x 8 KB per wave, ~740 MB of L2 reads per launch at cfg2).  The next tile's x rows
-// are loaded into registers while the current tile computes.
-template <int D>
-__host__ __device__ constexpr int ffn_fwdp_xregs() { return FfnBf<D>::RT * D / 4 / 256; }   // f32x4 per thread
-
-template <int D, bool DROP>
-__global__ __launch_bounds__(256) void ffn_fwd_bfp_kernel(FfnArgs a) {
-  using T = FfnBf<D>;
-  constexpr int NXR = ffn_fwdp_xregs<D>();
-  extern __shared__ __attribute__((aligned(16))) char fsm[];
-  const int FF = a.FF, NCH = FF / 32;
-  bf16x8* iw1 = (bf16x8*)fsm;                        // [NCH][2][KH][64]
-  bf16x8* iw2 = iw1 + NCH * 2 * T::KH * 64;          // [NCH][NJ][64]
-  float* sb1 = (float*)(iw2 + NCH * T::NJ * 64);     // [FF]
-  float* xt = sb1 + FF;                              // [RT][S] fp32 x tile
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, c = lane & 15;
-  const int rb = w * T::RW;
-  if (a.wbf) {     // bf16 weight images for the backward: W1 (FF, D) | W2^T (FF, D) | W1^T (D, FF)
-    const int n = FF * D;
-    for (int e = blockIdx.x * 256 + tid; e < 3 * n; e += gridDim.x * 256) {
-      float v;
-      if (e < n) {
-        v = a.W1[e];
-      } else if (e < 2 * n) {
-        const int q = e - n;
-        v = a.W2[(q % D) * FF + q / D];
-      } else {
-        const int q = e - 2 * n;
-        v = a.W1[(q % FF) * D + q / FF];
-      }
-      a.wbf[e] = (__bf16)v;
-    }
-  }
-  for (int u = tid; u < NCH * 2 * T::KH * 64; u += 256) {
-    const int l = u & 63, q = u >> 6, kh = q % T::KH, sc = q / T::KH, s2 = sc & 1, ch = sc >> 1;
-    const float* p = a.W1 + (long)(32 * ch + 16 * s2 + (l & 15)) * D + 32 * kh + 8 * (l >> 4);
-    iw1[u] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 4));
-  }
-  for (int u = tid; u < NCH * T::NJ * 64; u += 256) {
-    const int l = u & 63, q = u >> 6, j = q % T::NJ, ch = q / T::NJ;
-    const float* p = a.W2 + (long)(16 * j + (l & 15)) * FF + 32 * ch + 4 * (l >> 4);
-    iw2[u] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 16));
-  }
-  for (int u = tid; u < FF; u += 256) sb1[u] = a.b1[u];
-
-  const int nb16 = (a.M + 15) / 16;
-  const auto rmask = buf_rsrc(a.mask, DROP ? (uint32_t)nb16 * 16 * (FF / 32) * 4 : 0u);
-  const uint32_t thr = a.drop.thresh;
-  const float dsc = a.drop.scale;
-  struct Wc {
-    bf16x8 w1[2][T::KH], w2[T::NJ];
-    f32x4 b[2];
-  };
-  auto load_w = [&](int f0, Wc& W) {
-    const int ch = f0 >> 5;
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-      for (int kh = 0; kh < T::KH; ++kh) W.w1[s2][kh] = iw1[((ch * 2 + s2) * T::KH + kh) * 64 + lane];
-#pragma unroll
-    for (int j = 0; j < T::NJ; ++j) W.w2[j] = iw2[(ch * T::NJ + j) * 64 + lane];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) W.b[s2] = *(const f32x4*)(sb1 + f0 + 16 * s2 + 4 * g);
-  };
-  // x rows of tile t: thread tid holds f32x4 q = tid + 256 k (row q / (D/4), columns 4 (q % (D/4)) ..)
-  f32x4 xr[NXR];
-  auto fetch_x = [&](int t) {
-#pragma unroll
-    for (int k = 0; k < NXR; ++k) {
-      const int q = tid + 256 * k, i = q / (D / 4), c4 = (q % (D / 4)) * 4;
-      const long m = (long)t * T::RT + i;
-      xr[k] = m < a.M ? *(const f32x4*)(a.x + m * D + c4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  };
-  const int ntiles = (a.M + T::RT - 1) / T::RT;
-  if ((int)blockIdx.x < ntiles) fetch_x(blockIdx.x);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int m0 = tile * T::RT;
-    __syncthreads();      // the previous tile's readers of xt are done (first tile: the images are written)
-#pragma unroll
-    for (int k = 0; k < NXR; ++k) {
-      const int q = tid + 256 * k, i = q / (D / 4), c4 = (q % (D / 4)) * 4;
-      *(f32x4*)(xt + i * T::S + c4) = xr[k];
-    }
-    __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) fetch_x(tile + gridDim.x);
-    const float* xw = xt + rb * T::S;
-    bf16x8 xf[T::NI][T::KH];
-#pragma unroll
-    for (int i = 0; i < T::NI; ++i)
-#pragma unroll
-      for (int kh = 0; kh < T::KH; ++kh) {
-        const float* p = xw + (16 * i + c) * T::S + 32 * kh + 8 * g;
-        xf[i][kh] = pack8(*(const f32x4*)p, *(const f32x4*)(p + 4));
-      }
-    f32x4 yacc[T::NI][T::NJ];
-#pragma unroll
-    for (int i = 0; i < T::NI; ++i)
-#pragma unroll
-      for (int j = 0; j < T::NJ; ++j) yacc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto chunk = [&](int f0, const Wc& W) {
-      f32x4 p[T::NI][2];
-#pragma unroll
-      for (int i = 0; i < T::NI; ++i)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          p[i][s2] = W.b[s2];      // pre^T accumulates onto b1 (register r of lane group g: column 4g + r)
-#pragma unroll
-          for (int kh = 0; kh < T::KH; ++kh) p[i][s2] = mfma_bf(W.w1[s2][kh], xf[i][kh], p[i][s2]);
-        }
-#pragma unroll
-      for (int i = 0; i < T::NI; ++i) {
-        const uint32_t m = (uint32_t)(m0 + rb + 16 * i + c);
-        uint32_t kb = 0;
-        f32x4 fo[2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const f32x2 z = {p[i][s2][2 * q], p[i][s2][2 * q + 1]};
-            f32x2 v = gelu_as2(z);
-            if (DROP) {
-              const uint32_t hb = drop_pair_bits(a.drop, (m * (uint32_t)FF + f0 + 16 * s2 + 4 * g + 2 * q) >> 1);
-              const bool k0 = (hb & 0xFFFFu) >= thr, k1 = (hb >> 16) >= thr;
-              v = v * f32x2{k0 ? dsc : 0.f, k1 ? dsc : 0.f};
-              kb |= (k0 ? 1u : 0u) << (4 * s2 + 2 * q);
-              kb |= (k1 ? 1u : 0u) << (4 * s2 + 2 * q + 1);
-            }
-            fo[s2][2 * q] = v.x;
-            fo[s2][2 * q + 1] = v.y;
-          }
-        const bf16x8 af = pack8(fo[0], fo[1]);
-#pragma unroll
-        for (int j = 0; j < T::NJ; ++j) yacc[i][j] = mfma_bf(af, W.w2[j], yacc[i][j]);
-        if (DROP) {
-          uint32_t kw = ((kb & 0xFu) << (4 * g)) | ((kb >> 4) << (16 + 4 * g));
-          kw |= (uint32_t)__shfl_xor((int)kw, 16, 64);
-          kw |= (uint32_t)__shfl_xor((int)kw, 32, 64);
-          const uint32_t wi = rw_word(f0 >> 5, nb16, (m0 + rb) / 16 + i, c);
-          buf_st_u32(kw, rmask, (g == 0 && (int)m < a.M) ? wi * 4 : BUF_OOB);
-        }
-      }
-    };
-    Wc wa, wb;
-    load_w(0, wa);
-    int f0 = 0;
-    for (; f0 + 64 <= FF; f0 += 64) {
-      load_w(f0 + 32, wb);
-      chunk(f0, wa);
-      __builtin_amdgcn_sched_barrier(0);
-      load_w(min(f0 + 64, FF - 32), wa);
-      chunk(f0 + 32, wb);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (f0 < FF) chunk(f0, wa);
-    ffn_fwd_epilogue<D, T>(a, yacc, xw, m0 + rb);
-  }
-}
-
 // Wave-independent forward (D = 32, round 5): no x tile in LDS and no barrier after the weight staging, so a
 // workgroup's eight waves run free of each other and two workgroups (51 KB of weight images each) fit a CU at four
 // waves per SIMD (<= 128 registers).  A wave owns 32-row tiles t = wave, + total waves, ...; its x rows are read
@@ -1406,11 +1243,6 @@ __global__ __launch_bounds__(FfnFw<D>::NWAVE * 64) __attribute__((amdgpu_waves_p
 
 template <int D>
 static size_t ffn_fwdw_lds(int FF) { return (size_t)FF * D * 2 * 2 + (size_t)FF * 4; }
-
-template <int D>
-static size_t ffn_fwdp_lds(int FF) {
-  return (size_t)FF * D * 2 * 2 + (size_t)FF * 4 + (size_t)FfnBf<D>::RT * FfnBf<D>::S * 4;
-}
 
 // Backward tile: D = 32 takes 128-row tiles (32 rows per wave), D = 64 64-row tiles (16 per wave) so two
 // workgroups fit a CU's LDS.  Per 32-column chunk every wave writes its fo / dact rows as bf16 [ff][rows]

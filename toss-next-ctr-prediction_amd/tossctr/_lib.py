@@ -205,7 +205,7 @@ class CtrError(RuntimeError):
     pass
 
 
-_timed = {}     # entry name -> list of (start, end, key) torch.cuda.Event pairs + report key, while timing is on
+_timed = {}     # entry name -> (list of (start, end, key) torch.cuda.Event pairs, shape keys to bracket or None = all)
 # entry points reported per call shape: one entry serves launches of different shapes (the three QNN MLP products)
 _TIME_KEY = {"ctr_gemm_bf16_ex": lambda a: f"ctr_gemm_bf16_ex@{a[0]}x{a[1]}x{a[2]}" + ("b" if a[15] else "")}
 
@@ -213,10 +213,17 @@ _TIME_KEY = {"ctr_gemm_bf16_ex": lambda a: f"ctr_gemm_bf16_ex@{a[0]}x{a[1]}x{a[2
 def time_calls(names):
     """Bracket every call of the named entry points with HIP events on the current stream (the stream
     the library launches on); ``timed_ms()`` reads the per-call averages.  ``time_calls(())`` stops.
-    A name may carry a shape key (``ctr_gemm_bf16_ex@MxNxK``): the entry point is bracketed."""
+    A name may carry a shape key (``ctr_gemm_bf16_ex@MxNxK``): only the entry's calls of that shape are bracketed
+    (the bench times just the dominant launch; events around the entry's other shapes would cost step time)."""
     _timed.clear()
     for n in names:
-        _timed[n.split("@")[0]] = []
+        base = n.split("@")[0]
+        evs, keys = _timed.setdefault(base, ([], set()))
+        if keys is not None:
+            if "@" in n:
+                keys.add(n)
+            else:
+                _timed[base] = (evs, None)
 
 
 def timed_ms():
@@ -225,7 +232,7 @@ def timed_ms():
     import torch
     torch.cuda.synchronize()
     out = {}
-    for evs in _timed.values():
+    for evs, _ in _timed.values():
         acc = {}
         for a, b, key in evs:
             acc.setdefault(key, []).append(a.elapsed_time(b))
@@ -241,14 +248,20 @@ def call(name, *args):
     fn = _fns.get(name)
     if fn is None:
         fn = _fns[name] = getattr(load(), name)
-    if _timed and name in _timed:
+    ent = _timed.get(name) if _timed else None
+    key = None
+    if ent is not None:
+        kf = _TIME_KEY.get(name)
+        key = kf(args) if kf else name
+        if ent[1] is not None and key not in ent[1]:
+            ent = None
+    if ent is not None:
         import torch
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         ev[0].record()
         rc = fn(*args)
         ev[1].record()
-        kf = _TIME_KEY.get(name)
-        _timed[name].append((ev[0], ev[1], kf(args) if kf else name))
+        ent[0].append((ev[0], ev[1], key))
     else:
         rc = fn(*args)
     if rc != 0:

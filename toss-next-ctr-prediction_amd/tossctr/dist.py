@@ -29,6 +29,17 @@ def allreduce_sum_(t: torch.Tensor, group=None):
     return t
 
 
+def allreduce_max_(t: torch.Tensor, group=None):
+    """In-place elementwise max across ranks."""
+    if _needs_host_staging(group, t):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t
+
+
 def allreduce_sum_async(t: torch.Tensor, group=None):
     """Start an in-place sum across ranks and return its handle (``wait()`` makes the current stream wait
     for it; None when it already completed).  Under RCCL the collective runs on the process group's own

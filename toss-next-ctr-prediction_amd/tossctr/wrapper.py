@@ -9,11 +9,16 @@ Two training paths:
     a custom autograd.Function runs the HIP backward and hands torch ordinary dense ``.grad`` tensors
     (tables included; fine for tests / small vocabularies).  With row-sharded tables the backward is
     collective (dense grads averaged over the ranks, row grads sent to their owners; a table's ``.grad``
-    is its local shard's) and ``model.clip_grad_norm_`` replaces ``nn.utils.clip_grad_norm_`` (global norm);
+    is its local shard's) and ``model.clip_grad_norm_`` replaces ``nn.utils.clip_grad_norm_`` (global norm):
+    the reference's own call would clip each rank by its local norm, and the next optimizer step raises
+    (``_check_replicated_grads``) rather than let the replicas drift; with FusedAdamW bound the table grads stay
+    compact and its ``step()`` routes and clips them on the global norm;
   * fused (what tossctr.train and bench.py use): ``model.train_step(...)`` via tossctr.optim --
     table grads stay compact (sorted unique rows) and clip + AdamW + EMA run as one HBM stream.
 """
 from __future__ import annotations
+
+import weakref
 
 import torch
 import torch.nn as nn
@@ -21,6 +26,28 @@ import torch.nn as nn
 from .arch import Arch
 from .engine import Engine, ParamArena, ptr
 from . import _lib
+
+# Row-sharded models whose autograd backward left replicated dense grads that the next optimizer step must find still
+# identical on every rank (CTRModel._check_replicated_grads).  The reference loop clips with
+# nn.utils.clip_grad_norm_(model.parameters()) (src/train.py:189,194): on row-sharded tables that norm is per rank
+# (a table's .grad is the local shard's), each rank would scale its replicated dense grads by its own coefficient
+# and the replicas would drift apart silently.  The check turns that into an error at the step.
+_PENDING_CHECK = weakref.WeakSet()
+_STEP_HOOK = None
+
+
+def _step_pre_hook(optimizer, args, kwargs):
+    for model in list(_PENDING_CHECK):
+        _PENDING_CHECK.discard(model)
+        model._check_replicated_grads()
+
+
+def _arm_step_check(model):
+    global _STEP_HOOK
+    if _STEP_HOOK is None:
+        from torch.optim.optimizer import register_optimizer_step_pre_hook
+        _STEP_HOOK = register_optimizer_step_pre_hook(_step_pre_hook)
+    _PENDING_CHECK.add(model)
 
 
 def _tree_module(root: nn.Module, key: str) -> tuple:
@@ -63,6 +90,7 @@ class _CTRFunction(torch.autograd.Function):
             # grads all-reduced and averaged, each table's row grads sent to their owners (the fused step's
             # exchange, tossctr/shard.py route) and averaged; .grad of a table is then its local shard's
             routed = model._reduce_sharded_grads()
+            _arm_step_check(model)
         grads = []
         for k in model.arena.order:
             if model.arena.kind[k] == "table":
@@ -73,7 +101,7 @@ class _CTRFunction(torch.autograd.Function):
                     # norm itself, so no dense shard grad is materialised
                     grads.append(None)
                 else:
-                    grads.append(eng.dense_table_grad(k, routed, 1.0 / sh.world))
+                    grads.append(eng.dense_table_grad(k, routed, 1.0 / model._contributors()))
             elif k in model.no_grad and not (k.startswith("dare.aux_head") and daux is not None):
                 grads.append(None)
             else:
@@ -235,15 +263,42 @@ class CTRModel(nn.Module):
         return logits.clone(), prob.clone(), aux.clone()
 
     # ------------------------------------------------------------------ row-sharded tables, autograd path
+    # ranks holding rows in the current step (row-sharded autograd path; None: every rank), as train_step's
+    # ``contributors``: an epoch's short last step leaves some ranks without rows (tossctr.train.rank_slice), their
+    # zero gradients do not count in the mean
+    contributors = None
+
     def _reduce_sharded_grads(self):
-        """Collective (every rank, in the backward): dense grads all-reduced and divided by the world size
-        (DDP's mean), the compact table row grads routed to their owners; returns the routed grads."""
+        """Collective (every rank, in the backward): dense grads all-reduced and divided by the number of
+        contributing ranks (DDP's mean; ``self.contributors``, default the world size), the compact table row grads
+        routed to their owners; returns the routed grads (the caller scales them by the same 1 / contributors)."""
         from . import dist as D
         sh, ar = self.shards, self.arena
         n = ar.n_dense_grad
         D.allreduce_sum_(ar.grad[:n], sh.group)
-        ar.grad[:n].mul_(1.0 / sh.world)
+        ar.grad[:n].mul_(1.0 / self._contributors())
         return sh.route(self.engine.tg, self.engine.tg["fx"])
+
+    def _contributors(self):
+        return self.shards.world if self.contributors is None else int(self.contributors)
+
+    @torch.no_grad()
+    def _check_replicated_grads(self):
+        """Collective, before the optimizer step that follows a row-sharded autograd backward: the dense grads are
+        replicas (all-reduced in the backward), so any per-rank rescaling since -- above all
+        ``nn.utils.clip_grad_norm_(model.parameters())``, whose norm on row-sharded tables is the local one -- shows
+        as ranks disagreeing on them.  Raises instead of letting the replicas drift apart."""
+        from . import dist as D
+        gs = [p.grad for k, p in self.named_parameters() if self.arena.kind[k] != "table" and p.grad is not None]
+        s = torch.stack([g.double().sum() for g in gs]).sum() if gs else torch.zeros((), dtype=torch.float64,
+                                                                                   device=self.arena.device)
+        t = torch.stack([s, -s])
+        D.allreduce_max_(t, self.shards.group)
+        if bool(t[0] != -t[1]):
+            raise RuntimeError(
+                "row-sharded tables: the replicated dense gradients differ between ranks at the optimizer step. "
+                "nn.utils.clip_grad_norm_(model.parameters(), ...) takes each rank's LOCAL table shards' norm here; "
+                "clip with model.clip_grad_norm_(max_norm) (the global norm over all shards, collective) instead")
 
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm: float, norm_type: float = 2.0):
