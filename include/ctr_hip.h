@@ -530,6 +530,10 @@ int ctr_ensemble(const float* P, int M, int B, int method, const float* w, int k
 /* misc: prob = sigmoid(logits) (src/models/wrapper.py:175); strided 2-D copy; compact -> dense rows */
 int ctr_sigmoid(const float* x, int n, float* y, void* stream);
 int ctr_copy2d(const float* src, long lds, float* dst, long ldd, int rows, int cols, void* stream);
+/* dst[0, n) = 0 (16-byte aligned dst): the dense grad arena before each backward -- a native kernel where
+ * torch's zero_() would put an at::native fill into the step (no reference counterpart: the reference's
+ * optimizer.zero_grad(set_to_none=True), src/train.py:157, drops the grads instead)                     */
+int ctr_zero_f32(float* dst, long n, void* stream);
 /* profiling aid (no reference counterpart): an empty one-wave kernel, step_marker_kernel, launched on the
  * stream so a rocprofv3 kernel trace can be cut at the timed region's boundaries (tools/prof_summary.py) */
 int ctr_step_marker(int tag, void* stream);

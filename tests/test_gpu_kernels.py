@@ -1386,3 +1386,14 @@ def test_colsum_multi_matches_sums_and_is_deterministic():
     L.call("ctr_colsum_multi", arr, len(segs), ptr(ws), nb, stream())
     for a, b in zip(first, outs):
         assert torch.equal(a[:-1], b[:-1])
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1027, 4_482_602])
+def test_zero_f32(n):
+    """ctr_zero_f32 (the grad arena's clear before each backward): every element of [0, n) zero, nothing past it
+    touched (tails of 1-3 elements after the 16-byte stores)."""
+    L = _lib()
+    buf = torch.full((n + 8,), 7.0, device="cuda")
+    L.call("ctr_zero_f32", ptr(buf), n, stream())
+    torch.cuda.synchronize()
+    assert (buf[:n] == 0).all() and (buf[n:] == 7.0).all()

@@ -741,7 +741,24 @@ extern "C" int ctr_gather_rows(const void* src, long row_words, const long* idx,
 
 namespace ctr {
 __global__ void step_marker_kernel(int tag) { (void)tag; }
+
+// dst[0, n) = 0: 16-byte stores, grid-stride (the dense grad arena before each backward)
+__global__ void zero_f32_kernel(float* __restrict__ dst, long n) {
+  typedef float zf4 __attribute__((ext_vector_type(4)));
+  const long n4 = n / 4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+    ((zf4*)dst)[i] = zf4{0.f, 0.f, 0.f, 0.f};
+  for (long i = 4 * n4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) dst[i] = 0.f;
+}
 }  // namespace ctr
+
+extern "C" int ctr_zero_f32(float* dst, long n, void* stream) {
+  CTR_REQUIRE(n >= 0 && (((uintptr_t)dst) & 15) == 0, "ctr_zero_f32: needs a 16-byte aligned buffer");
+  if (n == 0) return 0;
+  const int blocks = (int)std::min<long>((n / 4 + 255) / 256 + 1, 2048);
+  zero_f32_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(dst, n);
+  return check_launch("zero_f32");
+}
 
 // an empty dispatch that marks a point of the stream in a rocprofv3 kernel trace (bench.py --markers)
 extern "C" int ctr_step_marker(int tag, void* stream) {

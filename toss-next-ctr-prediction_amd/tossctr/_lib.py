@@ -165,6 +165,7 @@ SIGS = {
     "ctr_ensemble": (i, [p, i, i, i, p, i, p, p]),
     "ctr_sigmoid": (i, [p, i, p, p]),
     "ctr_copy2d": (i, [p, l, p, l, i, i, p]),
+    "ctr_zero_f32": (i, [p, l, p]),
     "ctr_step_marker": (i, [i, p]),
     "ctr_gather_rows": (i, [p, l, p, i, p, p]),
     "ctr_scatter_rows": (i, [p, p, p, i, i, i, u, l, p, p]),

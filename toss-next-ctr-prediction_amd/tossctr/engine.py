@@ -750,7 +750,7 @@ class Engine:
         seed, training = sv["seed"], sv["training"]
         xF = sv["xF"]
         num_off, mask_off, cat_off = D, D + a.Fn * D, D + (a.Fn + a.Fm) * D
-        self.arena.grad.zero_()
+        call("ctr_zero_f32", ptr(self.arena.grad), self.arena.grad.numel(), st)
         dxF = W.get("dxF", (B, FD))
         dfc = None
         # ---------------- head
