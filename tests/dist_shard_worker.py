@@ -79,6 +79,8 @@ def run(rank, world, port, args):
         m = fx.meta
         cfg, Fn, Fm, L, Bs = m["cfg"], m["Fn"], m["Fm"], int(m["L"]), B
         clip = m["train"]["clip"] or 1.0
+        if args.autograd == 2:
+            clip = 1e-3          # every rank's local norm above it: the per-rank coefficients differ
         vocab = int(m["vocab"]) * 8                 # sparse tables: most rows skip most ticks
         cards = {k: v * 4 + 1 for k, v in fx.cat_cards.items()}
     elif args.config == "cfg5w":
@@ -224,6 +226,7 @@ def run(rank, world, port, args):
         local_rows = int(model.arena.shapes["dare.emb_att.weight"][0])
         if rank == 0:
             torch.save({"sd": sd, "ema": shadow, "m": mom, "v": vel, "losses": losses, "logits": logits, "eval_tok": eval_tok, "eval_vals": eval_vals,
+                        "replica_checks": int(model.__dict__.get("replica_checks", 0)),
                         "eval_idx": eval_idx,
                         "gnorm": float(opt.norm_out[0]) if opt else float("nan"), "local_rows": local_rows, "vocab": vocab, "cards": cards,
                         "cfg": cfg, "Fn": Fn, "Fm": Fm, "L": L, "B": Bs, "lr0": lr0, "clip": clip,

@@ -113,6 +113,64 @@ def oracle_step(shape):
     yield out
 
 
+@pytest.fixture(scope="module")
+def oracle64(shape):
+    """On first use: the oracle's step-0 gradients in fp64 (oracle.model.forward at float64, the same batch, init
+    and dropout masks) for the dense parameters, as the moments they give: m64 = 0.1 c g, v64 = 0.001 (c g)^2 with
+    the fp64 clip coefficient c.  The arbiter where the fp32 HIP step and the fp32 oracle differ by more than the
+    moment tolerance: a gradient that is a sum over 4096 x K rows with heavy cancellation is no better than a few
+    1e-4 in fp32, in either implementation (~20 GB of host memory, ~1 min)."""
+    cache = {}
+
+    def get():
+        if not cache:
+            from oracle.model import Dropper, bce_wll_style, forward
+            A, b = shape["A"], shape["b"]
+            P = {k: v.double().requires_grad_(True) for k, v in shape["P0"].items()}
+            drop = Dropper(shape["seed"], training=True)
+            logits, _, aux = forward(P, to_torch_batch(b), A, drop, dtype=torch.float64)
+            y = torch.from_numpy(b["y"]).double()
+            loss = bce_wll_style(logits, y)
+            if A.aux_w > 0:
+                loss = loss + A.aux_w * bce_wll_style(aux, y)
+            loss.backward()
+            keys = A.grad_params()
+            sq = sum(float(P[k].grad.pow(2).sum()) for k in keys)
+            coef = min(1.0, CLIP / (sq ** 0.5 + 1e-6))
+            for k in keys:
+                if k not in shape["touched"]:
+                    g = P[k].grad.detach() * coef
+                    cache[k] = (0.1 * g, 0.001 * g * g)
+            del P, logits, aux, loss
+        return cache
+
+    yield get
+    cache.clear()
+
+
+def _check_moments_fp32(k, g, r, oracle64):
+    """m, v of the HIP step against the fp32 oracle (2e-4 / 4e-4 norm-wise, golden_util.Fixture.check_moment); a
+    dense tensor beyond that passes if the HIP step is no further from the fp64 oracle than 2x the fp32 oracle is
+    (the gradient itself is that ill-conditioned in fp32).  Returns a note for the report, or None."""
+    try:
+        close_enough(g["m"].numpy().ravel(), r["m"].numpy().ravel(), 2e-4, 0.0, f"m:{k}")
+        close_enough(g["v"].numpy().ravel(), r["v"].numpy().ravel(), 4e-4, 0.0, f"v:{k}")
+        return None
+    except AssertionError:
+        ref64 = oracle64().get(k)
+        if ref64 is None:
+            raise
+    notes = []
+    for name, gm, rm, t64, rtol in (("m", g["m"], r["m"], ref64[0], 2e-4), ("v", g["v"], r["v"], ref64[1], 4e-4)):
+        t = t64.numpy().ravel()
+        n64 = np.linalg.norm(t)
+        e_hip = np.linalg.norm(gm.numpy().ravel() - t) / n64
+        e_or = np.linalg.norm(rm.numpy().ravel() - t) / n64
+        assert e_hip <= max(rtol, 2.0 * e_or), (f"{name}:{k}", e_hip, e_or)
+        notes.append(f"{name}:{k} vs fp64: HIP {e_hip:.2e}, fp32 oracle {e_or:.2e}")
+    return "; ".join(notes)
+
+
 def _hip_step(shape, amp, record=()):
     """One fused HIP training step (compact table grads, exact lazy AdamW / EMA) on the shared batch; the
     entry points named in ``record`` are counted (tossctr._lib.time_calls)."""
@@ -199,7 +257,7 @@ def _check_topk_fp32(got, ref, A, b):
 
 
 @pytest.mark.timeout(900)
-def test_full_shape_step_matches_oracle(shape, oracle_step):
+def test_full_shape_step_matches_oracle(shape, oracle_step, oracle64):
     ref, A, b = oracle_step, shape["A"], shape["b"]
     # the oracle itself at this shape: the reference's own fp32 step on the same batch, init and masks
     # (tests/golden/gen_amp_band_full.py records its loss and grad norm)
@@ -222,9 +280,11 @@ def test_full_shape_step_matches_oracle(shape, oracle_step):
         if k in shape["touched"]:
             p0 = p0[torch.from_numpy(shape["touched"][k])]
             _check_untouched(shape, k, g, r)
+        note = None
         if r["m"] is not None:
-            close_enough(g["m"].numpy().ravel(), r["m"].numpy().ravel(), 2e-4, 0.0, f"m:{k}")
-            close_enough(g["v"].numpy().ravel(), r["v"].numpy().ravel(), 4e-4, 0.0, f"v:{k}")
+            note = _check_moments_fp32(k, g, r, oracle64)
+            if note:
+                print("  " + note)
         base = p0.double().numpy().ravel()
         dg = g["p"].numpy().ravel() - base
         dr = r["p"].numpy().ravel() - base
@@ -239,9 +299,20 @@ def test_full_shape_step_matches_oracle(shape, oracle_step):
             kb = key_bias_mask(A, k)
             if kb is not None:
                 strong &= ~kb
-            assert (np.abs(dg - dr)[strong] <= 1e-2 * LR + ulp[strong]).all(), k
             good = np.sqrt(r["v"].numpy().ravel() / (1 - 0.999)) >= 100 * 1e-8
-            close_enough(dg[good], dr[good], 1e-4, 0.0, f"dp:{k}", ulp[good], elem_rtol=1e-2)
+            if note:
+                # a gradient the fp32 oracle itself gets only to a few 1e-4 (the moments went to the fp64 arbiter):
+                # the update of the first AdamW step from the fp64 moments, d64; the HIP step within 1e-2 lr of it
+                # where the fp32 oracle is, and no further from it than twice the oracle anywhere
+                m64, v64 = (t.numpy().ravel() for t in oracle64()[k])
+                d64 = base * (1 - LR * WD) - LR * (m64 / 0.1) / (np.sqrt(v64 / 1e-3) + 1e-8) - base
+                tol = np.maximum(1e-2 * LR, 2.0 * np.abs(dr - d64)) + ulp
+                assert (np.abs(dg - d64)[strong] <= tol[strong]).all(), k
+                assert np.linalg.norm(dg[good] - d64[good]) <= max(1e-4 * np.linalg.norm(d64[good]),
+                                                                   2.0 * np.linalg.norm(dr[good] - d64[good])), k
+            else:
+                assert (np.abs(dg - dr)[strong] <= 1e-2 * LR + ulp[strong]).all(), k
+                close_enough(dg[good], dr[good], 1e-4, 0.0, f"dp:{k}", ulp[good], elem_rtol=1e-2)
         if r["e"] is not None:
             eg = g["e"].numpy().ravel() - base
             er = r["e"].numpy().ravel() - base
@@ -290,7 +361,19 @@ def test_full_shape_bf16_step(shape, oracle_step):
     # little about the spread, so they also pass within one bf16 unit roundoff (2^-9) of the value
     within("loss", abs(got["loss"] - ref["loss"]), abs(ref["loss"]), band["scalars"]["loss"],
            SCALAR_FLOOR * abs(ref["loss"]))
-    within("gnorm", abs(got["gnorm"] - ref["gnorm"]), ref["gnorm"], band["scalars"]["gnorm"], SCALAR_FLOOR * ref["gnorm"])
+    # the grad norm cannot move by more than the whole gradient does (|‖g + e‖ - ‖g‖| <= ‖e‖): besides its own band it
+    # is allowed the reference's per-tensor gradient bands aggregated over the step, sqrt(sum_k (band_k ‖m_k‖)^2) /
+    # ‖m‖ (m = 0.1 c g: the oracle's clipped gradient, tables at the touched rows -- zero elsewhere)
+    num = den = 0.0
+    for k, _ in A.param_shapes():
+        mk = ref["params"][k]["m"]
+        if mk is not None and k in band["grads"]:
+            n2 = float((mk.double() ** 2).sum())
+            num += (band["grads"][k] ** 2) * n2
+            den += n2
+    agg = (num / den) ** 0.5 if den > 0 else 0.0
+    within("gnorm", abs(got["gnorm"] - ref["gnorm"]), ref["gnorm"], max(band["scalars"]["gnorm"], agg),
+           SCALAR_FLOOR * ref["gnorm"])
     within("logits", float(np.linalg.norm(got["logits"] - ref["logits"])), float(np.linalg.norm(ref["logits"])),
            band["outputs"]["logits"])
     # top-K: the scores come from the query path (its GEMMs on bf16 operands), so a slot may differ where two

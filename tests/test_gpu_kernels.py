@@ -284,9 +284,9 @@ def _bfr32(t):
 def attn_bf_emulate(qkv, B, K, H, D, scale, rel, keep, dscale, do=None, do_stat=None, o_kernel=None):
     """fp64 emulation of the amp bf16 attention (attn_mf.hip): every MFMA operand rounded to bf16 exactly where the
     kernels round it -- q * scale (the fp32 product), k, v, dO, the masked unnormalised p (exp(s - max), before the
-    1 / l and dropout scales) in the forward, dS and p~ = p keep / (1 - p) in the backward -- everything else in
-    fp64: s = q k^T + rel (natural units; the kernels' log2 units are a change of base), softmax statistics, dS =
-    p (dp~ - D_i).  ``rel``: (K, K) bias or None; ``keep``: (B, H, K, K) bool or None; ``do_stat``: the dO
+    1 / l and dropout scales; for K > 64 as the two-term split hi + lo) in the forward, dS and p~ = p keep / (1 - p)
+    in the backward -- everything else in fp64: s = q k^T + rel (natural units; the kernels' log2 units are a change
+    of base), softmax statistics, dS = p (dp~ - D_i) with D_i = bf16(dO_i) . o_i.  ``rel``: (K, K) bias or None; ``keep``: (B, H, K, K) bool or None; ``do_stat``: the dO
     whose fp32 values form D_i = dO_i . o_i (the kernels take the fp32 dO and the forward's fp32 o,
     ``o_kernel``).  Returns o, and with ``do``: dq, dk, dv and the per-offset dS sums (2K - 1,) over samples and
     heads (offset j - i + K - 1)."""
@@ -302,13 +302,16 @@ def attn_bf_emulate(qkv, B, K, H, D, scale, rel, keep, dscale, do=None, do_stat=
     lsum = pe.sum(-1, keepdim=True)
     kf = keep.double() * dscale if keep is not None else None
     pm = pe * (keep.double() if keep is not None else 1.0)
-    o = (_bfr32(pm) @ vb) * ((dscale if keep is not None else 1.0) / lsum)
+    pmb = _bfr32(pm)
+    if K > 64:      # the two-term split of p (attn_mf.hip lo_bf4): hi = bf16(p), lo = bf16(p - hi)
+        pmb = pmb + _bfr32(pm - pmb)
+    o = (pmb @ vb) * ((dscale if keep is not None else 1.0) / lsum)
     o = o.transpose(1, 2).reshape(B * K, D)
     if do is None:
         return o
     dob = sh(_bfr32(do))
     ok = sh(o_kernel.double() if o_kernel is not None else o)
-    dst = sh(do_stat.double() if do_stat is not None else do.double())
+    dst = sh(_bfr32(do_stat) if do_stat is not None else _bfr32(do))      # D_i from bf16(dO), as the kernels
     Di = (dst * ok).sum(-1, keepdim=True)
     p_ = pe / lsum
     dp = dob @ vb.transpose(-1, -2)

@@ -255,6 +255,8 @@ def test_sharded_autograd_loop_matches_fused_step(tmp_path_factory):
     tables gathered from the shards, after 4 steps."""
     a = _run(tmp_path_factory, "sharded", 0, autograd=1)
     b = _run(tmp_path_factory, "sharded", 0)
+    # the optimizer step's replica check ran after every backward (and found the dense grads identical)
+    assert a["replica_checks"] == 4, a["replica_checks"]
     close_enough(np.asarray(a["losses"], np.float64), np.asarray(b["losses"], np.float64), 1e-5, 1e-6, "loss")
     assert a["sd"].keys() == b["sd"].keys()
     for k in a["sd"]:
@@ -271,8 +273,14 @@ def test_sharded_autograd_fused_optimizer_matches_fused_step(tmp_path_factory):
     b = _run(tmp_path_factory, "sharded", 0)
     close_enough(np.asarray(a["losses"], np.float64), np.asarray(b["losses"], np.float64), 1e-5, 1e-6, "loss")
     for k in b["sd"]:
-        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), 1e-5, 1e-6, k)
-        close_enough(a["m"][k].double().numpy().ravel(), b["m"][k].double().numpy().ravel(), 1e-4, 1e-9, "m:" + k)
+        # as the torch.optim loop above (1e-4: the MHA key bias's exact gradient is 0, so its rounding noise takes
+        # +-lr AdamW steps of either sign; its moments are left out of the comparison)
+        close_enough(a["sd"][k].double().numpy().ravel(), b["sd"][k].double().numpy().ravel(), 1e-4, 1e-6, k)
+        ma, mb = a["m"][k].double().numpy().ravel(), b["m"][k].double().numpy().ravel()
+        if k.endswith("mha.in_proj_bias"):
+            D = ma.size // 3
+            ma, mb = np.delete(ma, np.s_[D:2 * D]), np.delete(mb, np.s_[D:2 * D])
+        close_enough(ma, mb, 1e-4, 1e-9, "m:" + k)
 
 
 def test_sharded_autograd_reference_clip_is_refused(tmp_path_factory):

@@ -112,6 +112,28 @@ __device__ __forceinline__ u32x2 pk_bf4(f32x4 v) {
   return u32x2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
 }
 
+// The forward's P V product at K > 64 on a two-term bf16 split of p: hi = bf16(p) (the operand autocast's bf16 bmm
+// takes) and lo = bf16(p - hi) (the difference is exact in fp32), both against the same bf16 v, so o carries p to ~16
+// bits (K <= 64: bf16(p) alone, attn_fwd_mf_kernel).  The
+// backward's softmax statistic D_i = bf16(dO_i) . o_i is then the row sum of p_ij dP_ij (dP = bf16(dO) bf16(v)^T, the
+// MFMA product) to within that: the two sides of dS = p (dP - D) agree, as in the reference's fp32 softmax backward
+// (torch: p * (dP - sum(p * dP))).  With o from bf16(p) alone, D differed from sum p dP by the rounding of p (and,
+// with fp32 dO in D, of dO), and rows whose value vectors are all equal (a history of pads only: exact dS = 0) got a
+// dS of that rounding's size -- amplified by 1 / rms of the zero rows at the first layer's norm (cfg4 at B = 1024:
+// 11 % on the layer-0 MHA bias grads against the reference's own 0.8 %).
+__device__ __forceinline__ bf16x4 lo_bf4(const float (&pe)[4], bf16x4 hi) {
+  f32x4 d;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) d[r] = pe[r] - (float)hi[r];
+  return __builtin_bit_cast(bf16x4, pk_bf4(d));
+}
+
+// four fp32 values rounded to bf16 (RNE) and back
+__device__ __forceinline__ f32x4 bfr4(f32x4 v) {
+  const bf16x4 b = __builtin_bit_cast(bf16x4, pk_bf4(v));
+  return f32x4{(float)b[0], (float)b[1], (float)b[2], (float)b[3]};
+}
+
 // all-reduce over the four 16-lane groups (lanes c, c+16, c+32, c+48) by two permlane swaps of two copies of
 // the value: v_permlane16_swap leaves rows (r0 r0 r2 r2) in one copy and (r1 r1 r3 r3) in the other,
 // v_permlane32_swap (lo lo) / (hi hi).  In asm: through __builtin_amdgcn_permlane16/32_swap the compiler
@@ -323,7 +345,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
     mx = grp_max(mx);
     float l = 0.f;
     uint32_t dropped = 0u;
-    bf16x4 pb[NT];
+    f32x4 oacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int tj = 0; tj < NT; ++tj) {
       float pe[4];
@@ -369,12 +391,13 @@ __global__ __launch_bounds__(256) void attn_fwd_mf_kernel(AttnBfArgs a) {
           dropped |= m & (1u << (4 * tj + r));
         }
       }
-      pb[tj] = __builtin_bit_cast(bf16x4, pk_bf4(f32x4{pe[0], pe[1], pe[2], pe[3]}));
+      const bf16x4 pb = __builtin_bit_cast(bf16x4, pk_bf4(f32x4{pe[0], pe[1], pe[2], pe[3]}));
+      oacc = mma(vtop[tj], pb, oacc);                                                  // o^T [d][i]
+      // K > 64: p as hi + lo (lo_bf4); K <= 64 keeps bf16(p) alone -- the bits of attn_layer_fwd_kernel, whose
+      // registers (64 at eight waves per SIMD) hold no lo term
+      if constexpr (NT > 4) oacc = mma(vtop[tj], lo_bf4(pe, pb), oacc);
     }
     l = grp_sum(l);
-    f32x4 oacc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int tj = 0; tj < NT; ++tj) oacc = mma(vtop[tj], pb[tj], oacc);               // o^T [d][i]
     if (i < K) {
       const float inv = dsc / l;
       if (4 * g < DH) *(f32x4*)(a.o + ((long)b * K + i) * D + h * DH + 4 * g) = oacc * inv;
@@ -518,7 +541,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       float s = 0.f;
 #pragma unroll
       for (int q = 0; q < DH / 4; ++q) {
-        const f32x4 x = opj ? *(const f32x4*)(dot + lane * GD + w * DH + 4 * q) : do_row[q], y = o_row[q];
+        // D_i from bf16(dO): the dO operand the dP product takes (lo_bf4 above)
+        const f32x4 x = bfr4(opj ? *(const f32x4*)(dot + lane * GD + w * DH + 4 * q) : do_row[q]), y = o_row[q];
         s = fmaf(x[0], y[0], s);
         s = fmaf(x[1], y[1], s);
         s = fmaf(x[2], y[2], s);
@@ -755,11 +779,12 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
     const int row = lane + 64 * u;
     float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < DH / 4; ++q) {
-      s = fmaf(rdo[u][q][0], ro[u][q][0], s);
-      s = fmaf(rdo[u][q][1], ro[u][q][1], s);
-      s = fmaf(rdo[u][q][2], ro[u][q][2], s);
-      s = fmaf(rdo[u][q][3], ro[u][q][3], s);
+    for (int q = 0; q < DH / 4; ++q) {     // D_i from bf16(dO), as attn_bwd_mf_kernel
+      const f32x4 x = bfr4(rdo[u][q]);
+      s = fmaf(x[0], ro[u][q][0], s);
+      s = fmaf(x[1], ro[u][q][1], s);
+      s = fmaf(x[2], ro[u][q][2], s);
+      s = fmaf(x[3], ro[u][q][3], s);
     }
     if (row < KT) stw[row] = row < K ? f32x4{rm[u], 1.0f / rl[u], s, 0.f} : f32x4{0.f, 0.f, 0.f, 0.f};
   }

@@ -289,6 +289,7 @@ class CTRModel(nn.Module):
         ``nn.utils.clip_grad_norm_(model.parameters())``, whose norm on row-sharded tables is the local one -- shows
         as ranks disagreeing on them.  Raises instead of letting the replicas drift apart."""
         from . import dist as D
+        self.__dict__["replica_checks"] = self.__dict__.get("replica_checks", 0) + 1
         gs = [p.grad for k, p in self.named_parameters() if self.arena.kind[k] != "table" and p.grad is not None]
         s = torch.stack([g.double().sum() for g in gs]).sum() if gs else torch.zeros((), dtype=torch.float64,
                                                                                    device=self.arena.device)
