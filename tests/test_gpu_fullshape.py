@@ -304,12 +304,22 @@ def test_full_shape_step_matches_oracle(shape, oracle_step, oracle64):
                 # a gradient the fp32 oracle itself gets only to a few 1e-4 (the moments went to the fp64 arbiter):
                 # the update of the first AdamW step from the fp64 moments, d64; the HIP step within 1e-2 lr of it
                 # where the fp32 oracle is, and no further from it than twice the oracle anywhere
+                # "resolved" elements: |m64| at least 10x the fp32 oracle's rms error on the tensor's moments -- where
+                # fp32 resolves the gradient at all, the step (lr g / (|g| + eps) from zero moments) is fixed to far
+                # below 1e-2 lr; elsewhere fp32 rounding decides it, in the oracle as here (within one lr, above)
                 m64, v64 = (t.numpy().ravel() for t in oracle64()[k])
                 d64 = base * (1 - LR * WD) - LR * (m64 / 0.1) / (np.sqrt(v64 / 1e-3) + 1e-8) - base
-                tol = np.maximum(1e-2 * LR, 2.0 * np.abs(dr - d64)) + ulp
-                assert (np.abs(dg - d64)[strong] <= tol[strong]).all(), k
-                assert np.linalg.norm(dg[good] - d64[good]) <= max(1e-4 * np.linalg.norm(d64[good]),
-                                                                   2.0 * np.linalg.norm(dr[good] - d64[good])), k
+                noise = np.sqrt(np.mean((r["m"].numpy().ravel() - m64) ** 2))
+                res = np.abs(m64) >= 10.0 * noise
+                # + what that noise moves the step by where |g| is not far above eps: d/dg lr g / (|g| + eps) =
+                # lr eps / (|g| + eps)^2, times 3x the gradient noise (g = m / 0.1 after a first step)
+                g64 = np.abs(m64) / 0.1
+                sens = LR * 1e-8 / (g64 + 1e-8) ** 2 * (3.0 * noise / 0.1)
+                bad = res & (np.abs(dg - d64) > 1e-2 * LR + sens + ulp)
+                assert not bad.any(), (k, int(res.sum()), np.argwhere(bad)[:5].ravel(), (dg - d64)[bad][:5] / LR)
+                rg = good & res
+                assert np.linalg.norm(dg[rg] - d64[rg]) <= max(1e-4 * np.linalg.norm(d64[rg]),
+                                                               2.0 * np.linalg.norm(dr[rg] - d64[rg])), k
             else:
                 assert (np.abs(dg - dr)[strong] <= 1e-2 * LR + ulp[strong]).all(), k
                 close_enough(dg[good], dr[good], 1e-4, 0.0, f"dp:{k}", ulp[good], elem_rtol=1e-2)
