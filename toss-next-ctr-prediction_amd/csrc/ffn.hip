@@ -1831,6 +1831,10 @@ __global__ __launch_bounds__(512) void ffn_bwd_own_kernel(FfnArgs a, int steps_p
   };
 
   // ---- the step pipeline
+  // static priority for the second-dispatched half of the workgroup (MI355X_MICROARCH.md, two waves per SIMD item 4):
+  // the SIMD partners run the same step in lockstep and the younger half loses every arbitration (128.1 / 129.5 /
+  // 132.4 -> 127.4 / 126.0 / 131.6 us, profiles/r06/ab_ffn_bwd_prio.log)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
   Raw rc, rn;
   float dh2c[VPL], dh2n[VPL];
   if (s0 < s1) {
