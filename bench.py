@@ -114,11 +114,14 @@ def kernel_work(name, a, B, ffn_M, amp="bf16", ffn_flags=0):
         return {"flops": [(4.0 * B * K * K * D, "bf16")], "bytes": float(fwd_b + mask_bf)}
     if name == "ctr_attn_bwd_bf":
         return {"flops": [(8.0 * B * K * K * D, "bf16")], "bytes": float(bwd_b + mask_bf)}
-    if name == "ctr_attn_bwd_bf_oproj":     # reads dh1 rows in place of dO (same bytes)
-        return {"flops": [(8.0 * B * K * K * D, "bf16"), (2.0 * B * K * D * D, "f32")], "bytes": float(bwd_b + mask_bf)}
-    if name == "ctr_attn_layer_fwd_bf":
+    if name in ("ctr_attn_bwd_bf_oproj", "ctr_attn_bwd_bf_oproj16"):   # reads dh1 rows in place of dO (same bytes)
+        q16 = 12 * D * B * K if name.endswith("16") else 0                # qkv read, dqkv written in bf16
+        return {"flops": [(8.0 * B * K * K * D, "bf16"), (2.0 * B * K * D * D, "f32")],
+                "bytes": float(bwd_b - q16 + mask_bf)}
+    if name in ("ctr_attn_layer_fwd_bf", "ctr_attn_layer_fwd_bf16"):
+        qkv_b = 6 * D if name.endswith("16") else 12 * D
         return {"flops": [(4.0 * B * K * K * D, "bf16"), (8.0 * B * K * D * D, "f32")],
-                "bytes": float(B * K * (28 * D + 4 + 8 * H) + mask_bf)}
+                "bytes": float(B * K * (16 * D + qkv_b + 4 + 8 * H) + mask_bf)}
     if name in ("ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd") and a.use_qnn:
         F, QR = a.F, a.qh * a.qr
         if name == "ctr_qnn_gram_fwd":     # z read; zsum, G (D x D), S, quad written
@@ -305,7 +308,9 @@ def pmc_traffic(name):
              "ctr_attn_bwd": ("attn_bwd_wave_kernel", "attn_bwd_kernel"),
              "ctr_attn_fwd": ("attn_fwd_pk_kernel", "attn_fwd_kernel"),
              "ctr_attn_bwd_bf": ("attn_bwd_mf_kernel",), "ctr_attn_fwd_bf": ("attn_fwd_mf_kernel",),
-             "ctr_attn_layer_fwd_bf": ("attn_layer_fwd_kernel",), "ctr_attn_bwd_bf_oproj": ("attn_bwd_mf_kernel",)}.get(name)
+             "ctr_attn_layer_fwd_bf": ("attn_layer_fwd_kernel",), "ctr_attn_bwd_bf_oproj": ("attn_bwd_mf_kernel",),
+             "ctr_attn_layer_fwd_bf16": ("attn_layer_fwd_kernel",),
+             "ctr_attn_bwd_bf_oproj16": ("attn_bwd_mf_kernel",)}.get(name)
     if kerns is None:
         return None
     base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS
@@ -541,6 +546,7 @@ def main():
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd",
                   "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj",
+                  "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16",
                   "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd", "ctr_gemm_bf16_ex")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",

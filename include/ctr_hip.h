@@ -117,6 +117,14 @@ int ctr_rowgemm(int M, int K, int N, const float* A, int lda, const float* W, in
 int ctr_rowgemm_wgrad_rows(int M);
 int ctr_rowgemm_wgrad(const float* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN, float* slab,
                       long ld_slab, int o_db, void* stream);
+/* amp: bf16 -- the in-projection's backward on the bf16 dqkv of ctr_attn_bwd_bf_oproj16 (uint16_t = bf16 bits,
+ * widened exactly; W, X, the bias sums and the outputs fp32): ctr_rowgemm_a16 = ctr_rowgemm with a bf16 A,
+ * (K, N) = (96, 32), epilogue + bias / + add; ctr_rowgemm_wgrad_y16 = ctr_rowgemm_wgrad with a bf16 dY,
+ * (NO, NIN) = (96, 32).  Same bits as the fp32 forms on the widened values.                                  */
+int ctr_rowgemm_a16(int M, int K, int N, const uint16_t* A, int lda, const float* W, int tb, float* C, int ldc,
+                    const float* bias, const float* add, int ld_add, void* stream);
+int ctr_rowgemm_wgrad_y16(const uint16_t* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN, float* slab,
+                          long ld_slab, int o_db, void* stream);
 /* amp: bf16 forms of the two above for D = 64 (cfgs/v3_k148_s1.yaml; the reference's autocast F.linear,
  * src/train.py:158-168 over src/models/dare.py:53-62): operands rounded to bf16 (RNE), fp32 accumulation
  * and fp32 outputs, same arguments and epilogues.  (K, N): (64,64) (64,192) (192,64); wgrad (NO, NIN):
@@ -241,6 +249,20 @@ int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const floa
                           float drop_scale, uint32_t* mask, const float* w_out, const float* b_out, const float* nw1,
                           float eps, float* qkv, float* o, float* mrow, float* lrow, float* h1, float* r1, float* x1,
                           void* stream);
+/* amp: bf16 -- the saved projections in bf16 (uint16_t = bf16 bits).  ctr_attn_layer_fwd_bf16 writes qkv16 (B*K x 96)
+ * = the operands the attention products take: bf16(q * scale) | bf16(k) | bf16(v) (RNE of the fp32 qkv the fp32 form
+ * writes; all other outputs identical); ctr_attn_bwd_bf_oproj16 stages them as they are (the same dq / dk / dv as
+ * ctr_attn_bwd_bf_oproj on the fp32 qkv) and writes dqkv16 = bf16(dq) | bf16(dk) | bf16(dv) (RNE) -- the dtype of the
+ * reference's autocast in-projection output and its grad.  Consumers: ctr_rowgemm_a16, ctr_rowgemm_wgrad_y16.      */
+int ctr_attn_layer_fwd_bf16(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
+                            const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key,
+                            uint32_t drop_thresh, float drop_scale, uint32_t* mask, const float* w_out, const float* b_out,
+                            const float* nw1, float eps, uint16_t* qkv16, float* o, float* mrow, float* lrow, float* h1,
+                            float* r1, float* x1, void* stream);
+int ctr_attn_bwd_bf_oproj16(const uint16_t* qkv16, const float* o, const float* dh1, const float* w_out, int B, int K,
+                            int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
+                            uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
+                            const float* lrow, uint16_t* dqkv16, float* drel_part, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused position-wise FFN + residual + RMSNorm of DAREEncoderLayer, src/models/dare.py:53-70

@@ -234,7 +234,7 @@ def _hip_step(shape, amp, record=()):
     _lib.time_calls(())
     eng = model.engine
     flags = {"attn_bf": eng.attn_bf, "attn_layer": eng.attn_layer, "attn_oproj": eng.attn_oproj,
-             "ffn_flags": eng.ffn_flags, "bf16": eng.bf16, "rowgemm_bf": eng.rowgemm_bf}
+             "ffn_flags": eng.ffn_flags, "bf16": eng.bf16, "rowgemm_bf": eng.rowgemm_bf, "qkv16": eng.qkv16}
     sv = eng.last
     res = {"loss": loss, "logits": sv["logits"].double().cpu().numpy(), "idx": sv["idx"].cpu().numpy().astype(np.int64),
            "gnorm": float(opt.norm_out[0].item()), "calls": calls, "flags": flags, "params": {}}
@@ -352,7 +352,9 @@ def test_full_shape_step_matches_oracle(shape, oracle_step, oracle64):
 # the entry points of the step bench.py times under amp: bf16 (tossctr/engine.py), per config: the fused layer
 # forward / oproj-folded attention backward at K <= 64, D = 32 (cfg2); the separate bf16 attention kernels at K > 64
 # (cfg3, cfg4: attn_bwd_mfl_kernel) and the D = 64 bf16 row kernels (cfg4)
+# (cfg2 with the bf16 qkv / dqkv: the *16 forms and the in-projection backward on the bf16 grad)
 BF16_ENTRY_POINTS = ("ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj", "ctr_attn_fwd_bf", "ctr_attn_bwd_bf",
+                     "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16", "ctr_rowgemm_a16", "ctr_rowgemm_wgrad_y16",
                      "ctr_ffn_fwd", "ctr_ffn_bwd_norms", "ctr_gemm_bf16_ex", "ctr_rowgemm_bf", "ctr_rowgemm")
 
 
@@ -369,7 +371,8 @@ def test_full_shape_bf16_step(shape, oracle_step):
     assert fl["bf16"] and fl["attn_bf"] and fl["ffn_flags"] == 1, fl
     if A.top_k <= 64:
         assert fl["attn_layer"] and fl["attn_oproj"], fl
-        assert c.get("ctr_attn_layer_fwd_bf") == nl and c.get("ctr_attn_bwd_bf_oproj") == nl, c
+        assert c.get("ctr_attn_layer_fwd_bf16") == nl and c.get("ctr_attn_bwd_bf_oproj16") == nl, c
+        assert fl["qkv16"] and c.get("ctr_rowgemm_a16") == nl and c.get("ctr_rowgemm_wgrad_y16") == nl, (fl, c)
     else:
         assert not fl["attn_layer"] and not fl["attn_oproj"], fl
         assert c.get("ctr_attn_fwd_bf") == nl and c.get("ctr_attn_bwd_bf") == nl, c

@@ -610,13 +610,24 @@ def test_attn_layer_fwd_equals_three_launches(K, H, p, bias):
            ptr(f_relmean) if bias else None, tk, scale, *dk, ptr(f["mask"]),
            ptr(w_out), ptr(b_out), ptr(nw), 1e-6, ptr(f["qkv"]), ptr(f["o"]), ptr(f["mrow"]), ptr(f["lrow"]),
            ptr(f["h1"]), ptr(f["r1"]), ptr(f["x1"]), st)
+    # the bf16-qkv form: every other output the same bits, qkv16 = bf16(q * scale) | bf16(k) | bf16(v) (RNE)
+    h = bufs()
+    qkv16 = torch.full((B * K, 3 * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+    L.call("ctr_attn_layer_fwd_bf16", ptr(x), B, K, H, D, ptr(w_in), ptr(b_in), ptr(rel_w) if bias else None,
+           ptr(f_relmean) if bias else None, tk, scale, *dk, ptr(h["mask"]),
+           ptr(w_out), ptr(b_out), ptr(nw), 1e-6, ptr(qkv16), ptr(h["o"]), ptr(h["mrow"]), ptr(h["lrow"]),
+           ptr(h["h1"]), ptr(h["r1"]), ptr(h["x1"]), st)
     torch.cuda.synchronize()
     for name in r:
         a, b = r[name], f[name]
         assert torch.equal(a.view(torch.int32), b.view(torch.int32)), \
             (name, int((a.view(torch.int32) != b.view(torch.int32)).sum()), a.numel())
+        if name != "qkv":
+            assert torch.equal(a.view(torch.int32), h[name].view(torch.int32)), name
     if bias:     # the head-mean table the kernel formed and wrote for the backward
         assert torch.equal(relmean.view(torch.int32), f_relmean.view(torch.int32))
+    want = torch.cat([r["qkv"][:, :D] * scale, r["qkv"][:, D:]], 1).bfloat16()
+    assert torch.equal(qkv16.view(torch.int16), want.view(torch.int16)), int((qkv16 != want).sum())
 
 
 @pytest.mark.parametrize("K,H,p", [(60, 8, 0.1), (64, 8, 0.1), (61, 8, 0.1), (48, 4, 0.2), (33, 8, 0.0),
@@ -656,10 +667,56 @@ def test_attn_bwd_oproj_equals_two_launches(K, H, p, bias):
     f_drp = torch.full_like(r_drp, float("nan"))
     L.call("ctr_attn_bwd_bf_oproj", ptr(qkv), ptr(o), ptr(dh1), ptr(w_out), B, K, H, D, rm, tk, scale, *dk, ptr(mask),
            ptr(mrow), ptr(lrow), ptr(f_dqkv), ptr(f_drp), st)
+    # the bf16 form: qkv16 as the layer forward stores it, dqkv16 = the RNE bf16 of the same dq / dk / dv
+    qkv16 = torch.cat([qkv[:, :D] * scale, qkv[:, D:]], 1).bfloat16()
+    h_dqkv = torch.full((B * K, 3 * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+    h_drp = torch.full_like(r_drp, float("nan"))
+    L.call("ctr_attn_bwd_bf_oproj16", ptr(qkv16), ptr(o), ptr(dh1), ptr(w_out), B, K, H, D, rm, tk, scale, *dk,
+           ptr(mask), ptr(mrow), ptr(lrow), ptr(h_dqkv), ptr(h_drp), st)
     torch.cuda.synchronize()
     assert torch.equal(r_dqkv.view(torch.int32), f_dqkv.view(torch.int32)), int((r_dqkv != f_dqkv).sum())
+    assert torch.equal(h_dqkv.view(torch.int16), r_dqkv.bfloat16().view(torch.int16)), \
+        int((h_dqkv != r_dqkv.bfloat16()).sum())
     if bias:
         assert torch.equal(r_drp.view(torch.int32), f_drp.view(torch.int32))
+        assert torch.equal(r_drp.view(torch.int32), h_drp.view(torch.int32))
+
+
+@pytest.mark.parametrize("M", [245760, 1000, 33, 1])
+@pytest.mark.parametrize("add", [True, False])
+def test_rowgemm_bf16_operand_forms_equal_fp32_forms(M, add):
+    """amp: the in-projection backward on the bf16 dqkv -- ctr_rowgemm_a16 and ctr_rowgemm_wgrad_y16 -- give the bits
+    of ctr_rowgemm / ctr_rowgemm_wgrad on the same values widened to fp32 (M = 245,760 is cfg2's B*K)."""
+    L = _lib()
+    D = 32
+    g = torch.Generator(device="cuda").manual_seed(M + add)
+    dq16 = torch.randn(M, 3 * D, device="cuda", generator=g).bfloat16()
+    dq32 = dq16.float()
+    W = torch.randn(3 * D, D, device="cuda", generator=g) * D ** -0.5
+    dh1 = torch.randn(M, D, device="cuda", generator=g)
+    x = torch.randn(M, D, device="cuda", generator=g)
+    st = stream()
+    ref = torch.full((M, D), float("nan"), device="cuda")
+    got = torch.full_like(ref, float("nan"))
+    L.call("ctr_rowgemm", M, 3 * D, D, ptr(dq32), 3 * D, ptr(W), 0, ptr(ref), D, None, ptr(dh1) if add else None,
+           D if add else 0, None, 0, None, None, None, 1e-6, st)
+    L.call("ctr_rowgemm_a16", M, 3 * D, D, ptr(dq16), 3 * D, ptr(W), 0, ptr(got), D, None, ptr(dh1) if add else None,
+           D if add else 0, st)
+    rows = L.query("ctr_rowgemm_wgrad_rows", M)
+    o_db = 3 * D * D
+    ld = (o_db + 3 * D + 3) // 4 * 4
+    s_ref = torch.zeros(rows, ld, device="cuda")
+    s_got = torch.zeros(rows, ld, device="cuda")
+    L.call("ctr_rowgemm_wgrad", ptr(dq32), 3 * D, ptr(x), D, M, 3 * D, D, ptr(s_ref), ld, o_db, st)
+    L.call("ctr_rowgemm_wgrad_y16", ptr(dq16), 3 * D, ptr(x), D, M, 3 * D, D, ptr(s_got), ld, o_db, st)
+    torch.cuda.synchronize()
+    assert torch.equal(ref.view(torch.int32), got.view(torch.int32)), int((ref != got).sum())
+    assert torch.equal(s_ref.view(torch.int32), s_got.view(torch.int32)), int((s_ref != s_got).sum())
+    want = dq32.double() @ W.double() + (dh1.double() if add else 0.0)
+    assert float((ref.double() - want).norm() / want.norm()) < 1e-6
+    dw = s_ref.double().sum(0)
+    assert float((dw[:o_db].view(3 * D, D) - dq32.double().t() @ x.double()).norm() /
+                 (dq32.double().t() @ x.double()).norm()) < 1e-6
 
 
 @pytest.mark.parametrize("B,F,D,fe,bias", [(4096, 82, 32, 16, True), (4096, 82, 32, 16, False), (1000, 35, 64, 8, True),

@@ -24,7 +24,7 @@ pmc() {  # name config counters...
   local name=$1 cfg=$2
   shift 2
   timeout -s KILL 150 rocprofv3 --pmc "$@" --output-format csv -d "$out/pmc_$name" -o "$name" -- \
-      python bench.py --config "$cfg" --steps 3 --warmup 2 --no-cpu-baseline --markers > "$out/pmc_$name.log" 2>&1
+      python bench.py --config "$cfg" --steps 3 --warmup 2 --no-cpu-baseline --no-fp32-secondary --markers > "$out/pmc_$name.log" 2>&1
 }
 pmc_groups() {  # suffix config
   pmc "fetch$1" "$2" FETCH_SIZE
@@ -41,12 +41,12 @@ for s in $steps; do
   case $s in
     trace)
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o trace -- \
-          python bench.py --steps 20 --warmup 10 --no-cpu-baseline --markers > "$out/trace.log" 2>&1 ;;
+          python bench.py --steps 20 --warmup 10 --no-cpu-baseline --no-fp32-secondary --markers > "$out/trace.log" 2>&1 ;;
     pmc) pmc_groups "" cfg2 ;;
     pmc4) pmc_groups "_cfg4" cfg4 ;;
     trace4)
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace4" -o trace4 -- \
-          python bench.py --config cfg4 --steps 6 --warmup 3 --no-cpu-baseline --markers > "$out/trace4.log" 2>&1 ;;
+          python bench.py --config cfg4 --steps 6 --warmup 3 --no-cpu-baseline --no-fp32-secondary --markers > "$out/trace4.log" 2>&1 ;;
     bench)
       timeout -k 10 240 python bench.py > "$out/bench_n1.log" 2>&1
       timeout -k 10 120 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$out/bench_n1_s20.log" 2>&1 ;;

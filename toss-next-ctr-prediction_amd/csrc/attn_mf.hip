@@ -61,6 +61,12 @@ struct AttnBfArgs {
   int ngrp;              // head groups per sample (H / G)
   const float* dh1;      // backward with the out-projection fused (nt <= 4, D = 32): dO = dh1 W_out computed in
   const float* w_out;    // the kernel from the (B*K, 32) rows dh1 and W_out (32, 32); dO is then unused
+  // amp: the bf16 forms of the saved projections (null: the fp32 ones above).  qkv16 (B*K, 3D) holds the staged
+  // operands themselves -- bf16(q * scale), bf16(k), bf16(v), the values both attention products take -- so the
+  // backward stages them as they are; dqkv16 (B*K, 3D) receives bf16(dq), bf16(dk), bf16(dv) (RNE), the dtype of
+  // the reference's autocast in-projection output grad
+  const __bf16* qkv16;
+  __bf16* dqkv16;
 };
 
 // workgroup -> (sample, head group), 1-D grid: with ngrp > 1 head groups a sample's workgroups are 8 apart in
@@ -89,6 +95,7 @@ __device__ __forceinline__ bf16x4 tr4(const __bf16* p) {
 __device__ __forceinline__ bf16x4 ld4(const __bf16* p) { return *(const bf16x4*)p; }
 
 __device__ __forceinline__ bf16x4 to_bf4(f32x4 v) { return __builtin_convertvector(v, bf16x4); }
+__device__ __forceinline__ f32x4 to_f4(bf16x4 v) { return __builtin_convertvector(v, f32x4); }
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 // all ones where x's sign bit is set (v_ashrrev_i32 in asm: as C the compiler turns it back into a compare +
 // select, which keeps the lane masks in SGPRs)
@@ -110,6 +117,12 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u32x2 pk_bf4(f32x4 v) {
   const bf16x2 lo = __builtin_convertvector(f32x2{v[0], v[1]}, bf16x2), hi = __builtin_convertvector(f32x2{v[2], v[3]}, bf16x2);
   return u32x2{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+}
+
+// one 4-column piece of a dq / dk / dv row at element offset off of the (B*K, 3D) gradient: fp32, or bf16 (RNE)
+__device__ __forceinline__ void store_dqkv(const AttnBfArgs& a, long off, f32x4 v) {
+  if (a.dqkv16) *(u32x2*)(a.dqkv16 + off) = pk_bf4(v);
+  else *(f32x4*)(a.dqkv + off) = v;
 }
 
 // The forward's P V product at K > 64 on a two-term bf16 split of p: hi = bf16(p) (the operand autocast's bf16 bmm
@@ -207,10 +220,18 @@ __device__ __forceinline__ void stage(const AttnBfArgs& a, int b, int hg, __bf16
       const int u = ch / NCD, dc = ch - u * NCD;
       o = j * S::RS + u * DH + 4 * dc;
       if (u < G && j < K) {
-        const float* r = base + (long)j * 3 * D + u * DH + 4 * dc;
-        q = *(const f32x4*)r * a.scale;
-        k = *(const f32x4*)(r + D);
-        v = *(const f32x4*)(r + 2 * D);
+        const long e0 = (long)j * 3 * D + u * DH + 4 * dc;
+        if (a.qkv16) {      // the forward's staged values (q already scaled): converted back exactly
+          const __bf16* r = a.qkv16 + (long)b * K * 3 * D + hg * G * DH + e0;
+          q = to_f4(*(const bf16x4*)r);
+          k = to_f4(*(const bf16x4*)(r + D));
+          v = to_f4(*(const bf16x4*)(r + 2 * D));
+        } else {
+          const float* r = base + e0;
+          q = *(const f32x4*)r * a.scale;
+          k = *(const f32x4*)(r + D);
+          v = *(const f32x4*)(r + 2 * D);
+        }
         if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * dc);
       }
     } else if (ch == 4 * NCD) {                   // the row's mask chunk
@@ -611,16 +632,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     }
     __builtin_amdgcn_wave_barrier();
     if (4 * g < DH && j < K) {
-      float* dst = a.dqkv + ((long)b * K + j) * 3 * D + h * DH + 4 * g;
-      *(f32x4*)(dst + D) = dk;
-      *(f32x4*)(dst + 2 * D) = dv;
+      const long off = ((long)b * K + j) * 3 * D + h * DH + 4 * g;
+      store_dqkv(a, off + D, dk);
+      store_dqkv(a, off + 2 * D, dv);
     }
   }
   if (4 * g < DH) {
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int i = 16 * ti + c;
-      if (i < K) *(f32x4*)(a.dqkv + ((long)b * K + i) * 3 * D + h * DH + 4 * g) = dq[ti] * a.scale;
+      if (i < K) store_dqkv(a, ((long)b * K + i) * 3 * D + h * DH + 4 * g, dq[ti] * a.scale);
     }
   }
   if (BIAS) {
@@ -881,9 +902,9 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
 #endif
     }
     if (4 * g < DH && j < K) {
-      float* dst = a.dqkv + ((long)b * K + j) * 3 * D + h * DH + 4 * g;
-      *(f32x4*)(dst + D) = dk;
-      *(f32x4*)(dst + 2 * D) = dv;
+      const long off = ((long)b * K + j) * 3 * D + h * DH + 4 * g;
+      store_dqkv(a, off + D, dk);
+      store_dqkv(a, off + 2 * D, dv);
     }
     if (BIAS) {
       fold(tj, win[0]);
@@ -899,7 +920,7 @@ void attn_bwd_mfl_kernel(AttnBfArgs a) {
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int i = 16 * ti + c;
-      if (i < K) *(f32x4*)(a.dqkv + ((long)b * K + i) * 3 * D + h * DH + 4 * g) = dq[ti] * a.scale;
+      if (i < K) store_dqkv(a, ((long)b * K + i) * 3 * D + h * DH + 4 * g, dq[ti] * a.scale);
     }
   }
   if (BIAS) {
@@ -953,7 +974,8 @@ struct LayerFwdArgs {
   const float* rel_w;     // pbias.rel.weight (2tk+1, H): the head-mean bias formed here (null: no bias) ...
   float* relmean;         // ... and written by workgroup 0 for the backward (ctr_pos_bias_mean's bits)
   float eps;
-  float* qkv;             // (B*K, 96) saved for the backward
+  float* qkv;             // (B*K, 96) saved for the backward, or (qkv16, amp) its bf16 staged form:
+  __bf16* qkv16;          // bf16(q * scale) | bf16(k) | bf16(v), copied from the LDS images
   float* h1;              // (B*K, 32) pre-norm sum, r1 (B*K) its rsqrt, x1 (B*K, 32) the layer's next input
   float* r1;
   float* x1;
@@ -1022,12 +1044,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) void a
     for (int r = 0; r < 4; ++r) {
       const int i = 16 * rb + 4 * g + r;
       const float v = acc[r] + bias;
-      if (i < K) L.qkv[(row0 + i) * (3 * lf::D) + n] = v;
+      if (i < K && !L.qkv16) L.qkv[(row0 + i) * (3 * lf::D) + n] = v;
       __bf16* dst = sec == 0 ? sq : sec == 1 ? sk : sv;
       dst[i * lf::RS + col] = (__bf16)(i < K ? (sec == 0 ? v * a.scale : v) : 0.f);
     }
   }
   lds_barrier();
+  if (L.qkv16) {    // amp: the staged images are what the backward stages -- 16-byte row pieces, 12 a row
+    for (int e = tid; e < K * 12; e += 64 * G) {
+      const int i = e / 12, ch = e - 12 * i, sec = ch >> 2, c8 = 8 * (ch & 3);
+      const __bf16* src = (sec == 0 ? sq : sec == 1 ? sk : sv) + i * lf::RS + c8;
+      *(uint4*)(L.qkv16 + (row0 + i) * (3 * lf::D) + 32 * sec + c8) = *(const uint4*)src;
+    }
+  }
   // ---- attention, wave w = head h (attn_fwd_mf_kernel's per-head body at nt = 4)
   {
     const int h = w, hs = h * DH;
@@ -1336,10 +1365,10 @@ extern "C" int ctr_attn_bwd_bf_oproj_ok(int K, int H, int D) {
   return (bf_ok(K, H, D) && K <= 64 && D == 32 && pick_g(H) == 4 && (4 * (D / H)) % 16 == 0) ? 1 : 0;
 }
 
-extern "C" int ctr_attn_bwd_bf_oproj(const float* qkv, const float* o, const float* dh1, const float* w_out, int B, int K,
-                                     int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
-                                     uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
-                                     const float* lrow, float* dqkv, float* drel_part, void* stream) {
+static int attn_bwd_oproj(const float* qkv, const __bf16* qkv16, const float* o, const float* dh1, const float* w_out,
+                          int B, int K, int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
+                          uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
+                          const float* lrow, float* dqkv, __bf16* dqkv16, float* drel_part, void* stream) {
   if (B == 0) return 0;
   CTR_REQUIRE(ctr_attn_bwd_bf_oproj_ok(K, H, D), "ctr_attn_bwd_bf_oproj: K <= 64, D = 32, 4 or 8 heads");
   CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
@@ -1349,22 +1378,39 @@ extern "C" int ctr_attn_bwd_bf_oproj(const float* qkv, const float* o, const flo
   a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
   a.mask = const_cast<uint32_t*>(mask); a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow);
   a.lrow = const_cast<float*>(lrow); a.dO = nullptr; a.dqkv = dqkv; a.drel_part = drel_part;
-  a.dh1 = dh1; a.w_out = w_out;
+  a.dh1 = dh1; a.w_out = w_out; a.qkv16 = qkv16; a.dqkv16 = dqkv16;
   hipStream_t s = (hipStream_t)stream;
   if (D / H == 4) launch_bwd2<4>(a, s);
   else launch_bwd2<8>(a, s);
   return check_launch("attn_bwd_bf_oproj");
 }
 
+extern "C" int ctr_attn_bwd_bf_oproj(const float* qkv, const float* o, const float* dh1, const float* w_out, int B, int K,
+                                     int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
+                                     uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
+                                     const float* lrow, float* dqkv, float* drel_part, void* stream) {
+  return attn_bwd_oproj(qkv, nullptr, o, dh1, w_out, B, K, H, D, relmean, tk, scale, drop_key, drop_thresh, drop_scale,
+                        mask, mrow, lrow, dqkv, nullptr, drel_part, stream);
+}
+
+extern "C" int ctr_attn_bwd_bf_oproj16(const uint16_t* qkv16, const float* o, const float* dh1, const float* w_out, int B,
+                                       int K, int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
+                                       uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
+                                       const float* lrow, uint16_t* dqkv16, float* drel_part, void* stream) {
+  CTR_REQUIRE(B == 0 || (qkv16 && dqkv16), "ctr_attn_bwd_bf_oproj16: qkv16 and dqkv16 are required");
+  return attn_bwd_oproj(nullptr, (const __bf16*)qkv16, o, dh1, w_out, B, K, H, D, relmean, tk, scale, drop_key,
+                        drop_thresh, drop_scale, mask, mrow, lrow, nullptr, (__bf16*)dqkv16, drel_part, stream);
+}
+
 extern "C" int ctr_attn_layer_fwd_ok(int K, int H, int D) {
   return (K >= 1 && K <= 64 && D == 32 && (H == 8 || H == 4)) ? 1 : 0;
 }
 
-extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
-                                     const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
-                                     float drop_scale, uint32_t* mask, const float* w_out, const float* b_out,
-                                     const float* nw1, float eps, float* qkv, float* o, float* mrow, float* lrow,
-                                     float* h1, float* r1, float* x1, void* stream) {
+static int attn_layer_fwd(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
+                          const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                          float drop_scale, uint32_t* mask, const float* w_out, const float* b_out, const float* nw1,
+                          float eps, float* qkv, __bf16* qkv16, float* o, float* mrow, float* lrow, float* h1, float* r1,
+                          float* x1, void* stream) {
   if (B == 0) return 0;
   CTR_REQUIRE(ctr_attn_layer_fwd_ok(K, H, D), "ctr_attn_layer_fwd_bf: K <= 64, D = 32, 4 or 8 heads");
   CTR_REQUIRE(!rel_w || (relmean && tk >= K - 1 && tk <= 64),
@@ -1377,7 +1423,7 @@ extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D,
   a.mask = mask; a.o = o; a.mrow = mrow; a.lrow = lrow;
   L.rel_w = rel_w; L.relmean = relmean;
   L.x = x; L.w_in = w_in; L.b_in = b_in; L.w_out = w_out; L.b_out = b_out; L.nw1 = nw1; L.eps = eps;
-  L.qkv = qkv; L.h1 = h1; L.r1 = r1; L.x1 = x1;
+  L.qkv = qkv; L.qkv16 = qkv16; L.h1 = h1; L.r1 = r1; L.x1 = x1;
   hipStream_t s = (hipStream_t)stream;
   const int nth = 64 * H;
   const int dk = drop_thresh == 0 ? 0 : (K & 1) ? 2 : 1;
@@ -1398,4 +1444,23 @@ extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D,
     if (rel_w) go(I8{}, BT{}); else go(I8{}, BF{});
   }
   return check_launch("attn_layer_fwd_bf");
+}
+
+extern "C" int ctr_attn_layer_fwd_bf(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
+                                     const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key, uint32_t drop_thresh,
+                                     float drop_scale, uint32_t* mask, const float* w_out, const float* b_out,
+                                     const float* nw1, float eps, float* qkv, float* o, float* mrow, float* lrow,
+                                     float* h1, float* r1, float* x1, void* stream) {
+  return attn_layer_fwd(x, B, K, H, D, w_in, b_in, rel_w, relmean, tk, scale, drop_key, drop_thresh, drop_scale, mask,
+                        w_out, b_out, nw1, eps, qkv, nullptr, o, mrow, lrow, h1, r1, x1, stream);
+}
+
+extern "C" int ctr_attn_layer_fwd_bf16(const float* x, int B, int K, int H, int D, const float* w_in, const float* b_in,
+                                       const float* rel_w, float* relmean, int tk, float scale, uint32_t drop_key,
+                                       uint32_t drop_thresh, float drop_scale, uint32_t* mask, const float* w_out,
+                                       const float* b_out, const float* nw1, float eps, uint16_t* qkv16, float* o,
+                                       float* mrow, float* lrow, float* h1, float* r1, float* x1, void* stream) {
+  CTR_REQUIRE(B == 0 || qkv16, "ctr_attn_layer_fwd_bf16: qkv16 is required");
+  return attn_layer_fwd(x, B, K, H, D, w_in, b_in, rel_w, relmean, tk, scale, drop_key, drop_thresh, drop_scale, mask,
+                        w_out, b_out, nw1, eps, nullptr, (__bf16*)qkv16, o, mrow, lrow, h1, r1, x1, stream);
 }

@@ -30,7 +30,7 @@ __device__ __forceinline__ f32x4 rg_mfma(float a, float b, f32x4 c) {
 
 struct RowGemmArgs {
   int M;
-  const float* A;
+  const void* A;           // float, or bf16 (the A16 forms: amp's bf16 dqkv, exact in fp32)
   int lda;
   const float* W;          // tb: (N, K) (nn.Linear weight: C = A W^T); else (K, N) (C = A W)
   int tb;
@@ -52,7 +52,9 @@ struct RowGemmArgs {
 #define RG_NI 2
 #endif
 
-template <int K, int N, bool SIDE>
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+template <int K, int N, bool SIDE, bool A16 = false>
 __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
   constexpr int KQ = K / 4, NJ = N / 16, NI = RG_NI;
   constexpr int NS = SIDE ? NJ : 1;      // per-row epilogue operand (add / residual) slots
@@ -92,8 +94,19 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
       // rows clamped into range, not skipped (a conditional load is a branch that waits for every load before
       // it); the results of rows past M are never stored
       const long row = min(b0 + 16 * i + c, a.M - 1);
+      if constexpr (A16) {     // 16-byte loads of 8 bf16, widened exactly
+        static_assert(KQ % 8 == 0, "bf16 A rows in 16-byte pieces");
+        const __bf16* ap = (const __bf16*)a.A + row * a.lda + g * KQ;
 #pragma unroll
-      for (int q = 0; q < KQ / 4; ++q) A[i][q] = *(const f32x4*)(a.A + row * a.lda + g * KQ + 4 * q);
+        for (int q = 0; q < KQ / 8; ++q) {
+          const bf16x8 v = *(const bf16x8*)(ap + 8 * q);
+          A[i][2 * q] = f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+          A[i][2 * q + 1] = f32x4{(float)v[4], (float)v[5], (float)v[6], (float)v[7]};
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < KQ / 4; ++q) A[i][q] = *(const f32x4*)((const float*)a.A + row * a.lda + g * KQ + 4 * q);
+      }
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const long orow = min(b0 + 16 * i + 4 * g + rr, a.M - 1);
@@ -169,8 +182,8 @@ __global__ __launch_bounds__(256) void rowgemm_kernel(RowGemmArgs a) {
 // unconditional, at rows clamped into the range, and dY of a row past it is zeroed at use).  db = colsum(dY) is a
 // per-lane VALU sum over the lane's rows, reduced over the four lane groups at the end.  The waves' partials are
 // summed in LDS in a fixed wave order and the workgroup writes one slab row -- deterministic.
-template <int NO, int NIN>
-__global__ __launch_bounds__(256) void rowgemm_wgrad_kernel(const float* __restrict__ dY, int ldy,
+template <int NO, int NIN, typename TY = float>
+__global__ __launch_bounds__(256) void rowgemm_wgrad_kernel(const TY* __restrict__ dY, int ldy,
                                                             const float* __restrict__ X, int ldx, int M,
                                                             int rows_per_wg, float* __restrict__ slab,
                                                             long ld_slab, int o_db) {
@@ -195,7 +208,7 @@ __global__ __launch_bounds__(256) void rowgemm_wgrad_kernel(const float* __restr
     for (int u = 0; u < U; ++u) {
       const long m = min(m0 + 4 * u + g, m_end - 1);
 #pragma unroll
-      for (int i = 0; i < IO; ++i) ay[u][i] = dY[m * ldy + 16 * i + c];
+      for (int i = 0; i < IO; ++i) ay[u][i] = (float)dY[m * ldy + 16 * i + c];
 #pragma unroll
       for (int j = 0; j < JW; ++j) bx[u][j] = X[m * ldx + 16 * j + c];
     }
@@ -266,12 +279,12 @@ __global__ __launch_bounds__(256) void rowgemm_wgrad_kernel(const float* __restr
 }
 
 // persistent grid: as many workgroups as fit the chip at once (register-limited occupancy)
-template <int K, int N, bool SIDE>
+template <int K, int N, bool SIDE, bool A16 = false>
 static int resident_grid(int M) {
   static int per_cu = 0;
   if (per_cu == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rowgemm_kernel<K, N, SIDE>, 256, 0) != hipSuccess || nb < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rowgemm_kernel<K, N, SIDE, A16>, 256, 0) != hipSuccess || nb < 1)
       nb = 1;
     per_cu = std::min(nb, 4);
   }
@@ -346,4 +359,28 @@ extern "C" int ctr_rowgemm_wgrad(const float* dY, int ldy, const float* X, int l
   else if (NO == 32) rowgemm_wgrad_kernel<32, 32><<<grid, 256, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
   else rowgemm_wgrad_kernel<96, 32><<<grid, 256, 0, s>>>(dY, ldy, X, ldx, M, rpw, slab, ld_slab, o_db);
   return check_launch("rowgemm_wgrad");
+}
+
+extern "C" int ctr_rowgemm_a16(int M, int K, int N, const uint16_t* A, int lda, const float* W, int tb, float* C, int ldc,
+                               const float* bias, const float* add, int ld_add, void* stream) {
+  CTR_REQUIRE(K == 96 && N == 32, "ctr_rowgemm_a16: (K, N) = (96, 32)");
+  CTR_REQUIRE((lda & 7) == 0 && (((uintptr_t)A) & 15) == 0, "ctr_rowgemm_a16: A rows must be 16-byte aligned");
+  if (M <= 0) return 0;
+  RowGemmArgs a{M, A, lda, W, tb, C, ldc, bias, add, ld_add, nullptr, 0, nullptr, nullptr, nullptr, 0.f};
+  hipStream_t s = (hipStream_t)stream;
+  if (add) rowgemm_kernel<96, 32, true, true><<<resident_grid<96, 32, true, true>(M), 256, 0, s>>>(a);
+  else rowgemm_kernel<96, 32, false, true><<<resident_grid<96, 32, false, true>(M), 256, 0, s>>>(a);
+  return check_launch("rowgemm_a16");
+}
+
+extern "C" int ctr_rowgemm_wgrad_y16(const uint16_t* dY, int ldy, const float* X, int ldx, int M, int NO, int NIN,
+                                     float* slab, long ld_slab, int o_db, void* stream) {
+  CTR_REQUIRE(NO == 96 && NIN == 32, "ctr_rowgemm_wgrad_y16: (NO, NIN) = (96, 32)");
+  CTR_REQUIRE(o_db >= NO * NIN && ld_slab >= (long)o_db + NO, "ctr_rowgemm_wgrad_y16: slab layout");
+  if (M <= 0) return 0;
+  int rpw, grid;
+  wgrad_split(M, &rpw, &grid);
+  rowgemm_wgrad_kernel<96, 32, __bf16><<<grid, 256, 0, (hipStream_t)stream>>>((const __bf16*)dY, ldy, X, ldx, M, rpw,
+                                                                             slab, ld_slab, o_db);
+  return check_launch("rowgemm_wgrad_y16");
 }

@@ -67,6 +67,8 @@ SIGS = {
     "ctr_rowgemm": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
     "ctr_rowgemm_wgrad_rows": (i, [i]),
     "ctr_rowgemm_wgrad": (i, [p, i, p, i, i, i, i, p, l, i, p]),
+    "ctr_rowgemm_a16": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p]),
+    "ctr_rowgemm_wgrad_y16": (i, [p, i, p, i, i, i, i, p, l, i, p]),
     "ctr_rowgemm_bf_supported": (i, [i, i]),
     "ctr_rowgemm_bf": (i, [i, i, i, p, i, p, i, p, i, p, p, i, p, i, p, p, p, f, p]),
     "ctr_rowgemm_bf_wgrad_rows": (i, [i]),
@@ -95,8 +97,10 @@ SIGS = {
     "ctr_attn_fwd_bf": (i, [p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p]),
     "ctr_attn_bwd_bf_oproj_ok": (i, [i, i, i]),
     "ctr_attn_bwd_bf_oproj": (i, [p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
+    "ctr_attn_bwd_bf_oproj16": (i, [p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_attn_layer_fwd_ok": (i, [i, i, i]),
     "ctr_attn_layer_fwd_bf": (i, [p, i, i, i, i, p, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),
+    "ctr_attn_layer_fwd_bf16": (i, [p, i, i, i, i, p, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),
     "ctr_attn_bwd_bf_nparts": (i, [i]),
     "ctr_attn_bwd_bf": (i, [p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_ffn_supported": (i, [i, i, i]),

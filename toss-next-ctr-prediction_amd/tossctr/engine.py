@@ -201,6 +201,10 @@ class Engine:
         # (ctr_attn_bwd_bf_oproj: same bits, dO never written)
         self.attn_oproj = bool(self.attn_bf and self.rowgemm and
                                _lib.query("ctr_attn_bwd_bf_oproj_ok", a.top_k, a.H, a.D))
+        # ... and with both: qkv and its grad saved in bf16 (the staged operands / the reference's autocast dtype),
+        # the in-projection's backward reading the bf16 grad (ctr_rowgemm_a16 / ctr_rowgemm_wgrad_y16)
+        # (-67 us a step at cfg2, profiles/r06/ab_qkv16.log)
+        self.qkv16 = bool(self.attn_layer and self.attn_oproj and not self.rowgemm_bf)
 
     def _tab_array(self, keys, bases):
         """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
@@ -392,9 +396,10 @@ class Engine:
         call("ctr_rowgemm_bf" if self.rowgemm_bf else "ctr_rowgemm", M, K, N, A, K, W, tb, C, N, bias, add,
              N if add else 0, resid, N if resid else 0, norm_w, norm_h, norm_r, 1e-6, self.s())
 
-    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey, tag="", defer=False):
+    def wgrad_rows(self, W, dY, X, M, n_out, n_in, wkey, bkey, tag="", defer=False, y16=False):
         """dW = dY^T X and db = colsum(dY) of one nn.Linear in one pass (rowgemm.hip): per-wave partial
-        slab rows laid out like the grad arena from the weight on, reduced by one fixed-order colsum."""
+        slab rows laid out like the grad arena from the weight on, reduced by one fixed-order colsum.
+        ``y16``: dY in bf16 (ctr_rowgemm_wgrad_y16)."""
         o0 = self.arena.offsets[wkey]
         o_db = self.arena.offsets[bkey] - o0
         n_sl = o_db + n_out
@@ -402,7 +407,8 @@ class Engine:
         bf = "_bf" if self.rowgemm_bf else ""
         rows = _lib.query(f"ctr_rowgemm{bf}_wgrad_rows", M)
         slab = W.get_zeroed(f"wg_slab_{n_out}x{n_in}_{tag}", (rows, ld))     # padding columns stay zero
-        call(f"ctr_rowgemm{bf}_wgrad", dY, n_out, X, n_in, M, n_out, n_in, ptr(slab), ld, o_db, self.s())
+        call("ctr_rowgemm_wgrad_y16" if y16 else f"ctr_rowgemm{bf}_wgrad", dY, n_out, X, n_in, M, n_out, n_in,
+             ptr(slab), ld, o_db, self.s())
         self.colsum(ptr(slab), ld, rows, n_sl, ptr(self.arena.grad, o0), defer=defer)
 
     def colsum(self, X, ld, M, N, out, div=1.0, defer=False):
@@ -490,7 +496,7 @@ class Engine:
             pre = f"dare.layers.{li}."
             Ls = {}
             x = xs[-1]
-            qkv = W.get(f"qkv{li}", (M, 3 * D))
+            qkv = W.get(f"qkv{li}", (M, 3 * D), torch.bfloat16 if self.qkv16 else torch.float32)
             relmean = None
             if a.add_pos:
                 relmean = W.get(f"relmean{li}", (2 * a.top_k + 1,))
@@ -507,7 +513,8 @@ class Engine:
             x1 = W.get(f"x1_{li}", (M, D))
             if self.attn_layer:
                 # in_proj -> attention -> out_proj + residual + RMSNorm in one launch (attn_mf.hip)
-                call("ctr_attn_layer_fwd_bf", ptr(x), B, K, a.H, D, ptr(P[pre + "mha.in_proj_weight"]),
+                call("ctr_attn_layer_fwd_bf16" if self.qkv16 else "ctr_attn_layer_fwd_bf", ptr(x), B, K, a.H, D,
+                     ptr(P[pre + "mha.in_proj_weight"]),
                      ptr(P[pre + "mha.in_proj_bias"]), ptr(P[pre + "pbias.rel.weight"]) if a.add_pos else None,
                      ptr(relmean), a.top_k, scale, *da, ptr(amask),
                      ptr(P[pre + "mha.out_proj.weight"]), ptr(P[pre + "mha.out_proj.bias"]), ptr(P[pre + "norm1.w"]),
@@ -951,7 +958,7 @@ class Engine:
                        bias_grad=ptr(G[pre + "mha.out_proj.bias"]))
             self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
         # attention core
-        dqkv = W.get(f"dqkv{li}", (M, 3 * D))
+        dqkv = W.get(f"dqkv{li}", (M, 3 * D), torch.bfloat16 if self.qkv16 else torch.float32)
         nparts = (_lib.query("ctr_attn_bwd_bf_nparts", a.H) if self.attn_bf else
                   _lib.query("ctr_attn_bwd_nparts", a.H, K, D)) * B
         nrel = 2 * a.top_k + 1
@@ -959,7 +966,7 @@ class Engine:
         da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
         scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
         if self.attn_oproj:
-            call("ctr_attn_bwd_bf_oproj", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]),
+            call("ctr_attn_bwd_bf_oproj16" if self.qkv16 else "ctr_attn_bwd_bf_oproj", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]),
                  B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale, *da, ptr(Ls["amask"]), ptr(Ls["mrow"]),
                  ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
         else:
@@ -973,9 +980,12 @@ class Engine:
                 call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), self.s())
             if self.rowgemm:
                 self.wgrad_rows(W, ptr(dqkv), ptr(x_in), M, 3 * D, D, pre + "mha.in_proj_weight",
-                                pre + "mha.in_proj_bias", tag=li, defer=True)
+                                pre + "mha.in_proj_bias", tag=li, defer=True, y16=self.qkv16)
         # in_proj
-        if self.rowgemm:
+        if self.qkv16:
+            call("ctr_rowgemm_a16", M, 3 * D, D, ptr(dqkv), 3 * D, ptr(P[pre + "mha.in_proj_weight"]), 0,
+                 ptr(dout_buf), D, None, ptr(dh1), D, st)
+        elif self.rowgemm:
             self.rowgemm_call(M, 3 * D, D, ptr(dqkv), ptr(P[pre + "mha.in_proj_weight"]), 0, ptr(dout_buf),
                               add=ptr(dh1))
         else:
