@@ -294,7 +294,7 @@ def opt_algorithmic_bytes(opt, with_ema):
     return b
 
 
-PMC_ROUNDS = ("r05", "r04", "r03", "r02", "r01")      # newest committed PMC summaries first
+PMC_ROUNDS = ("r06", "r05", "r04", "r03", "r02", "r01")      # newest committed PMC summaries first
 
 
 def pmc_traffic(name):
