@@ -122,14 +122,16 @@ def kernel_work(name, a, B, ffn_M, amp="bf16", ffn_flags=0):
         qkv_b = 6 * D if name.endswith("16") else 12 * D
         return {"flops": [(4.0 * B * K * K * D, "bf16"), (8.0 * B * K * D * D, "f32")],
                 "bytes": float(B * K * (16 * D + qkv_b + 4 + 8 * H) + mask_bf)}
-    if name in ("ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd") and a.use_qnn:
+    if name in ("ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd", "ctr_qnn_gram_fwd_zbf", "ctr_qnn_gram_bwd_zbf") and a.use_qnn:
         F, QR = a.F, a.qh * a.qr
-        if name == "ctr_qnn_gram_fwd":     # z read; zsum, G (D x D), S, quad written
-            return {"flops": [(2.0 * B * F * D * QR, "f32")], "bytes": float(B * (4 * F * D + 4 * D + 4 * D * D + 8 * QR)),
+        zb, dt = (2, "bf16") if name.endswith("_zbf") else (4, "f32")    # the bf16-z forms read z's bf16 image
+        if name.startswith("ctr_qnn_gram_fwd"):     # z read; zsum, G (D x D), S, quad written
+            return {"flops": [(2.0 * B * F * D * QR, dt)],
+                    "bytes": float(B * (zb * F * D + 4 * D + 4 * D * D + 8 * QR)),
                     "flop_note": "reference A = z U (2 F D QR per sample); the Gram form executes 2 F D^2 + 2 D^2 QR"}
         add = 2 if amp == "bf16" else 4    # the MLP's input grad, bf16 under amp
-        return {"flops": [(4.0 * B * F * D * QR, "f32")],
-                "bytes": float(B * ((8 + add) * F * D + 12 * QR)),
+        return {"flops": [(4.0 * B * F * D * QR, dt)],
+                "bytes": float(B * ((zb + 4 + add) * F * D + 12 * QR)),
                 "flop_note": "reference A recompute + dz = dA U^T (4 F D QR per sample); the Gram form executes less"}
     if name.startswith("ctr_gemm_bf16_ex@"):
         shp = name.split("@")[1]
@@ -547,7 +549,8 @@ def main():
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd",
                   "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj",
                   "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16",
-                  "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd", "ctr_gemm_bf16_ex")
+                  "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd", "ctr_qnn_gram_fwd_zbf", "ctr_qnn_gram_bwd_zbf",
+                  "ctr_gemm_bf16_ex")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",
                           "ctr_lazy_touch", "ctr_lazy_touch_pair", "ctr_lazy_touch_pair_hot", "ctr_lazy_update", "ctr_lazy_update_pair",
                           "ctr_adamw_ema", "ctr_adamw_ema_hist")

@@ -306,7 +306,8 @@ int ctr_ffn_bwd_norms(const float* x, const float* dy, const float* h2, const fl
 /* RMSNorm.forward for long rows (QNN pre_norm, src/models/qnn_alpha.py:110-113) */
 int ctr_rmsnorm_fwd(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy, float* r,
                     void* stream);
-/* ... also writing y's bf16 (RNE) image, row stride ldybf (amp: the QNN MLP's [z | inter] GEMM operand) */
+/* ... also writing y's bf16 (RNE) image, row stride ldybf (amp: the QNN MLP's [z | inter] GEMM operand); y may be
+ * null when every consumer reads the image (the bf16-z pair interaction, ctr_qnn_gram_*_zbf) */
 int ctr_rmsnorm_fwd_bf(const float* x, long ldx, int M, int N, const float* w, float eps, float* y, long ldy, float* r,
                        void* ybf, long ldybf, void* stream);
 int ctr_rmsnorm_bwd_nparts(int M, int N);
@@ -362,6 +363,16 @@ int ctr_qnn_gram_fwd(const float* z, int B, int F, int D, const float* ucat, int
  * bf16 when add_bf16 -- the MLP's input grad under amp: bf16); DS = dquad o S (for dUcat)           */
 int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float* ucat, int QR, const float* S,
                      const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS, void* stream);
+/* amp: the pair interaction on bf16(z) (the reference's autocast A = z @ U_h takes z in bf16): z read from the bf16
+ * image of [z | inter] (uint16_t = bf16 bits, row stride ldz, 16-byte aligned rows); G = bf16(z)^T bf16(z) on bf16
+ * MFMA with fp32 accumulation, zsum the fp32 sum of the bf16 values, S / quad as ctr_qnn_gram_fwd_ex -- the exact
+ * sums of the bf16-z function; backward dz_f = 2 w - 2 bf16(M) bf16(z_f) (+ dz_add), M = U diag(dquad) U^T in fp32
+ * (dz_add and dz rows: stride ld).  D in {32, 64}; other arguments as the fp32-z forms.                          */
+int ctr_qnn_gram_fwd_zbf(const uint16_t* zbf, long ldz, int B, int F, int D, const float* ucat, int QR, float* zsum,
+                         float* G, float* S, float* quad, int accumulate, void* stream);
+int ctr_qnn_gram_bwd_zbf(const uint16_t* zbf, long ldz, long ld, int B, int F, int D, const float* ucat, int QR,
+                         const float* S, const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS,
+                         void* stream);
 /* the same over one feature block of the rows (pair_grouping 'block', src/models/qnn_alpha.py:99-116, block slices
  * src/models/wrapper.py:66-75): z (and dz_add, dz) rows of stride ld >= F D, F the block's features; accumulate != 0
  * adds G and quad to what the buffers hold (the blocks' quads summed, qnn_alpha.py:108), zsum / S per block     */

@@ -355,7 +355,8 @@ def test_full_shape_step_matches_oracle(shape, oracle_step, oracle64):
 # (cfg2 with the bf16 qkv / dqkv: the *16 forms and the in-projection backward on the bf16 grad)
 BF16_ENTRY_POINTS = ("ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj", "ctr_attn_fwd_bf", "ctr_attn_bwd_bf",
                      "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16", "ctr_rowgemm_a16", "ctr_rowgemm_wgrad_y16",
-                     "ctr_ffn_fwd", "ctr_ffn_bwd_norms", "ctr_gemm_bf16_ex", "ctr_rowgemm_bf", "ctr_rowgemm")
+                     "ctr_ffn_fwd", "ctr_ffn_bwd_norms", "ctr_gemm_bf16_ex", "ctr_rowgemm_bf", "ctr_rowgemm",
+                     "ctr_qnn_gram_fwd_zbf", "ctr_qnn_gram_bwd_zbf")
 
 
 @pytest.mark.timeout(900)
@@ -378,6 +379,11 @@ def test_full_shape_bf16_step(shape, oracle_step):
         assert c.get("ctr_attn_fwd_bf") == nl and c.get("ctr_attn_bwd_bf") == nl, c
     if A.D == 64:
         assert fl["rowgemm_bf"] and c.get("ctr_rowgemm_bf", 0) >= 2 * nl and not c.get("ctr_rowgemm"), (fl, c)
+    # the pair interaction on bf16(z), read from the MLP's [z | inter] image at D = 32 (cfg2, cfg3); D = 64 (cfg4)
+    # keeps the fp32-z Gram products (with bf16 z its step measured 1.15 x the reference's own band on the last MLP
+    # layer's grad, profiles/r06/gputest_gram_zbf.log)
+    want = 1 if A.D == 32 else 0
+    assert c.get("ctr_qnn_gram_fwd_zbf", 0) == want and c.get("ctr_qnn_gram_bwd_zbf", 0) == want, c
     gemm_bf = sum(v for n, v in c.items() if n.startswith("ctr_gemm_bf16_ex"))     # keyed per shape (_lib)
     assert c.get("ctr_ffn_fwd") == nl and c.get("ctr_ffn_bwd_norms") == nl and gemm_bf >= 3, c
     K = AMP_BAND_K

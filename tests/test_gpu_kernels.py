@@ -1160,6 +1160,49 @@ def test_qnn_gram_vs_torch(B, F, D, QR):
     assert rel(du.double(), Ur.grad) < 1e-5
 
 
+@pytest.mark.parametrize("B,F,D,QR", [(64, 200, 32, 96), (4096, 200, 32, 96), (9, 27, 64, 96), (5, 3, 32, 20),
+                                      (37, 33, 32, 8), (16, 40, 64, 40)])
+def test_qnn_gram_zbf_vs_fp64(B, F, D, QR):
+    """amp: the pair interaction on bf16(z) read from the [z | inter] bf16 image (ctr_qnn_gram_fwd_zbf / _bwd_zbf):
+    forward S, quad, G, zsum = the exact function of bf16(z) (fp64 reference of the same bf16 values, 1e-5); backward
+    dz against an fp64 emulation with M = U diag(dquad) U^T rounded to bf16 as the kernel's product takes it (1e-4)
+    and against the exact gradient of the bf16-z function (bf16-level, 1e-2); B = 4096 / F = 200 / QR = 96 is cfg2's."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(B * F + D + 7)
+    ldz = F * D + 24                                   # the image's row: z, then the interaction columns
+    img = torch.randn(B, ldz, device="cuda", generator=g).bfloat16()
+    zb = img[:, :F * D].reshape(B, F, D)
+    U = torch.randn(D, QR, device="cuda", generator=g) * 0.1
+    zsum, G = torch.empty(B, D, device="cuda"), torch.empty(B, D * D, device="cuda")
+    S, quad = torch.empty(B, QR, device="cuda"), torch.empty(B, QR, device="cuda")
+    L.call("ctr_qnn_gram_fwd_zbf", ptr(img), ldz, B, F, D, ptr(U), QR, ptr(zsum), ptr(G), ptr(S), ptr(quad), 0,
+           stream())
+    zr, Ur = zb.double().requires_grad_(), U.double()
+    A = zr @ Ur
+    s_ref = A.sum(1)
+    q_ref = s_ref * s_ref - (A * A).sum(1)
+    assert rel(zsum.double(), zr.detach().sum(1)) < 1e-6
+    assert rel(G.double().view(B, D, D), (zr.transpose(1, 2) @ zr).detach()) < 1e-6
+    assert rel(S.double(), s_ref.detach()) < 1e-5
+    assert rel(quad.double(), q_ref.detach()) < 1e-5
+    dquad = torch.randn(B, QR, device="cuda", generator=g)
+    dz_add = torch.randn(B, F, D, device="cuda", generator=g).bfloat16()
+    q_ref.backward(dquad.double())
+    dz, DS = torch.full((B, F, D), float("nan"), device="cuda"), torch.empty(B, QR, device="cuda")
+    L.call("ctr_qnn_gram_bwd_zbf", ptr(img), ldz, F * D, B, F, D, ptr(U), QR, ptr(S), ptr(dquad), ptr(dz_add), 1,
+           ptr(dz), ptr(DS), stream())
+    torch.cuda.synchronize()
+    dqd = dquad.double()
+    M = torch.einsum("dk,bk,ek->bde", Ur, dqd, Ur)
+    Mb = M.float().bfloat16().double()            # the kernel forms M in fp32, then rounds it to bf16
+    w = 2.0 * torch.einsum("dk,bk->bd", Ur, dqd * S.double())
+    emu = w[:, None, :] - 2.0 * torch.einsum("bfd,bde->bfe", zr.detach(), Mb) + dz_add.double()
+    # (an fp32 M within ~1e-7 of a bf16 rounding midpoint may round the other way than the fp64-then-fp32 emulation's)
+    assert rel(dz.double(), emu) < 1e-4
+    assert rel(dz.double(), zr.grad + dz_add.double()) < 1e-2
+    assert rel(DS.double(), dqd * S.double()) < 1e-6
+
+
 def test_qnn_vfull_roundtrip():
     L = _lib()
     H, R, P = 3, 4, 5

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--which", default="pair,cat")
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--no-ema", action="store_true")
+    ap.add_argument("--round4", action="store_true", help="cat widths rounded up to a multiple of 4 (probe)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev).cuda_stream
@@ -102,6 +103,8 @@ def main():
         a = Arch.from_cfg(cfg, 10_000_000, N_NUM_NEXT, N_NUM_NEXT, cards, list(cfg["data"]["cat_cols"]))
         rows = list(a.cat_cards)
         widths = list(a.cat_dims)
+        if args.round4:
+            widths = [(w + 3) // 4 * 4 for w in widths]
         tot_rows = sum(rows)
         s0 = state(tot_rows)
         last = torch.empty(tot_rows, dtype=torch.int32, device=dev)

@@ -339,6 +339,255 @@ __global__ __launch_bounds__(256) void qnn_gram_bwd_kernel(const float* __restri
   }
 }
 
+// ---------------- amp: the pair interaction on bf16(z) ----------------
+// Under autocast(bfloat16) the reference's A = z @ U_h (qnn_alpha.py:90) takes z rounded to bf16.  These forms read
+// z from the bf16 image of [z | inter] the QNN pre-norm writes for the MLP (RNE of the fp32 z, row stride ldz) and
+// compute the same Gram-form sums exactly as a function of bf16(z): G = bf16(z)^T bf16(z) on
+// v_mfma_f32_16x16x32_bf16 (products exact, fp32 accumulation) and zsum = sum of the bf16 values in fp32 -- so
+// s^2 - sum A^2 cancels consistently -- and, backward, dz_f = 2 w - 2 M bf16(z_f) with M = U diag(dquad) U^T in
+// fp32 rounded to bf16 for the product (the reference rounds dA and U to bf16 for dA @ U^T).  D in {32, 64}.
+typedef __bf16 gbf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t gu32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma_g(gbf16x8 a, gbf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float bfw(uint32_t h) { return __builtin_bit_cast(float, h << 16); }
+
+// One wave per sample (as qnn_gram_fwd_kernel).  K-step of 32 rows: lane (g, c) holds rows 8g .. 8g+7 of column
+// 16i + c -- the A operand of tile (i, j) and the B operand of tile (j, i) at once (G is symmetric); the next
+// step's rows are loaded while this step multiplies.
+template <int D>
+__global__ __launch_bounds__(256) void qnn_gram_fwd_bf_kernel(const unsigned short* __restrict__ zbf, long ldz, int B,
+                                                              int F, const float* __restrict__ ucat, int QR,
+                                                              float* __restrict__ zsum_out, float* __restrict__ G_out,
+                                                              float* __restrict__ S_out, float* __restrict__ quad_out,
+                                                              int acc_out) {
+  constexpr int NT = D / 16;
+  extern __shared__ float sU[];
+  const int QRp = (QR + 15) / 16 * 16, US = QRp + 1;
+  float* szs = sU + D * US;
+  stage_ucat<D>(ucat, QR, QRp, sU);
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  const int b = blockIdx.x * 4 + w;
+  if (b >= B) return;
+  const unsigned short* zb = zbf + (long)b * ldz;
+  f32x4 acc[NT][NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float zs[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) zs[i] = 0.f;
+  uint32_t cur[NT][8], nxt[NT][8];
+  auto load = [&](int f0, uint32_t (&v)[NT][8]) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int f = f0 + 8 * g + t;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) v[i][t] = f < F ? (uint32_t)zb[(long)f * D + 16 * i + c] : 0u;
+    }
+  };
+  if (F > 0) load(0, cur);
+  for (int f0 = 0; f0 < F; f0 += 32) {
+    if (f0 + 32 < F) load(f0 + 32, nxt);
+    gbf16x8 fr[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) zs[i] += bfw(cur[i][t]);
+      const gu32x4 u = {cur[i][0] | (cur[i][1] << 16), cur[i][2] | (cur[i][3] << 16), cur[i][4] | (cur[i][5] << 16),
+                        cur[i][6] | (cur[i][7] << 16)};
+      fr[i] = __builtin_bit_cast(gbf16x8, u);
+    }
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = mfma_g(fr[i], fr[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) cur[i][t] = nxt[i][t];
+  }
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    zs[i] += __shfl_xor(zs[i], 16);
+    zs[i] += __shfl_xor(zs[i], 32);
+  }
+  float* zw = szs + w * D;
+  if (g == 0) {
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      zw[16 * i + c] = zs[i];
+      zsum_out[(long)b * D + 16 * i + c] = zs[i];
+    }
+  }
+  float* Gb = G_out + (long)b * D * D;
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* gp = Gb + (16 * i + 4 * g + r) * D + 16 * j + c;
+        *gp = acc_out ? *gp + acc[i][j][r] : acc[i][j][r];
+      }
+  __builtin_amdgcn_wave_barrier();
+  for (int t = 0; t < QRp / 16; ++t) {        // S = zsum U, sum_f A^2 = diag(U^T G U): as qnn_gram_fwd_kernel
+    const int cc = 16 * t + c;
+    float sv = 0.f;
+#pragma unroll 8
+    for (int d = 0; d < D; ++d) sv = fmaf(zw[d], sU[d * US + cc], sv);
+    float sa2 = 0.f;
+#pragma unroll
+    for (int jd = 0; jd < NT; ++jd) {
+      f32x4 h = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h = mfma4q(acc[i][jd][r], sU[(16 * i + 4 * g + r) * US + cc], h);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sa2 = fmaf(h[r], sU[(16 * jd + 4 * g + r) * US + cc], sa2);
+    }
+    sa2 += __shfl_xor(sa2, 16);
+    sa2 += __shfl_xor(sa2, 32);
+    if (g == 0 && cc < QR) {
+      S_out[(long)b * QR + cc] = sv;
+      float* qp = quad_out + (long)b * QR + cc;
+      *qp = acc_out ? *qp + (sv * sv - sa2) : sv * sv - sa2;
+    }
+  }
+}
+
+// One sample per 4-wave workgroup (as qnn_gram_bwd_kernel): M and w in fp32 as there; then each wave takes every
+// fourth 16-row F block: dz_f = 2 w - 2 M bf16(z_f) (+ dz_add) on v_mfma_f32_16x16x32_bf16 -- A = the block's bf16 z
+// rows (lane (g, c): row f0 + c, columns 32 kh + 8g .. +7, one 16-byte load), B = bf16(M) columns read from the fp32
+// M tiles in LDS once per wave.  dz_add / dz rows have their own stride ld.
+template <int D, class TA, bool ADD>
+__global__ __launch_bounds__(256) void qnn_gram_bwd_bf_kernel(const unsigned short* __restrict__ zbf, long ldz, long ld,
+                                                              int B, int F, const float* __restrict__ ucat, int QR,
+                                                              const float* __restrict__ S,
+                                                              const float* __restrict__ dquad,
+                                                              const TA* __restrict__ dz_add, float* __restrict__ dz,
+                                                              float* __restrict__ DS) {
+  constexpr int NT = D / 16, KH = D / 32;
+  extern __shared__ float sU[];
+  const int QRp = (QR + 15) / 16 * 16, US = QRp + 1;
+  float* dq = sU + D * US;
+  float* dqs = dq + QRp;
+  float* sM = dqs + QRp;                         // [NT*NT tiles][4][64] M (C layout)
+  float* sW = sM + NT * NT * 4 * 64;
+  const int b = blockIdx.x;
+  const unsigned short* zb = zbf + (long)b * ldz;
+  const TA* ab = ADD ? dz_add + (long)b * ld : nullptr;
+  using AR = typename GramAdd<TA>::R;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
+  // this wave's first block's z rows and addends, loaded before the staging (their round trips overlap it)
+  auto load_blk = [&](int f0, gu32x4 (&zq)[KH], AR (&aq)[4][NT]) {
+    const int fa = min(f0 + c, F - 1);           // rows past F: row F - 1 re-read (never stored)
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) zq[kh] = *(const gu32x4*)(zb + (long)fa * D + 32 * kh + 8 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = min(f0 + 4 * g + r, F - 1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) aq[r][j] = ADD ? GramAdd<TA>::load(ab + (long)f * D + 16 * j + c) : AR(0);
+    }
+  };
+  gu32x4 zc[KH], zn[KH];
+  AR ac[4][NT], an[4][NT];
+  if (16 * w < F) load_blk(16 * w, zc, ac);
+  stage_ucat<D>(ucat, QR, QRp, sU);
+  for (int q = threadIdx.x; q < QRp; q += 256) {
+    const float d = q < QR ? dquad[(long)b * QR + q] : 0.f;
+    const float sv = q < QR ? S[(long)b * QR + q] : 0.f;
+    dq[q] = d;
+    dqs[q] = d * sv;
+    if (q < QR) DS[(long)b * QR + q] = d * sv;
+  }
+  __syncthreads();
+  for (int t = w; t < NT * NT; t += 4) {
+    const int i = t / NT, j = t - i * NT;
+    f32x4 Mt = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < QRp; k0 += 4) {
+      const int k = k0 + g;
+      const float bi = sU[(16 * i + c) * US + k];
+      const float bj = sU[(16 * j + c) * US + k];
+      Mt = mfma4q(bi * dq[k], bj, Mt);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sM[(t * 4 + r) * 64 + lane] = Mt[r];
+  }
+  {
+    const int kq = QRp / 4;
+    const int k0w = w * kq, k1w = k0w + kq;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      float a = 0.f;
+      for (int q = k0w + g; q < k1w; q += 4) a = fmaf(sU[(16 * j + c) * US + q], dqs[q], a);
+      a += __shfl_xor(a, 16);
+      a += __shfl_xor(a, 32);
+      if (g == 0) sW[w * D + 16 * j + c] = a;
+    }
+  }
+  __syncthreads();
+  // B operand of output column block j, k-step kh: lane (g, c) <- bf16(M[32 kh + 8g + t][16 j + c]), t < 8; M's C
+  // layout keeps M[16 i + 4 g' + r][16 j + c'] at sM[((i NT + j) 4 + r) 64 + 16 g' + c']
+  gbf16x8 mb[NT][KH];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      float mv[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int row = 32 * kh + 8 * g + t, i = row >> 4, gg = (row & 15) >> 2, r = row & 3;
+        mv[t] = sM[((i * NT + j) * 4 + r) * 64 + 16 * gg + c];
+      }
+      mb[j][kh] = gbf16x8{(__bf16)mv[0], (__bf16)mv[1], (__bf16)mv[2], (__bf16)mv[3],
+                          (__bf16)mv[4], (__bf16)mv[5], (__bf16)mv[6], (__bf16)mv[7]};
+    }
+  float wv[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int e = 16 * j + c;
+    wv[j] = 2.f * (((sW[e] + sW[D + e]) + sW[2 * D + e]) + sW[3 * D + e]);
+  }
+  float* ob = dz + (long)b * ld;
+  for (int f0 = 16 * w; f0 < F; f0 += 64) {
+    const bool more = f0 + 64 < F;
+    if (more) load_blk(f0 + 64, zn, an);
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) acc[j] = mfma_g(__builtin_bit_cast(gbf16x8, zc[kh]), mb[j][kh], acc[j]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = f0 + 4 * g + r;
+      if (f < F) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          float v = wv[j] - 2.f * acc[j][r];
+          if (ADD) v += GramAdd<TA>::widen(ac[r][j]);
+          ob[(long)f * D + 16 * j + c] = v;
+        }
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) zc[kh] = zn[kh];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) ac[r][j] = an[r][j];
+    }
+  }
+}
+
 // dUcat[d][c] = 2 (T1[d][c] - sum_e U[e][c] T[d*D + e][c])
 __global__ void qnn_du_combine_kernel(const float* __restrict__ T1, const float* __restrict__ T,
                                       const float* __restrict__ ucat, int D, int QR, float* __restrict__ du) {
@@ -581,6 +830,57 @@ extern "C" int ctr_qnn_gram_bwd(const float* z, int B, int F, int D, const float
                                 const float* dquad, const void* dz_add, int add_bf16, float* dz, float* DS,
                                 void* stream) {
   return ctr_qnn_gram_bwd_ex(z, (long)F * D, B, F, D, ucat, QR, S, dquad, dz_add, add_bf16, dz, DS, stream);
+}
+
+extern "C" int ctr_qnn_gram_fwd_zbf(const uint16_t* zbf, long ldz, int B, int F, int D, const float* ucat, int QR,
+                                    float* zsum, float* G, float* S, float* quad, int accumulate, void* stream) {
+  CTR_REQUIRE(D == 32 || D == 64, "qnn gram (bf16 z): D must be 32 or 64");
+  CTR_REQUIRE(ldz >= (long)F * D && (ldz % 8) == 0, "qnn gram (bf16 z): row stride");
+  if (B == 0) return 0;
+  const size_t sm = gram_lds(D, QR);
+  CTR_REQUIRE(sm <= 64 * 1024, "qnn gram: U exceeds LDS");
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = cdiv(B, 4);
+  const unsigned short* z = (const unsigned short*)zbf;
+  if (D == 32) qnn_gram_fwd_bf_kernel<32><<<blocks, 256, sm, s>>>(z, ldz, B, F, ucat, QR, zsum, G, S, quad, accumulate);
+  else qnn_gram_fwd_bf_kernel<64><<<blocks, 256, sm, s>>>(z, ldz, B, F, ucat, QR, zsum, G, S, quad, accumulate);
+  return check_launch("qnn_gram_fwd_zbf");
+}
+
+template <class TA, bool ADD>
+static void gram_bwd_bf_launch(int D, size_t sm, hipStream_t s, const unsigned short* z, long ldz, long ld, int B,
+                               int F, const float* ucat, int QR, const float* S, const float* dquad, const TA* dz_add,
+                               float* dz, float* DS) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_bf_kernel<32, TA, ADD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)qnn_gram_bwd_bf_kernel<64, TA, ADD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  if (D == 32) qnn_gram_bwd_bf_kernel<32, TA, ADD><<<B, 256, sm, s>>>(z, ldz, ld, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+  else qnn_gram_bwd_bf_kernel<64, TA, ADD><<<B, 256, sm, s>>>(z, ldz, ld, B, F, ucat, QR, S, dquad, dz_add, dz, DS);
+}
+
+extern "C" int ctr_qnn_gram_bwd_zbf(const uint16_t* zbf, long ldz, long ld, int B, int F, int D, const float* ucat,
+                                    int QR, const float* S, const float* dquad, const void* dz_add, int add_bf16,
+                                    float* dz, float* DS, void* stream) {
+  CTR_REQUIRE(D == 32 || D == 64, "qnn gram (bf16 z): D must be 32 or 64");
+  CTR_REQUIRE(ldz >= (long)F * D && (ldz % 8) == 0 && ld >= (long)F * D, "qnn gram (bf16 z): row strides");
+  CTR_REQUIRE((((uintptr_t)zbf) & 15) == 0, "qnn gram (bf16 z): 16-byte aligned rows");
+  if (B == 0) return 0;
+  const int QRp = (QR + 15) / 16 * 16, NT = D / 16;
+  const size_t sm = ((size_t)D * (QRp + 1) + 2 * (size_t)QRp + (size_t)NT * NT * 4 * 64 + 4 * (size_t)D) *
+                    sizeof(float);
+  CTR_REQUIRE(sm <= 160 * 1024, "qnn gram bwd: U + M partials exceed LDS");
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned short* z = (const unsigned short*)zbf;
+  if (!dz_add) gram_bwd_bf_launch<float, false>(D, sm, s, z, ldz, ld, B, F, ucat, QR, S, dquad, nullptr, dz, DS);
+  else if (add_bf16)
+    gram_bwd_bf_launch<__bf16, true>(D, sm, s, z, ldz, ld, B, F, ucat, QR, S, dquad, (const __bf16*)dz_add, dz, DS);
+  else gram_bwd_bf_launch<float, true>(D, sm, s, z, ldz, ld, B, F, ucat, QR, S, dquad, (const float*)dz_add, dz, DS);
+  return check_launch("qnn_gram_bwd_zbf");
 }
 
 // pair_grouping 'block': the rows' columns outside every interaction block (single-feature blocks, e.g. the DARE

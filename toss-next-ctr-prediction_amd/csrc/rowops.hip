@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void rmsnorm_fwd_big_vec(const float* __restri
     const int j = threadIdx.x + 256 * k;
     if (j < n4) {
       const f4 o = wv[k] * v[k] * rr;
-      yr[j] = o;
+      if (y) yr[j] = o;
       if (ybf) *(b4*)(ybf + row * ldybf + 4 * j) = __builtin_convertvector(o, b4);   // amp: the GEMM's bf16 image
     }
   }
@@ -579,6 +579,7 @@ extern "C" int ctr_rmsnorm_fwd_bf(const float* x, long ldx, int M, int N, const 
   const bool vec = (N % 4) == 0 && (ldx % 4) == 0 && (ldy % 4) == 0 && (ldybf % 4) == 0 &&
                    ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)w)) & 15) == 0 && (((uintptr_t)ybf) & 7) == 0;
   CTR_REQUIRE(vec && N <= 1024 * 16, "ctr_rmsnorm_fwd_bf: needs N % 4 == 0, N <= 16384 and aligned rows");
+  CTR_REQUIRE(ybf != nullptr, "ctr_rmsnorm_fwd_bf: the bf16 image is required (y may be null)");
   if (N <= 1024 * 8)
     rmsnorm_fwd_big_vec<8><<<M, 256, 0, (hipStream_t)stream>>>(x, ldx, N, w, eps, y, ldy, r, (__bf16*)ybf, ldybf);
   else

@@ -130,6 +130,8 @@ SIGS = {
     "ctr_qnn_passthrough": (i, [p, i, l, i, i, p, l, p]),
     "ctr_qnn_gram_fwd": (i, [p, i, i, i, p, i, p, p, p, p, p]),
     "ctr_qnn_gram_bwd": (i, [p, i, i, i, p, i, p, p, p, i, p, p, p]),
+    "ctr_qnn_gram_fwd_zbf": (i, [p, l, i, i, i, p, i, p, p, p, p, i, p]),
+    "ctr_qnn_gram_bwd_zbf": (i, [p, l, l, i, i, i, p, i, p, p, p, i, p, p, p]),
     "ctr_qnn_du_combine": (i, [p, p, p, i, i, p, p]),
     "ctr_se_fwd_gate": (i, [p, i, i, p, p, p, p, p, p, p]),
     "ctr_scale_drop": (i, [p, i, i, p, u, u, f, p, l, p]),

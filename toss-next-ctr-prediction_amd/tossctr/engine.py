@@ -636,11 +636,16 @@ class Engine:
         # amp: the MLP's first GEMM runs on a bf16 image of [z | inter], written by z's and inter's producers
         zi_bf = W.get("zi_bf", (B, din), torch.bfloat16) if (self.bf_ok(B, H0, din, din, 0, din, 1) and
                                                               FD % 8 == 0 and FD % 4 == 0) else None
+        # amp: the pair interaction reads the same bf16 image (z as the reference's autocast A = z @ U_h takes it,
+        # qnn.hip ctr_qnn_gram_*_zbf); with the MLP weight grad on the image too, nothing reads the fp32 z
+        # (D = 32: -67 us a step at cfg2, profiles/r06/ab_gram_zbf.log; D = 64 keeps the fp32-z products, whose
+        # bf16 form left cfg4's full-shape step outside the reference's band, gputest_gram_zbf.log)
+        gram_zbf = bool(zi_bf is not None and D == 32 and self.bf_ok(H0, din, B, H0, 1, din, 0))
         if a.qnn_layer_norm:
             self._ln_fwd(xF, B, FD, "qnn.pre_norm", z, W.get("muq", (B,)), rq, ybf=zi_bf, ldybf=din)
         elif zi_bf is not None:
-            call("ctr_rmsnorm_fwd_bf", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq),
-                 ptr(zi_bf), din, st)
+            call("ctr_rmsnorm_fwd_bf", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6,
+                 None if gram_zbf else ptr(z), FD, ptr(rq), ptr(zi_bf), din, st)
         else:
             call("ctr_rmsnorm_fwd", ptr(xF), FD, B, FD, ptr(P["qnn.pre_norm.w"]), 1e-6, ptr(z), FD, ptr(rq), st)
         ucat = W.get("ucat", (D, QR))
@@ -652,7 +657,11 @@ class Engine:
         gram = W.get("qgram", (B, D * D))
         S = W.get("qS", (nb, B, QR))
         quad = W.get("qquad", (B, QR))
-        if blocks:     # pair_grouping 'block' (qnn_alpha.py:99-108): quad and G summed over the blocks
+        if gram_zbf:
+            for i, (f0, f1) in enumerate(blocks or [(0, F)]):
+                call("ctr_qnn_gram_fwd_zbf", ptr(zi_bf, f0 * D), din, B, f1 - f0, D, ptr(ucat), QR, ptr(zsum[i]),
+                     ptr(gram), ptr(S[i]), ptr(quad), int(i > 0), st)
+        elif blocks:     # pair_grouping 'block' (qnn_alpha.py:99-108): quad and G summed over the blocks
             for i, (f0, f1) in enumerate(blocks):
                 call("ctr_qnn_gram_fwd_ex", ptr(z, f0 * D), FD, B, f1 - f0, D, ptr(ucat), QR, ptr(zsum[i]), ptr(gram),
                      ptr(S[i]), ptr(quad), int(i > 0), st)
@@ -707,7 +716,7 @@ class Engine:
                 acts.append(pre)
         return dict(z=z, rq=rq, ucat=ucat, zsum=zsum, gram=gram, vfull=vfull, S=S, quad=quad, inter_pre=inter_pre,
                     mean=mean, g1=g1, gate=gate, inter=inter, hs=hs, acts=acts,
-                    zi_bf=zi_bf, w0_bf=W.t.get("w0_bf") if zi_bf is not None else None)
+                    zi_bf=zi_bf, w0_bf=W.t.get("w0_bf") if zi_bf is not None else None, gram_zbf=gram_zbf)
 
     def _fc_forward(self, W, fcin, ctx, cat_e, B, seed, training, logits):
         """QNN disabled: fc head on [u, mean(num_e), mean(mask_e), cat_embs] (wrapper.py:95-100,167-173)."""
@@ -1076,8 +1085,15 @@ class Engine:
                          ptr(dz, f_prev * D), FD, st)
                 f_prev = f1
             for i, (f0, f1) in enumerate(blocks):
-                call("ctr_qnn_gram_bwd_ex", ptr(q["z"], f0 * D), FD, B, f1 - f0, D, ptr(q["ucat"]), QR,
-                     ptr(q["S"][i]), ptr(dquad), ptr(dadd, f0 * D), int(dz_bf), ptr(dz, f0 * D), ptr(DS[i]), st)
+                if q["gram_zbf"]:
+                    call("ctr_qnn_gram_bwd_zbf", ptr(q["zi_bf"], f0 * D), din, FD, B, f1 - f0, D, ptr(q["ucat"]), QR,
+                         ptr(q["S"][i]), ptr(dquad), ptr(dadd, f0 * D), int(dz_bf), ptr(dz, f0 * D), ptr(DS[i]), st)
+                else:
+                    call("ctr_qnn_gram_bwd_ex", ptr(q["z"], f0 * D), FD, B, f1 - f0, D, ptr(q["ucat"]), QR,
+                         ptr(q["S"][i]), ptr(dquad), ptr(dadd, f0 * D), int(dz_bf), ptr(dz, f0 * D), ptr(DS[i]), st)
+        elif q["gram_zbf"]:
+            call("ctr_qnn_gram_bwd_zbf", ptr(q["zi_bf"]), din, FD, B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]),
+                 ptr(dquad), ptr(dadd), int(dz_bf), ptr(dz), ptr(DS), st)
         else:
             call("ctr_qnn_gram_bwd", ptr(q["z"]), B, F, D, ptr(q["ucat"]), QR, ptr(q["S"]), ptr(dquad),
                  ptr(dadd), int(dz_bf), ptr(dz), ptr(DS), st)
