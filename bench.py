@@ -557,7 +557,7 @@ def main():
     # a HIP event recorded between two kernels costs a boundary of its own (≈ 5 µs each on MI355X: 10–12 µs gaps around
     # every bracketed launch), so the candidates are ranked on a few untimed probe steps first and the timed steps
     # bracket only the dominant one -- the roofline kernel, still timed live in the timed region
-    probe, roof_kernel = {}, None
+    probe, roof_kernel, roof_every = {}, None, 1
     if args.kernel_events == "all":
         a_ = model.arch
         _lib.time_calls(roof_timed)
@@ -572,7 +572,10 @@ def main():
         roof_kernel = next((n for n in ranked if price(n, a_, args.batch, fm_, args.amp, model.engine.ffn_flags,
                                                        probe[n][1]) is not None), None)     # may carry a shape key
         if roof_kernel is not None:
-            _lib.time_calls((roof_kernel,))
+            # one launch of the dominant kernel per step is bracketed, the layers' launches of it (the same shape) in
+            # turn: each bracketed launch costs the step two event boundaries (≈ 13 µs idle after it in the trace)
+            roof_every = max(1, round(probe[roof_kernel][0] / PROFILE_STEPS))
+            _lib.time_calls((roof_kernel,), every=roof_every)
         torch.cuda.synchronize()
     # the host issues the step a few hundred dispatches ahead of the device at most (the HIP queue depth): a cyclic
     # garbage collection of the interpreter's heap mid-step (≈ 2 ms, once in ~20 steps in the kernel trace) leaves the
@@ -633,7 +636,7 @@ def main():
         per_step = {n: c * ms / PROFILE_STEPS for n, (c, ms) in kstats.items()}
         kernels = {n: {"calls_per_step": round(kstats[n][0] / PROFILE_STEPS, 2), "avg_launch_ms": round(kstats[n][1], 4),
                        "ms_per_step": round(per_step[n], 4)} for n in kstats}
-        per_step_t = {n: c * ms / args.steps for n, (c, ms) in kstats_timed.items()}
+        per_step_t = {n: c * roof_every * ms / args.steps for n, (c, ms) in kstats_timed.items()}
         roof = None
         for n in sorted(per_step_t, key=per_step_t.get, reverse=True):
             pr = price(n, a, args.batch, ffn_M, args.amp, model.engine.ffn_flags, kstats_timed[n][1])
@@ -646,7 +649,9 @@ def main():
                     "floor_us": pr["floor_us"], "hbm_floor_us": pr["hbm_floor_us"],
                     "compute_floor_us": pr["compute_floor_us"],
                     "avg_launch_ms": round(kstats_timed[n][1], 4), "ms_per_step": round(per_step_t[n], 4),
-                    "share_of_step": round(per_step_t[n] / ms, 4), "timing": "HIP events in the timed steps",
+                    "share_of_step": round(per_step_t[n] / ms, 4),
+                    "timing": f"HIP events in the timed steps (1 of every {roof_every} launches, "
+                              f"{kstats_timed[n][0]} bracketed)",
                     "pricing": "binding roof: frac = max(sum flop / dense MFMA peak of the dtype, algorithmic bytes / "
                                "8 TB/s) / measured launch time (kernel_work)"}
             # every priced candidate, dominant first: the roofline kernel from the timed steps, the others from the

@@ -147,6 +147,16 @@ int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, const float
 size_t ctr_feat_embed_bwd_ws(int B, int F, int D);
 int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, const float* bias, const float* P, int fe, int D,
                        const float* dout, long dout_ld, float* dW, float* dbias, float* dP, float* ws, void* stream);
+/* both groups (numeric, binary: src/models/wrapper.py:95-100 embeds both into the same rows) in one launch per
+ * kernel: group 0's arguments then group 1's, as ctr_feat_embed_fwd / _bwd (each group its own ws); out / dout rows
+ * share the stride.  Same sums, products and orders as two single-group calls.                                  */
+int ctr_feat_embed_fwd2(const float* x0, int F0, const float* W0, const float* bias0, const float* P0, float* out0,
+                        const float* x1, int F1, const float* W1, const float* bias1, const float* P1, float* out1, int B,
+                        int fe, int D, long out_ld, void* stream);
+int ctr_feat_embed_bwd2(const float* x0, int F0, const float* W0, const float* bias0, const float* P0,
+                        const float* dout0, float* dW0, float* dbias0, float* dP0, float* ws0, const float* x1, int F1,
+                        const float* W1, const float* bias1, const float* P1, const float* dout1, float* dW1,
+                        float* dbias1, float* dP1, float* ws1, int B, int fe, int D, long dout_ld, void* stream);
 /* CTRModel._embed_cats + emb_dropout, src/models/wrapper.py:106-112,149-150: hashed-bucket gather of
  * X_cat[b,c] from table c (tab_base + tab_off[c], row stride row_ld, or dims[c] when row_ld == 0;
  * tab_base NULL = arena) projected by P_c (arena + proj_off[c]).  Row-sharded tables pass the

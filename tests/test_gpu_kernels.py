@@ -719,6 +719,46 @@ def test_rowgemm_bf16_operand_forms_equal_fp32_forms(M, add):
                  (dq32.double().t() @ x.double()).norm()) < 1e-6
 
 
+@pytest.mark.parametrize("B,F0,F1,D,fe", [(4096, 82, 82, 32, 16), (1000, 35, 7, 64, 8), (37, 5, 3, 16, 4)])
+def test_feat_embed_two_groups_equal_two_calls(B, F0, F1, D, fe):
+    """ctr_feat_embed_fwd2 / _bwd2 (numeric + binary group in one launch per kernel) write the bits of two
+    single-group calls: the outputs, dW, dbias (group 0 only, as the binary embedding has none) and dP."""
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(B + F0 + F1)
+    xs = [torch.randn(B, F, device="cuda", generator=g) for F in (F0, F1)]
+    Ws = [torch.randn(F, fe, device="cuda", generator=g) for F in (F0, F1)]
+    bias = torch.randn(F0, fe, device="cuda", generator=g)
+    Ps = [torch.randn(D, fe, device="cuda", generator=g) / fe ** 0.5 for _ in range(2)]
+    ld = (F0 + F1) * D + 8
+    st = stream()
+    outs = [torch.full((B, ld), float("nan"), device="cuda") for _ in range(2)]
+    offs = (0, F0 * D)
+    L.call("ctr_feat_embed_fwd", ptr(xs[0]), B, F0, ptr(Ws[0]), ptr(bias), ptr(Ps[0]), fe, D, ptr(outs[0], offs[0]), ld, st)
+    L.call("ctr_feat_embed_fwd", ptr(xs[1]), B, F1, ptr(Ws[1]), None, ptr(Ps[1]), fe, D, ptr(outs[0], offs[1]), ld, st)
+    L.call("ctr_feat_embed_fwd2", ptr(xs[0]), F0, ptr(Ws[0]), ptr(bias), ptr(Ps[0]), ptr(outs[1], offs[0]),
+           ptr(xs[1]), F1, ptr(Ws[1]), None, ptr(Ps[1]), ptr(outs[1], offs[1]), B, fe, D, ld, st)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    dout = torch.randn(B, ld, device="cuda", generator=g)
+    ws = [torch.empty(L.query("ctr_feat_embed_bwd_ws", B, F, D) // 4 + 1, device="cuda") for F in (F0, F1, F0, F1)]
+
+    def grads():
+        return ([torch.full((F, fe), float("nan"), device="cuda") for F in (F0, F1)],
+                torch.full((F0, fe), float("nan"), device="cuda"),
+                [torch.full((D, fe), float("nan"), device="cuda") for _ in range(2)])
+    (dWa, dba, dPa), (dWb, dbb, dPb) = grads(), grads()
+    L.call("ctr_feat_embed_bwd", ptr(xs[0]), B, F0, ptr(Ws[0]), ptr(bias), ptr(Ps[0]), fe, D, ptr(dout, offs[0]), ld,
+           ptr(dWa[0]), ptr(dba), ptr(dPa[0]), ptr(ws[0]), st)
+    L.call("ctr_feat_embed_bwd", ptr(xs[1]), B, F1, ptr(Ws[1]), None, ptr(Ps[1]), fe, D, ptr(dout, offs[1]), ld,
+           ptr(dWa[1]), None, ptr(dPa[1]), ptr(ws[1]), st)
+    L.call("ctr_feat_embed_bwd2", ptr(xs[0]), F0, ptr(Ws[0]), ptr(bias), ptr(Ps[0]), ptr(dout, offs[0]), ptr(dWb[0]),
+           ptr(dbb), ptr(dPb[0]), ptr(ws[2]), ptr(xs[1]), F1, ptr(Ws[1]), None, ptr(Ps[1]), ptr(dout, offs[1]),
+           ptr(dWb[1]), None, ptr(dPb[1]), ptr(ws[3]), B, fe, D, ld, st)
+    torch.cuda.synchronize()
+    for a_, b_ in zip(dWa + [dba] + dPa, dWb + [dbb] + dPb):
+        assert torch.equal(a_.view(torch.int32), b_.view(torch.int32))
+
+
 @pytest.mark.parametrize("B,F,D,fe,bias", [(4096, 82, 32, 16, True), (4096, 82, 32, 16, False), (1000, 35, 64, 8, True),
                                            (37, 5, 16, 4, True), (300, 3, 256, 16, True), (257, 7, 48, 24, False)])
 def test_feat_embed_vs_fp64(B, F, D, fe, bias):

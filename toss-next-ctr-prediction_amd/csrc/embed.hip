@@ -21,13 +21,47 @@ namespace ctr {
 constexpr int FE_NB = 32;                           // samples per thread
 __host__ __device__ __forceinline__ int fe_rows_d(int D) { return FE_NB * (256 / D); }
 
-__global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __restrict__ x, int B, int F,
-                                                             const float* __restrict__ W,
-                                                             const float* __restrict__ bias,
-                                                             const float* __restrict__ P, int fe, int D,
-                                                             float* __restrict__ out, long out_ld) {
+// One or two feature groups (numeric, binary) in one launch: the groups' workgroups side by side in the grid
+// (group 1's after group 0's), each with its own x, weights and output -- one launch and one boundary fewer per
+// direction than a launch per group.
+struct FeGrp {
+  const float* x;
+  int F;
+  const float* W;
+  const float* bias;      // nullable
+  const float* P;
+  float* out;             // forward output (row stride ld) / backward: the incoming grad dout
+  float* dW;
+  float* dbias;           // nullable
+  float* dP;
+  float* ws;              // backward chunk partials (ctr_feat_embed_bwd_ws)
+};
+struct FeGrps {
+  FeGrp g[2];
+  int n;
+  long ld;                // out / dout row stride
+};
+// block index along the groups' concatenation -> (group, index inside it)
+__device__ __forceinline__ const FeGrp& fe_pick(const FeGrps& a, int& i, int per0) {
+  if (a.n > 1 && i >= per0) {
+    i -= per0;
+    return a.g[1];
+  }
+  return a.g[0];
+}
+
+__global__ __launch_bounds__(256) void feat_embed_fwd_kernel(FeGrps ga, int B, int fe, int D) {
   extern __shared__ float sfe[];         // P [D][fe+1] | W row [fe] | bias row [fe]
-  const int f = blockIdx.y, b0 = blockIdx.x * fe_rows_d(D);
+  int f = blockIdx.y;
+  const FeGrp& gr = fe_pick(ga, f, ga.g[0].F);
+  const float* __restrict__ x = gr.x;
+  const float* __restrict__ W = gr.W;
+  const float* __restrict__ bias = gr.bias;
+  const float* __restrict__ P = gr.P;
+  float* __restrict__ out = gr.out;
+  const int F = gr.F;
+  const long out_ld = ga.ld;
+  const int b0 = blockIdx.x * fe_rows_d(D);
   const int RG = 256 / D, d = threadIdx.x % D, rg = threadIdx.x / D;
   const int FP = fe + 1;
   float* sP = sfe;
@@ -59,11 +93,16 @@ __global__ __launch_bounds__(256) void feat_embed_fwd_kernel(const float* __rest
 
 // per (feature f, sample chunk): S1[f,d] = sum_b x[b,f] dout[b,f,d], S0[f,d] = sum_b dout[b,f,d]
 // lanes = d, 256/D row groups stride the chunk, combined in fixed order -> part[chunk][2][F][D]
-__global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restrict__ x, int B, int F, int D,
-                                                          const float* __restrict__ dout, long dout_ld,
-                                                          int rows_per_chunk, float* __restrict__ part) {
+__global__ __launch_bounds__(256) void feat_embed_bwd_sums(FeGrps ga, int B, int D, int rows_per_chunk) {
   __shared__ float r1[256], r0[256];
-  const int f = blockIdx.x, chunk = blockIdx.y, t = threadIdx.x;
+  int f = blockIdx.x;
+  const FeGrp& gr = fe_pick(ga, f, ga.g[0].F);
+  const float* __restrict__ x = gr.x;
+  const float* __restrict__ dout = gr.out;
+  float* __restrict__ part = gr.ws;
+  const int F = gr.F;
+  const long dout_ld = ga.ld;
+  const int chunk = blockIdx.y, t = threadIdx.x;
   const int RG = 256 / D;
   const int d = t % D, rg = t / D;
   const int b0 = chunk * rows_per_chunk, b1 = min(B, b0 + rows_per_chunk);
@@ -103,16 +142,22 @@ __global__ __launch_bounds__(256) void feat_embed_bwd_sums(const float* __restri
 // workgroup f < F sums the chunk partials of S1[f, :], S0[f, :] (fixed chunk order) and forms dW[f, :] = S1[f] @ P,
 // dbias[f, :] = S0[f] @ P; workgroup F + d sums those of S1[:, d], S0[:, d] and forms dP[d, :] = sum_f (S1[f, d]
 // W[f, :] + S0[f, d] bias[f, :]) in feature order -- the same sums, products and orders as the one-workgroup form
-__global__ __launch_bounds__(256) void feat_embed_bwd_final(int nchunk, int F, int D, int fe,
-                                                           const float* __restrict__ part, const float* __restrict__ W,
-                                                           const float* __restrict__ bias, const float* __restrict__ P,
-                                                           float* __restrict__ dW, float* __restrict__ dbias,
-                                                           float* __restrict__ dP) {
+__global__ __launch_bounds__(256) void feat_embed_bwd_final(FeGrps ga, int nchunk, int D, int fe) {
   extern __shared__ float sfb[];       // row f: S [2][D] | P [D][fe];  column d: S [2][F] | W [F][fe] | bias [F][fe]
+  int blk = blockIdx.x;
+  const FeGrp& gr = fe_pick(ga, blk, ga.g[0].F + D);
+  const float* __restrict__ part = gr.ws;
+  const float* __restrict__ W = gr.W;
+  const float* __restrict__ bias = gr.bias;
+  const float* __restrict__ P = gr.P;
+  float* __restrict__ dW = gr.dW;
+  float* __restrict__ dbias = gr.dbias;
+  float* __restrict__ dP = gr.dP;
+  const int F = gr.F;
   const int tid = threadIdx.x;
   const long n2 = 2L * F * D;
-  const bool rowf = blockIdx.x < F;
-  const int f = blockIdx.x, dd = blockIdx.x - F;
+  const bool rowf = blk < F;
+  const int f = blk, dd = blk - F;
   const int nS = rowf ? 2 * D : 2 * F;
   for (int q = tid; q < nS; q += 256) {
     // element of S (S1 then S0): row f -> (h, d) = (q / D, q % D); column d -> (h, f) = (q / F, q % F)
@@ -655,15 +700,35 @@ __global__ __launch_bounds__(CTXB_T) void context_bwd_kernel(CtxBwdArgs a) {
 
 using namespace ctr;
 
-extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, const float* bias, const float* P,
-                                  int fe, int D, float* out, long out_ld, void* stream) {
-  if (B == 0 || F == 0) return 0;
+static int fe_fwd(const FeGrps& ga, int B, int fe, int D, hipStream_t s) {
+  const int Ft = ga.g[0].F + (ga.n > 1 ? ga.g[1].F : 0);
+  if (B == 0 || Ft == 0) return 0;
   CTR_REQUIRE(D <= 256, "D > 256");
   const size_t sm = ((size_t)D * (fe + 1) + 2 * fe) * sizeof(float);
   CTR_REQUIRE(sm <= 64 * 1024, "feat_embed: D x fe projection exceeds LDS");
-  feat_embed_fwd_kernel<<<dim3(cdiv(B, fe_rows_d(D)), F), 256, sm, (hipStream_t)stream>>>(x, B, F, W, bias, P, fe, D,
-                                                                                          out, out_ld);
+  feat_embed_fwd_kernel<<<dim3(cdiv(B, fe_rows_d(D)), Ft), 256, sm, s>>>(ga, B, fe, D);
   return check_launch("feat_embed_fwd");
+}
+
+extern "C" int ctr_feat_embed_fwd(const float* x, int B, int F, const float* W, const float* bias, const float* P,
+                                  int fe, int D, float* out, long out_ld, void* stream) {
+  FeGrps ga{};
+  ga.g[0] = FeGrp{x, F, W, bias, P, out, nullptr, nullptr, nullptr, nullptr};
+  ga.n = 1;
+  ga.ld = out_ld;
+  return fe_fwd(ga, B, fe, D, (hipStream_t)stream);
+}
+
+extern "C" int ctr_feat_embed_fwd2(const float* x0, int F0, const float* W0, const float* bias0, const float* P0,
+                                   float* out0, const float* x1, int F1, const float* W1, const float* bias1,
+                                   const float* P1, float* out1, int B, int fe, int D, long out_ld, void* stream) {
+  FeGrps ga{};
+  ga.g[0] = FeGrp{x0, F0, W0, bias0, P0, out0, nullptr, nullptr, nullptr, nullptr};
+  ga.g[1] = FeGrp{x1, F1, W1, bias1, P1, out1, nullptr, nullptr, nullptr, nullptr};
+  ga.n = 2;
+  ga.ld = out_ld;
+  CTR_REQUIRE(F0 > 0 && F1 > 0, "ctr_feat_embed_fwd2: both groups need features");
+  return fe_fwd(ga, B, fe, D, (hipStream_t)stream);
 }
 
 static int fe_chunks(int B) { return std::max(1, std::min(16, cdiv(B, 256))); }   // <= 16: feat_embed_bwd_final
@@ -672,23 +737,46 @@ extern "C" size_t ctr_feat_embed_bwd_ws(int B, int F, int D) {
   return (size_t)fe_chunks(B) * 2 * F * D * sizeof(float);
 }
 
+static int fe_bwd(const FeGrps& ga, int B, int fe, int D, hipStream_t s) {
+  const int F0 = ga.g[0].F, F1 = ga.n > 1 ? ga.g[1].F : 0, Fmax = std::max(F0, F1);
+  if (F0 + F1 == 0) return 0;
+  CTR_REQUIRE(D <= 256, "D > 256");
+  const size_t sm_row = ((size_t)2 * D + (size_t)D * fe) * sizeof(float);
+  const size_t sm_col = ((size_t)2 * Fmax + (size_t)2 * Fmax * fe) * sizeof(float);
+  const size_t sm = sm_row > sm_col ? sm_row : sm_col;
+  CTR_REQUIRE(sm <= 160 * 1024, "feat_embed_bwd: sums + weights exceed LDS");
+  const int nch = fe_chunks(B);
+  const int rpc = cdiv(B, nch);
+  feat_embed_bwd_sums<<<dim3(F0 + F1, nch), 256, 0, s>>>(ga, B, D, rpc);
+  if (sm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)feat_embed_bwd_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  feat_embed_bwd_final<<<F0 + D + (ga.n > 1 ? F1 + D : 0), 256, sm, s>>>(ga, nch, D, fe);
+  return check_launch("feat_embed_bwd");
+}
+
 extern "C" int ctr_feat_embed_bwd(const float* x, int B, int F, const float* W, const float* bias, const float* P,
                                   int fe, int D, const float* dout, long dout_ld, float* dW, float* dbias,
                                   float* dP, float* ws, void* stream) {
   if (F == 0) return 0;
-  CTR_REQUIRE(D <= 256, "D > 256");
-  const size_t sm_row = ((size_t)2 * D + (size_t)D * fe) * sizeof(float);
-  const size_t sm_col = ((size_t)2 * F + (size_t)2 * F * fe) * sizeof(float);
-  const size_t sm = sm_row > sm_col ? sm_row : sm_col;
-  CTR_REQUIRE(sm <= 160 * 1024, "feat_embed_bwd: sums + weights exceed LDS");
-  hipStream_t s = (hipStream_t)stream;
-  const int nch = fe_chunks(B);
-  const int rpc = cdiv(B, nch);
-  feat_embed_bwd_sums<<<dim3(F, nch), 256, 0, s>>>(x, B, F, D, dout, dout_ld, rpc, ws);
-  if (sm > 64 * 1024)
-    (void)hipFuncSetAttribute((const void*)feat_embed_bwd_final, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-  feat_embed_bwd_final<<<F + D, 256, sm, s>>>(nch, F, D, fe, ws, W, bias, P, dW, dbias, dP);
-  return check_launch("feat_embed_bwd");
+  FeGrps ga{};
+  ga.g[0] = FeGrp{x, F, W, bias, P, const_cast<float*>(dout), dW, dbias, dP, ws};
+  ga.n = 1;
+  ga.ld = dout_ld;
+  return fe_bwd(ga, B, fe, D, (hipStream_t)stream);
+}
+
+extern "C" int ctr_feat_embed_bwd2(const float* x0, int F0, const float* W0, const float* bias0, const float* P0,
+                                   const float* dout0, float* dW0, float* dbias0, float* dP0, float* ws0,
+                                   const float* x1, int F1, const float* W1, const float* bias1, const float* P1,
+                                   const float* dout1, float* dW1, float* dbias1, float* dP1, float* ws1, int B, int fe,
+                                   int D, long dout_ld, void* stream) {
+  CTR_REQUIRE(F0 > 0 && F1 > 0, "ctr_feat_embed_bwd2: both groups need features");
+  FeGrps ga{};
+  ga.g[0] = FeGrp{x0, F0, W0, bias0, P0, const_cast<float*>(dout0), dW0, dbias0, dP0, ws0};
+  ga.g[1] = FeGrp{x1, F1, W1, bias1, P1, const_cast<float*>(dout1), dW1, dbias1, dP1, ws1};
+  ga.n = 2;
+  ga.ld = dout_ld;
+  return fe_bwd(ga, B, fe, D, (hipStream_t)stream);
 }
 
 extern "C" int ctr_cat_embed_fwd(const int* xcat, int B, int Fc, const float* arena, const float* tab_base,

@@ -76,6 +76,8 @@ SIGS = {
     "ctr_feat_embed_fwd": (i, [p, i, i, p, p, p, i, i, p, l, p]),
     "ctr_feat_embed_bwd_ws": (z, [i, i, i]),
     "ctr_feat_embed_bwd": (i, [p, i, i, p, p, p, i, i, p, l, p, p, p, p, p]),
+    "ctr_feat_embed_fwd2": (i, [p, i, p, p, p, p, p, i, p, p, p, p, i, i, i, l, p]),
+    "ctr_feat_embed_bwd2": (i, [p, i, p, p, p, p, p, p, p, p, p, i, p, p, p, p, p, p, p, p, i, i, i, l, p]),
     "ctr_cat_embed_fwd": (i, [p, i, i, p, p, p, p, p, i, i, p, p, l, u, u, f, p]),
     "ctr_cat_embed_bwd_ws": (z, [i, i]),
     "ctr_cat_embed_bwd": (i, [p, i, i, p, p, p, p, p, i, i, p, p, p, p, p, p, p, p]),
@@ -213,16 +215,22 @@ class CtrError(RuntimeError):
 
 
 _timed = {}     # entry name -> (list of (start, end, key) torch.cuda.Event pairs, shape keys to bracket or None = all)
+_every = [1, {}]   # bracket one call in `every` of each entry (per-entry call counters): the rest run unbracketed
 # entry points reported per call shape: one entry serves launches of different shapes (the three QNN MLP products)
 _TIME_KEY = {"ctr_gemm_bf16_ex": lambda a: f"ctr_gemm_bf16_ex@{a[0]}x{a[1]}x{a[2]}" + ("b" if a[15] else "")}
 
 
-def time_calls(names):
+def time_calls(names, every=1):
     """Bracket every call of the named entry points with HIP events on the current stream (the stream
     the library launches on); ``timed_ms()`` reads the per-call averages.  ``time_calls(())`` stops.
     A name may carry a shape key (``ctr_gemm_bf16_ex@MxNxK``): only the entry's calls of that shape are bracketed
-    (the bench times just the dominant launch; events around the entry's other shapes would cost step time)."""
+    (the bench times just the dominant launch; events around the entry's other shapes would cost step time).
+    ``every`` > 1: one call in each group of ``every`` calls of an entry is bracketed, position (group index mod
+    every) in the group -- the layers' launches sampled in turn (an event record between two kernels costs a
+    boundary of its own); timed_ms() averages per bracketed call."""
     _timed.clear()
+    _every[0] = max(1, int(every))
+    _every[1] = {}
     for n in names:
         base = n.split("@")[0]
         evs, keys = _timed.setdefault(base, ([], set()))
@@ -262,6 +270,12 @@ def call(name, *args):
         key = kf(args) if kf else name
         if ent[1] is not None and key not in ent[1]:
             ent = None
+        elif _every[0] > 1:      # one call in each group of `every`, the phase rotating group to group (every
+            k = _every[1].get(key, 0)     # position -- e.g. every encoder layer's launch -- is sampled in turn)
+            _every[1][key] = k + 1
+            e = _every[0]
+            if k % e != (k // e) % e:
+                ent = None
     if ent is not None:
         import torch
         ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

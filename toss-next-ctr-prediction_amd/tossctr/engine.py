@@ -459,10 +459,14 @@ class Engine:
         xF = W.get("xF", (B, FD))
         num_off, mask_off, cat_off = D, D + a.Fn * D, D + (a.Fn + a.Fm) * D
         # ---- numeric / binary embeddings straight into their xF slots (feature_embed.py:19-27,42-48)
-        if a.Fn > 0:
+        if a.Fn > 0 and a.Fm > 0:      # both groups in one launch
+            call("ctr_feat_embed_fwd2", ptr(X_num), a.Fn, ptr(P["num_embed.weight"]), ptr(P["num_embed.bias"]),
+                 ptr(P["num_embed.out_proj.weight"]), ptr(xF, num_off), ptr(X_mask), a.Fm, ptr(P["mask_embed.weight"]),
+                 None, ptr(P["mask_embed.out_proj.weight"]), ptr(xF, mask_off), B, a.f_embed, D, FD, st)
+        elif a.Fn > 0:
             call("ctr_feat_embed_fwd", ptr(X_num), B, a.Fn, ptr(P["num_embed.weight"]), ptr(P["num_embed.bias"]),
                  ptr(P["num_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, num_off), FD, st)
-        if a.Fm > 0:
+        elif a.Fm > 0:
             call("ctr_feat_embed_fwd", ptr(X_mask), B, a.Fm, ptr(P["mask_embed.weight"]), None,
                  ptr(P["mask_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, mask_off), FD, st)
         # ---- hashed categorical gather + projection (+ emb dropout into xF) (wrapper.py:106-112,149-150)
@@ -829,14 +833,23 @@ class Engine:
             self.wgrad(ptr(dpre), D, ptr(sv["ctx"]), a.nctx * D, B, D, a.nctx * D, ptr(G["ctx_mlp.0.weight"]),
                        bias_grad=ptr(G["ctx_mlp.0.bias"]))
         # ---------------- numeric / binary embeddings
-        if a.Fn > 0:
+        if a.Fn > 0 and a.Fm > 0:      # both groups in one launch per kernel
+            fwn = W.get("fe_ws_num", (_lib.query("ctr_feat_embed_bwd_ws", B, a.Fn, D) // 4 + 1,))
+            fwm = W.get("fe_ws_mask", (_lib.query("ctr_feat_embed_bwd_ws", B, a.Fm, D) // 4 + 1,))
+            call("ctr_feat_embed_bwd2", ptr(sv["X_num"]), a.Fn, ptr(P["num_embed.weight"]), ptr(P["num_embed.bias"]),
+                 ptr(P["num_embed.out_proj.weight"]), ptr(dxF, num_off), ptr(G["num_embed.weight"]),
+                 ptr(G["num_embed.bias"]), ptr(G["num_embed.out_proj.weight"]), ptr(fwn),
+                 ptr(sv["X_mask"]), a.Fm, ptr(P["mask_embed.weight"]), None, ptr(P["mask_embed.out_proj.weight"]),
+                 ptr(dxF, mask_off), ptr(G["mask_embed.weight"]), None, ptr(G["mask_embed.out_proj.weight"]),
+                 ptr(fwm), B, a.f_embed, D, FD, st)
+        elif a.Fn > 0:
             wsz = _lib.query("ctr_feat_embed_bwd_ws", B, a.Fn, D)
             fw = W.get("fe_ws_num", (wsz // 4 + 1,))
             call("ctr_feat_embed_bwd", ptr(sv["X_num"]), B, a.Fn, ptr(P["num_embed.weight"]),
                  ptr(P["num_embed.bias"]), ptr(P["num_embed.out_proj.weight"]), a.f_embed, D, ptr(dxF, num_off), FD,
                  ptr(G["num_embed.weight"]), ptr(G["num_embed.bias"]), ptr(G["num_embed.out_proj.weight"]), ptr(fw),
                  st)
-        if a.Fm > 0:
+        elif a.Fm > 0:
             wsz = _lib.query("ctr_feat_embed_bwd_ws", B, a.Fm, D)
             fw = W.get("fe_ws_mask", (wsz // 4 + 1,))
             call("ctr_feat_embed_bwd", ptr(sv["X_mask"]), B, a.Fm, ptr(P["mask_embed.weight"]), None,
