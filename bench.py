@@ -86,7 +86,8 @@ def kernel_work(name, a, B, ffn_M, amp="bf16", ffn_flags=0):
     dP, dS K, dK, dV = 8 K^2 D backward; bytes per (sample, candidate) row: qkv (12 D), o (4 D), row max / sum
     (8 H) forward, + dO, and dqkv written (32 D) backward, plus the keep bits per (sample, head) in the kernels' lane
     layout.  The fused layer forward adds in_proj and out_proj (8 D^2 flop per row on fp32 MFMA) and reads x (4 D),
-    writes h1, x1 (8 D) and r1 (4); ``_oproj`` forms dO = dh1 W_out inside (2 D^2 flop per row, fp32 MFMA).
+    writes h1, x1 (8 D) and r1 (4); ``_oproj`` forms dO = dh1 W_out inside (2 D^2 flop per row, fp32 MFMA), the layer
+    backward (``_layer16``) also dx = dqkv W_in + dh1 (6 D^2 flop, dx written: 4 D).
     QNN pair interaction (src/models/qnn_alpha.py:86-97): the reference's A = z U projection, 2 F D QR flop per
     sample (the north star's "feature_embed_dim x proj_dim projection"), forward; its backward recomputes A and forms
     dz = dA U^T, 4 F D QR (the Gram form executes fewer flops -- priced at the reference's); bytes: z (4 F D) read,
@@ -118,6 +119,9 @@ def kernel_work(name, a, B, ffn_M, amp="bf16", ffn_flags=0):
         q16 = 12 * D * B * K if name.endswith("16") else 0                # qkv read, dqkv written in bf16
         return {"flops": [(8.0 * B * K * K * D, "bf16"), (2.0 * B * K * D * D, "f32")],
                 "bytes": float(bwd_b - q16 + mask_bf)}
+    if name == "ctr_attn_bwd_bf_layer16":     # + dx = dqkv W_in + dh1 (6 D^2 flop per row, fp32 MFMA; dx written)
+        return {"flops": [(8.0 * B * K * K * D, "bf16"), (8.0 * B * K * D * D, "f32")],
+                "bytes": float(bwd_b - 12 * D * B * K + 4 * D * B * K + mask_bf)}
     if name in ("ctr_attn_layer_fwd_bf", "ctr_attn_layer_fwd_bf16"):
         qkv_b = 6 * D if name.endswith("16") else 12 * D
         return {"flops": [(4.0 * B * K * K * D, "bf16"), (8.0 * B * K * D * D, "f32")],
@@ -312,7 +316,7 @@ def pmc_traffic(name):
              "ctr_attn_bwd_bf": ("attn_bwd_mf_kernel",), "ctr_attn_fwd_bf": ("attn_fwd_mf_kernel",),
              "ctr_attn_layer_fwd_bf": ("attn_layer_fwd_kernel",), "ctr_attn_bwd_bf_oproj": ("attn_bwd_mf_kernel",),
              "ctr_attn_layer_fwd_bf16": ("attn_layer_fwd_kernel",),
-             "ctr_attn_bwd_bf_oproj16": ("attn_bwd_mf_kernel",)}.get(name)
+             "ctr_attn_bwd_bf_oproj16": ("attn_bwd_mf_kernel",), "ctr_attn_bwd_bf_layer16": ("attn_bwd_mf_kernel",)}.get(name)
     if kerns is None:
         return None
     base = next((os.path.join(REPO, "profiles", r) for r in PMC_ROUNDS
@@ -548,7 +552,7 @@ def main():
     # algorithmic work count, kernel_work); the per-kernel table comes from extra steps after the timed region
     roof_timed = ("ctr_ffn_bwd", "ctr_ffn_bwd_norms", "ctr_ffn_fwd", "ctr_attn_bwd", "ctr_attn_fwd",
                   "ctr_attn_bwd_bf", "ctr_attn_fwd_bf", "ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj",
-                  "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16",
+                  "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16", "ctr_attn_bwd_bf_layer16",
                   "ctr_qnn_gram_fwd", "ctr_qnn_gram_bwd", "ctr_qnn_gram_fwd_zbf", "ctr_qnn_gram_bwd_zbf",
                   "ctr_gemm_bf16_ex")
     timed = roof_timed + ("ctr_lazy_flush", "ctr_lazy_flush_pair",

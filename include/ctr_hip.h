@@ -273,6 +273,18 @@ int ctr_attn_bwd_bf_oproj16(const uint16_t* qkv16, const float* o, const float* 
                             int H, int D, const float* relmean, int tk, float scale, uint32_t drop_key,
                             uint32_t drop_thresh, float drop_scale, const uint32_t* mask, const float* mrow,
                             const float* lrow, uint16_t* dqkv16, float* drel_part, void* stream);
+/* amp: bf16 -- the attention half of an encoder layer's backward in one launch, src/models/dare.py:53-62 (out_proj,
+ * attention and in_proj backward plus the skip connection): ctr_attn_bwd_bf_oproj16 on one workgroup per sample (all H
+ * heads; K <= 64, D = 32, 4 or 8 heads: ctr_attn_bwd_bf_layer_ok) followed, in the same workgroup, by
+ * dx = dqkv16 W_in + dh1 with W_in = in_proj_weight (3D x D) -- the bits of ctr_rowgemm_a16(dqkv16, W_in, tb = 0,
+ * add = dh1), which it replaces.  dqkv16 is still written (the in-projection's weight grad reads it); drel_part has
+ * ONE row per sample (B x (2tk+1)) instead of H / 4.                                                          */
+int ctr_attn_bwd_bf_layer_ok(int K, int H, int D);
+int ctr_attn_bwd_bf_layer16(const uint16_t* qkv16, const float* o, const float* dh1, const float* w_out,
+                            const float* w_in, int B, int K, int H, int D, const float* relmean, int tk, float scale,
+                            uint32_t drop_key, uint32_t drop_thresh, float drop_scale, const uint32_t* mask,
+                            const float* mrow, const float* lrow, uint16_t* dqkv16, float* drel_part, float* dx,
+                            void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Fused position-wise FFN + residual + RMSNorm of DAREEncoderLayer, src/models/dare.py:53-70

@@ -234,7 +234,8 @@ def _hip_step(shape, amp, record=()):
     _lib.time_calls(())
     eng = model.engine
     flags = {"attn_bf": eng.attn_bf, "attn_layer": eng.attn_layer, "attn_oproj": eng.attn_oproj,
-             "ffn_flags": eng.ffn_flags, "bf16": eng.bf16, "rowgemm_bf": eng.rowgemm_bf, "qkv16": eng.qkv16}
+             "ffn_flags": eng.ffn_flags, "bf16": eng.bf16, "rowgemm_bf": eng.rowgemm_bf, "qkv16": eng.qkv16,
+             "attn_layer_bwd": eng.attn_layer_bwd}
     sv = eng.last
     res = {"loss": loss, "logits": sv["logits"].double().cpu().numpy(), "idx": sv["idx"].cpu().numpy().astype(np.int64),
            "gnorm": float(opt.norm_out[0].item()), "calls": calls, "flags": flags, "params": {}}
@@ -356,7 +357,7 @@ def test_full_shape_step_matches_oracle(shape, oracle_step, oracle64):
 BF16_ENTRY_POINTS = ("ctr_attn_layer_fwd_bf", "ctr_attn_bwd_bf_oproj", "ctr_attn_fwd_bf", "ctr_attn_bwd_bf",
                      "ctr_attn_layer_fwd_bf16", "ctr_attn_bwd_bf_oproj16", "ctr_rowgemm_a16", "ctr_rowgemm_wgrad_y16",
                      "ctr_ffn_fwd", "ctr_ffn_bwd_norms", "ctr_gemm_bf16_ex", "ctr_rowgemm_bf", "ctr_rowgemm",
-                     "ctr_qnn_gram_fwd_zbf", "ctr_qnn_gram_bwd_zbf")
+                     "ctr_qnn_gram_fwd_zbf", "ctr_qnn_gram_bwd_zbf", "ctr_attn_bwd_bf_layer16")
 
 
 @pytest.mark.timeout(900)
@@ -374,6 +375,8 @@ def test_full_shape_bf16_step(shape, oracle_step):
         assert fl["attn_layer"] and fl["attn_oproj"], fl
         assert c.get("ctr_attn_layer_fwd_bf16") == nl and c.get("ctr_attn_bwd_bf_oproj16") == nl, c
         assert fl["qkv16"] and c.get("ctr_rowgemm_a16") == nl and c.get("ctr_rowgemm_wgrad_y16") == nl, (fl, c)
+        # the one-launch attention half of the layer backward is opt-in (CTR_ATTN_LAYER_BWD=1: slower, engine.py)
+        assert not fl["attn_layer_bwd"] and not c.get("ctr_attn_bwd_bf_layer16"), (fl, c)
     else:
         assert not fl["attn_layer"] and not fl["attn_oproj"], fl
         assert c.get("ctr_attn_fwd_bf") == nl and c.get("ctr_attn_bwd_bf") == nl, c

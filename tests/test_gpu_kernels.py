@@ -682,6 +682,58 @@ def test_attn_bwd_oproj_equals_two_launches(K, H, p, bias):
         assert torch.equal(r_drp.view(torch.int32), h_drp.view(torch.int32))
 
 
+@pytest.mark.parametrize("K,H,p", [(60, 8, 0.1), (64, 8, 0.1), (61, 8, 0.1), (48, 4, 0.2), (33, 8, 0.0),
+                                   (17, 4, 0.1), (1, 8, 0.1), (50, 4, 0.0)])
+@pytest.mark.parametrize("bias", [True, False])
+def test_attn_bwd_layer_equals_two_launches(K, H, p, bias):
+    """amp: ctr_attn_bwd_bf_layer16 (one workgroup per sample: dO = dh1 W_out, the attention backward, then
+    dx = dqkv16 W_in + dh1 from the workgroup's own rows) writes bit for bit what ctr_attn_bwd_bf_oproj16 +
+    ctr_rowgemm_a16(add = dh1) write: dqkv16 and dx; its one positional-bias row per sample is the sum of the H / 4
+    head-group rows (the same bits at H = 4, one group)."""
+    L = _lib()
+    D = 32
+    assert L.query("ctr_attn_bwd_bf_layer_ok", K, H, D) == 1
+    from tossctr.rng import drop_args
+    B, dh, tk = 37, D // H, K
+    g = torch.Generator(device="cuda").manual_seed(K * 31 + H)
+    qkv = torch.randn(B * K, 3 * D, device="cuda", generator=g)
+    dh1 = torch.randn(B * K, D, device="cuda", generator=g)
+    w_out = torch.randn(D, D, device="cuda", generator=g) * D ** -0.5
+    w_in = torch.randn(3 * D, D, device="cuda", generator=g) * D ** -0.5
+    relmean = torch.randn(2 * tk + 1, device="cuda", generator=g)
+    rm = ptr(relmean) if bias else None
+    dk = drop_args(556, 5, p, True)
+    scale = float(np.float32(math.sqrt(1.0 / dh)))
+    st = stream()
+    o = torch.empty(B * K, D, device="cuda")
+    mrow = torch.empty(B * H * K, device="cuda")
+    lrow = torch.empty(B * H * K, device="cuda")
+    mask = torch.zeros(L.query("ctr_attn_mask_words", B, K, H), dtype=torch.int32, device="cuda")
+    L.call("ctr_attn_fwd_bf", ptr(qkv), B, K, H, D, rm, tk, scale, *dk, ptr(mask), ptr(o), ptr(mrow), ptr(lrow), st)
+    qkv16 = torch.cat([qkv[:, :D] * scale, qkv[:, D:]], 1).bfloat16()
+    ng = L.query("ctr_attn_bwd_bf_nparts", H)
+    r_dqkv = torch.full((B * K, 3 * D), float("nan"), device="cuda", dtype=torch.bfloat16)
+    r_drp = torch.full((ng * B, 2 * tk + 1), float("nan"), device="cuda")
+    L.call("ctr_attn_bwd_bf_oproj16", ptr(qkv16), ptr(o), ptr(dh1), ptr(w_out), B, K, H, D, rm, tk, scale, *dk,
+           ptr(mask), ptr(mrow), ptr(lrow), ptr(r_dqkv), ptr(r_drp), st)
+    r_dx = torch.full((B * K, D), float("nan"), device="cuda")
+    L.call("ctr_rowgemm_a16", B * K, 3 * D, D, ptr(r_dqkv), 3 * D, ptr(w_in), 0, ptr(r_dx), D, None, ptr(dh1), D, st)
+    f_dqkv = torch.full_like(r_dqkv, float("nan"))
+    f_drp = torch.full((B, 2 * tk + 1), float("nan"), device="cuda")
+    f_dx = torch.full_like(r_dx, float("nan"))
+    L.call("ctr_attn_bwd_bf_layer16", ptr(qkv16), ptr(o), ptr(dh1), ptr(w_out), ptr(w_in), B, K, H, D, rm, tk, scale,
+           *dk, ptr(mask), ptr(mrow), ptr(lrow), ptr(f_dqkv), ptr(f_drp), ptr(f_dx), st)
+    torch.cuda.synchronize()
+    assert torch.equal(f_dqkv.view(torch.int16), r_dqkv.view(torch.int16)), int((f_dqkv != r_dqkv).sum())
+    assert torch.equal(f_dx.view(torch.int32), r_dx.view(torch.int32)), int((f_dx != r_dx).sum())
+    if bias:
+        want = r_drp.view(B, ng, -1).sum(1)
+        if ng == 1:
+            assert torch.equal(f_drp.view(torch.int32), want.view(torch.int32))
+        else:
+            torch.testing.assert_close(f_drp, want, rtol=1e-5, atol=1e-5 * float(want.abs().max()))
+
+
 @pytest.mark.parametrize("M", [245760, 1000, 33, 1])
 @pytest.mark.parametrize("add", [True, False])
 def test_rowgemm_bf16_operand_forms_equal_fp32_forms(M, add):

@@ -67,6 +67,11 @@ struct AttnBfArgs {
   // the reference's autocast in-projection output grad
   const __bf16* qkv16;
   __bf16* dqkv16;
+  // the layer backward (ctr_attn_bwd_bf_layer16: one workgroup holds every head of a sample): the in-projection's
+  // input grad dx = dqkv W_in + dh1 from the workgroup's own dqkv16 rows, W_in = in_proj_weight (3D, D)
+  const float* w_in;
+  float* dx;
+  int dx_lds;            // byte offset of the workgroup's LDS dqkv copy
 };
 
 // workgroup -> (sample, head group), 1-D grid: with ngrp > 1 head groups a sample's workgroups are 8 apart in
@@ -192,31 +197,32 @@ __device__ __forceinline__ void lds_barrier() {
 // 4g < dh, the row's mask chunk at 4g == dh, the zero chunk beyond.  Column (transposed) reads take 16 slots from
 // the head's first dim: the slots past its dims land in output rows d >= dh of the product, which are never
 // stored.  (A mask chunk per head took 52 instead of 40 slots per row at dh = 8.)
-template <int DH, int NT>
+// HG: the heads a row holds (4; 8 for the layer backward at dh = 4, which stages all of D = 32 in one workgroup)
+template <int DH, int NT, int HG = 4>
 struct Stg {
   static constexpr int KT = Kt<NT>::KT;
   static constexpr int HS = DH;                     // slots per head
-  static constexpr int RS = 4 * DH + 8;             // row stride (bf16 elements), <= 4 heads
+  static constexpr int RS = HG * DH + 8;            // row stride (bf16 elements), <= HG heads
   static constexpr int IM = KT * RS;                // elements per staged operand
   static constexpr int PAD = 16;                    // transposed reads past the last head of the last row
-  static constexpr int MOFF = 4 * DH;               // the row's mask chunk
-  static constexpr int ZOFF = 4 * DH + 4;           // the row's zero chunk
+  static constexpr int MOFF = HG * DH;              // the row's mask chunk
+  static constexpr int ZOFF = HG * DH + 4;          // the row's zero chunk
 };
 constexpr float NEG_BIG = -3.0e38f;
 
-template <int DH, int NT, bool WITH_DO>
+template <int DH, int NT, bool WITH_DO, int HG = 4>
 __device__ __forceinline__ void stage(const AttnBfArgs& a, int b, int hg, __bf16* sq, __bf16* sk, __bf16* sv, __bf16* sdo) {
-  using S = Stg<DH, NT>;
+  using S = Stg<DH, NT, HG>;
   constexpr int KT = S::KT;
   const int K = a.K, D = a.D, G = a.G;
   const float* base = a.qkv + (long)b * K * 3 * D + hg * G * DH;
   const float* dob = WITH_DO ? a.dO + (long)b * K * D + hg * G * DH : nullptr;
-  constexpr int NCD = DH / 4, NCR = 4 * NCD + 2;  // chunks per row: 4 heads' dims, mask, zero
+  constexpr int NCD = DH / 4, NCR = HG * NCD + 2;  // chunks per row: HG heads' dims, mask, zero
   for (int e = threadIdx.x; e < KT * NCR; e += blockDim.x) {
     const int j = e / NCR, ch = e - j * NCR;
     f32x4 q = {0.f, 0.f, 0.f, 0.f}, k = q, v = q, d = q;
     int o;
-    if (ch < 4 * NCD) {
+    if (ch < HG * NCD) {
       const int u = ch / NCD, dc = ch - u * NCD;
       o = j * S::RS + u * DH + 4 * dc;
       if (u < G && j < K) {
@@ -234,7 +240,7 @@ __device__ __forceinline__ void stage(const AttnBfArgs& a, int b, int hg, __bf16
         }
         if (WITH_DO) d = *(const f32x4*)(dob + (long)j * D + u * DH + 4 * dc);
       }
-    } else if (ch == 4 * NCD) {                   // the row's mask chunk
+    } else if (ch == HG * NCD) {                  // the row's mask chunk
       o = j * S::RS + S::MOFF;
       q[0] = NEG_BIG;
       k[0] = j >= K ? 1.f : 0.f;
@@ -275,14 +281,14 @@ __host__ __device__ constexpr int img_elems() { return Kt<NT>::KT * 16; }   // b
 // operand reads: row access (lane (g, c) <- slots 4g .. 4g+3 of row `row`; zeros past the head's slots) and
 // transposed column access (lane (g, c) <- column c of rows row0 + 4g .. row0 + 4g + 3)
 // (the row read is unconditional: lanes past the head's slots read the zero chunk at ZOFF of the image)
-template <int DH, int NT>
+template <int DH, int NT, int HG = 4>
 __device__ __forceinline__ bf16x4 op_row(const __bf16* img, int row, int hs, int g) {
-  using S = Stg<DH, NT>;
+  using S = Stg<DH, NT, HG>;
   return ld4(img + row * S::RS + (4 * g < DH ? hs + 4 * g : 4 * g == DH ? S::MOFF : S::ZOFF));
 }
-template <int DH, int NT>
+template <int DH, int NT, int HG = 4>
 __device__ __forceinline__ bf16x4 op_col(const __bf16* img, int row0, int hs, int g, int c) {
-  return tr4(img + (row0 + 4 * g + (c >> 2)) * Stg<DH, NT>::RS + hs + 4 * (c & 3));
+  return tr4(img + (row0 + 4 * g + (c >> 2)) * Stg<DH, NT, HG>::RS + hs + 4 * (c & 3));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -455,11 +461,11 @@ __device__ __forceinline__ int diag_off(int ee) {
   return n <= 16 ? n * (n + 1) / 2 : 256 - (31 - n) * (32 - n) / 2;
 }
 
-template <int NT, int DH, bool BIAS, bool DROP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_mf_kernel(AttnBfArgs a) {
+template <int NT, int DH, bool BIAS, bool DROP, int HG = 4, bool DX = false>
+__global__ __launch_bounds__(64 * HG) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_mf_kernel(AttnBfArgs a) {
   const int b = wg_sample(a), hgrp = wg_group(a);
   if (b >= a.B) return;      // the grid's tail past the last sample
-  using S = Stg<DH, NT>;
+  using S = Stg<DH, NT, HG>;
   using KB = Kt<NT>;
   constexpr int ND = 2 * NT - 1, IMG = img_elems<NT>(), KT = KB::KT;
   extern __shared__ __attribute__((aligned(16))) __bf16 smb[];
@@ -469,7 +475,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   __bf16* sv = sk + S::IM;
   __bf16* sdo = sv + S::IM;
   __bf16* simg = sdo + S::IM + S::PAD;              // per wave: dS image, p~ image
-  float* srel = (float*)(simg + 4 * 2 * IMG);
+  float* srel = (float*)(simg + HG * 2 * IMG);
+  // DX: the bf16 dqkv rows [KT][DXS] past the staging / epilogue space (a.dx_lds bytes from the base)
+  constexpr int DXS = 104;                  // 208-byte rows: the tail's 16-byte row reads hit distinct banks
+  __bf16* sdx = (__bf16*)((char*)smb + (DX ? a.dx_lds : 0));
   const bool opj = a.dh1 != nullptr;      // block-uniform
   const int GD = G * DH;                    // the workgroup's columns of dO
   float* dot = (float*)simg;                // opj: the dO tile [KT][GD] (fp32), in the image space until the loop
@@ -526,7 +535,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       for (int kk = 0; kk < 8; ++kk)
         acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk < 4 ? x0[kk] : x1[kk - 4], wv[kk], acc[q], 0, 0, 0);
     }
-    stage<DH, NT, false>(a, b, hgrp, sq, sk, sv, nullptr);
+    stage<DH, NT, false, HG>(a, b, hgrp, sq, sk, sv, nullptr);
     for (int j = threadIdx.x; j < KT; j += blockDim.x) {   // sdo's mask / zero chunks
       *(bf16x4*)(sdo + j * S::RS + S::MOFF) = bf16x4{};
       *(bf16x4*)(sdo + j * S::RS + S::ZOFF) = bf16x4{};
@@ -546,7 +555,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       }
     }
   } else {
-    stage<DH, NT, true>(a, b, hgrp, sq, sk, sv, sdo);
+    stage<DH, NT, true, HG>(a, b, hgrp, sq, sk, sv, sdo);
     if (BIAS) stage_rel<NT>(a, srel);
   }
   lds_barrier();
@@ -588,14 +597,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   for (int tj = 0; tj < NT; ++tj) {
     __builtin_amdgcn_sched_barrier(0);     // one key tile at a time: bounds the live registers
     const int j = 16 * tj + c;
-    const bf16x4 kop = op_row<DH, NT>(sk, j, hs, g);                                       // A = k [j][d]
-    const bf16x4 vop = op_row<DH, NT>(sv, j, hs, g);                                       // A = v [j][d]
-    const bf16x4 ktop = op_col<DH, NT>(sk, 16 * tj, hs, g, c);                             // A = k^T [d][j]
+    const bf16x4 kop = op_row<DH, NT, HG>(sk, j, hs, g);                                       // A = k [j][d]
+    const bf16x4 vop = op_row<DH, NT, HG>(sv, j, hs, g);                                       // A = v [j][d]
+    const bf16x4 ktop = op_col<DH, NT, HG>(sk, 16 * tj, hs, g, c);                             // A = k^T [d][j]
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int i = 16 * ti + c;
-      const bf16x4 qop = op_row<DH, NT>(sq, i, hs, g);                                     // B = q^T [d][i]
-      const bf16x4 doop = op_row<DH, NT>(sdo, i, hs, g);                                   // B = do^T [d][i]
+      const bf16x4 qop = op_row<DH, NT, HG>(sq, i, hs, g);                                     // B = q^T [d][i]
+      const bf16x4 doop = op_row<DH, NT, HG>(sdo, i, hs, g);                                   // B = do^T [d][i]
       const f32x4 s = mma(kop, qop, f32x4{0.f, 0.f, 0.f, 0.f});                       // S^T [j][i]
       const f32x4 dp = mma(vop, doop, f32x4{0.f, 0.f, 0.f, 0.f});                     // dP~^T [j][i]
       const f32x4 st = stw[i];
@@ -627,22 +636,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int rw = 16 * ti + 4 * g + (c >> 2);
-      dk = mma(op_col<DH, NT>(sq, 16 * ti, hs, g, c), tr4(ids + swz(rw, c & 3)), dk);      // B = dS [i][j]
-      dv = mma(op_col<DH, NT>(sdo, 16 * ti, hs, g, c), tr4(ipt + swz(rw, c & 3)), dv);     // B = p~ [i][j]
+      dk = mma(op_col<DH, NT, HG>(sq, 16 * ti, hs, g, c), tr4(ids + swz(rw, c & 3)), dk);      // B = dS [i][j]
+      dv = mma(op_col<DH, NT, HG>(sdo, 16 * ti, hs, g, c), tr4(ipt + swz(rw, c & 3)), dv);     // B = p~ [i][j]
     }
     __builtin_amdgcn_wave_barrier();
     if (4 * g < DH && j < K) {
       const long off = ((long)b * K + j) * 3 * D + h * DH + 4 * g;
       store_dqkv(a, off + D, dk);
       store_dqkv(a, off + 2 * D, dv);
+      if constexpr (DX) {      // the workgroup's copy of its bf16 dqkv rows for the in-projection product below
+        *(u32x2*)(sdx + j * DXS + D + h * DH + 4 * g) = pk_bf4(dk);
+        *(u32x2*)(sdx + j * DXS + 2 * D + h * DH + 4 * g) = pk_bf4(dv);
+      }
     }
   }
   if (4 * g < DH) {
 #pragma unroll
     for (int ti = 0; ti < NT; ++ti) {
       const int i = 16 * ti + c;
-      if (i < K) store_dqkv(a, ((long)b * K + i) * 3 * D + h * DH + 4 * g, dq[ti] * a.scale);
+      if (i < K) {
+        store_dqkv(a, ((long)b * K + i) * 3 * D + h * DH + 4 * g, dq[ti] * a.scale);
+        if constexpr (DX) *(u32x2*)(sdx + i * DXS + h * DH + 4 * g) = pk_bf4(dq[ti] * a.scale);
+      }
     }
+  }
+  // DX: the in-projection product's operands that do not come from this kernel, issued before the bias epilogue
+  // (wave w: column block w & 1, row blocks w / 2 (+ 2 with four waves); W_in (96, 32) row-major, tb = 0)
+  const long r0 = (long)b * K;
+  float wv[DX ? 24 : 1], res[DX ? 8 / HG : 1][4];
+  if constexpr (DX) {
+    const int n = 16 * (w & 1) + c;
+#pragma unroll
+    for (int kk = 0; kk < 24; ++kk) wv[kk] = a.w_in[(24 * g + kk) * 32 + n];
+#pragma unroll
+    for (int q = 0; q < 8 / HG; ++q)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) res[q][rr] = a.dh1[(r0 + min(16 * ((w >> 1) + 2 * q) + 4 * g + rr, K - 1)) * 32 + n];
   }
   if (BIAS) {
     // diagonal sums of dS: register (dt, r) of lane (g, c) holds the sum over the tiles of diagonal dt of
@@ -663,16 +692,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     for (int p = threadIdx.x; p < 256; p += blockDim.x) {
       const int aa = p >> 4, cc = p & 15;
       const int o = diag_off(aa - cc) + (aa < cc ? aa : cc);
-      float v[ND][4];
+      float v[ND][HG];
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[dt][u] = sd[((u < G ? u : 0) * ND + dt) * 256 + p];
+        for (int u = 0; u < HG; ++u) v[dt][u] = sd[((u < G ? u : 0) * ND + dt) * 256 + p];
 #pragma unroll
       for (int dt = 0; dt < ND; ++dt) {
         float s = 0.f;
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < HG; ++u)
           if (u < G) s += v[dt][u];
         sh[dt * 256 + o] = s;
       }
@@ -717,8 +746,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       if (d < -(16 * NT - 1) || d > 16 * NT - 1) out[e] = 0.f;
     }
   }
+  if constexpr (DX) {
+    // The in-projection's input grad of the sample's rows plus the residual, dx = dqkv W_in + dh1 (dare.py:53-70:
+    // the in_proj backward of MHA and the skip connection around it), from the workgroup's LDS copy of the bf16 dqkv
+    // rows it stored: rowgemm_kernel<96, 32, true, true>'s products in its k order and its epilogue -- lane group g
+    // holds k = 24 g .. 24 g + 23 of row 16 rb + c, one v_mfma_f32_16x16x4f32 per k step, (acc + 0) + dh1 -- so the
+    // bits of the ctr_rowgemm_a16 launch this replaces.  Tiles (row block rb, column block cb) of the K x 32 result.
+    if (!BIAS) lds_barrier();                         // (the bias epilogue's barriers order the copy otherwise)
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    const int cb = w & 1, n = 16 * cb + c;
+#pragma unroll
+    for (int q = 0; q < 8 / HG; ++q) {
+      const int rb = (w >> 1) + 2 * q;
+      if (16 * rb >= K) break;                        // wave-uniform
+      const __bf16* ap = sdx + min(16 * rb + c, K - 1) * DXS + 24 * g;
+      const bf16x8 v0 = *(const bf16x8*)ap, v1 = *(const bf16x8*)(ap + 8), v2 = *(const bf16x8*)(ap + 16);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 24; ++kk) {
+        const float av = kk < 8 ? (float)v0[kk] : kk < 16 ? (float)v1[kk - 8] : (float)v2[kk - 16];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, wv[kk], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int i = 16 * rb + 4 * g + rr;
+        if (i < K) {
+          float v = acc[rr] + 0.f;
+          v += res[q][rr];
+          a.dx[(r0 + i) * 32 + n] = v;
+        }
+      }
+    }
+  }
 }
-
 // ------------------------------------------------------------------------------------------------
 // backward for K > 64 (nt > 4).  The nt <= 4 kernel's per-wave [KT][16] dS / p~ images and its (2 nt - 1) x 4
 // diagonal registers would take ~120 KB of LDS and ~500 registers per wave at nt = 10; here
@@ -1215,10 +1275,11 @@ int pick_g(int H) {
 template <int DH, int NT>
 size_t fwd_lds(int tk) { return ((size_t)3 * Stg<DH, NT>::IM + Stg<DH, NT>::PAD) * 2 + (size_t)rel_floats<NT>(tk) * 4; }
 
-template <int DH, int NT>
+template <int DH, int NT, int HG = 4>
 size_t bwd_lds(int G, int tk) {
-  const size_t main = ((size_t)4 * Stg<DH, NT>::IM + Stg<DH, NT>::PAD) * 2 + (size_t)4 * 2 * img_elems<NT>() * 2 +
-                      (size_t)rel_floats<NT>(tk) * 4 + (size_t)4 * Kt<NT>::KT * 16;
+  using S = Stg<DH, NT, HG>;
+  const size_t main = ((size_t)4 * S::IM + S::PAD) * 2 + (size_t)HG * 2 * img_elems<NT>() * 2 +
+                      (size_t)rel_floats<NT>(tk) * 4 + (size_t)HG * Kt<NT>::KT * 16;
   const size_t ND = 2 * NT - 1, diag = ((size_t)G * ND * 256 + ND * 256 + 16) * 4;
   return main > diag ? main : diag;
 }
@@ -1307,6 +1368,34 @@ void launch_bwd2(const AttnBfArgs& a, hipStream_t s) {
     case 8: launch_bwd3<8, DH>(a, s); break;
     case 9: launch_bwd3<9, DH>(a, s); break;
     default: launch_bwd3<10, DH>(a, s); break;
+  }
+}
+
+// the layer backward: one workgroup of H waves per sample, every head staged in its rows (HG = H = D / dh)
+template <int NT, int DH, bool BIAS, bool DROP>
+void launch_bwd_layer4(const AttnBfArgs& a, hipStream_t s) {
+  constexpr int HG = 32 / DH;
+  AttnBfArgs b = a;
+  b.dx_lds = (int)bwd_lds<DH, NT, HG>(a.G, BIAS ? a.tk : 0);
+  const size_t sm = (size_t)b.dx_lds + (size_t)Kt<NT>::KT * 104 * 2;
+  allow_lds(attn_bwd_mf_kernel<NT, DH, BIAS, DROP, HG, true>, sm);
+  attn_bwd_mf_kernel<NT, DH, BIAS, DROP, HG, true><<<a.B, dim3(64 * HG), sm, s>>>(b);
+}
+template <int NT, int DH>
+void launch_bwd_layer3(const AttnBfArgs& a, hipStream_t s) {
+  const bool bias = a.relmean != nullptr, drop = a.drop.thresh != 0;
+  if (bias && drop) launch_bwd_layer4<NT, DH, true, true>(a, s);
+  else if (bias) launch_bwd_layer4<NT, DH, true, false>(a, s);
+  else if (drop) launch_bwd_layer4<NT, DH, false, true>(a, s);
+  else launch_bwd_layer4<NT, DH, false, false>(a, s);
+}
+template <int DH>
+void launch_bwd_layer2(const AttnBfArgs& a, hipStream_t s) {
+  switch (a.nt) {
+    case 1: launch_bwd_layer3<1, DH>(a, s); break;
+    case 2: launch_bwd_layer3<2, DH>(a, s); break;
+    case 3: launch_bwd_layer3<3, DH>(a, s); break;
+    default: launch_bwd_layer3<4, DH>(a, s); break;
   }
 }
 
@@ -1400,6 +1489,33 @@ extern "C" int ctr_attn_bwd_bf_oproj16(const uint16_t* qkv16, const float* o, co
   CTR_REQUIRE(B == 0 || (qkv16 && dqkv16), "ctr_attn_bwd_bf_oproj16: qkv16 and dqkv16 are required");
   return attn_bwd_oproj(nullptr, (const __bf16*)qkv16, o, dh1, w_out, B, K, H, D, relmean, tk, scale, drop_key,
                         drop_thresh, drop_scale, mask, mrow, lrow, nullptr, (__bf16*)dqkv16, drel_part, stream);
+}
+
+extern "C" int ctr_attn_bwd_bf_layer_ok(int K, int H, int D) {
+  return (bf_ok(K, H, D) && K <= 64 && D == 32 && (H == 8 || H == 4)) ? 1 : 0;
+}
+
+extern "C" int ctr_attn_bwd_bf_layer16(const uint16_t* qkv16, const float* o, const float* dh1, const float* w_out,
+                                       const float* w_in, int B, int K, int H, int D, const float* relmean, int tk,
+                                       float scale, uint32_t drop_key, uint32_t drop_thresh, float drop_scale,
+                                       const uint32_t* mask, const float* mrow, const float* lrow, uint16_t* dqkv16,
+                                       float* drel_part, float* dx, void* stream) {
+  if (B == 0) return 0;
+  CTR_REQUIRE(ctr_attn_bwd_bf_layer_ok(K, H, D), "ctr_attn_bwd_bf_layer16: K <= 64, D = 32, 4 or 8 heads");
+  CTR_REQUIRE(qkv16 && dqkv16 && dh1 && w_out && w_in && dx, "ctr_attn_bwd_bf_layer16: null operand");
+  CTR_REQUIRE(!relmean || tk >= K - 1, "positional-bias table shorter than K");
+  CTR_REQUIRE(!drop_thresh || mask, "attention backward with dropout needs the forward's keep bits");
+  AttnBfArgs a{};
+  a.B = B; a.K = K; a.H = H; a.D = D; a.G = H; a.ngrp = 1; a.nt = (K + 15) / 16; a.tk = tk;
+  a.relmean = relmean; a.scale = scale; a.drop = Drop{drop_key, drop_thresh, drop_scale};
+  a.mask = const_cast<uint32_t*>(mask); a.o = const_cast<float*>(o); a.mrow = const_cast<float*>(mrow);
+  a.lrow = const_cast<float*>(lrow); a.drel_part = drel_part;
+  a.dh1 = dh1; a.w_out = w_out; a.qkv16 = (const __bf16*)qkv16; a.dqkv16 = (__bf16*)dqkv16;
+  a.w_in = w_in; a.dx = dx;
+  hipStream_t s = (hipStream_t)stream;
+  if (D / H == 4) launch_bwd_layer2<4>(a, s);
+  else launch_bwd_layer2<8>(a, s);
+  return check_launch("attn_bwd_bf_layer16");
 }
 
 extern "C" int ctr_attn_layer_fwd_ok(int K, int H, int D) {

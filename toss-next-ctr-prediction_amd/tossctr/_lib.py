@@ -100,6 +100,8 @@ SIGS = {
     "ctr_attn_bwd_bf_oproj_ok": (i, [i, i, i]),
     "ctr_attn_bwd_bf_oproj": (i, [p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
     "ctr_attn_bwd_bf_oproj16": (i, [p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p]),
+    "ctr_attn_bwd_bf_layer_ok": (i, [i, i, i]),
+    "ctr_attn_bwd_bf_layer16": (i, [p, p, p, p, p, i, i, i, i, p, i, f, u, u, f, p, p, p, p, p, p, p]),
     "ctr_attn_layer_fwd_ok": (i, [i, i, i]),
     "ctr_attn_layer_fwd_bf": (i, [p, i, i, i, i, p, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),
     "ctr_attn_layer_fwd_bf16": (i, [p, i, i, i, i, p, p, p, p, i, f, u, u, f, p, p, p, p, f, p, p, p, p, p, p, p, p]),

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import numpy as np
 import torch
@@ -205,6 +206,12 @@ class Engine:
         # the in-projection's backward reading the bf16 grad (ctr_rowgemm_a16 / ctr_rowgemm_wgrad_y16)
         # (-67 us a step at cfg2, profiles/r06/ab_qkv16.log)
         self.qkv16 = bool(self.attn_layer and self.attn_oproj and not self.rowgemm_bf)
+        # ... and, opt-in (CTR_ATTN_LAYER_BWD=1), the in-projection's input grad + residual inside the attention
+        # backward too (ctr_attn_bwd_bf_layer16: ctr_rowgemm_a16's bits).  Not the default: it needs every head of a
+        # sample in one 8-wave workgroup, and that form of the attention backward ran 124 -> 173 us a launch, more
+        # than the 26 us in_proj launch and its boundary it removes (step +20 us, profiles/r06/ab_attn_layer_bwd.log)
+        self.attn_layer_bwd = bool(self.qkv16 and os.environ.get("CTR_ATTN_LAYER_BWD", "0") == "1" and
+                                   _lib.query("ctr_attn_bwd_bf_layer_ok", a.top_k, a.H, a.D))
 
     def _tab_array(self, keys, bases):
         """Device ctr_lazy_tab_t array (no lazy state) describing arena tables."""
@@ -981,13 +988,17 @@ class Engine:
             self.gemm(M, D, D, ptr(dh1), D, 0, ptr(P[pre + "mha.out_proj.weight"]), D, 0, ptr(do), D)
         # attention core
         dqkv = W.get(f"dqkv{li}", (M, 3 * D), torch.bfloat16 if self.qkv16 else torch.float32)
-        nparts = (_lib.query("ctr_attn_bwd_bf_nparts", a.H) if self.attn_bf else
+        nparts = (1 if self.attn_layer_bwd else _lib.query("ctr_attn_bwd_bf_nparts", a.H) if self.attn_bf else
                   _lib.query("ctr_attn_bwd_nparts", a.H, K, D)) * B
         nrel = 2 * a.top_k + 1
         drp = W.get(f"drel_part{li}", (nparts, nrel))
         da = drop_args(seed, SITE_ATTN0 + 2 * li, a.mha_p, training)
         scale = float(np.float32(math.sqrt(1.0 / float(D // a.H))))
-        if self.attn_oproj:
+        if self.attn_layer_bwd:          # + dout = dqkv W_in + dh1 (the in_proj launch below is not needed)
+            call("ctr_attn_bwd_bf_layer16", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]),
+                 ptr(P[pre + "mha.in_proj_weight"]), B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale, *da,
+                 ptr(Ls["amask"]), ptr(Ls["mrow"]), ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), ptr(dout_buf), st)
+        elif self.attn_oproj:
             call("ctr_attn_bwd_bf_oproj16" if self.qkv16 else "ctr_attn_bwd_bf_oproj", ptr(Ls["qkv"]), ptr(Ls["o"]), ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]),
                  B, K, a.H, D, ptr(Ls["relmean"]), a.top_k, scale, *da, ptr(Ls["amask"]), ptr(Ls["mrow"]),
                  ptr(Ls["lrow"]), ptr(dqkv), ptr(drp), st)
@@ -1004,7 +1015,9 @@ class Engine:
                 self.wgrad_rows(W, ptr(dqkv), ptr(x_in), M, 3 * D, D, pre + "mha.in_proj_weight",
                                 pre + "mha.in_proj_bias", tag=li, defer=True, y16=self.qkv16)
         # in_proj
-        if self.qkv16:
+        if self.attn_layer_bwd:
+            pass
+        elif self.qkv16:
             call("ctr_rowgemm_a16", M, 3 * D, D, ptr(dqkv), 3 * D, ptr(P[pre + "mha.in_proj_weight"]), 0,
                  ptr(dout_buf), D, None, ptr(dh1), D, st)
         elif self.rowgemm:
