@@ -473,6 +473,18 @@ int ctr_norm_nparts_per_call(void);
 int ctr_sqnorm_dense(const float* x, long n, float* part, void* stream);
 int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint32_t* n_uniq, int width, int ld,
                     uint32_t invalid_key, float* part, void* stream);
+/* ctr_sqnorm_dense(x, n) and ctr_sqnorm_rows of each of rows[0 .. nrows) (nrows <= CTR_SQNORM_MAX_ROWS) in one launch:
+ * part[0 .. P) the dense partials, part[(1 + j) P ..) table j's, P = ctr_norm_nparts_per_call() -- the same values
+ * (bits) the separate calls write, so ctr_clip_finalize over (1 + nrows) P partials gives the same norm.       */
+#define CTR_SQNORM_MAX_ROWS 4
+typedef struct {
+  const uint32_t* keys;
+  const float* G;
+  const uint32_t* n_uniq;
+  int width, ld;
+} ctr_sqnorm_rows_t;
+int ctr_sqnorm_all(const float* x, long n, const ctr_sqnorm_rows_t* rows, int nrows, uint32_t invalid_key, float* part,
+                   void* stream);
 /* out[0] = global L2 norm of (summed grads * grad_scale); out[1] = grad_scale * min(1, max_norm/(norm+1e-6))
  * (grad_scale alone if max_norm <= 0) -- the multiplier the AdamW stream applies to raw grads      */
 int ctr_clip_finalize(const float* part, int nparts, float max_norm, float grad_scale, float* out, void* stream);

@@ -1592,3 +1592,50 @@ def test_zero_f32(n):
     L.call("ctr_zero_f32", ptr(buf), n, stream())
     torch.cuda.synchronize()
     assert (buf[:n] == 0).all() and (buf[n:] == 7.0).all()
+
+
+@pytest.mark.parametrize("case", ["cfg2", "ragged", "empty"])
+def test_sqnorm_all_equals_separate_calls(case):
+    """ctr_sqnorm_all (dense + three compact row-grad tables in one launch) writes bit for bit the partials of
+    ctr_sqnorm_dense + ctr_sqnorm_rows x 3, so ctr_clip_finalize gives the same norm: trailing INVALID key group,
+    a row stride that is not a multiple of 4 (strided path), an empty table."""
+    import ctypes as C
+    from tossctr import _lib as TL
+    L = _lib()
+    g = torch.Generator(device="cuda").manual_seed(len(case))
+    inv = 0xFFFFFFFF
+    n_dense = {"cfg2": 1_234_567, "ragged": 1001, "empty": 0}[case]
+    dense = torch.randn(n_dense + 1, device="cuda", generator=g)[1:] if case == "ragged" else \
+        torch.randn(max(n_dense, 1), device="cuda", generator=g)[:n_dense]
+    tabs = []
+    for j, (rows, width, ld, n_valid, with_inv) in enumerate({
+            "cfg2": [(300_000, 32, 32, 250_000, True), (300_000, 32, 32, 250_000, True), (80_000, 33, 36, 70_000, False)],
+            "ragged": [(1000, 33, 33, 999, True), (17, 8, 8, 3, False), (5, 64, 64, 4, True)],
+            "empty": [(16, 32, 32, 0, False), (16, 32, 32, 0, False), (16, 33, 36, 0, False)]}[case]):
+        G = torch.randn(rows, ld, device="cuda", generator=g)
+        G[:, width:] = 0.0
+        nu = n_valid + (1 if with_inv else 0)
+        keys = torch.arange(rows, device="cuda", dtype=torch.int32)
+        if with_inv:
+            keys[nu - 1] = -1                   # 0xFFFFFFFF as uint32
+        tabs.append((keys, G, torch.tensor([nu], device="cuda", dtype=torch.int32), width, ld))
+    P = L.query("ctr_norm_nparts_per_call")
+    st = stream()
+    ref = torch.full((4 * P,), float("nan"), device="cuda")
+    L.call("ctr_sqnorm_dense", ptr(dense), n_dense, ptr(ref), st)
+    for j, (keys, G, nu, width, ld) in enumerate(tabs):
+        L.call("ctr_sqnorm_rows", ptr(keys), ptr(G), ptr(nu), width, ld, inv, ptr(ref, (j + 1) * P), st)
+    arr = (TL.SqnormRows * 3)()
+    for o, (keys, G, nu, width, ld) in zip(arr, tabs):
+        o.keys, o.G, o.n_uniq, o.width, o.ld = ptr(keys), ptr(G), ptr(nu), width, ld
+    got = torch.full_like(ref, float("nan"))
+    L.call("ctr_sqnorm_all", ptr(dense), n_dense, arr, 3, inv, ptr(got), st)
+    out_r = torch.zeros(2, device="cuda")
+    out_g = torch.zeros(2, device="cuda")
+    L.call("ctr_clip_finalize", ptr(ref), 4 * P, 1.0, 1.0, ptr(out_r), st)
+    L.call("ctr_clip_finalize", ptr(got), 4 * P, 1.0, 1.0, ptr(out_g), st)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), int((got != ref).sum())
+    assert torch.equal(out_g.view(torch.int32), out_r.view(torch.int32))
+    want = float(dense.double().pow(2).sum()) + sum(float(G[:int(nu.item()) - (1 if int(nu.item()) and int(k[int(nu.item()) - 1].item()) == -1 else 0)].double().pow(2).sum()) for k, G, nu, _, _ in tabs)
+    assert abs(float(out_g[0]) - math.sqrt(want)) <= 1e-5 * math.sqrt(want) + 1e-30

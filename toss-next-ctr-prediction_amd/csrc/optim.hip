@@ -130,16 +130,15 @@ __global__ __launch_bounds__(256) void adamw_ema_kernel(const ctr_opt_chunk_t* _
 // ---------------- global grad norm (clip_grad_norm_) ----------------
 constexpr int NORM_BLOCKS = 256;
 
-__global__ __launch_bounds__(256) void sqnorm_dense_kernel(const float* __restrict__ x, long n,
-                                                           float* __restrict__ part) {
-  __shared__ float red[4];
+// block bx of gx: its partial of sum x^2 (the thread's own sum; the caller reduces the block)
+__device__ __forceinline__ float sqnorm_dense_part(const float* __restrict__ x, long n, int bx, int gx) {
   float s = 0.f;
   if ((((uintptr_t)x) & 15) == 0) {   // 16-byte loads, four independent chains; scalar tail
     const long n4 = n >> 2;
     const float4* x4 = (const float4*)x;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll 4
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    for (long i = bx * 256L + threadIdx.x; i < n4; i += (long)gx * 256) {
       const float4 v = x4[i];
       s0 = fmaf(v.x, v.x, s0);
       s1 = fmaf(v.y, v.y, s1);
@@ -147,21 +146,25 @@ __global__ __launch_bounds__(256) void sqnorm_dense_kernel(const float* __restri
       s3 = fmaf(v.w, v.w, s3);
     }
     s = (s0 + s1) + (s2 + s3);
-    for (long i = 4 * n4 + blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+    for (long i = 4 * n4 + bx * 256L + threadIdx.x; i < n; i += (long)gx * 256) s = fmaf(x[i], x[i], s);
   } else {
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) s = fmaf(x[i], x[i], s);
+    for (long i = bx * 256L + threadIdx.x; i < n; i += (long)gx * 256) s = fmaf(x[i], x[i], s);
   }
-  s = block_sum(s, red);
+  return s;
+}
+
+__global__ __launch_bounds__(256) void sqnorm_dense_kernel(const float* __restrict__ x, long n,
+                                                           float* __restrict__ part) {
+  __shared__ float red[4];
+  const float s = block_sum(sqnorm_dense_part(x, n, blockIdx.x, gridDim.x), red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
 // Compact row grads: rows are sorted by key and the INVALID group (if any) is the last row, so the
 // valid rows are one contiguous prefix -- summed as a flat float4 stream (padding columns are zero).
-__global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __restrict__ keys,
-                                                          const float* __restrict__ G,
-                                                          const uint32_t* __restrict__ n_uniq, int width, int ld,
-                                                          uint32_t invalid_key, float* __restrict__ part) {
-  __shared__ float red[4];
+__device__ __forceinline__ float sqnorm_rows_part(const uint32_t* __restrict__ keys, const float* __restrict__ G,
+                                                 const uint32_t* __restrict__ n_uniq, int width, int ld,
+                                                 uint32_t invalid_key, int bx, int gx) {
   const uint32_t nu = *n_uniq;
   const uint32_t nv = (nu > 0 && keys[nu - 1] == invalid_key) ? nu - 1 : nu;
   float s = 0.f;
@@ -170,7 +173,7 @@ __global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __rest
     const float4* G4 = (const float4*)G;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // four chains, four loads in flight
 #pragma unroll 4
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total4; i += (long)gridDim.x * 256) {
+    for (long i = bx * 256L + threadIdx.x; i < total4; i += (long)gx * 256) {
       const float4 g = G4[i];
       s0 = fmaf(g.x, g.x, s0);
       s1 = fmaf(g.y, g.y, s1);
@@ -180,14 +183,43 @@ __global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __rest
     s = (s0 + s1) + (s2 + s3);
   } else {
     const long total = (long)nv * width;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    for (long i = bx * 256L + threadIdx.x; i < total; i += (long)gx * 256) {
       const long u = i / width;
       const float g = G[u * ld + (i - u * width)];
       s = fmaf(g, g, s);
     }
   }
-  s = block_sum(s, red);
+  return s;
+}
+
+__global__ __launch_bounds__(256) void sqnorm_rows_kernel(const uint32_t* __restrict__ keys,
+                                                          const float* __restrict__ G,
+                                                          const uint32_t* __restrict__ n_uniq, int width, int ld,
+                                                          uint32_t invalid_key, float* __restrict__ part) {
+  __shared__ float red[4];
+  const float s = block_sum(sqnorm_rows_part(keys, G, n_uniq, width, ld, invalid_key, blockIdx.x, gridDim.x), red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// the dense grads and up to CTR_SQNORM_MAX_ROWS compact row-grad tables in ONE launch: grid row y = 0 the dense
+// stream, y = 1 + j table j, each row of NORM_BLOCKS blocks writing the partials ctr_sqnorm_dense /
+// ctr_sqnorm_rows write (the same per-block sums: the same bits) at part[y * NORM_BLOCKS ..]
+struct SqnormRowsSet {
+  ctr_sqnorm_rows_t r[CTR_SQNORM_MAX_ROWS];
+};
+__global__ __launch_bounds__(256) void sqnorm_all_kernel(const float* __restrict__ x, long n, SqnormRowsSet rs,
+                                                         uint32_t invalid_key, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int y = blockIdx.y;
+  float s;
+  if (y == 0) {
+    s = sqnorm_dense_part(x, n, blockIdx.x, gridDim.x);
+  } else {
+    const ctr_sqnorm_rows_t& r = rs.r[y - 1];
+    s = sqnorm_rows_part(r.keys, r.G, r.n_uniq, r.width, r.ld, invalid_key, blockIdx.x, gridDim.x);
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[(long)y * gridDim.x + blockIdx.x] = s;
 }
 
 // grad_scale = 1/world under data parallelism: grads were summed across ranks, the reference
@@ -247,6 +279,15 @@ extern "C" int ctr_sqnorm_rows(const uint32_t* keys, const float* G, const uint3
                                uint32_t invalid_key, float* part, void* stream) {
   sqnorm_rows_kernel<<<NORM_BLOCKS, 256, 0, (hipStream_t)stream>>>(keys, G, n_uniq, width, ld, invalid_key, part);
   return check_launch("sqnorm_rows");
+}
+
+extern "C" int ctr_sqnorm_all(const float* x, long n, const ctr_sqnorm_rows_t* rows, int nrows, uint32_t invalid_key,
+                              float* part, void* stream) {
+  CTR_REQUIRE(nrows >= 0 && nrows <= CTR_SQNORM_MAX_ROWS && (nrows == 0 || rows), "ctr_sqnorm_all: bad row tables");
+  SqnormRowsSet rs{};
+  for (int j = 0; j < nrows; ++j) rs.r[j] = rows[j];
+  sqnorm_all_kernel<<<dim3(NORM_BLOCKS, 1 + nrows), 256, 0, (hipStream_t)stream>>>(x, n, rs, invalid_key, part);
+  return check_launch("sqnorm_all");
 }
 
 extern "C" int ctr_clip_finalize(const float* part, int nparts, float max_norm, float grad_scale, float* out,

@@ -34,6 +34,10 @@ class OptSeg(C.Structure):
                 ("key_base", C.c_uint32)]
 
 
+class SqnormRows(C.Structure):
+    _fields_ = [("keys", p), ("G", p), ("n_uniq", p), ("width", i), ("ld", i)]
+
+
 class OptChunk(C.Structure):
     _fields_ = [("seg", C.c_int32), ("pad", C.c_int32), ("e0", C.c_int64), ("e1", C.c_int64)]
 
@@ -151,6 +155,7 @@ SIGS = {
     "ctr_norm_nparts_per_call": (i, []),
     "ctr_sqnorm_dense": (i, [p, l, p, p]),
     "ctr_sqnorm_rows": (i, [p, p, p, i, i, u, p, p]),
+    "ctr_sqnorm_all": (i, [p, l, C.POINTER(SqnormRows), i, u, p, p]),
     "ctr_clip_finalize": (i, [p, i, f, f, p, p]),
     "ctr_mask_tail_keys": (i, [p, i, i, p, p]),
     "ctr_opt_hist_entry_bytes": (i, []),

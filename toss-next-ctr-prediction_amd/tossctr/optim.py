@@ -166,6 +166,8 @@ class FusedAdamW:
         self.norm_parts = torch.zeros(4 * self.nparts_call, dtype=torch.float32, device=dev)
         self._seg_key = None
         self._segs_dev = None
+        self._norm_key = None
+        self._norm_arr = None
         self._build_chunks()
         # exact lazy table update (csrc/lazy.hip): tables leave the dense stream; rows are replayed to
         # the current tick when read, when they get a gradient, or at flush()
@@ -372,16 +374,26 @@ class FusedAdamW:
         return self._segs_dev
 
     # -------------------------------------------------------------- step
-    def clip(self, tg):
+    def _norm_rows(self, tg):
+        """The three compact row-grad tables as ctr_sqnorm_all's host array (rebuilt only when the buffers move)."""
+        ts = [tg[name] for name in ("att", "rep", "cat")]
+        key = tuple((ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["width"], t["G"].shape[1]) for t in ts)
+        if key != self._norm_key:
+            arr = (_lib.SqnormRows * len(key))()
+            for o, k in zip(arr, key):
+                o.keys, o.G, o.n_uniq, o.width, o.ld = k
+            self._norm_arr, self._norm_key = arr, key
+        return self._norm_arr
+
+    def clip(self, tg, rows=None):
         """Global grad L2 norm over dense grads + deduplicated table rows -> (norm, coef) on device."""
         st = self.engine.s()
         parts = self.norm_parts
         n = self.nparts_call
-        call("ctr_sqnorm_dense", ptr(self.arena.grad), self.arena.n_dense_grad, ptr(parts, 0), st)
-        for j, name in enumerate(("att", "rep", "cat")):
-            t = tg[name]
-            call("ctr_sqnorm_rows", ptr(t["keys"]), ptr(t["G"]), ptr(t["n_uniq"]), t["width"], t["G"].shape[1],
-                 INVALID_KEY, ptr(parts, (j + 1) * n), st)
+        # dense + the three tables' partials in one launch (the bits of ctr_sqnorm_dense + 3 ctr_sqnorm_rows)
+        rows = rows if rows is not None else self._norm_rows(tg)
+        call("ctr_sqnorm_all", ptr(self.arena.grad), self.arena.n_dense_grad, rows, len(rows), INVALID_KEY,
+             ptr(parts, 0), st)
         if self.shards is not None:     # each rank holds its own rows' grads: sum the table partials
             from . import dist as D
             D.allreduce_sum_(parts[n:], self.pg)
@@ -444,8 +456,10 @@ class FusedAdamW:
             tg = self.exchange(tg)
             self.engine.tg = tg
         g = self.param_groups[0]
-        self.clip(tg)
-        self.step_count += 1
+        # everything the update launches need is put together BEFORE the clip is issued: the clip's kernels are short
+        # and the device drains them faster than the host issues them, so host work between the clip and the update
+        # sat in the trace as an idle gap (24 us a step, profiles/r06/gaps_final.md); issued here it overlaps the
+        # backward's long kernels instead
         do_ema = 0
         decay = 0.0
         if self.ema is not None and global_step is not None and self.ema.wants_update(global_step):
@@ -454,39 +468,45 @@ class FusedAdamW:
         segs = self._segs_device(tg)
         chunks, n = self._chunks_dev[("all" if do_ema else "adam") + ("_dense" if self.lazy else "")]
         b1, b2 = g["betas"]
-        st = self.engine.s()
-        if self._timing:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
         shadow = ptr(self.ema.shadow) if self.ema is not None else ptr(self.arena.buf)
+        tick = self.tick + 1 if self.lazy else self.tick
+        head = (ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m), ptr(self.v), shadow,
+                ptr(self.arena.grad), ptr(self.norm_out, 1), float(g["lr"]), float(g["weight_decay"]), float(b1),
+                float(b2), float(g["eps"]), self.step_count + 1, float(decay))
+        rows = self._norm_rows(tg)
+        updates = []
         if self.lazy:
-            # the tick's scalars go to the lazy tables' history in the same launches as the dense update
-            self.tick += 1
-            call("ctr_adamw_ema_hist", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
-                 ptr(self.v), shadow, ptr(self.arena.grad), ptr(self.norm_out, 1), float(g["lr"]),
-                 float(g["weight_decay"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(decay),
-                 do_ema, ptr(self._hist_for(self.tick)), self.tick, st)
-        else:
-            call("ctr_adamw_ema", ptr(chunks), n, ptr(segs), ptr(self.krange), ptr(self.arena.buf), ptr(self.m),
-                 ptr(self.v), shadow, ptr(self.arena.grad), ptr(self.norm_out, 1), float(g["lr"]),
-                 float(g["weight_decay"]), float(b1), float(b2), float(g["eps"]), self.step_count, float(decay), 1,
-                 do_ema, st)
-        if self.lazy:
+            hist = ptr(self._hist_for(tick))
             ta, tr, tc = tg["att"], tg["rep"], tg["cat"]
             if ta["keys"] is tr["keys"] and ta["G"].shape[1] == tr["G"].shape[1]:
                 # att and rep grads share their keys: one wave per key updates both rows
-                call("ctr_lazy_update_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width, ptr(ta["keys"]),
-                     ptr(ta["G"]), ptr(tr["G"]), ta["G"].shape[1], ptr(ta["n_uniq"]), ta["n"], ptr(self.norm_out, 1),
-                     ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(), ptr(self.hist), self.tick, st)
+                updates.append(("ctr_lazy_update_pair", ptr(self._lazy_tabs["seq"][0]), self._seq_width,
+                                ptr(ta["keys"]), ptr(ta["G"]), ptr(tr["G"]), ta["G"].shape[1], ptr(ta["n_uniq"]),
+                                ta["n"], ptr(self.norm_out, 1), ptr(self.arena.buf), ptr(self.m), ptr(self.v),
+                                self._ema_ptr(), hist, tick))
                 names = ("cat",)
             else:
                 names = ("att", "rep", "cat")
             for name in names:
                 t = tg[name]
                 tabs, nt = self._lazy_tabs[name]
-                call("ctr_lazy_update", ptr(tabs), nt, ptr(t["keys"]), ptr(t["G"]), t["G"].shape[1], ptr(t["n_uniq"]),
-                     t["n"], ptr(self.norm_out, 1), ptr(self.arena.buf), ptr(self.m), ptr(self.v), self._ema_ptr(),
-                     ptr(self.hist), self.tick, st)
+                updates.append(("ctr_lazy_update", ptr(tabs), nt, ptr(t["keys"]), ptr(t["G"]), t["G"].shape[1],
+                                ptr(t["n_uniq"]), t["n"], ptr(self.norm_out, 1), ptr(self.arena.buf), ptr(self.m),
+                                ptr(self.v), self._ema_ptr(), hist, tick))
+        self.clip(tg, rows)
+        self.step_count += 1
+        st = self.engine.s()
+        if self._timing:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        if self.lazy:
+            # the tick's scalars go to the lazy tables' history in the same launches as the dense update
+            self.tick = tick
+            call("ctr_adamw_ema_hist", *head, do_ema, hist, tick, st)
+        else:
+            call("ctr_adamw_ema", *head, 1, do_ema, st)
+        for u in updates:
+            call(*u, st)
         if self._timing:
             ev[1].record()
             self._events.append(ev)
