@@ -463,8 +463,9 @@ int ctr_opt_chunk_elems(void);
 int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, uint32_t* krange, float* P,
                   float* M, float* V, float* E, const float* dgrad, const float* coef, float lr, float wd, float beta1,
                   float beta2, float eps, int step, float ema_decay, int do_adam, int do_ema, void* stream);
-/* ctr_adamw_ema (do_adam = 1) with hist[tick] = the same tick's scalars recorded in the same launches
- * (ctr_opt_hist_record + ctr_adamw_ema of a lazy FusedAdamW step, one dispatch fewer)                        */
+/* ctr_adamw_ema (do_adam = 1) with hist[tick] = the same tick's scalars recorded in the same launch
+ * (ctr_opt_hist_record + ctr_adamw_ema of a lazy FusedAdamW step: one dispatch where those were three; sparse chunks'
+ * key ranges are searched inside it, krange is then unused)                                                    */
 int ctr_adamw_ema_hist(const ctr_opt_chunk_t* chunks, int nchunks, const ctr_opt_seg_t* segs, uint32_t* krange,
                        float* P, float* M, float* V, float* E, const float* dgrad, const float* coef, float lr, float wd,
                        float beta1, float beta2, float eps, int step, float ema_decay, int do_ema, void* hist, int tick,

@@ -257,3 +257,49 @@ def test_cat_flush_classified_equals_touch_replay(ema):
             assert torch.equal(a.view(torch.int32), b.view(torch.int32)), (name, int((a != b).sum()))
     assert torch.equal(ref[4], got[4])
     assert bool(((ref[4] & 0x7FFFFFFF) == T).all())
+
+
+def test_adamw_ema_hist_one_launch_equals_two_kernel_form():
+    """ctr_adamw_ema_hist runs as ONE launch (the tick's history record and the sparse chunks' key-range searches
+    inside adamw_ema_kernel<true>): on the dense optimizer's full chunk list -- sparse table chunks included, which
+    the lazy step never hands it -- it writes bit for bit what ctr_adamw_ema (chunk_key_range_kernel + adamw_ema_kernel)
+    writes, and records the tick's scalars."""
+    from tossctr import ArenaEMA, FusedAdamW
+    from tossctr._lib import call
+    from tossctr.engine import ptr
+    fx = Fixture("tiny_concat")
+    m, tr = fx.meta, fx.meta["train"]
+    vocab = int(m["vocab"]) * 40
+    cards = {k: v * 50 for k, v in fx.cat_cards.items()}
+    md, _ = _models(fx, vocab, cards)
+    ema = ArenaEMA(md, base_decay=0.99, warmup_steps=5, warmup_type="cosine")
+    od = FusedAdamW(md, lr=1e-3, weight_decay=tr["wd"], max_grad_norm=tr["clip"], ema=ema, lazy=False)
+    b = make_batch(48, m["Fn"], m["Fm"], list(cards.values()), int(m["L"]), vocab, seed=77)
+    md.train()
+    md.train_step(md.stage(to_torch_batch(b)), torch.from_numpy(b["y"]).float().cuda(), od, global_step=1, seed=5)
+    tg = md.engine.tg
+    segs = od._segs_device(tg)
+    chunks, n = od._chunks_dev["all"]
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for form in ("two", "one"):
+        P, M, V, E = md.arena.buf.clone(), od.m.clone(), od.v.clone(), ema.shadow.clone()
+        krange = torch.full((2 * n,), -1, dtype=torch.int32, device="cuda")
+        hist = torch.zeros(64 * 64, dtype=torch.uint8, device="cuda")
+        args = (ptr(chunks), n, ptr(segs), ptr(krange), ptr(P), ptr(M), ptr(V), ptr(E), ptr(md.arena.grad),
+                ptr(od.norm_out, 1), 1e-3, float(tr["wd"]), 0.9, 0.999, 1e-8, 2, 0.97)
+        if form == "two":
+            call("ctr_adamw_ema", *args, 1, 1, st)
+        else:
+            call("ctr_adamw_ema_hist", *args, 1, ptr(hist), 3, st)
+        outs.append((P, M, V, E, hist))
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0][:4], outs[1][:4]):
+        assert torch.equal(a, c)
+    assert not torch.equal(outs[0][0], md.arena.buf)                 # the launch stepped something
+    from tossctr import _lib
+    hb = _lib.query("ctr_opt_hist_entry_bytes")
+    h = outs[1][4]
+    assert int(h[:3 * hb].sum()) == 0 and int(h[3 * hb:4 * hb].sum()) != 0 and int(h[4 * hb:].sum()) == 0   # tick 3 only
+    kinds = {int(s["kind"]) for s in od._segments(tg)}
+    assert 1 in kinds                                                  # sparse table chunks were in the list

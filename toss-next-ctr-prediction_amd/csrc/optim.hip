@@ -61,14 +61,21 @@ __device__ __forceinline__ float row_grad(const ctr_opt_seg_t& sg, const int* ma
 // scratch).  Segments are streamed in whole float4s: the tail float4 lies inside the param's
 // 64-element arena padding.  Sparse segments: the touched rows of the chunk are mapped into an LDS
 // slot table from the precomputed key range; untouched rows get grad 0 (dense AdamW semantics).
+// INLINE (ctr_adamw_ema_hist): no chunk_key_range launch before it -- block 0 records the tick's scalars in the
+// history, and a sparse chunk's key range is searched by the workgroup itself (the same binary searches: the same
+// range).  The lazy step's chunk lists hold no sparse segment, so there the launch and its boundary simply go.
+template <bool INLINE = false>
 __global__ __launch_bounds__(256) void adamw_ema_kernel(const ctr_opt_chunk_t* __restrict__ chunks,
                                                         const ctr_opt_seg_t* __restrict__ segs,
                                                         const uint32_t* __restrict__ krange,
                                                         float* __restrict__ P, float* __restrict__ M,
                                                         float* __restrict__ V, float* __restrict__ E,
                                                         const float* __restrict__ dgrad,
-                                                        const float* __restrict__ coef_ptr, OptScalars s) {
+                                                        const float* __restrict__ coef_ptr, OptScalars s,
+                                                        OptScalars* __restrict__ hist = nullptr, int tick = 0) {
   __shared__ int map[OPT_MAXROWS];
+  __shared__ uint32_t srange[2];
+  if (INLINE && blockIdx.x == 0 && threadIdx.x == 0) hist[tick] = s;
   const ctr_opt_chunk_t ch = chunks[blockIdx.x];
   const ctr_opt_seg_t sg = segs[ch.seg];
   const float coef = coef_ptr ? *coef_ptr : 1.0f;
@@ -83,7 +90,26 @@ __global__ __launch_bounds__(256) void adamw_ema_kernel(const ctr_opt_chunk_t* _
     nrows = (int)((ch.e1 - 1) / width - r0 + 1);
     for (int i = tid; i < nrows; i += 256) map[i] = -1;
     __syncthreads();
-    const uint32_t lo = krange[2 * blockIdx.x], hi = krange[2 * blockIdx.x + 1];
+    uint32_t lo, hi;
+    if (INLINE) {
+      if (tid == 0) {      // chunk_key_range_kernel's searches for this chunk
+        const uint32_t nu = *sg.n_uniq;
+        const uint32_t k0 = sg.key_base + (uint32_t)(ch.e0 / sg.width);
+        const uint32_t k1 = sg.key_base + (uint32_t)((min(ch.e1, sg.n) - 1) / sg.width);
+        uint32_t a = 0, b = nu;
+        while (a < b) { const uint32_t mid = (a + b) >> 1; if (sg.keys[mid] < k0) a = mid + 1; else b = mid; }
+        srange[0] = a;
+        b = nu;
+        while (a < b) { const uint32_t mid = (a + b) >> 1; if (sg.keys[mid] <= k1) a = mid + 1; else b = mid; }
+        srange[1] = a;
+      }
+      __syncthreads();
+      lo = srange[0];
+      hi = srange[1];
+    } else {
+      lo = krange[2 * blockIdx.x];
+      hi = krange[2 * blockIdx.x + 1];
+    }
     const uint32_t k0 = sg.key_base + (uint32_t)r0;
     for (uint32_t i = lo + tid; i < hi; i += 256) map[sg.keys[i] - k0] = (int)i;
     __syncthreads();
@@ -251,7 +277,7 @@ extern "C" int ctr_adamw_ema(const ctr_opt_chunk_t* chunks, int nchunks, const c
   const OptScalars s = make_opt_scalars(lr, wd, beta1, beta2, eps, step, ema_decay, do_adam, do_ema);
   hipStream_t st = (hipStream_t)stream;
   if (do_adam) chunk_key_range_kernel<<<cdiv(nchunks, 256), 256, 0, st>>>(chunks, nchunks, segs, krange);
-  adamw_ema_kernel<<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);
+  adamw_ema_kernel<false><<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);
   return check_launch("adamw_ema");
 }
 
@@ -262,9 +288,11 @@ extern "C" int ctr_adamw_ema_hist(const ctr_opt_chunk_t* chunks, int nchunks, co
   CTR_REQUIRE(hist != nullptr && tick > 0, "ctr_adamw_ema_hist: bad history / tick");
   const OptScalars s = make_opt_scalars(lr, wd, beta1, beta2, eps, step, ema_decay, 1, do_ema);
   hipStream_t st = (hipStream_t)stream;
-  chunk_key_range_kernel<<<std::max(1, cdiv(nchunks, 256)), 256, 0, st>>>(chunks, nchunks, segs, krange,
-                                                                        (OptScalars*)hist, tick, s);
-  if (nchunks > 0) adamw_ema_kernel<<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s);
+  if (nchunks > 0)     // one launch: the history record and any sparse chunk's key range inside (adamw_ema_kernel<true>)
+    adamw_ema_kernel<true><<<nchunks, 256, 0, st>>>(chunks, segs, krange, P, M, V, E, dgrad, coef, s, (OptScalars*)hist,
+                                                    tick);
+  else
+    chunk_key_range_kernel<<<1, 256, 0, st>>>(chunks, 0, segs, krange, (OptScalars*)hist, tick, s);
   return check_launch("adamw_ema_hist");
 }
 
