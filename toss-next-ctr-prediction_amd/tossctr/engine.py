@@ -961,12 +961,13 @@ class Engine:
                 self.colsum(ptr(dwp), D, npart, D, ptr(G[pre + "norm1.w"]))
         # out_proj
         do = W.get("do", (M, D))
-        if self.attn_oproj:              # dO is formed inside the attention backward below
-            with self.side():
-                if slab_sum is not None:
-                    self.colsum(*slab_sum, defer=True)
-                self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
-                                pre + "mha.out_proj.bias", tag=li, defer=True)
+        # dO formed inside the attention backward below (attn_oproj): the FFN slab sums and out_proj's weight grad go to
+        # the side stream together with the attention backward's side work -- one fork (event record + wait) per
+        # layer instead of two, a boundary fewer on the main stream (3.260 -> 3.222 ms a step over four same-box
+        # pairs, profiles/r06/ab_merge_fork.log)
+        oproj_side = self.attn_oproj
+        if oproj_side:
+            pass
         elif self.rowgemm:
             if slab_sum is not None:     # main-stream product first, then the side stream's slab sums
                 self.rowgemm_call(M, D, D, ptr(dh1), ptr(P[pre + "mha.out_proj.weight"]), 0, ptr(do))
@@ -1009,6 +1010,11 @@ class Engine:
         x_in = sv["xs"][li]
         # (here the side work goes first: queuing the in_proj input grad ahead of it measured 0.02 ms/step slower)
         with self.side():
+            if oproj_side:
+                if slab_sum is not None:
+                    self.colsum(*slab_sum, defer=True)
+                self.wgrad_rows(W, ptr(dh1), ptr(Ls["o"]), M, D, D, pre + "mha.out_proj.weight",
+                                pre + "mha.out_proj.bias", tag=li, defer=True)
             if a.add_pos:
                 call("ctr_pos_bias_grad", ptr(drp), nparts, a.H, nrel, ptr(G[pre + "pbias.rel.weight"]), self.s())
             if self.rowgemm:
