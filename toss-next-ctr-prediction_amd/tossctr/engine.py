@@ -465,6 +465,9 @@ class Engine:
               "X_cat": X_cat, "seq": seq}
         xF = W.get("xF", (B, FD))
         num_off, mask_off, cat_off = D, D + a.Fn * D, D + (a.Fn + a.Fm) * D
+        # table rows brought current first (the DARE pair's on the side stream: joined before the top-K select)
+        tv = self._table_views(X_cat, seq)
+        sv["tv"] = tv
         # ---- numeric / binary embeddings straight into their xF slots (feature_embed.py:19-27,42-48)
         if a.Fn > 0 and a.Fm > 0:      # both groups in one launch
             call("ctr_feat_embed_fwd2", ptr(X_num), a.Fn, ptr(P["num_embed.weight"]), ptr(P["num_embed.bias"]),
@@ -478,8 +481,6 @@ class Engine:
                  ptr(P["mask_embed.out_proj.weight"]), a.f_embed, D, ptr(xF, mask_off), FD, st)
         # ---- hashed categorical gather + projection (+ emb dropout into xF) (wrapper.py:106-112,149-150)
         cat_e = W.get("cat_e", (B, a.Fc, D))
-        tv = self._table_views(X_cat, seq)
-        sv["tv"] = tv
         if prefetch is not None and self.shards is not None:
             self.shards.prefetch(*prefetch)
         dk = drop_args(seed, SITE_EMB, a.p_emb, training)
@@ -497,6 +498,7 @@ class Engine:
         tok = W.get("topk_tok", (B, K), torch.int32)
         vals = W.get("topk_vals", (B, K))
         xs = [W.get("x0", (B, K, D))]
+        self.join()                     # the DARE rows' touch (side stream, _table_views)
         call("ctr_dare_topk_fwd", ptr(tv["seq"]), B, L, ptr(query), tv["att"], tv["rep"], D, ptr(self.decay_log(L)), K,
              tv["pad"], ptr(idx), ptr(tok), ptr(vals), ptr(xs[0]), st)
         # ---- encoder layers (dare.py:53-70)
@@ -625,7 +627,10 @@ class Engine:
         if self.shards is None:
             if self.lazy is not None:
                 self.lazy.touch_rows(X_cat, "cat")
-                self.lazy.touch_rows(seq, "seq")
+                # the DARE rows' catch-up (the longest touch, latency-bound) on the side stream beside the
+                # embedding / categorical / context forward; the main stream joins it before the top-K select
+                with self.side():
+                    self.lazy.touch_rows(seq, "seq")
             return dict(fx=None, xcat=X_cat, seq=seq, pad=a.pad_id, cat_tab=None, cat_off=ptr(self.cat_tab_off),
                         cat_ld=0, att=ptr(P["dare.emb_att.weight"]), rep=ptr(P["dare.emb_rep.weight"]),
                         row_base=ptr(self.cat_row_base), seq_bits=self.seq_key_bits, cat_bits=self.cat_key_bits)
